@@ -1,0 +1,66 @@
+"""Loaders that rebuild the exact synthetic states behind each golden fixture.
+
+Test infrastructure. Mirrors the synthesis in make_goldens.py (same seeds, same sorted
+generation order) without touching /root/reference, so it works on the GPU box too.
+"""
+import os
+
+import numpy as np
+import torch
+
+from synth import synth_state, synth_wave, synth_codebooks, rng
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def load(name):
+    return np.load(os.path.join(HERE, name), allow_pickle=False)
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def model_state(cfg, seed):
+    from oracle.encodec_oracle import model_param_shapes
+    return {k: T(v) for k, v in synth_state(model_param_shapes(cfg), seed).items()}
+
+
+def disc_state(seed):
+    from oracle.encodec_oracle import disc_param_shapes
+    return {k: T(v) for k, v in synth_state(disc_param_shapes(), seed).items()}
+
+
+def codebooks_from_stats(stats, seed, n_used, n_total):
+    """Same draws as make_goldens.fill_codebooks."""
+    cbs = synth_codebooks(stats, seed)
+    g = rng(seed + 1)
+    out = []
+    for i in range(n_total):
+        if i < n_used:
+            cs = g.uniform(0.5, 4.0, size=(1024,)).astype(np.float32)
+            out.append({'inited': torch.ones(1), 'cluster_size': T(cs), 'embed': T(cbs[i]),
+                        'embed_avg': T((cbs[i] * cs[:, None]).astype(np.float32))})
+        else:
+            out.append({'inited': torch.ones(1), 'cluster_size': torch.zeros(1024),
+                        'embed': torch.zeros(1024, 128), 'embed_avg': torch.zeros(1024, 128)})
+    return out
+
+
+def g3_codebooks(d):
+    stats = d['stats']
+    cbs = synth_codebooks(stats, 32)
+    return [{'inited': torch.ones(1), 'cluster_size': T(d[f'cs_init{i}']), 'embed': T(cbs[i]),
+             'embed_avg': T(d[f'ea_init{i}'])} for i in range(2)]
+
+
+def certified(gaps, x_norm2, e_norm2, factor=256):
+    """Rows whose fp64 top-2 distance gap exceeds fp32 rounding of the expanded distance
+    (factor * eps32 * (|x|^2 + |e|^2)): there the argmin is decided, and codes must match
+    bit-exactly. Returns a bool mask."""
+    eps = np.finfo(np.float32).eps
+    return gaps > factor * eps * (x_norm2 + e_norm2)
+
+
+__all__ = ['load', 'T', 'model_state', 'disc_state', 'codebooks_from_stats', 'g3_codebooks',
+           'certified', 'synth_wave', 'rng']

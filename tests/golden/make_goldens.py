@@ -1,0 +1,386 @@
+"""Generate the golden fixtures in tests/golden/*.npz by RUNNING THE REFERENCE.
+
+Test infrastructure; runs only in the build container, where /root/reference exists
+(`python tests/golden/make_goldens.py`). The reference is imported with the shims of
+ref_shims.py; every parameter / input is synthesised by synth.py from PCG64 seeds so the
+tests can regenerate them bit-identically without any weight file.
+
+Fixture map:
+  g1_eval24k.npz   config 1: 24 kHz causal weight-norm model, eval forward, bw 1.5 (n_q 2)
+  g2_convs.npz     SConv1d / SConvTranspose1d outputs + grads (dx, dv, dg, db)
+  g3_rvq.npz       RVQ train forward (n_q 2, K 1024) + EMA buffers + emb grad; kmeans
+  g4_mel.npz       Audio2Mel 7 scales, Spectrogram 3 scales, l_t / l_f and d l_f / d y
+  g5_disc.npz      MS-STFT discriminator logits, fmap checksums, input grad
+  g6_balancer.npz  Balancer known-answer test (balancer.py:121-139) + a 4-loss case
+  g7_step.npz      one full train step (gen-only and GAN), B 2, T 4800, n_q 2
+  g8_sched.npz     WarmupCosineLrScheduler learning-rate trace
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+from ref_shims import import_reference  # noqa: E402
+from synth import synth_state, synth_wave, synth_codebooks, rng  # noqa: E402
+
+torch.set_num_threads(8)
+R = import_reference()
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def load_synth(module, seed):
+    sd = module.state_dict()
+    shapes = {k: tuple(v.shape) for k, v in sd.items()
+              if v.dtype == torch.float32 and '_codebook' not in k and 'spec_transform' not in k}
+    st = synth_state(shapes, seed)
+    new = dict(sd)
+    for k, v in st.items():
+        new[k] = t(v)
+    module.load_state_dict(new)
+    return st
+
+
+def save(name, **arrs):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
+    print('wrote', path, os.path.getsize(path) // 1024, 'KB')
+
+
+def fill_codebooks(model, stats, seed, n_used):
+    cbs = synth_codebooks(stats, seed)
+    g = rng(seed + 1)
+    for i, layer in enumerate(model.quantizer.vq.layers):
+        c = layer._codebook
+        if i < n_used:
+            c.embed.data.copy_(t(cbs[i]))
+            cs = g.uniform(0.5, 4.0, size=(1024,)).astype(np.float32)
+            c.cluster_size.data.copy_(t(cs))
+            c.embed_avg.data.copy_(t((cbs[i] * cs[:, None]).astype(np.float32)))
+        c.inited.data.fill_(1.0)
+
+
+def emb_stats(model, x, n_q):
+    """Per-dim mean/std of the encoder output and of each RVQ residual (used to synthesise
+    codebooks near the data)."""
+    model.eval()
+    with torch.no_grad():
+        xn = x / (1e-8 + x.mean(1, keepdim=True).pow(2).mean(2, keepdim=True).sqrt())
+        emb = model.encoder(xn)
+    return emb
+
+
+def top2_gaps(emb, embeds, codes):
+    """fp64 certificate per frame and layer: distance of the 2nd-best code minus the best,
+    along the residual chain the reference's own codes define (eval: residual -= q)."""
+    res = emb.double().permute(0, 2, 1).reshape(-1, emb.shape[1])
+    gaps = []
+    for i, E in enumerate(embeds):
+        E = E.double()
+        d = (res ** 2).sum(1, keepdim=True) - 2 * res @ E.t() + (E ** 2).sum(1)[None]
+        s = torch.sort(d, dim=1).values
+        gaps.append((s[:, 1] - s[:, 0]).numpy())
+        ind = codes[:, i].reshape(-1).long() if codes.dim() == 3 else codes[i].reshape(-1).long()
+        res = res - E[ind]
+    return np.stack(gaps)
+
+
+# ------------------------------------------------------------------------------------ G1
+def g1():
+    m = R.model.EncodecModel._get_model([1.5, 3., 6., 12., 24.], 24000, 1, causal=True,
+                                        model_norm='weight_norm', audio_normalize=False,
+                                        segment=None, name='encodec_24khz')
+    load_synth(m, 1)
+    x = t(synth_wave((1, 1, 24000), 1234))
+    m.eval()
+    with torch.no_grad():
+        emb = m.encoder(x)
+    e = emb[0].t().double()
+    stats = np.zeros((2, 2, 128), np.float32)
+    stats[0, 0] = e.mean(0).float().numpy()
+    stats[0, 1] = e.std(0).float().numpy()
+    cb0 = synth_codebooks(stats[:1], 77)[0]
+    # residual after layer 0 with that codebook
+    xf = emb[0].t()
+    ind = R.quantization.core_vq.EuclideanCodebook.quantize(
+        type('o', (), {'embed': t(cb0)})(), xf)
+    r1 = (xf - t(cb0)[ind]).double()
+    stats[1, 0] = r1.mean(0).float().numpy()
+    stats[1, 1] = r1.std(0).float().numpy()
+    fill_codebooks(m, stats, 77, 2)
+    m.set_target_bandwidth(1.5)
+    with torch.no_grad():
+        y = m(x)
+        codes = m.encode(x)[0][0]
+        gaps = top2_gaps(emb, [m.quantizer.vq.layers[i]._codebook.embed for i in range(2)], codes)
+    save('g1_eval24k.npz', x=x.numpy(), emb=emb.numpy(), codes=codes.numpy().astype(np.int16),
+         y=y.numpy(), stats=stats, gaps=gaps)
+
+
+# ------------------------------------------------------------------------------------ G2
+CONV_CASES = [
+    # name, kind, cin, cout, K, s, causal, pre_elu, T
+    ('c_k7_1to8', 'conv', 1, 8, 7, 1, True, False, 480),
+    ('c_k3_16to8_elu', 'conv', 16, 8, 3, 1, True, True, 480),
+    ('c_k1_8to16_elu', 'conv', 8, 16, 1, 1, True, True, 480),
+    ('c_k1_16to16', 'conv', 16, 16, 1, 1, True, False, 480),
+    ('c_k4s2_16to32_elu', 'conv', 16, 32, 4, 2, True, True, 480),
+    ('c_k10s5_16to32_elu', 'conv', 16, 32, 10, 5, True, True, 480),
+    ('c_k16s8_32to64_elu', 'conv', 32, 64, 16, 8, True, True, 480),
+    ('c_k7_64to16_elu', 'conv', 64, 16, 7, 1, True, True, 30),
+    ('c_k7_short_reflect', 'conv', 8, 8, 7, 1, True, False, 5),
+    ('c_k7s1_nc', 'conv', 8, 8, 7, 1, False, False, 100),
+    ('c_k10s5_nc_odd', 'conv', 8, 16, 10, 5, False, True, 97),
+    ('t_k4s2_32to16_elu', 'convtr', 32, 16, 4, 2, True, True, 240),
+    ('t_k10s5_32to16_elu', 'convtr', 32, 16, 10, 5, True, True, 96),
+    ('t_k16s8_64to32_elu', 'convtr', 64, 32, 16, 8, True, True, 60),
+    ('t_k8s4_nc', 'convtr', 16, 8, 8, 4, False, False, 50),
+]
+
+
+def g2():
+    out = {}
+    for ci, (name, kind, cin, cout, K, s, causal, pre_elu, T) in enumerate(CONV_CASES):
+        if kind == 'conv':
+            mod = R.modules.SConv1d(cin, cout, K, stride=s, causal=causal, norm='weight_norm')
+        else:
+            mod = R.modules.SConvTranspose1d(cin, cout, K, stride=s, causal=causal, norm='weight_norm')
+        load_synth(mod, 100 + ci)
+        x = t(synth_wave((2, cin, T), 200 + ci, amp=1.0)).requires_grad_(True)
+        xin = torch.nn.functional.elu(x) if pre_elu else x
+        y = mod(xin)
+        gy = t(synth_wave(tuple(y.shape), 300 + ci, amp=1.0))
+        y.backward(gy)
+        params = dict(mod.named_parameters())
+        pre = [k for k in params if k.endswith('weight_v')][0][:-len('weight_v')]
+        out[name + '/x'] = x.detach().numpy()
+        out[name + '/y'] = y.detach().numpy()
+        out[name + '/gy'] = gy.numpy()
+        out[name + '/dx'] = x.grad.numpy()
+        out[name + '/dv'] = params[pre + 'weight_v'].grad.numpy()
+        out[name + '/dg'] = params[pre + 'weight_g'].grad.numpy()
+        out[name + '/db'] = params[pre + 'bias'].grad.numpy()
+    save('g2_convs.npz', **out)
+
+
+# ------------------------------------------------------------------------------------ G3
+def g3():
+    q = R.quantization.ResidualVectorQuantizer(dimension=128, n_q=2, bins=1024)
+    emb = t(synth_wave((2, 128, 75), 31, amp=1.0))
+    stats = np.zeros((2, 2, 128), np.float32)
+    stats[0, 1] = 1.0
+    stats[1, 1] = 0.6
+    cbs = synth_codebooks(stats, 32)
+    g = rng(33)
+    init = {}
+    for i, layer in enumerate(q.vq.layers):
+        c = layer._codebook
+        c.embed.data.copy_(t(cbs[i]))
+        cs = g.uniform(0.0, 4.0, size=(1024,)).astype(np.float32)
+        c.cluster_size.data.copy_(t(cs))
+        ea = g.standard_normal(size=(1024, 128)).astype(np.float32)
+        c.embed_avg.data.copy_(t(ea))
+        c.inited.data.fill_(1.0)
+        init[f'cs{i}'] = cs
+        init[f'ea{i}'] = ea
+    q.train()
+    x = emb.clone().requires_grad_(True)
+    res = q(x, 75, 1.5)
+    gq = t(synth_wave(tuple(res.quantized.shape), 34, amp=1.0))
+    torch.autograd.backward([res.quantized, res.penalty], [gq, torch.tensor(1.0)])
+    outs = dict(emb=emb.numpy(), stats=stats, quantized=res.quantized.detach().numpy(),
+                codes=res.codes.numpy().astype(np.int16), penalty=res.penalty.detach().numpy(),
+                gaps=top2_gaps(emb, [t(cbs[0]), t(cbs[1])], res.codes),
+                gq=gq.numpy(), demb=x.grad.numpy())
+    for i, layer in enumerate(q.vq.layers):
+        c = layer._codebook
+        outs[f'cs_init{i}'] = init[f'cs{i}']
+        outs[f'ea_init{i}'] = init[f'ea{i}']
+        outs[f'cluster_size{i}'] = c.cluster_size.numpy()
+        outs[f'embed_avg{i}'] = c.embed_avg.numpy()
+        outs[f'embed{i}'] = c.embed.numpy()
+    # kmeans with the sample_vectors draw injected (core_vq.py:69-77, 80-102)
+    samples = t(synth_wave((600, 128), 35, amp=1.0))
+    init_idx = torch.from_numpy(rng(36).permutation(600)[:64].astype(np.int64))
+    orig = R.quantization.core_vq.sample_vectors
+    R.quantization.core_vq.sample_vectors = lambda s, n: s[init_idx]
+    means, bins = R.quantization.core_vq.kmeans(samples, 64, 10)
+    R.quantization.core_vq.sample_vectors = orig
+    outs.update(km_samples=samples.numpy(), km_init=init_idx.numpy(), km_means=means.numpy(),
+                km_bins=bins.numpy())
+    save('g3_rvq.npz', **outs)
+
+
+# ------------------------------------------------------------------------------------ G4
+def g4():
+    x = t(synth_wave((2, 1, 4800), 41))
+    y = t(synth_wave((2, 1, 4800), 42)).requires_grad_(True)
+    out = {'x': x.numpy(), 'y': y.detach().numpy()}
+    for i in range(5, 12):
+        n = 2 ** i
+        a2m = R.audio_to_mel.Audio2Mel(n_fft=n, win_length=n, hop_length=n // 4,
+                                       n_mel_channels=64, sampling_rate=24000)
+        out[f'mel{n}'] = a2m(x).numpy()
+        out[f'melbasis{n}'] = a2m.mel_basis.numpy()
+    for n, h in zip((1024, 2048, 512), (256, 512, 128)):
+        sp = sys.modules['torchaudio'].transforms.Spectrogram(
+            n_fft=n, hop_length=h, win_length=n, window_fn=torch.hann_window,
+            normalized=True, center=False, pad_mode=None, power=None)
+        z = sp(x)
+        out[f'spec{n}'] = torch.view_as_real(z).numpy()
+    losses = R.losses.total_loss([[torch.ones(1)]], [torch.zeros(1)], [[torch.ones(1)]], x, y)
+    out['l_t'] = losses['l_t'].detach().numpy()
+    out['l_f'] = losses['l_f'].detach().numpy()
+    gf, = torch.autograd.grad(losses['l_f'], [y])
+    gt, = torch.autograd.grad(losses['l_t'], [y])
+    out['dlf_dy'] = gf.numpy()
+    out['dlt_dy'] = gt.numpy()
+    save('g4_mel.npz', **out)
+
+
+# ------------------------------------------------------------------------------------ G5
+def g5():
+    d = R.msstftd.MultiScaleSTFTDiscriminator(filters=32)
+    load_synth(d, 51)
+    x = t(synth_wave((1, 1, 4800), 52)).requires_grad_(True)
+    logits, fmaps = d(x)
+    r = rng(53)
+    f = 0
+    out = {'x': x.detach().numpy()}
+    for k, lg in enumerate(logits):
+        out[f'logits{k}'] = lg.detach().numpy()
+        wl = t(r.standard_normal(size=tuple(lg.shape)).astype(np.float32))
+        f = f + (lg * wl).sum()
+        for j, fm in enumerate(fmaps[k]):
+            out[f'fmap{k}_{j}_sum'] = fm.detach().double().sum().numpy()
+            out[f'fmap{k}_{j}_sq'] = fm.detach().double().pow(2).sum().numpy()
+            out[f'fmap{k}_{j}_shape'] = np.array(fm.shape)
+            out[f'fmap{k}_{j}_head'] = fm.detach().reshape(-1)[:256].numpy()
+            f = f + fm.mean()
+    f.backward()
+    out['dx'] = x.grad.numpy()
+    save('g5_disc.npz', **out)
+
+
+# ------------------------------------------------------------------------------------ G6
+def g6():
+    out = {}
+    # balancer.py:121-139 known answer
+    from torch.nn import functional as F
+    for rescale in (False, True):
+        x = torch.zeros(1, requires_grad=True)
+        one = torch.ones_like(x)
+        losses = {'1': F.l1_loss(x, one), '2': 100 * F.l1_loss(x, -one)}
+        R.balancer.Balancer(weights={'1': 1, '2': 1}, rescale_grads=rescale).backward(losses, x)
+        out[f'kat_{int(rescale)}'] = x.grad.numpy()
+    # 4 losses, 3 consecutive calls (EMA state), per-item norms on [B,1,T]
+    r = rng(61)
+    b = R.balancer.Balancer(weights={'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3})
+    for it in range(3):
+        y = torch.zeros(4, 1, 300, requires_grad=True)
+        gs = {k: t(r.standard_normal(size=(4, 1, 300)).astype(np.float32) * s)
+              for k, s in (('l_t', 0.01), ('l_f', 1.0), ('l_g', 0.1), ('l_feat', 3.0))}
+        losses = {k: (y * g).sum() for k, g in gs.items()}
+        b.backward(losses, y)
+        for k, g in gs.items():
+            out[f'it{it}_{k}'] = g.numpy()
+        out[f'it{it}_out'] = y.grad.numpy()
+    save('g6_balancer.npz', **out)
+
+
+# ------------------------------------------------------------------------------------ G7
+def one_step(gan):
+    m = R.model.EncodecModel._get_model([1.5], 24000, 1, causal=True, model_norm='weight_norm',
+                                        audio_normalize=True, segment=None, name='x')
+    load_synth(m, 71)
+    x = t(synth_wave((2, 1, 4800), 72))
+    with torch.no_grad():
+        emb = m.encoder(x / (1e-8 + x.pow(2).mean(2, keepdim=True).sqrt()))
+    e = emb.permute(0, 2, 1).reshape(-1, 128).double()
+    stats = np.zeros((2, 2, 128), np.float32)
+    stats[0, 0] = e.mean(0).float().numpy()
+    stats[0, 1] = e.std(0).float().numpy()
+    stats[1, 1] = 0.5 * stats[0, 1]
+    fill_codebooks(m, stats, 73, 2)
+    d = R.msstftd.MultiScaleSTFTDiscriminator(filters=32)
+    load_synth(d, 74)
+    opt = torch.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=3e-4, betas=(0.5, 0.9))
+    optd = torch.optim.Adam([p for p in d.parameters() if p.requires_grad], lr=3e-4, betas=(0.5, 0.9))
+    weights = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3} if gan else {'l_t': 0.1, 'l_f': 1}
+    bal = R.balancer.Balancer(weights)
+    m.train()
+    d.train()
+    out = {'x': x.numpy(), 'stats': stats}
+    for it in range(2):
+        opt.zero_grad()
+        y, loss_w, _ = m(x)
+        if gan:
+            lr_, fr = d(x)
+            lf_, ff = d(y)
+            losses = R.losses.total_loss(fr, lf_, ff, x, y, sample_rate=24000)
+        else:
+            l_t = torch.nn.functional.l1_loss(x, y)
+            l_f = R.losses.total_loss([[torch.ones(1)]], [torch.zeros(1)], [[torch.ones(1)]], x, y)['l_f']
+            losses = {'l_t': l_t, 'l_f': l_f}
+        bal.backward(losses, y, retain_graph=True)
+        loss_w.backward()
+        opt.step()
+        for k, v in losses.items():
+            out[f'it{it}_{k}'] = v.detach().numpy()
+        out[f'it{it}_loss_w'] = loss_w.detach().numpy()
+        out[f'it{it}_y'] = y.detach().numpy()
+        if gan:
+            optd.zero_grad()
+            lr2, _ = d(x)
+            lf2, _ = d(y.detach())
+            ld = R.losses.disc_loss(lr2, lf2)
+            ld.backward()
+            optd.step()
+            out[f'it{it}_l_d'] = ld.detach().numpy()
+    for k, v in m.state_dict().items():
+        if v.dtype == torch.float32:
+            out['p/' + k] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+    if gan:
+        for k, v in d.state_dict().items():
+            out['d/' + k] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+    # a few full tensors for sharper checks
+    sd = m.state_dict()
+    for k in ('encoder.model.0.conv.conv.weight_v', 'decoder.model.15.conv.conv.weight_v',
+              'quantizer.vq.layers.0._codebook.cluster_size'):
+        out['full/' + k] = sd[k].numpy()
+    return out
+
+
+def g7():
+    out = {}
+    for gan in (False, True):
+        o = one_step(gan)
+        out.update({('gan/' if gan else 'gen/') + k: v for k, v in o.items()})
+    save('g7_step.npz', **out)
+
+
+def g8():
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.Adam([p], lr=3e-4)
+    s = R.scheduler.WarmupCosineLrScheduler(opt, max_iter=400, eta_ratio=0.1, warmup_iter=50, warmup_ratio=1e-4)
+    lrs = []
+    for _ in range(400):
+        lrs.append(opt.param_groups[0]['lr'])
+        opt.step()
+        s.step()
+    save('g8_sched.npz', lr=np.array(lrs))
+
+
+if __name__ == '__main__':
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8']
+    for w in which:
+        torch.manual_seed(0)
+        globals()[w]()

@@ -1,0 +1,250 @@
+"""Pin the CPU oracle to the golden fixtures generated from the real reference (CPU only).
+
+These tests are what make the oracle trustworthy as the parity checker for the HIP path.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import encodec_oracle as O
+from fixtures import load, T, model_state, disc_state, codebooks_from_stats, g3_codebooks, certified
+from synth import synth_state
+
+torch.set_num_threads(min(8, torch.get_num_threads()))
+
+
+def close(a, b, rtol=1e-5, atol=1e-6):
+    a = a.detach().numpy() if torch.is_tensor(a) else np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol)
+
+
+# --------------------------------------------------------------------------- mel filters
+def test_mel_filterbank_matches_fixture_and_transformers():
+    d = load('g4_mel.npz')
+    for i in range(5, 12):
+        n = 2 ** i
+        mine = O.mel_filterbank(24000, n, 64)
+        close(mine, d[f'melbasis{n}'], rtol=0, atol=0)
+    try:
+        from transformers.audio_utils import mel_filter_bank
+    except Exception:  # pragma: no cover
+        pytest.skip('transformers not importable')
+    for i in range(5, 12):
+        n = 2 ** i
+        ref = mel_filter_bank(num_frequency_bins=n // 2 + 1, num_mel_filters=64, min_frequency=0.0,
+                              max_frequency=12000.0, sampling_rate=24000, norm='slaney',
+                              mel_scale='slaney').T
+        np.testing.assert_allclose(O.mel_filterbank(24000, n, 64), ref, rtol=1e-5, atol=1e-9)
+
+
+# --------------------------------------------------------------------------- convs
+CASES = [
+    ('c_k7_1to8', 'conv', 1, 8, 7, 1, True, False, 480),
+    ('c_k3_16to8_elu', 'conv', 16, 8, 3, 1, True, True, 480),
+    ('c_k1_8to16_elu', 'conv', 8, 16, 1, 1, True, True, 480),
+    ('c_k1_16to16', 'conv', 16, 16, 1, 1, True, False, 480),
+    ('c_k4s2_16to32_elu', 'conv', 16, 32, 4, 2, True, True, 480),
+    ('c_k10s5_16to32_elu', 'conv', 16, 32, 10, 5, True, True, 480),
+    ('c_k16s8_32to64_elu', 'conv', 32, 64, 16, 8, True, True, 480),
+    ('c_k7_64to16_elu', 'conv', 64, 16, 7, 1, True, True, 30),
+    ('c_k7_short_reflect', 'conv', 8, 8, 7, 1, True, False, 5),
+    ('c_k7s1_nc', 'conv', 8, 8, 7, 1, False, False, 100),
+    ('c_k10s5_nc_odd', 'conv', 8, 16, 10, 5, False, True, 97),
+    ('t_k4s2_32to16_elu', 'convtr', 32, 16, 4, 2, True, True, 240),
+    ('t_k10s5_32to16_elu', 'convtr', 32, 16, 10, 5, True, True, 96),
+    ('t_k16s8_64to32_elu', 'convtr', 64, 32, 16, 8, True, True, 60),
+    ('t_k8s4_nc', 'convtr', 16, 8, 8, 4, False, False, 50),
+]
+
+
+def conv_case_state(ci, kind, cin, cout, K):
+    pre = 'convtr.convtr' if kind == 'convtr' else 'conv.conv'
+    wshape = (cin, cout, K) if kind == 'convtr' else (cout, cin, K)
+    shapes = {pre + '.bias': (cout,), pre + '.weight_g': (wshape[0], 1, 1), pre + '.weight_v': wshape}
+    st = synth_state(shapes, 100 + ci)
+    return {('m.' + k): T(v) for k, v in st.items()}, pre
+
+
+@pytest.mark.parametrize('ci', range(len(CASES)))
+def test_oracle_conv_fixture(ci):
+    d = load('g2_convs.npz')
+    name, kind, cin, cout, K, s, causal, pre_elu, Tn = CASES[ci]
+    p, pre = conv_case_state(ci, kind, cin, cout, K)
+    p = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    x = T(d[name + '/x']).clone().requires_grad_(True)
+    xin = F.elu(x) if pre_elu else x
+    if kind == 'conv':
+        y = O.sconv1d(xin, p, 'm', K, s, causal=causal)
+    else:
+        y = O.sconvtr1d(xin, p, 'm', K, s, causal=causal)
+    close(y, d[name + '/y'])
+    y.backward(T(d[name + '/gy']))
+    close(x.grad, d[name + '/dx'], rtol=1e-4, atol=1e-5)
+    close(p['m.' + pre + '.weight_v'].grad, d[name + '/dv'], rtol=1e-4, atol=1e-5)
+    close(p['m.' + pre + '.weight_g'].grad, d[name + '/dg'], rtol=1e-4, atol=1e-5)
+    close(p['m.' + pre + '.bias'].grad, d[name + '/db'], rtol=1e-4, atol=1e-4)
+
+
+# --------------------------------------------------------------------------- G1 eval model
+def test_oracle_eval_24k_fixture():
+    d = load('g1_eval24k.npz')
+    cfg = O.Config(audio_normalize=False)
+    p = model_state(cfg, 1)
+    cbs = codebooks_from_stats(d['stats'], 77, 2, cfg.n_q)
+    with torch.no_grad():
+        y, codes, emb = O.encodec_forward_eval(T(d['x']), p, cbs, cfg, 1.5)
+    close(emb, d['emb'], rtol=1e-4, atol=1e-6)
+    ref_codes = d['codes'].astype(np.int64)
+    mine = codes.numpy()
+    assert mine.shape == ref_codes.shape
+    e2 = max(float((cb['embed'] ** 2).sum(1).max()) for cb in cbs[:2])
+    x2 = float((emb ** 2).sum(1).max())
+    cert = certified(d['gaps'], x2, e2)
+    assert cert.sum() > 0
+    assert (mine[0][cert] == ref_codes[0][cert]).all()
+    # where every code agrees, the decoded waveform must agree too
+    if (mine == ref_codes).all():
+        close(y, d['y'], rtol=1e-3, atol=1e-6)
+
+
+# --------------------------------------------------------------------------- G3 RVQ
+def test_oracle_rvq_train_fixture():
+    d = load('g3_rvq.npz')
+    cbs = g3_codebooks(d)
+    emb = T(d['emb']).clone().requires_grad_(True)
+    q, codes, penalty, new = O.rvq_train(emb, cbs, 2)
+    assert (codes.numpy() == d['codes']).all()
+    close(q, d['quantized'])
+    close(penalty, d['penalty'])
+    torch.autograd.backward([q, penalty], [T(d['gq']), torch.tensor(1.0)])
+    close(emb.grad, d['demb'], rtol=1e-5, atol=1e-6)
+    for i in range(2):
+        close(new[i]['cluster_size'], d[f'cluster_size{i}'], rtol=1e-6, atol=1e-7)
+        close(new[i]['embed_avg'], d[f'embed_avg{i}'], rtol=1e-5, atol=1e-6)
+        close(new[i]['embed'], d[f'embed{i}'], rtol=1e-5, atol=1e-6)
+
+
+def test_oracle_kmeans_fixture():
+    d = load('g3_rvq.npz')
+    means, bins = O.kmeans(T(d['km_samples']), 64, 10, T(d['km_init']))
+    close(means, d['km_means'], rtol=1e-5, atol=1e-6)
+    assert (bins.numpy() == d['km_bins']).all()
+
+
+# --------------------------------------------------------------------------- G4 mel
+def test_oracle_mel_and_spec_fixture():
+    d = load('g4_mel.npz')
+    x = T(d['x'])
+    for i in range(5, 12):
+        n = 2 ** i
+        close(O.audio2mel(x, n, n // 4, n, 24000), d[f'mel{n}'], rtol=1e-4, atol=1e-4)
+    for n, h in zip((1024, 2048, 512), (256, 512, 128)):
+        close(torch.view_as_real(O.spectrogram(x, n, h, n)), d[f'spec{n}'], rtol=1e-4, atol=1e-5)
+
+
+def test_oracle_losses_fixture():
+    d = load('g4_mel.npz')
+    x = T(d['x'])
+    y = T(d['y']).clone().requires_grad_(True)
+    lt = O.loss_t(x, y)
+    lf = O.loss_f(x, y)
+    close(lt, d['l_t'])
+    close(lf, d['l_f'], rtol=1e-5)
+    gf, = torch.autograd.grad(lf, [y])
+    gt, = torch.autograd.grad(lt, [y])
+    close(gf, d['dlf_dy'], rtol=1e-4, atol=1e-7)
+    close(gt, d['dlt_dy'])
+
+
+# --------------------------------------------------------------------------- G5 disc
+def test_oracle_disc_fixture():
+    d = load('g5_disc.npz')
+    p = disc_state(51)
+    x = T(d['x']).clone().requires_grad_(True)
+    logits, fmaps = O.msstft_forward(x, p)
+    r = np.random.Generator(np.random.PCG64(53))
+    f = 0
+    for k, lg in enumerate(logits):
+        close(lg, d[f'logits{k}'], rtol=1e-4, atol=1e-5)
+        wl = T(r.standard_normal(size=tuple(lg.shape)).astype(np.float32))
+        f = f + (lg * wl).sum()
+        for j, fm in enumerate(fmaps[k]):
+            assert tuple(fm.shape) == tuple(d[f'fmap{k}_{j}_shape'])
+            np.testing.assert_allclose(fm.detach().double().sum().item(), d[f'fmap{k}_{j}_sum'], rtol=1e-4)
+            np.testing.assert_allclose(fm.detach().double().pow(2).sum().item(), d[f'fmap{k}_{j}_sq'], rtol=1e-4)
+            close(fm.reshape(-1)[:256], d[f'fmap{k}_{j}_head'], rtol=1e-4, atol=1e-5)
+            f = f + fm.mean()
+    f.backward()
+    close(x.grad, d['dx'], rtol=1e-3, atol=1e-5)
+
+
+# --------------------------------------------------------------------------- G6 balancer
+def test_oracle_balancer_fixture():
+    d = load('g6_balancer.npz')
+    # known answer, balancer.py:121-139 (rescale off: plain weighted sum)
+    assert float(d['kat_0'][0]) == 99.0 and float(d['kat_1'][0]) == 0.0
+    b = O.Balancer({'1': 1, '2': 1})
+    out = b.combine({'1': torch.tensor([-1.0]), '2': torch.tensor([100.0])})
+    assert abs(float(out)) < 1e-6
+    b = O.Balancer({'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3})
+    for it in range(3):
+        grads = {k: T(d[f'it{it}_{k}']) for k in ('l_t', 'l_f', 'l_g', 'l_feat')}
+        close(b.combine(grads), d[f'it{it}_out'], rtol=1e-5, atol=1e-8)
+
+
+# --------------------------------------------------------------------------- G7 train step
+@pytest.mark.parametrize('gan', [False, True])
+def test_oracle_train_step_fixture(gan):
+    d = load('g7_step.npz')
+    pre = 'gan/' if gan else 'gen/'
+    cfg = O.Config(target_bandwidths=(1.5,), audio_normalize=True)
+    p = model_state(cfg, 71)
+    cbs = codebooks_from_stats(d[pre + 'stats'], 73, 2, cfg.n_q)
+    dp = disc_state(74) if gan else None
+    weights = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3} if gan else {'l_t': 0.1, 'l_f': 1}
+    bal = O.Balancer(weights)
+    st, dst = {}, {}
+    x = T(d[pre + 'x'])
+    for it in range(2):
+        out = O.train_step(x, p, cbs, cfg, 1.5, bal, st, 3e-4, disc_p=dp, disc_adam_state=dst, disc_lr=3e-4)
+        for k in weights:
+            np.testing.assert_allclose(out[k], float(d[f'{pre}it{it}_{k}'].reshape(-1)[0]), rtol=2e-4)
+        np.testing.assert_allclose(out['loss_w'], float(d[f'{pre}it{it}_loss_w'].reshape(-1)[0]), rtol=2e-3, atol=1e-7)
+        if gan:
+            np.testing.assert_allclose(out['l_d'], float(d[f'{pre}it{it}_l_d'].reshape(-1)[0]), rtol=1e-5)
+    keys = [k[len(pre) + 2:] for k in d.files if k.startswith(pre + 'p/')]
+    names = set(p) | {f'quantizer.vq.layers.{i}._codebook.{b}' for i in range(cfg.n_q)
+                      for b in ('inited', 'cluster_size', 'embed', 'embed_avg')}
+    assert set(keys) == names
+    for k in p:
+        ref = d[pre + 'p/' + k]
+        v = p[k].double()
+        np.testing.assert_allclose([v.sum().item(), v.abs().sum().item()], ref, rtol=2e-4, atol=2e-5)
+    for i in range(2):
+        for b in ('cluster_size', 'embed', 'embed_avg'):
+            ref = d[f'{pre}p/quantizer.vq.layers.{i}._codebook.{b}']
+            v = cbs[i][b].double()
+            np.testing.assert_allclose([v.sum().item(), v.abs().sum().item()], ref, rtol=1e-4, atol=1e-4)
+    if gan:
+        for k in dp:
+            np.testing.assert_allclose([dp[k].double().sum().item(), dp[k].double().abs().sum().item()],
+                                       d['gan/d/' + k], rtol=2e-4, atol=2e-5)
+
+
+# --------------------------------------------------------------------------- G8 scheduler
+def test_oracle_scheduler_fixture():
+    d = load('g8_sched.npz')
+    lrs = [O.warmup_cosine_lr(3e-4, i, 400, 50) for i in range(400)]
+    np.testing.assert_allclose(lrs, d['lr'], rtol=1e-12)
+
+
+def test_rvq_bandwidth_rule():
+    # vq.py:101-113 at 75 Hz
+    assert [O.rvq_num_quantizers(b, 75) for b in (1.5, 3., 6., 12., 24.)] == [2, 4, 8, 16, 32]
+    assert [O.rvq_num_quantizers(b, 150) for b in (3., 6., 12., 24.)] == [2, 4, 8, 16]
+    assert math.isclose(O.Config().frame_rate, 75)
