@@ -1,0 +1,156 @@
+"""EnCodec 24 kHz training throughput on MI355X (BASELINE.json metric).
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--config gen|gan]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step = one train_multi_gpu.py:train_one_step iteration on one batch of 32 synthetic 1 s clips
+per GPU (config 2, the metric's configuration: generator + RVQ (n_q 8) + l_t/l_f through the
+Balancer + Adam; `--config gan` adds the MS-STFT discriminator, config 3). Inputs are resident
+in HBM before the timed region. Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'encodec-pytorch_amd'))
+
+MI355X_FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+MI355X_HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', choices=['gen', 'gan'], default='gen')
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-roofline', action='store_true')
+    return ap.parse_args()
+
+
+def cpu_baseline(config, threads):
+    """The CPU oracle's train step (oracle/encodec_oracle.py, the reference algorithm restated on
+    torch-CPU) on a bounded sample: 8 clips, 1 warm + 2 timed steps, initialised codebooks."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+    from oracle import encodec_oracle as O
+    from fixtures import model_state, codebooks_from_stats, disc_state
+    from synth import synth_wave
+    torch.set_num_threads(threads)
+    cfg = O.Config(target_bandwidths=(6.0,), audio_normalize=True)
+    p = model_state(cfg, 3)
+    stats = np.zeros((8, 2, 128), np.float32)
+    stats[:, 1] = 0.05
+    cbs = codebooks_from_stats(stats, 4, 8, cfg.n_q)
+    gan = config == 'gan'
+    dp = disc_state(5) if gan else None
+    w = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3} if gan else {'l_t': 0.1, 'l_f': 1}
+    bal = O.Balancer(w)
+    st, dst = {}, {}
+    B = 8
+    x = torch.from_numpy(synth_wave((B, 1, 24000), 99))
+    O.train_step(x, p, cbs, cfg, 6.0, bal, st, 3e-4, dp, dst, 3e-4)
+    t0 = time.perf_counter()
+    n = 2
+    for _ in range(n):
+        O.train_step(x, p, cbs, cfg, 6.0, bal, st, 3e-4, dp, dst, 3e-4)
+    dt = time.perf_counter() - t0
+    return {'value': B * n / dt, 'unit': 'audio-seconds/sec', 'cores': threads, 'kind': 'port',
+            'sample': f'oracle train step ({config}), {B} x 1 s clips, {n} timed steps after 1 warm-up, '
+                      f'{dt:.1f} s of CPU time'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        torch.distributed.init_process_group('nccl', device_id=dev)
+    import encx
+    from encx.model import EncodecModel
+    from encx.train import Trainer
+    from encx._lib import lib
+
+    torch.manual_seed(3401 + rank)
+    model = EncodecModel._get_model([6.0], 24000, 1, causal=True, model_norm='weight_norm',
+                                    audio_normalize=True, name='my_encodec').to(dev)
+    disc = None
+    if args.config == 'gan':
+        from encx.msstftd import MultiScaleSTFTDiscriminator
+        disc = MultiScaleSTFTDiscriminator(filters=32).to(dev)
+    trainer = Trainer(model, disc, lr=3e-4, disc_lr=3e-4, max_iter=100000, warmup_iter=500)
+    B = args.batch
+    g = np.random.Generator(np.random.PCG64(1234 + rank))
+    batches = [torch.from_numpy((0.1 * g.standard_normal((B, 1, 24000))).astype(np.float32)).to(dev)
+               for _ in range(4)]
+
+    for i in range(args.warmup):
+        trainer.step(batches[i % 4])
+    torch.cuda.synchronize()
+
+    prof = not args.no_roofline
+    if prof:
+        lib.encx_prof_enable(1)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        trainer.step(batches[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    roof = None
+    if prof:
+        import ctypes
+        ms, fl, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        lib.encx_prof_read(ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by), ctypes.byref(n))
+        lib.encx_prof_enable(0)
+        achieved = fl.value / (ms.value * 1e-3) / 1e12 if ms.value > 0 else 0.0
+        roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MI355X_FP32_PEAK_TFLOPS,
+                'unit': 'TFLOP/s', 'frac': round(achieved / MI355X_FP32_PEAK_TFLOPS, 4), 'traffic': None,
+                'kernel': 'encx conv/convtr fwd + bwd-data + bwd-weight (implicit-GEMM f32 MFMA)',
+                'launches': int(n.value), 'kernel_ms_per_step': round(ms.value / args.steps, 3),
+                'algorithmic_bytes_per_step': by.value / args.steps,
+                'algorithmic_flops_per_step': fl.value / args.steps}
+
+    value = B * world * args.steps * 1.0 / dt
+    if rank == 0:
+        out = {
+            'metric': 'audio-seconds/sec EnCodec24k train step, batch 32x1s',
+            'value': round(value, 2), 'unit': 'audio-seconds/sec', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt * 1e3 / args.steps, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+            'data': 'synthetic (0.1*N(0,1) clips, random-init weights)',
+            'config': {'workload': ('config 2: 24 kHz mono SEANet + RVQ n_q=8, generator-only (l_t, l_f '
+                                    'via Balancer, commit loss, Adam)') if args.config == 'gen' else
+                       'config 3: 24 kHz mono full GAN (MS-STFT disc + Balancer)',
+                       'global_batch': B * world, 'clip_seconds': 1.0, 'sample_rate': 24000,
+                       'parallelism': f'dp{world}'},
+            'roofline': roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out['cpu_baseline'] = cpu_baseline(args.config, min(16, os.cpu_count() or 1))
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,90 @@
+// Library entry points: version, error strings, device selection, launch profiling.
+#include <string.h>
+
+#include <atomic>
+#include <mutex>
+
+#include "common.h"
+#include "prof.h"
+
+namespace {
+constexpr int kMaxSlots = 1 << 14;
+struct ProfState {
+    std::mutex mu;
+    bool on = false;
+    int next = 0;
+    hipEvent_t ev0[kMaxSlots];
+    hipEvent_t ev1[kMaxSlots];
+    double flops[kMaxSlots];
+    double bytes[kMaxSlots];
+    bool created = false;
+};
+ProfState g_prof;
+std::atomic<bool> g_prof_on{false};
+}  // namespace
+
+encx_prof_scope::encx_prof_scope(hipStream_t s, double f, double b) : st(s), slot(-1) {
+    if (!g_prof_on.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    if (!g_prof.on || g_prof.next >= kMaxSlots) return;
+    slot = g_prof.next++;
+    g_prof.flops[slot] = f;
+    g_prof.bytes[slot] = b;
+    (void)hipEventRecord(g_prof.ev0[slot], st);
+}
+
+encx_prof_scope::~encx_prof_scope() {
+    if (slot >= 0) (void)hipEventRecord(g_prof.ev1[slot], st);
+}
+
+extern "C" {
+
+int encx_version(void) { return 1; }
+
+const char* encx_strerror(int code) {
+    if (code == ENCX_OK) return "ok";
+    if (code == ENCX_EINVAL) return "encx: invalid argument (shape, stride or null pointer)";
+    return hipGetErrorString((hipError_t)code);
+}
+
+int encx_init(int device) {
+    hipError_t e = hipSetDevice(device);
+    return (int)e;
+}
+
+int encx_prof_enable(int on) {
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    if (on && !g_prof.created) {
+        for (int i = 0; i < kMaxSlots; ++i) {
+            if (hipEventCreate(&g_prof.ev0[i]) != hipSuccess) return ENCX_EINVAL;
+            if (hipEventCreate(&g_prof.ev1[i]) != hipSuccess) return ENCX_EINVAL;
+        }
+        g_prof.created = true;
+    }
+    g_prof.on = on != 0;
+    g_prof.next = 0;
+    g_prof_on.store(g_prof.on);
+    return 0;
+}
+
+int encx_prof_read(double* total_ms, double* total_flops, double* total_bytes, int64_t* launches) {
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    double ms = 0, fl = 0, by = 0;
+    for (int i = 0; i < g_prof.next; ++i) {
+        hipError_t e = hipEventSynchronize(g_prof.ev1[i]);
+        if (e != hipSuccess) return (int)e;
+        float t = 0.f;
+        e = hipEventElapsedTime(&t, g_prof.ev0[i], g_prof.ev1[i]);
+        if (e != hipSuccess) return (int)e;
+        ms += t;
+        fl += g_prof.flops[i];
+        by += g_prof.bytes[i];
+    }
+    if (total_ms) *total_ms = ms;
+    if (total_flops) *total_flops = fl;
+    if (total_bytes) *total_bytes = by;
+    if (launches) *launches = g_prof.next;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+// encx -- MI355X (gfx950) kernels for the EnCodec training hot path.
+// Shared device helpers. Every kernel is fp32 in / fp32 accumulate (the reference trains in
+// fp32 with AMP off: config/config.yaml:7); matrix work uses the exact-f32 MFMA
+// v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md: 157 TF/s, bitwise an fmaf chain).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/encx.h"
+
+#define ENCX_DEV __device__ __forceinline__
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---- error plumbing: no exceptions cross the C ABI ---------------------------------------
+#define ENCX_CHECK_LAUNCH()                                                    \
+    do {                                                                       \
+        hipError_t _e = hipGetLastError();                                     \
+        if (_e != hipSuccess) return (int)_e;                                  \
+    } while (0)
+#define ENCX_REQUIRE(cond)                                                     \
+    do {                                                                       \
+        if (!(cond)) return ENCX_EINVAL;                                       \
+    } while (0)
+
+// ---- activations ---------------------------------------------------------------------------
+// nn.ELU(alpha=1) (modules/seanet.py:49 etc.): x > 0 ? x : expm1(x)
+ENCX_DEV float elu(float x) { return x > 0.f ? x : expm1f(x); }
+// d ELU / dx evaluated at the pre-activation x: 1 or exp(x) (= elu(x) + 1)
+ENCX_DEV float elu_grad(float x) { return x > 0.f ? 1.f : expf(x); }
+// nn.LeakyReLU(0.2) (msstftd.py:50,61)
+ENCX_DEV float lrelu(float x) { return x > 0.f ? x : 0.2f * x; }
+ENCX_DEV float lrelu_grad(float y_or_x) { return y_or_x > 0.f ? 1.f : 0.2f; }
+
+ENCX_DEV float act_apply(int act, float x) { return act == ENCX_ACT_ELU ? elu(x) : x; }
+ENCX_DEV float act_grad(int act, float x) { return act == ENCX_ACT_ELU ? elu_grad(x) : 1.f; }
+
+// ---- padding -------------------------------------------------------------------------------
+// Source index of padded position p for pad1d (modules/conv.py:79-96): reflect (with the
+// short-input zero extension `e`, :86-94) or zero padding. Returns -1 for a zero.
+ENCX_DEV int pad_src(int p, int pl, int T, int e, int mode) {
+    int i = p - pl;
+    if (mode == ENCX_PAD_REFLECT) {
+        int L = T + e;
+        if (i < 0) i = -i;
+        else if (i >= L) i = 2 * (L - 1) - i;
+        return (i >= 0 && i < T) ? i : -1;
+    }
+    return (i >= 0 && i < T) ? i : -1;
+}
+
+// ---- MFMA ----------------------------------------------------------------------------------
+// 32x32x2 f32: lane l holds A[l&31][l>>5], B[l>>5][l&31]; D row = (r&3)+8*(r>>2)+4*(l>>5), col l&31
+ENCX_DEV f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+ENCX_DEV int mfma_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// ---- reductions ----------------------------------------------------------------------------
+ENCX_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+ENCX_DEV double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block-wide sum, blockDim.x multiple of 64 and <= 1024; result valid in every thread
+ENCX_DEV float block_sum(float v, float* red /* >= 16 floats of LDS */) {
+    v = wave_sum(v);
+    int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    int nw = blockDim.x >> 6;
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += red[i];
+    return t;
+}
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

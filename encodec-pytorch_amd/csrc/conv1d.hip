@@ -1,0 +1,742 @@
+// SEANet 1-D convolution family on gfx950 (modules/conv.py SConv1d / SConvTranspose1d).
+//
+// Three MFMA kernels (v_mfma_f32_32x32x2_f32, exact fp32), 4 waves per workgroup, each wave
+// owning a (32*TM) x (32*TN) output sub-tile:
+//   conv_fwd     implicit GEMM  Y[co, t]  = W[co, (ci,k)] * act(Xpad)[(ci,k), t]
+//                The X window of a channel chunk is staged once in LDS (act applied once per
+//                element) and stored phase-major, Xs[ci][t mod s][t div s], so strided taps
+//                read consecutive LDS words.
+//   conv_poly    polyphase transposed conv: rows (o, r), columns u, reduction (i, q):
+//                out[o][u*s + r] = sum_{i,q} Wp[i][q][o*s+r] * in[i][u-q]. Serves
+//                ConvTranspose1d forward and Conv1d backward-data (with the reflect pad
+//                folded back and act' applied in the epilogue; pad positions go to a side
+//                buffer that conv_fold_edges adds in a fixed order).
+//   conv_wgrad   dW[a][(c,k)] = sum_{b,t} L[b][a][t] * R[b][c][t*s + k*d - pl], split over
+//                (b, t) ranges into a workspace and summed by wgrad_reduce in a fixed order.
+// Plus VALU kernels for the 1-channel ends of the stack (Cout = 1 forward, tiny wgrads),
+// where a 32-wide MFMA tile would be >90% padding.
+#include "common.h"
+#include "prof.h"
+
+namespace {
+
+constexpr int NT = 256;  // threads per workgroup (4 waves)
+
+// ------------------------------------------------------------------------- conv forward
+struct FwdArgs {
+    const float* x;
+    const float* wf;  // [Cin][K][Cout]
+    const float* bias;
+    const float* res;
+    float* y;
+    const float* xact;  // epilogue act' source (backward-data use), or null
+    int B, Cin, Tin, Cout, Tout, K, s, d, pl, e, mode, act;
+    int epi_act, accumulate;
+    int CK;  // channels per LDS chunk (even)
+    int Up;  // LDS words per (ci, phase) row
+};
+
+// y = [acc ? y : 0] + act'(xact) * (v + bias) + res
+ENCX_DEV void fwd_store(const FwdArgs& a, int64_t o, int co, float v) {
+    v += a.bias ? a.bias[co] : 0.f;
+    if (a.xact) v *= act_grad(a.epi_act, a.xact[o]);
+    if (a.res) v += a.res[o];
+    if (a.accumulate) v += a.y[o];
+    a.y[o] = v;
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    extern __shared__ float smem[];
+    const int CK = a.CK, S = a.s, Up = a.Up, K = a.K;
+    float* Xs = smem;                       // [CK][S][Up]
+    float* Ws = smem + CK * S * Up;         // [K][CK][BM]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int t0 = blockIdx.x * BN, co0 = blockIdx.y * BM, b = blockIdx.z;
+    const float* xb = a.x + (int64_t)b * a.Cin * a.Tin;
+    const int span = S * Up;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+
+    for (int c0 = 0; c0 < a.Cin; c0 += CK) {
+        __syncthreads();
+        // stage activated input window, phase-major
+        for (int i = tid; i < CK * span; i += NT) {
+            int cl = i / span, q = i - cl * span;
+            int u = q / S, ph = q - u * S;
+            int c = c0 + cl;
+            float v = 0.f;
+            if (c < a.Cin) {
+                int m = pad_src(t0 * S + q, a.pl, a.Tin, a.e, a.mode);
+                if (m >= 0) v = act_apply(a.act, xb[(int64_t)c * a.Tin + m]);
+            }
+            Xs[(cl * S + ph) * Up + u] = v;
+        }
+        // stage weights [k][ci][co]
+        for (int i = tid; i < K * CK * BM; i += NT) {
+            int col = i % BM, r = i / BM;
+            int cl = r % CK, k = r / CK;
+            int c = c0 + cl, co = co0 + col;
+            float v = 0.f;
+            if (c < a.Cin && co < a.Cout) v = a.wf[((int64_t)c * K + k) * a.Cout + co];
+            Ws[(k * CK + cl) * BM + col] = v;
+        }
+        __syncthreads();
+        const int h = lane >> 5, l32 = lane & 31;
+        for (int k = 0; k < K; ++k) {
+            const int kd = k * a.d, ph = kd % S, off = kd / S;
+            const float* wk = Ws + (k * CK + h) * BM + wm0 + l32;
+            const float* xk = Xs + (h * S + ph) * Up + wn0 + l32 + off;
+            for (int cp = 0; cp < CK; cp += 2) {
+                float av[TM], bv[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = wk[cp * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xk[cp * S * Up + j * 32];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+            }
+        }
+    }
+    // epilogue: bias (+ residual), coalesced along t
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int t = t0 + wn0 + j * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = co0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (co < a.Cout && t < a.Tout)
+                    fwd_store(a, ((int64_t)b * a.Cout + co) * a.Tout + t, co, acc[i][j][r]);
+            }
+        }
+}
+
+// ------------------------------------------------------------------------- polyphase
+struct PolyArgs {
+    const float* in;   // [B][Ci][Tin]
+    const float* wp;   // [Ci][J][Co*s]
+    const float* bias; // convtr mode
+    const float* xact; // dgrad mode: pre-activation input for act'
+    float* out;        // convtr: y [B][Co][Tout]; dgrad: dx [B][Co][Tx]
+    float* side;       // dgrad: [B][Co][pl+pr]
+    int B, Ci, Tin, Co, s, J;
+    int mode;          // 0 convtr store, 1 dgrad fold
+    int trim;          // convtr: trim_left
+    int Tout;          // convtr output length
+    int pl, pr, Tx;    // dgrad: pads, unpadded length
+    int act, in_act, accumulate;
+    int CK, Ub;        // chunk channels, LDS row length (BN + J - 1 [+pad])
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    extern __shared__ float smem[];
+    const int CK = a.CK, J = a.J, Ub = a.Ub, S = a.s;
+    const int M = a.Co * S;
+    float* Xs = smem;               // [CK][Ub]
+    float* As = smem + CK * Ub;     // [J][CK][BM]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int u0 = blockIdx.x * BN, m0 = blockIdx.y * BM, b = blockIdx.z;
+    const float* ib = a.in + (int64_t)b * a.Ci * a.Tin;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+
+    const int wlen = BN + J - 1;
+    for (int c0 = 0; c0 < a.Ci; c0 += CK) {
+        __syncthreads();
+        for (int i = tid; i < CK * wlen; i += NT) {
+            int cl = i / wlen, w = i - cl * wlen;
+            int c = c0 + cl, t = u0 - (J - 1) + w;
+            float v = 0.f;
+            if (c < a.Ci && t >= 0 && t < a.Tin) v = act_apply(a.in_act, ib[(int64_t)c * a.Tin + t]);
+            Xs[cl * Ub + w] = v;
+        }
+        for (int i = tid; i < J * CK * BM; i += NT) {
+            int col = i % BM, r = i / BM;
+            int cl = r % CK, q = r / CK;
+            int c = c0 + cl, row = m0 + col;
+            float v = 0.f;
+            if (c < a.Ci && row < M) v = a.wp[((int64_t)c * J + q) * M + row];
+            As[(q * CK + cl) * BM + col] = v;
+        }
+        __syncthreads();
+        const int h = lane >> 5, l32 = lane & 31;
+        for (int q = 0; q < J; ++q) {
+            const float* aq = As + (q * CK + h) * BM + wm0 + l32;
+            const float* xq = Xs + h * Ub + wn0 + l32 + (J - 1) - q;
+            for (int cp = 0; cp < CK; cp += 2) {
+                float av[TM], bv[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = aq[cp * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xq[cp * Ub + j * 32];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int u = u0 + wn0 + j * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (row >= M) continue;
+                const int o = row / S, rr = row - o * S;
+                const int qpos = u * S + rr;
+                const float v = acc[i][j][r];
+                if (a.mode == 0) {
+                    const int p = qpos - a.trim;
+                    if (p >= 0 && p < a.Tout)
+                        a.out[((int64_t)b * a.Co + o) * a.Tout + p] = v + (a.bias ? a.bias[o] : 0.f);
+                } else {
+                    const int m = qpos - a.pl;
+                    if (m >= 0 && m < a.Tx) {
+                        const int64_t idx = ((int64_t)b * a.Co + o) * a.Tx + m;
+                        float g = v;
+                        if (a.act != ENCX_ACT_NONE) g *= act_grad(a.act, a.xact[idx]);
+                        a.out[idx] = a.accumulate ? a.out[idx] + g : g;
+                    } else if (qpos >= 0 && qpos < a.pl + a.Tx + a.pr) {
+                        const int slot = m < 0 ? qpos : a.pl + (m - a.Tx);
+                        a.side[((int64_t)b * a.Co + o) * (a.pl + a.pr) + slot] = v;
+                    }
+                }
+            }
+        }
+}
+
+// Add the gradients that landed on pad positions back onto their reflect sources, in slot
+// order (deterministic). One thread per (b, channel) row.
+__global__ void conv_fold_edges(const float* side, const float* xact, float* dx, int rows, int Tx,
+                                int pl, int pr, int e, int mode, int act) {
+    int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= rows) return;
+    const int np = pl + pr;
+    for (int slot = 0; slot < np; ++slot) {
+        int qpos = slot < pl ? slot : pl + Tx + (slot - pl);
+        int m = pad_src(qpos, pl, Tx, e, mode);
+        if (m < 0) continue;
+        int64_t idx = (int64_t)row * Tx + m;
+        float g = side[(int64_t)row * np + slot];
+        if (act != ENCX_ACT_NONE) g *= act_grad(act, xact[idx]);
+        dx[idx] += g;
+    }
+}
+
+// ------------------------------------------------------------------------- weight grad
+struct WgArgs {
+    const float* L;  // [B][A][Tl]
+    const float* R;  // [B][C][Tr]
+    float* ws;       // [S][A][C*K]
+    int B, A, Tl, C, Tr, K, s, d, pl, e, mode, actL, actR;
+    int BT;          // t per LDS chunk (even)
+    int items;       // total work items = B * ceil(Tl / BT)
+    int per_split;   // work items per split
+    int WLp;         // LDS row length of the R window
+    int NCmax;       // R window rows
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    extern __shared__ float smem[];
+    const int BT = a.BT, WLp = a.WLp, K = a.K, N = a.C * a.K;
+    float* Ls = smem;              // [BT][BM]
+    float* Rs = smem + BT * BM;    // [NCmax][WLp]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int a0 = blockIdx.y * BM, n0 = blockIdx.x * BN, split = blockIdx.z;
+    const int c_first = n0 / K;
+    const int nchunks_t = (a.Tl + BT - 1) / BT;
+    const int h = lane >> 5, l32 = lane & 31;
+
+    int boff[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        int n = n0 + wn0 + j * 32 + l32;
+        int c = n / K, k = n - c * K;
+        boff[j] = (c - c_first) * WLp + k * a.d;
+        if (n >= N) boff[j] = 0;
+    }
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+
+    const int it_beg = split * a.per_split;
+    const int it_end = min(a.items, it_beg + a.per_split);
+    const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
+    for (int it = it_beg; it < it_end; ++it) {
+        const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
+        const float* Lb = a.L + (int64_t)b * a.A * a.Tl;
+        const float* Rb = a.R + (int64_t)b * a.C * a.Tr;
+        __syncthreads();
+        for (int i = tid; i < BT * BM; i += NT) {
+            int tl = i % BT, al = i / BT;
+            int t = tc + tl, aa = a0 + al;
+            float v = 0.f;
+            if (t < a.Tl && aa < a.A) v = act_apply(a.actL, Lb[(int64_t)aa * a.Tl + t]);
+            Ls[tl * BM + al] = v;
+        }
+        for (int i = tid; i < a.NCmax * WL; i += NT) {
+            int cr = i / WL, w = i - cr * WL;
+            int c = c_first + cr;
+            float v = 0.f;
+            if (c < a.C) {
+                int m = pad_src(tc * a.s + w, a.pl, a.Tr, a.e, a.mode);
+                if (m >= 0) v = act_apply(a.actR, Rb[(int64_t)c * a.Tr + m]);
+            }
+            Rs[cr * WLp + w] = v;
+        }
+        __syncthreads();
+        for (int tp = 0; tp < BT; tp += 2) {
+            const int tl = tp + h;
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) av[i] = Ls[tl * BM + wm0 + i * 32 + l32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bv[j] = Rs[boff[j] + tl * a.s];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+        }
+    }
+    float* wsb = a.ws + (int64_t)split * a.A * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int aa = a0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (aa < a.A && n < N) wsb[(int64_t)aa * N + n] = acc[i][j][r];
+            }
+        }
+}
+
+// VALU weight grad for tiny A*N (first / last conv of the stack): thread per output element.
+__global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
+    extern __shared__ float smem[];
+    const int BT = a.BT, K = a.K, N = a.C * K, AN = a.A * N;
+    float* Ls = smem;               // [A][BT]
+    float* Rs = smem + a.A * BT;    // [C][WLp]
+    const int split = blockIdx.x, tid = threadIdx.x;
+    const int nchunks_t = (a.Tl + BT - 1) / BT;
+    const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // AN <= 4 * NT
+    const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
+    for (int it = it_beg; it < it_end; ++it) {
+        const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
+        const float* Lb = a.L + (int64_t)b * a.A * a.Tl;
+        const float* Rb = a.R + (int64_t)b * a.C * a.Tr;
+        __syncthreads();
+        for (int i = tid; i < a.A * BT; i += NT) {
+            int al = i / BT, tl = i - al * BT, t = tc + tl;
+            Ls[i] = t < a.Tl ? act_apply(a.actL, Lb[(int64_t)al * a.Tl + t]) : 0.f;
+        }
+        for (int i = tid; i < a.C * WL; i += NT) {
+            int c = i / WL, w = i - c * WL;
+            int m = pad_src(tc * a.s + w, a.pl, a.Tr, a.e, a.mode);
+            Rs[c * a.WLp + w] = m >= 0 ? act_apply(a.actR, Rb[(int64_t)c * a.Tr + m]) : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+            int o = tid + z * NT;
+            if (o < AN) {
+                int aa = o / N, n = o - aa * N, c = n / K, k = n - c * K;
+                const float* lp = Ls + aa * BT;
+                const float* rp = Rs + c * a.WLp + k * a.d;
+                float sacc = acc[z];
+                for (int tl = 0; tl < BT; ++tl) sacc = fmaf(lp[tl], rp[tl * a.s], sacc);
+                acc[z] = sacc;
+            }
+        }
+    }
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+        int o = tid + z * NT;
+        if (o < AN) a.ws[(int64_t)split * AN + o] = acc[z];
+    }
+}
+
+__global__ void wgrad_reduce(const float* ws, float* dw, int64_t AN, int S, int accumulate) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= AN) return;
+    float v = 0.f;
+    for (int sidx = 0; sidx < S; ++sidx) v += ws[(int64_t)sidx * AN + i];
+    dw[i] = accumulate ? dw[i] + v : v;
+}
+
+// VALU forward for Cout <= 4 (decoder's final 32 -> 1 conv): thread per output sample.
+__global__ __launch_bounds__(NT) void conv_fwd_small_kernel(FwdArgs a) {
+    extern __shared__ float smem[];
+    const int K = a.K, S = a.s, CK = a.CK;
+    const int WL = (NT - 1) * S + (K - 1) * a.d + 1;
+    float* Xs = smem;            // [CK][WL]
+    float* Wsm = smem + CK * WL; // [Cout][CK][K]
+    const int tid = threadIdx.x, t0 = blockIdx.x * NT, b = blockIdx.z;
+    const float* xb = a.x + (int64_t)b * a.Cin * a.Tin;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < a.Cin; c0 += CK) {
+        __syncthreads();
+        for (int i = tid; i < CK * WL; i += NT) {
+            int cl = i / WL, w = i - cl * WL, c = c0 + cl;
+            float v = 0.f;
+            if (c < a.Cin) {
+                int m = pad_src(t0 * S + w, a.pl, a.Tin, a.e, a.mode);
+                if (m >= 0) v = act_apply(a.act, xb[(int64_t)c * a.Tin + m]);
+            }
+            Xs[i] = v;
+        }
+        for (int i = tid; i < a.Cout * CK * K; i += NT) {
+            int co = i / (CK * K), r = i - co * CK * K, cl = r / K, k = r - cl * K, c = c0 + cl;
+            Wsm[i] = c < a.Cin ? a.wf[((int64_t)c * K + k) * a.Cout + co] : 0.f;
+        }
+        __syncthreads();
+        for (int co = 0; co < a.Cout; ++co) {
+            float s = acc[co];
+            for (int cl = 0; cl < CK; ++cl) {
+                const float* xr = Xs + cl * WL + tid * S;
+                const float* wr = Wsm + (co * CK + cl) * K;
+                for (int k = 0; k < K; ++k) s = fmaf(wr[k], xr[k * a.d], s);
+            }
+            acc[co] = s;
+        }
+    }
+    const int t = t0 + tid;
+    if (t < a.Tout)
+        for (int co = 0; co < a.Cout; ++co)
+            fwd_store(a, ((int64_t)b * a.Cout + co) * a.Tout + t, co, acc[co]);
+}
+
+// ------------------------------------------------------------------------- launch helpers
+template <int BM, int BN, int WM, int WN>
+int launch_fwd(const FwdArgs& a, hipStream_t st) {
+    dim3 grid(cdiv(a.Tout, BN), cdiv(a.Cout, BM), a.B);
+    size_t lds = (size_t)(a.CK * a.s * a.Up + a.K * a.CK * BM) * sizeof(float);
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    return 0;
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_poly(const PolyArgs& a, int ncols, hipStream_t st) {
+    dim3 grid(cdiv(ncols, BN), cdiv((int64_t)a.Co * a.s, BM), a.B);
+    size_t lds = (size_t)(a.CK * a.Ub + a.J * a.CK * BM) * sizeof(float);
+    hipLaunchKernelGGL((conv_poly_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    return 0;
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_wg(const WgArgs& a, int splits, hipStream_t st) {
+    dim3 grid(cdiv((int64_t)a.C * a.K, BN), cdiv(a.A, BM), splits);
+    size_t lds = (size_t)(a.BT * BM + a.NCmax * a.WLp) * sizeof(float);
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    return 0;
+}
+
+static int even_up(int v) { return (v + 1) & ~1; }
+
+// tile-shape choice: M rows (output channels / polyphase rows), N columns (time)
+enum Tile { T32x128, T64x64, T64x128, T128x32, T128x64, T128x128 };
+static Tile pick_tile(int64_t M, int64_t N) {
+    if (N <= 48) return T128x32;
+    if (M <= 32) return T32x128;
+    if (M <= 64) return N <= 96 ? T64x64 : T64x128;
+    if (N <= 96) return T128x64;
+    return T128x128;
+}
+static int tile_bm(Tile t) { return (t == T32x128) ? 32 : (t == T64x64 || t == T64x128) ? 64 : 128; }
+
+int conv_fwd_dispatch(FwdArgs a, hipStream_t st) {
+    // chunk size: ~64 reduction elements per LDS stage
+    int ck = 64 / a.K;
+    if (ck < 2) ck = 2;
+    ck = even_up(ck);
+    if (ck > even_up(a.Cin)) ck = even_up(a.Cin);
+    a.CK = ck;
+    Tile t = pick_tile(a.Cout, a.Tout);
+    int BN = (t == T128x32) ? 32 : (t == T64x64 || t == T128x64) ? 64 : 128;
+    a.Up = BN + ((a.K - 1) * a.d) / a.s + 1;
+    if ((a.Up & 31) == 0) a.Up += 1;
+    switch (t) {
+        case T32x128: return launch_fwd<32, 128, 1, 4>(a, st);
+        case T64x64: return launch_fwd<64, 64, 2, 2>(a, st);
+        case T64x128: return launch_fwd<64, 128, 2, 2>(a, st);
+        case T128x32: return launch_fwd<128, 32, 4, 1>(a, st);
+        case T128x64: return launch_fwd<128, 64, 2, 2>(a, st);
+        default: return launch_fwd<128, 128, 2, 2>(a, st);
+    }
+}
+
+int poly_dispatch(PolyArgs a, int ncols, hipStream_t st) {
+    int ck = 64 / a.J;
+    if (ck < 2) ck = 2;
+    ck = even_up(ck);
+    if (ck > even_up(a.Ci)) ck = even_up(a.Ci);
+    a.CK = ck;
+    Tile t = pick_tile((int64_t)a.Co * a.s, ncols);
+    int BN = (t == T128x32) ? 32 : (t == T64x64 || t == T128x64) ? 64 : 128;
+    a.Ub = BN + a.J - 1;
+    if ((a.Ub & 31) == 0) a.Ub += 1;
+    switch (t) {
+        case T32x128: return launch_poly<32, 128, 1, 4>(a, ncols, st);
+        case T64x64: return launch_poly<64, 64, 2, 2>(a, ncols, st);
+        case T64x128: return launch_poly<64, 128, 2, 2>(a, ncols, st);
+        case T128x32: return launch_poly<128, 32, 4, 1>(a, ncols, st);
+        case T128x64: return launch_poly<128, 64, 2, 2>(a, ncols, st);
+        default: return launch_poly<128, 128, 2, 2>(a, ncols, st);
+    }
+}
+
+// wgrad planning shared by the launcher and the workspace query
+struct WgPlan {
+    bool small;
+    int BM, BN, BT, splits, items, per_split, tiles;
+};
+static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
+    WgPlan p;
+    const int64_t N = C * K;
+    p.small = (A * N <= 4 * NT);
+    p.BT = p.small ? 256 : 32;
+    if (!p.small) {
+        Tile t = (A <= 32) ? T32x128 : (A <= 64 ? T64x128 : T128x128);
+        p.BM = tile_bm(t);
+        p.BN = (t == T32x128) ? 128 : 128;
+        p.tiles = (int)(cdiv(N, p.BN) * cdiv(A, p.BM));
+    } else {
+        p.BM = p.BN = 0;
+        p.tiles = 1;
+    }
+    p.items = (int)(B * cdiv(Tl, p.BT));
+    int64_t want = cdiv(2048, p.tiles);
+    int64_t cap = (64ll << 20) / (4 * A * N);  // <= 64 MB of partials
+    if (cap < 1) cap = 1;
+    int64_t sp = want < cap ? want : cap;
+    if (sp > p.items) sp = p.items;
+    if (sp < 1) sp = 1;
+    p.per_split = (int)cdiv(p.items, sp);
+    p.splits = (int)cdiv(p.items, p.per_split);
+    return p;
+}
+
+static int wlp_for(int WL, int K) {
+    // row stride == K (mod 32) so 32 consecutive (c,k) columns hit 32 distinct banks
+    int r = ((K % 32) - (WL % 32) + 32) % 32;
+    return WL + r;
+}
+
+int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, int64_t A,
+              int64_t Tl, int64_t C, int64_t Tr, int64_t K, int64_t s, int64_t d, int64_t pl,
+              int64_t e, int mode, int actL, int actR, int accumulate, hipStream_t st) {
+    WgPlan p = plan_wgrad(B, A, Tl, C, K);
+    WgArgs a;
+    a.L = L; a.R = R; a.ws = ws;
+    a.B = (int)B; a.A = (int)A; a.Tl = (int)Tl; a.C = (int)C; a.Tr = (int)Tr; a.K = (int)K;
+    a.s = (int)s; a.d = (int)d; a.pl = (int)pl; a.e = (int)e; a.mode = mode; a.actL = actL;
+    a.actR = actR; a.BT = p.BT; a.items = p.items; a.per_split = p.per_split;
+    const int WL = (p.BT - 1) * a.s + (a.K - 1) * a.d + 1;
+    const int64_t AN = A * C * K;
+    if (p.small) {
+        a.WLp = WL;
+        a.NCmax = (int)C;
+        size_t lds = (size_t)(A * p.BT + C * WL) * sizeof(float);
+        if (lds > 160 * 1024) return ENCX_EINVAL;
+        hipLaunchKernelGGL(conv_wgrad_small_kernel, dim3(p.splits), dim3(NT), lds, st, a);
+    } else {
+        a.WLp = wlp_for(WL, a.K);
+        a.NCmax = (int)((p.BN + a.K - 1) / a.K + 1);
+        if (a.NCmax > C) a.NCmax = (int)C;
+        if (p.BM == 32) launch_wg<32, 128, 1, 4>(a, p.splits, st);
+        else if (p.BM == 64) launch_wg<64, 128, 2, 2>(a, p.splits, st);
+        else launch_wg<128, 128, 2, 2>(a, p.splits, st);
+    }
+    ENCX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(wgrad_reduce, dim3(cdiv(AN, 256)), dim3(256), 0, st, ws, dw, AN, p.splits,
+                       accumulate);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+size_t wgrad_ws_bytes(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
+    WgPlan p = plan_wgrad(B, A, Tl, C, K);
+    return (size_t)p.splits * A * C * K * sizeof(float);
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+static int conv_fwd_impl(FwdArgs a, hipStream_t st) {
+    if (a.Cout <= 4) {
+        int ck = 64 / a.K;
+        if (ck < 1) ck = 1;
+        if (ck > a.Cin) ck = a.Cin;
+        a.CK = ck;
+        const int WL = (NT - 1) * a.s + (a.K - 1) * a.d + 1;
+        size_t lds = (size_t)(ck * WL + a.Cout * ck * a.K) * sizeof(float);
+        ENCX_REQUIRE(lds <= 160 * 1024);
+        hipLaunchKernelGGL(conv_fwd_small_kernel, dim3(cdiv(a.Tout, NT), 1, a.B), dim3(NT), lds, st, a);
+    } else {
+        conv_fwd_dispatch(a, st);
+    }
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_conv1d_fwd(const float* x, const float* wf, const float* bias, const float* residual,
+                    float* y, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                    int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
+                    int64_t short_ext, int pad_mode, int pre_act, encx_stream_t stream) {
+    ENCX_REQUIRE(x && wf && y && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0);
+    ENCX_REQUIRE(K > 0 && stride > 0 && dilation > 0 && pad_left >= 0 && short_ext >= 0);
+    hipStream_t st = (hipStream_t)stream;
+    FwdArgs a;
+    a.x = x; a.wf = wf; a.bias = bias; a.res = residual; a.y = y; a.xact = nullptr;
+    a.B = (int)B; a.Cin = (int)Cin; a.Tin = (int)Tin; a.Cout = (int)Cout; a.Tout = (int)Tout;
+    a.K = (int)K; a.s = (int)stride; a.d = (int)dilation; a.pl = (int)pad_left; a.e = (int)short_ext;
+    a.mode = pad_mode; a.act = pre_act; a.epi_act = ENCX_ACT_NONE; a.accumulate = 0;
+    encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
+                       4.0 * (B * Cin * Tin + B * Cout * Tout * (residual ? 2 : 1) + Cin * K * Cout));
+    return conv_fwd_impl(a, st);
+}
+
+size_t encx_conv1d_bwd_data_workspace(int64_t B, int64_t Cin, int64_t pad_left, int64_t pad_right) {
+    return (size_t)(B * Cin * (pad_left + pad_right) + 1) * sizeof(float);
+}
+
+int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float* dx,
+                         float* side, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
+                         int64_t Tout, int64_t K, int64_t stride, int64_t pad_left,
+                         int64_t pad_right, int64_t short_ext, int pad_mode, int pre_act,
+                         int accumulate, encx_stream_t stream) {
+    ENCX_REQUIRE(dy && wp && dx && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0);
+    ENCX_REQUIRE(pre_act == ENCX_ACT_NONE || x);
+    ENCX_REQUIRE((pad_left + pad_right) == 0 || side);
+    hipStream_t st = (hipStream_t)stream;
+    PolyArgs a;
+    a.in = dy; a.wp = wp; a.bias = nullptr; a.xact = x; a.out = dx; a.side = side;
+    a.B = (int)B; a.Ci = (int)Cout; a.Tin = (int)Tout; a.Co = (int)Cin; a.s = (int)stride;
+    a.J = (int)cdiv(K, stride); a.mode = 1; a.trim = 0; a.Tout = 0;
+    a.pl = (int)pad_left; a.pr = (int)pad_right; a.Tx = (int)Tin;
+    a.act = pre_act; a.in_act = ENCX_ACT_NONE; a.accumulate = accumulate;
+    const int64_t Tpad = pad_left + Tin + pad_right;
+    const int ncols = (int)cdiv(Tpad, stride);
+    encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
+                       4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout));
+    poly_dispatch(a, ncols, st);
+    ENCX_CHECK_LAUNCH();
+    if (pad_left + pad_right > 0 && pad_mode == ENCX_PAD_REFLECT) {
+        int rows = (int)(B * Cin);
+        hipLaunchKernelGGL(conv_fold_edges, dim3(cdiv(rows, 256)), dim3(256), 0, st, side, x, dx,
+                           rows, (int)Tin, (int)pad_left, (int)pad_right, (int)short_ext, pad_mode,
+                           pre_act);
+        ENCX_CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+int encx_conv1d_bwd_weight(const float* dy, const float* x, float* dw, float* db, float* ws,
+                           int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                           int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
+                           int64_t short_ext, int pad_mode, int pre_act, int accumulate,
+                           encx_stream_t stream) {
+    ENCX_REQUIRE(dy && x && dw && ws && B > 0);
+    hipStream_t st = (hipStream_t)stream;
+    encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K, 4.0 * (B * Cout * Tout + B * Cin * Tin + Cin * K * Cout));
+    int rc = wgrad_run(dy, x, dw, ws, B, Cout, Tout, Cin, Tin, K, stride, dilation, pad_left,
+                       short_ext, pad_mode, ENCX_ACT_NONE, pre_act, accumulate, st);
+    if (rc) return rc;
+    if (db) return encx_channel_sum(dy, db, ws, B, Cout, Tout, accumulate, stream);
+    return 0;
+}
+
+size_t encx_conv1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout,
+                                        int64_t K) {
+    size_t a = wgrad_ws_bytes(B, Cout, Tout, Cin, K), b = encx_channel_sum_workspace(Cout);
+    return a > b ? a : b;
+}
+
+int encx_convtr1d_fwd(const float* x, const float* wp, const float* bias, float* y, int64_t B,
+                      int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout, int64_t K,
+                      int64_t stride, int64_t trim_left, int pre_act, encx_stream_t stream) {
+    ENCX_REQUIRE(x && wp && y && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0);
+    hipStream_t st = (hipStream_t)stream;
+    PolyArgs a;
+    a.in = x; a.wp = wp; a.bias = bias; a.xact = nullptr; a.out = y; a.side = nullptr;
+    a.B = (int)B; a.Ci = (int)Cin; a.Tin = (int)Tin; a.Co = (int)Cout; a.s = (int)stride;
+    a.J = (int)cdiv(K, stride); a.mode = 0; a.trim = (int)trim_left; a.Tout = (int)Tout;
+    a.pl = a.pr = a.Tx = 0; a.act = ENCX_ACT_NONE; a.in_act = pre_act; a.accumulate = 0;
+    const int ncols = (int)cdiv(Tout + trim_left, stride);
+    encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K, 4.0 * (B * Cin * Tin + B * Cout * Tout + Cin * K * Cout));
+    poly_dispatch(a, ncols, st);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_convtr1d_bwd_data(const float* dy, const float* wf, const float* x, float* dx,
+                           int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                           int64_t K, int64_t stride, int64_t trim_left, int pre_act,
+                           int accumulate, encx_stream_t stream) {
+    // dx[ci,t] = [acc ? dx : 0] + act'(x) * sum_{co,k} Wt[ci,co,k] dy[co, t*s+k-trim_left]
+    // (zero outside [0,Tout)): a forward conv of dy with zero padding pad_left = trim_left.
+    ENCX_REQUIRE(dy && wf && dx && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0);
+    ENCX_REQUIRE(pre_act == ENCX_ACT_NONE || x);
+    hipStream_t st = (hipStream_t)stream;
+    FwdArgs a;
+    a.x = dy; a.wf = wf; a.bias = nullptr; a.res = nullptr; a.y = dx;
+    a.xact = pre_act != ENCX_ACT_NONE ? x : nullptr;
+    a.B = (int)B; a.Cin = (int)Cout; a.Tin = (int)Tout; a.Cout = (int)Cin; a.Tout = (int)Tin;
+    a.K = (int)K; a.s = (int)stride; a.d = 1; a.pl = (int)trim_left; a.e = 0;
+    a.mode = ENCX_PAD_ZERO; a.act = ENCX_ACT_NONE; a.epi_act = pre_act; a.accumulate = accumulate;
+    encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K,
+                       4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout));
+    return conv_fwd_impl(a, st);
+}
+
+int encx_convtr1d_bwd_weight(const float* x, const float* dy, float* dw, float* db, float* ws,
+                             int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                             int64_t K, int64_t stride, int64_t trim_left, int pre_act,
+                             int accumulate, encx_stream_t stream) {
+    ENCX_REQUIRE(x && dy && dw && ws && B > 0);
+    hipStream_t st = (hipStream_t)stream;
+    encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K, 4.0 * (B * Cout * Tout + B * Cin * Tin + Cin * K * Cout));
+    // L = act(x) [ci][t], R = dy [co][t*s + k - trim_left] zero-padded
+    int rc = wgrad_run(x, dy, dw, ws, B, Cin, Tin, Cout, Tout, K, stride, 1, trim_left, 0,
+                       ENCX_PAD_ZERO, pre_act, ENCX_ACT_NONE, accumulate, st);
+    if (rc) return rc;
+    if (db) return encx_channel_sum(dy, db, ws, B, Cout, Tout, accumulate, stream);
+    return 0;
+}
+
+size_t encx_convtr1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tin,
+                                          int64_t K) {
+    size_t a = wgrad_ws_bytes(B, Cin, Tin, Cout, K), b = encx_channel_sum_workspace(Cout);
+    return a > b ? a : b;
+}
+
+}  // extern "C"

@@ -1,0 +1,287 @@
+// Multi-scale mel-spectrogram loss (audio_to_mel.py:34-55, losses.py:40-42), forward and the
+// gradient w.r.t. the generator output, on the generic MFMA GEMM skeleton of gemm.h.
+//
+// Per scale n (hop h = n/4, reflect pad p = (n-h)/2, nb = n/2+1 bins, F frames):
+//   spec  [B*F][2nb] = frames(reflect_pad(wav)) @ [w*cos | -w*sin]      (DFT as a GEMM; frames
+//                      are gathered from the waveform while staging: no im2col in HBM)
+//   mel   [B*F][nm]  = (re^2 + im^2) @ mel_basis^T                       (power built on load)
+//   loss  += mean|lx - ly| + mean (lx - ly)^2, l = log10(clamp(mel, 1e-5))
+// and for d/dy: dmel = (sign(d) + 2d)/Nel / (mel ln10) [mel >= 1e-5]; dP = dmel @ mel_basis;
+// G = [2 re dP | 2 im dP]; dframe = G @ [w*cos | -w*sin]^T; overlap-add + reflect fold -> dy.
+#include "common.h"
+#include "gemm.h"
+
+namespace {
+
+struct Tab {  // device table pointers for one scale
+    const float* bt;  // [n][2nb]
+    const float* mt;  // [nb][nm]
+    const float* mb;  // [nm][nb]
+};
+ENCX_DEV Tab tab_at(const float* t, int n, int nm) {
+    const int nb = n / 2 + 1;
+    Tab r;
+    r.bt = t;
+    r.mt = t + (int64_t)n * 2 * nb;
+    r.mb = r.mt + (int64_t)nb * nm;
+    return r;
+}
+
+// ---------------------------------------------------------------- loaders / epilogues
+struct LdSpec {  // A: framed reflect-padded audio, B: DFT table
+    static constexpr bool A_K_FAST = true, B_N_FAST = true;
+    const float* wav; const float* bt;
+    int T, F, h, p, nb2;
+    ENCX_DEV float a(int m, int k) const {
+        int b = m / F, f = m - b * F;
+        int src = pad_src(f * h + k, p, T, 0, ENCX_PAD_REFLECT);
+        return wav[(int64_t)b * T + src];
+    }
+    ENCX_DEV float b(int k, int n) const { return bt[(int64_t)k * nb2 + n]; }
+};
+struct EpStore {
+    float* out; int ld;
+    ENCX_DEV void operator()(int m, int n, float v) const { out[(int64_t)m * ld + n] = v; }
+};
+struct LdMel {  // A: |X|^2 built from (re, im); B: mel basis^T
+    static constexpr bool A_K_FAST = true, B_N_FAST = true;
+    const float* spec; const float* mt;
+    int nb, nm;
+    ENCX_DEV float a(int m, int k) const {
+        const float* r = spec + (int64_t)m * 2 * nb;
+        float re = r[k], im = r[nb + k];
+        return re * re + im * im;
+    }
+    ENCX_DEV float b(int k, int n) const { return mt[(int64_t)k * nm + n]; }
+};
+struct EpLog {
+    float* out; int nm;
+    ENCX_DEV void operator()(int m, int n, float v) const {
+        out[(int64_t)m * nm + n] = log10f(fmaxf(v, 1e-5f));
+    }
+};
+struct EpLogT {  // log-mel in the reference layout [B][nm][F]
+    float* out; int nm, F;
+    ENCX_DEV void operator()(int m, int n, float v) const {
+        int b = m / F, f = m - b * F;
+        out[((int64_t)b * nm + n) * F + f] = log10f(fmaxf(v, 1e-5f));
+    }
+};
+struct LdDP {  // A: dmel [rows][nm]; B: mel basis [nm][nb]
+    static constexpr bool A_K_FAST = true, B_N_FAST = true;
+    const float* dmel; const float* mb;
+    int nb, nm;
+    ENCX_DEV float a(int m, int k) const { return dmel[(int64_t)m * nm + k]; }
+    ENCX_DEV float b(int k, int n) const { return mb[(int64_t)k * nb + n]; }
+};
+struct EpG {  // spec (re, im) -> (2 re dP, 2 im dP) in place
+    float* spec; int nb;
+    ENCX_DEV void operator()(int m, int n, float v) const {
+        float* r = spec + (int64_t)m * 2 * nb;
+        float re = r[n], im = r[nb + n];
+        r[n] = 2.f * re * v;
+        r[nb + n] = 2.f * im * v;
+    }
+};
+struct LdDF {  // A: G [rows][2nb]; B(k, t) = bt[t][k]
+    static constexpr bool A_K_FAST = true, B_N_FAST = false;
+    const float* g; const float* bt;
+    int nb2;
+    ENCX_DEV float a(int m, int k) const { return g[(int64_t)m * nb2 + k]; }
+    ENCX_DEV float b(int k, int n) const { return bt[(int64_t)n * nb2 + k]; }
+};
+
+// ---------------------------------------------------------------- element kernels
+__global__ void tables_kernel(float* t, const float* mel, int n, int nm) {
+    const int nb = n / 2 + 1, nb2 = 2 * nb;
+    Tab tb = tab_at(t, n, nm);
+    float* bt = (float*)tb.bt;
+    float* mt = (float*)tb.mt;
+    float* mb = (float*)tb.mb;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nbt = (int64_t)n * nb2;
+    if (i < nbt) {
+        int tt = (int)(i / nb2), c = (int)(i - (int64_t)tt * nb2);
+        int k = c < nb ? c : c - nb;
+        // torch.hann_window(n) (periodic): 0.5 - 0.5 cos(2 pi t / n)
+        double w = 0.5 - 0.5 * cos(2.0 * M_PI * (double)tt / (double)n);
+        double ang = 2.0 * M_PI * (double)(((int64_t)k * tt) % n) / (double)n;
+        bt[i] = (float)(c < nb ? w * cos(ang) : -w * sin(ang));
+        return;
+    }
+    i -= nbt;
+    if (i < (int64_t)nb * nm) {
+        int k = (int)(i / nm), m = (int)(i - (int64_t)k * nm);
+        mt[i] = mel[(int64_t)m * nb + k];
+        mb[(int64_t)m * nb + k] = mel[(int64_t)m * nb + k];
+    }
+}
+
+constexpr int LB = 1024;  // loss partial blocks
+
+// ly = log10(clamp(mel_y)); d = ly - lx; parts; dmel (in place over mel_y)
+__global__ __launch_bounds__(256) void mel_loss_kernel(const float* lx, float* mel_y, float* parts,
+                                                       int64_t total, float inv_n, int want_grad) {
+    __shared__ float red[16];
+    float s1 = 0.f, s2 = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        float mel = mel_y[i];
+        float ly = log10f(fmaxf(mel, 1e-5f));
+        float d = lx[i] - ly;  // l1Loss(mel(x), mel(y)): input = mel(x), target = mel(y)
+        s1 += fabsf(d);
+        s2 = fmaf(d, d, s2);
+        if (want_grad) {
+            float g = ((d < 0.f ? 1.f : (d > 0.f ? -1.f : 0.f)) - 2.f * d) * inv_n;  // d/d ly
+            mel_y[i] = mel >= 1e-5f ? g / (mel * 2.302585092994046f) : 0.f;
+        }
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (threadIdx.x == 0) {
+        parts[blockIdx.x] = s1;
+        parts[LB + blockIdx.x] = s2;
+    }
+}
+
+__global__ __launch_bounds__(256) void loss_add(const float* parts, int nblk, float inv_n, float* loss) {
+    __shared__ float red[16];
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = threadIdx.x; i < nblk; i += 256) {
+        s1 += parts[i];
+        s2 += parts[LB + i];
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (threadIdx.x == 0) loss[0] = (loss[0] + s1 * inv_n) + s2 * inv_n;
+}
+
+// dy[b][m] += sum over padded positions j mapping to m (reflect) of the overlapping frames
+__global__ void overlap_add(const float* dframe, float* grad, int Bn, int T, int n, int h, int p,
+                            int F) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Bn * T) return;
+    int b = (int)(i / T), m = (int)(i - (int64_t)b * T);
+    int js[3];
+    int nj = 0;
+    js[nj++] = m + p;
+    if (m >= 1 && m <= p) js[nj++] = p - m;
+    if (m >= T - 1 - p && m <= T - 2) js[nj++] = p + 2 * (T - 1) - m;
+    float s = 0.f;
+    for (int q = 0; q < nj; ++q) {
+        int j = js[q];
+        int flo = j - n + 1 > 0 ? (j - n + 1 + h - 1) / h : 0;
+        int fhi = j / h;
+        if (fhi > F - 1) fhi = F - 1;
+        for (int f = flo; f <= fhi; ++f) s += dframe[((int64_t)b * F + f) * n + (j - f * h)];
+    }
+    grad[i] += s;
+}
+
+struct Geo {
+    int n, h, p, nb, F, rows;
+    int64_t spec, lmx, mely, dframe;  // workspace offsets (floats)
+    int64_t parts, total;
+};
+Geo geo(int64_t B, int64_t T, int64_t n, int64_t nm) {
+    Geo g;
+    g.n = (int)n; g.h = (int)(n / 4); g.p = (int)((n - n / 4) / 2); g.nb = (int)(n / 2 + 1);
+    g.F = (int)((T + 2 * g.p - n) / g.h + 1);
+    g.rows = (int)(B * g.F);
+    g.spec = 0;
+    g.lmx = g.spec + (int64_t)g.rows * 2 * g.nb;
+    g.mely = g.lmx + (int64_t)g.rows * nm;
+    g.dframe = g.mely + (int64_t)g.rows * nm;
+    g.parts = g.dframe + (int64_t)g.rows * n;
+    g.total = g.parts + 2 * LB;
+    return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t encx_mel_tables_floats(int64_t n_fft, int64_t n_mels) {
+    int64_t nb = n_fft / 2 + 1;
+    return (size_t)(n_fft * 2 * nb + 2 * nb * n_mels);
+}
+
+int encx_mel_tables_init(float* tables, const float* mel_basis, int64_t n_fft, int64_t n_mels,
+                         encx_stream_t stream) {
+    ENCX_REQUIRE(tables && mel_basis && n_fft >= 4 && (n_fft % 4) == 0 && n_mels > 0);
+    int64_t tot = n_fft * 2 * (n_fft / 2 + 1) + (n_fft / 2 + 1) * n_mels;
+    hipLaunchKernelGGL(tables_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, (hipStream_t)stream, tables,
+                       mel_basis, (int)n_fft, (int)n_mels);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+size_t encx_mel_workspace_floats(int64_t B, int64_t T, int64_t n_fft, int64_t n_mels) {
+    return (size_t)geo(B, T, n_fft, n_mels).total;
+}
+
+int64_t encx_mel_frames(int64_t T, int64_t n_fft) { return geo(1, T, n_fft, 1).F; }
+
+int encx_mel_logmel(const float* x, const float* tables, float* ws, float* out, int64_t B,
+                    int64_t T, int64_t n_fft, int64_t n_mels, encx_stream_t stream) {
+    ENCX_REQUIRE(x && tables && ws && out && B > 0 && n_fft >= 4 && (n_fft % 4) == 0);
+    hipStream_t st = (hipStream_t)stream;
+    const int nm = (int)n_mels;
+    Geo g = geo(B, T, n_fft, n_mels);
+    ENCX_REQUIRE(g.p < T && g.F > 0);
+    const float* bt = tables;
+    const float* mt = tables + (int64_t)g.n * 2 * g.nb;
+    const int nb2 = 2 * g.nb;
+    int rc = gemm_launch(LdSpec{x, bt, (int)T, g.F, g.h, g.p, nb2}, EpStore{ws + g.spec, nb2}, g.rows,
+                         nb2, g.n, st);
+    if (rc) return rc;
+    return gemm_launch(LdMel{ws + g.spec, mt, g.nb, nm}, EpLogT{out, nm, g.F}, g.rows, nm, g.nb, st);
+}
+
+int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws, float* loss,
+                  float* grad, int64_t B, int64_t T, int64_t n_fft, int64_t n_mels,
+                  encx_stream_t stream) {
+    ENCX_REQUIRE(x && y && tables && ws && loss && B > 0 && n_fft >= 4 && (n_fft % 4) == 0);
+    hipStream_t st = (hipStream_t)stream;
+    const int nm = (int)n_mels;
+    Geo g = geo(B, T, n_fft, n_mels);
+    ENCX_REQUIRE(g.p < T && g.F > 0);
+    const float* bt = tables;
+    const float* mt = tables + (int64_t)g.n * 2 * g.nb;
+    const float* mb = mt + (int64_t)g.nb * nm;
+    float* spec = ws + g.spec;
+    float* lmx = ws + g.lmx;
+    float* mely = ws + g.mely;
+    float* dframe = ws + g.dframe;
+    float* parts = ws + g.parts;
+    const int nb2 = 2 * g.nb;
+    int rc;
+    // target: logmel(x)
+    rc = gemm_launch(LdSpec{x, bt, (int)T, g.F, g.h, g.p, nb2}, EpStore{spec, nb2}, g.rows, nb2, g.n, st);
+    if (rc) return rc;
+    rc = gemm_launch(LdMel{spec, mt, g.nb, nm}, EpLog{lmx, nm}, g.rows, nm, g.nb, st);
+    if (rc) return rc;
+    // output: mel(y)
+    rc = gemm_launch(LdSpec{y, bt, (int)T, g.F, g.h, g.p, nb2}, EpStore{spec, nb2}, g.rows, nb2, g.n, st);
+    if (rc) return rc;
+    rc = gemm_launch(LdMel{spec, mt, g.nb, nm}, EpStore{mely, nm}, g.rows, nm, g.nb, st);
+    if (rc) return rc;
+    const int64_t total = (int64_t)g.rows * nm;
+    const float inv_n = 1.f / (float)total;
+    const int nblk = (int)std::min<int64_t>(LB, cdiv(total, 256 * 4));
+    hipLaunchKernelGGL(mel_loss_kernel, dim3(nblk), dim3(256), 0, st, lmx, mely, parts, total, inv_n,
+                       grad ? 1 : 0);
+    ENCX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(loss_add, dim3(1), dim3(256), 0, st, parts, nblk, inv_n, loss);
+    ENCX_CHECK_LAUNCH();
+    if (!grad) return 0;
+    rc = gemm_launch(LdDP{mely, mb, g.nb, nm}, EpG{spec, g.nb}, g.rows, g.nb, nm, st);
+    if (rc) return rc;
+    rc = gemm_launch(LdDF{spec, bt, nb2}, EpStore{dframe, g.n}, g.rows, g.n, nb2, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(overlap_add, dim3(cdiv(B * T, 256)), dim3(256), 0, st, dframe, grad, (int)B,
+                       (int)T, g.n, g.h, g.p, g.F);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

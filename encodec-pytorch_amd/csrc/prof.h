@@ -1,0 +1,12 @@
+// In-library launch timing for bench.py's roofline line (encx_prof_enable / encx_prof_read).
+// When enabled, each public MFMA entry point brackets its launches with a hipEvent pair on the
+// caller's stream and books its algorithmic FLOPs / bytes. Disabled: one branch, no events.
+#pragma once
+#include <hip/hip_runtime.h>
+
+struct encx_prof_scope {
+    hipStream_t st;
+    int slot;
+    encx_prof_scope(hipStream_t s, double flops, double bytes);
+    ~encx_prof_scope();
+};

@@ -1,0 +1,404 @@
+// Residual vector quantizer kernels (quantization/core_vq.py).
+//
+//  rvq_argmin_mfma  EuclideanCodebook.quantize (core_vq.py:181-189). A 64-frame x 256-code tile
+//                   of dot products on v_mfma_f32_32x32x2_f32, then per element the reference's
+//                   own fp32 expression v = (|x|^2 - 2 x.e) + |e|^2, packed into an order-
+//                   preserving 64-bit key (dist bits << 32 | code) so that a wave min-reduction
+//                   and one 64-bit atomicMin per frame give argmin with FIRST-index tie break
+//                   exactly like torch.max(dim=-1) on -v. Integer atomics: order-independent.
+//  rvq_argmin_direct kmeans' direct form -sum_d (x-e)^2 (core_vq.py:86-91), VALU.
+//  rvq_apply        STE / residual / output / commit-loss pieces of one layer (:301-324,:346-349)
+//  bucket_sum       per-code counts and sums of the assigned frames, one wave per code, frames
+//                   visited in ascending order (deterministic), used by the EMA update (:227-235)
+//                   and by kmeans (:92-100).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+struct Rows {  // x_n[d] = p[b*sB + t*sT + d*sD], n = b*Tf + t
+    const float* p;
+    int64_t sB, sT, sD;
+    int Tf;
+    ENCX_DEV float at(int n, int d) const {
+        int b = n / Tf, t = n - b * Tf;
+        return p[b * sB + t * sT + d * sD];
+    }
+};
+
+ENCX_DEV uint32_t ord_key(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+ENCX_DEV uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+ENCX_DEV uint64_t shfl_xor64(uint64_t v, int o) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = __shfl_xor(lo, o, 64);
+    hi = __shfl_xor(hi, o, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+constexpr int AR_ROWS = 64, AR_CODES = 256, AR_DC = 32;
+
+__global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed, uint64_t* keys,
+                                                      int N, int D, int Kc) {
+    __shared__ float As[AR_DC][AR_ROWS];
+    __shared__ float Bs[AR_DC][AR_CODES + 1];
+    __shared__ float xx[AR_ROWS], ee[AR_CODES];
+    __shared__ uint64_t part[4][AR_ROWS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n0 = blockIdx.x * AR_ROWS, k0 = blockIdx.y * AR_CODES;
+    const int h = lane >> 5, l32 = lane & 31;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+    float xs = 0.f, es = 0.f;  // running |x|^2 (tid < 64) and |e|^2 (all tids), ascending d
+    for (int d0 = 0; d0 < D; d0 += AR_DC) {
+        __syncthreads();
+        for (int i = tid; i < AR_DC * AR_ROWS; i += NT) {
+            int r = i / AR_DC, dd = i - r * AR_DC;  // d fastest: contiguous for [N][D] rows
+            int n = n0 + r, d = d0 + dd;
+            As[dd][r] = (n < N && d < D) ? x.at(n, d) : 0.f;
+        }
+        for (int i = tid; i < AR_DC * AR_CODES; i += NT) {
+            int c = i / AR_DC, dd = i - c * AR_DC;
+            int k = k0 + c, d = d0 + dd;
+            Bs[dd][c] = (k < Kc && d < D) ? embed[(int64_t)k * D + d] : 0.f;
+        }
+        __syncthreads();
+        if (tid < AR_ROWS)
+            for (int dd = 0; dd < AR_DC; ++dd) xs = fmaf(As[dd][tid], As[dd][tid], xs);
+        for (int dd = 0; dd < AR_DC; ++dd) es = fmaf(Bs[dd][tid], Bs[dd][tid], es);
+        for (int dp = 0; dp < AR_DC; dp += 2) {
+            float av[2], bv[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) av[i] = As[dp + h][i * 32 + l32];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bv[j] = Bs[dp + h][wave * 64 + j * 32 + l32];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+        }
+    }
+    if (tid < AR_ROWS) xx[tid] = xs;
+    ee[tid] = es;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = i * 32 + mfma_row(r, lane);
+            uint64_t best = ~0ull;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int c = wave * 64 + j * 32 + l32;
+                const int k = k0 + c;
+                if (k < Kc) {
+                    float v = (xx[row] - 2.f * acc[i][j][r]) + ee[c];
+                    uint64_t key = ((uint64_t)ord_key(v) << 32) | (uint32_t)k;
+                    best = umin64(best, key);
+                }
+            }
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) best = umin64(best, shfl_xor64(best, o));
+            if (l32 == 0) part[wave][row] = best;
+        }
+    }
+    __syncthreads();
+    if (tid < AR_ROWS && n0 + tid < N) {
+        uint64_t b = umin64(umin64(part[0][tid], part[1][tid]), umin64(part[2][tid], part[3][tid]));
+        atomicMin((unsigned long long*)&keys[n0 + tid], (unsigned long long)b);
+    }
+}
+
+constexpr int DR_ROWS = 32;
+
+__global__ __launch_bounds__(NT) void rvq_argmin_direct(Rows x, const float* embed, uint64_t* keys,
+                                                        int N, int D, int Kc) {
+    extern __shared__ float sm[];
+    float* es = sm;                        // [256][D+1]
+    float* xs = sm + NT * (D + 1);         // [DR_ROWS][D]
+    __shared__ uint64_t part[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n0 = blockIdx.x * DR_ROWS, k = blockIdx.y * NT + tid;
+    for (int i = tid; i < NT * D; i += NT) {
+        int c = i / D, d = i - c * D, kk = blockIdx.y * NT + c;
+        es[c * (D + 1) + d] = kk < Kc ? embed[(int64_t)kk * D + d] : 0.f;
+    }
+    for (int i = tid; i < DR_ROWS * D; i += NT) {
+        int r = i / D, d = i - r * D;
+        xs[i] = (n0 + r < N) ? x.at(n0 + r, d) : 0.f;
+    }
+    __syncthreads();
+    for (int r = 0; r < DR_ROWS; ++r) {
+        float s = 0.f;
+        for (int d = 0; d < D; ++d) {
+            float df = xs[r * D + d] - es[tid * (D + 1) + d];
+            s = fmaf(df, df, s);
+        }
+        uint64_t key = k < Kc ? (((uint64_t)ord_key(s) << 32) | (uint32_t)k) : ~0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) key = umin64(key, shfl_xor64(key, o));
+        if (lane == 0) part[wave] = key;
+        __syncthreads();
+        if (tid == 0 && n0 + r < N) {
+            uint64_t b = umin64(umin64(part[0], part[1]), umin64(part[2], part[3]));
+            atomicMin((unsigned long long*)&keys[n0 + r], (unsigned long long)b);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void keys_to_idx(const uint64_t* keys, int64_t* idx, int N) {
+    int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n < N) idx[n] = (int64_t)(uint32_t)(keys[n] & 0xffffffffull);
+}
+
+__global__ void fill_u64(uint64_t* p, uint64_t v, int N) {
+    int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n < N) p[n] = v;
+}
+
+constexpr int AP_MAXB = 1024;
+
+// one train-mode VQ layer after its argmin; x = res (layer input)
+__global__ __launch_bounds__(NT) void rvq_apply_kernel(const float* xin, float* res,
+                                                       const float* embed, const int64_t* idx,
+                                                       float* out, float* cdir, float* parts, int D,
+                                                       int Tf, int64_t total, int first, int ste) {
+    __shared__ float red[16];
+    float s = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+        int64_t bd = i / Tf;
+        int t = (int)(i - bd * Tf);
+        int64_t b = bd / D;
+        int d = (int)(bd - b * D);
+        const int64_t k = idx[b * Tf + t];
+        const float x = xin[i];
+        const float q = embed[k * D + d];
+        const float qs = ste ? x + (q - x) : q;  // core_vq.py:309 (train) / exact q (eval encode)
+        res[i] = x - qs;                          // :348 residual - quantized.detach()
+        if (out) out[i] = first ? qs : out[i] + qs;
+        if (cdir) cdir[i] = first ? (x - qs) : cdir[i] + (x - qs);
+        const float df = qs - x;
+        s = fmaf(df, df, s);
+    }
+    s = block_sum(s, red);
+    if (parts && threadIdx.x == 0) parts[blockIdx.x] = s;
+}
+
+// ResidualVectorQuantization.decode (core_vq.py:369-375): out (+)= embed[idx] in [B][D][Tf]
+__global__ void rvq_gather_kernel(const float* embed, const int64_t* idx, float* out, int D, int Tf,
+                                  int64_t total, int acc) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    int64_t bd = i / Tf;
+    int t = (int)(i - bd * Tf);
+    int64_t b = bd / D;
+    int d = (int)(bd - b * D);
+    float q = embed[idx[b * Tf + t] * D + d];
+    out[i] = acc ? out[i] + q : q;
+}
+
+// wave per code: counts and sums over the frames assigned to it, ascending frame order
+template <int MODE>  // 0: EMA (core_vq.py:227-229), 1: kmeans (:92-100)
+__global__ __launch_bounds__(NT) void bucket_kernel(Rows x, const int64_t* idx, int N, int D, int Kc,
+                                                    float* cs, float* ea, float* means,
+                                                    int64_t* bins, float decay, float one_m) {
+    const int lane = threadIdx.x & 63, c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= Kc) return;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // D <= 256
+    int count = 0;
+    for (int n0 = 0; n0 < N; n0 += 64) {
+        const int n = n0 + lane;
+        const bool m = n < N && idx[n] == c;
+        uint64_t mask = __ballot(m);
+        while (mask) {
+            const int j = __ffsll((long long)mask) - 1;
+            mask &= mask - 1;
+            const int nn = n0 + j;
+#pragma unroll
+            for (int z = 0; z < 4; ++z) {
+                int d = lane + 64 * z;
+                if (d < D) acc[z] += x.at(nn, d);
+            }
+            ++count;
+        }
+    }
+    if (MODE == 0) {
+        if (lane == 0) cs[c] = fmaf((float)count, one_m, cs[c] * decay);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+            int d = lane + 64 * z;
+            if (d < D) {
+                float* p = ea + (int64_t)c * D + d;
+                *p = fmaf(acc[z], one_m, *p * decay);
+            }
+        }
+    } else {
+        if (lane == 0) bins[c] = count;
+        if (count > 0) {
+#pragma unroll
+            for (int z = 0; z < 4; ++z) {
+                int d = lane + 64 * z;
+                if (d < D) means[(int64_t)c * D + d] = acc[z] / (float)count;
+            }
+        }
+    }
+}
+
+// embed = embed_avg / (laplace(cluster_size) * sum(cluster_size)), core_vq.py:230-235
+__global__ void ema_normalize(const float* cs, const float* ea, float* embed, int D, int Kc,
+                              float eps, float keps) {
+    __shared__ float red[16];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < Kc; i += blockDim.x) s += cs[i];
+    s = block_sum(s, red);
+    const int c = blockIdx.x;
+    const float sm = (cs[c] + eps) / (s + keps) * s;
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+        embed[(int64_t)c * D + d] = ea[(int64_t)c * D + d] / sm;
+}
+
+ENCX_DEV uint64_t splitmix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// randperm(N)[:num] by rank of random keys (ties by index), or randint when num > N
+__global__ __launch_bounds__(NT) void sample_rows_kernel(const float* samples, float* out, int N,
+                                                         int D, int num, uint64_t seed) {
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (num > N) {  // core_vq.py:74-75 randint
+        if (i >= num) return;
+        int src = (int)(splitmix(seed ^ (0xA24BAED4963EE407ull * (uint64_t)(i + 1))) % (uint64_t)N);
+        for (int d = 0; d < D; ++d) out[(int64_t)i * D + d] = samples[(int64_t)src * D + d];
+        return;
+    }
+    if (i >= N) return;
+    const uint64_t ki = splitmix(seed + (uint64_t)i);
+    int rank = 0;
+    for (int j = 0; j < N; ++j) {
+        uint64_t kj = splitmix(seed + (uint64_t)j);
+        rank += (kj < ki) || (kj == ki && j < i);
+    }
+    if (rank < num)
+        for (int d = 0; d < D; ++d) out[(int64_t)rank * D + d] = samples[(int64_t)i * D + d];
+}
+
+Rows bdt_rows(const float* p, int64_t B, int64_t D, int64_t Tf) {
+    Rows r;
+    r.p = p; r.sB = D * Tf; r.sT = 1; r.sD = Tf; r.Tf = (int)Tf;
+    return r;
+}
+Rows nd_rows(const float* p, int64_t N, int64_t D) {
+    Rows r;
+    r.p = p; r.sB = 0; r.sT = D; r.sD = 1; r.Tf = (int)N;
+    return r;
+}
+
+int argmin_run(Rows x, const float* embed, int64_t* idx, uint64_t* keys, int N, int D, int Kc,
+               int direct, hipStream_t st) {
+    hipLaunchKernelGGL(fill_u64, dim3(cdiv(N, 256)), dim3(256), 0, st, keys, ~0ull, N);
+    if (!direct) {
+        hipLaunchKernelGGL(rvq_argmin_mfma, dim3(cdiv(N, AR_ROWS), cdiv(Kc, AR_CODES)), dim3(NT), 0,
+                           st, x, embed, keys, N, D, Kc);
+    } else {
+        size_t lds = (size_t)(NT * (D + 1) + DR_ROWS * D) * sizeof(float);
+        if (lds > 160 * 1024) return ENCX_EINVAL;
+        hipLaunchKernelGGL(rvq_argmin_direct, dim3(cdiv(N, DR_ROWS), cdiv(Kc, NT)), dim3(NT), lds, st,
+                           x, embed, keys, N, D, Kc);
+    }
+    ENCX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(keys_to_idx, dim3(cdiv(N, 256)), dim3(256), 0, st, keys, idx, N);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int encx_rvq_argmin(const float* res, const float* embed, int64_t* idx, uint64_t* keys,
+                    int64_t B, int64_t D, int64_t Tf, int64_t Kc, int direct,
+                    encx_stream_t stream) {
+    ENCX_REQUIRE(res && embed && idx && keys && B > 0 && D > 0 && D <= 256 && Tf > 0 && Kc > 0);
+    return argmin_run(bdt_rows(res, B, D, Tf), embed, idx, keys, (int)(B * Tf), (int)D, (int)Kc,
+                      direct, (hipStream_t)stream);
+}
+
+int64_t encx_rvq_apply_parts(int64_t B, int64_t D, int64_t Tf) {
+    int64_t total = B * D * Tf;
+    int64_t b = cdiv(total, NT);
+    return b < AP_MAXB ? b : AP_MAXB;
+}
+
+int encx_rvq_apply(const float* x, float* res_out, const float* embed, const int64_t* idx,
+                   float* out, float* commit_dir, float* commit_part, int64_t B, int64_t D,
+                   int64_t Tf, int first, int ste, encx_stream_t stream) {
+    ENCX_REQUIRE(x && res_out && embed && idx && B > 0 && D > 0 && Tf > 0);
+    int64_t total = B * D * Tf;
+    hipLaunchKernelGGL(rvq_apply_kernel, dim3(encx_rvq_apply_parts(B, D, Tf)), dim3(NT), 0,
+                       (hipStream_t)stream, x, res_out, embed, idx, out, commit_dir, commit_part,
+                       (int)D, (int)Tf, total, first, ste);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_rvq_gather(const float* embed, const int64_t* idx, float* out, int64_t B, int64_t D,
+                    int64_t Tf, int accumulate, encx_stream_t stream) {
+    ENCX_REQUIRE(embed && idx && out && B > 0 && D > 0 && Tf > 0);
+    int64_t total = B * D * Tf;
+    hipLaunchKernelGGL(rvq_gather_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                       embed, idx, out, (int)D, (int)Tf, total, accumulate);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float* embed_avg,
+                 float* embed, int64_t B, int64_t D, int64_t Tf, int64_t Kc, float decay,
+                 float eps, encx_stream_t stream) {
+    ENCX_REQUIRE(x && idx && cluster_size && embed_avg && embed && D <= 256 && Kc > 0);
+    hipStream_t st = (hipStream_t)stream;
+    const float one_m = (float)(1.0 - (double)decay);
+    hipLaunchKernelGGL(bucket_kernel<0>, dim3(cdiv(Kc, 4)), dim3(NT), 0, st, bdt_rows(x, B, D, Tf),
+                       idx, (int)(B * Tf), (int)D, (int)Kc, cluster_size, embed_avg, nullptr, nullptr,
+                       decay, one_m);
+    ENCX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(ema_normalize, dim3(Kc), dim3(D < 64 ? 64 : (D > 256 ? 256 : D)), 0, st,
+                       cluster_size, embed_avg, embed, (int)D, (int)Kc, eps,
+                       (float)((double)Kc * (double)eps));
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_kmeans_step(const float* samples, float* means, int64_t* bins, int64_t* idx,
+                     uint64_t* keys, int64_t N, int64_t D, int64_t Kc, encx_stream_t stream) {
+    ENCX_REQUIRE(samples && means && bins && idx && keys && N > 0 && D > 0 && D <= 256 && Kc > 0);
+    hipStream_t st = (hipStream_t)stream;
+    Rows r = nd_rows(samples, N, D);
+    int rc = argmin_run(r, means, idx, keys, (int)N, (int)D, (int)Kc, 1, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(bucket_kernel<1>, dim3(cdiv(Kc, 4)), dim3(NT), 0, st, r, idx, (int)N, (int)D,
+                       (int)Kc, nullptr, nullptr, means, bins, 0.f, 0.f);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_sample_rows(const float* samples, float* out, int64_t N, int64_t D, int64_t num,
+                     uint64_t seed, encx_stream_t stream) {
+    ENCX_REQUIRE(samples && out && N > 0 && D > 0 && num > 0);
+    int64_t threads = num > N ? num : N;
+    hipLaunchKernelGGL(sample_rows_kernel, dim3(cdiv(threads, NT)), dim3(NT), 0, (hipStream_t)stream,
+                       samples, out, (int)N, (int)D, (int)num, seed);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

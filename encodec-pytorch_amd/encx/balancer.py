@@ -1,0 +1,94 @@
+"""Loss balancer (balancer.py of the reference) with its statistics kept on the device.
+
+Per-item gradient norms, the EMA `averager` (fp64, like the reference's Python floats), the
+cross-rank `average_metrics` all-reduce and the rescaled gradient sum all run as encx kernels
+(and one RCCL all-reduce of nl+1 floats), so the balancer adds no host synchronisation.
+"""
+import torch
+from torch import autograd
+
+from . import distrib
+from ._lib import call, ptr, stream, lib
+
+
+class Balancer:
+    """balancer.py:31-118."""
+
+    def __init__(self, weights, rescale_grads: bool = True, total_norm: float = 1.,
+                 ema_decay: float = 0.999, per_batch_item: bool = True, epsilon: float = 1e-12,
+                 monitor: bool = False):
+        if len(weights) > 4:
+            raise NotImplementedError('encx Balancer combines up to 4 losses')
+        self.weights = weights
+        self.per_batch_item = per_batch_item
+        self.total_norm = total_norm
+        self.beta = ema_decay
+        self.epsilon = epsilon
+        self.monitor = monitor
+        self.rescale_grads = rescale_grads
+        self._metrics = {}
+        self._state = None
+
+    @property
+    def metrics(self):
+        return self._metrics
+
+    def _buffers(self, names, device):
+        if self._state is None or self._state['names'] != names:
+            nl = len(names)
+            tw = sum(self.weights[k] for k in names)
+            self._state = {
+                'names': names,
+                'total': torch.zeros(nl, device=device, dtype=torch.float64),
+                'fix': torch.zeros(nl, device=device, dtype=torch.float64),
+                'avg': torch.zeros(nl, device=device, dtype=torch.float64),
+                'red': torch.zeros(nl + 1, device=device, dtype=torch.float32),
+                'ratio': torch.tensor([self.weights[k] / tw for k in names], device=device,
+                                      dtype=torch.float64),
+                'plain': torch.tensor([float(self.weights[k]) for k in names], device=device,
+                                      dtype=torch.float32),
+                'norms': torch.zeros(nl, device=device, dtype=torch.float32),
+                'scales': torch.zeros(nl, device=device, dtype=torch.float32),
+            }
+        return self._state
+
+    def combine(self, grads):
+        """grads: ordered dict name -> d loss / d input. Returns the out_grad of :110-118."""
+        names = tuple(grads)
+        g0 = next(iter(grads.values()))
+        st = self._buffers(names, g0.device)
+        s = stream()
+        gl = [g.contiguous() for g in grads.values()]
+        if self.rescale_grads:
+            B = g0.shape[0] if self.per_batch_item else 1
+            L = g0.numel() // B
+            ws = torch.empty(lib.encx_item_norm_workspace(B) // 4, device=g0.device, dtype=torch.float32)
+            for i, g in enumerate(gl):
+                call('encx_item_norm_mean', ptr(g), ptr(st['norms'][i:i + 1]), ptr(ws), B, L, s)
+            call('encx_balancer_update', ptr(st['norms']), ptr(st['total']), ptr(st['fix']),
+                 ptr(st['avg']), ptr(st['red']), len(names), float(self.beta), float(B), s)
+            dist = distrib.is_distributed()
+            if dist:  # average_metrics (distrib.py:112-124)
+                torch.distributed.all_reduce(st['red'])
+            call('encx_balancer_scales', ptr(st['avg']), ptr(st['red']), ptr(st['ratio']),
+                 ptr(st['scales']), len(names), float(self.total_norm), float(self.epsilon), int(dist), s)
+            scales = st['scales']
+        else:
+            scales = st['plain']
+        out = torch.empty_like(gl[0])
+        gp = [ptr(g) for g in gl] + [None] * (4 - len(gl))
+        call('encx_balancer_combine', gp[0], gp[1], gp[2], gp[3], ptr(scales), ptr(out), out.numel(), s)
+        if self.monitor:
+            avg = st['avg'].tolist()
+            tot = sum(avg)
+            self._metrics = {f'ratio_{k}': v / tot for k, v in zip(names, avg)}
+        return out
+
+    def compute(self, losses, input):
+        grads = {}
+        for name, loss in losses.items():
+            grads[name], = autograd.grad(loss, [input], retain_graph=True)
+        return self.combine(grads)
+
+    def backward(self, losses, input, retain_graph=False):
+        input.backward(self.compute(losses, input), retain_graph=retain_graph)

@@ -1,0 +1,424 @@
+"""Autograd ops over the libencx C ABI. Every op runs the HIP kernels; none has a CPU path.
+
+Each Function below replaces the device work of one reference module (file:line in the
+docstrings); the nn.Module mirrors in encx.modules / encx.quantization / encx.losses call these.
+"""
+import math
+
+import numpy as np
+import torch
+
+from ._lib import (call, ptr, stream, lib, ensure_device, ENCX_PAD_ZERO, ENCX_PAD_REFLECT,
+                   ENCX_ACT_NONE, ENCX_ACT_ELU)
+
+ACT = {None: ENCX_ACT_NONE, 'none': ENCX_ACT_NONE, 'elu': ENCX_ACT_ELU}
+PAD = {'reflect': ENCX_PAD_REFLECT, 'zero': ENCX_PAD_ZERO, 'constant': ENCX_PAD_ZERO}
+
+
+def _f32(n, like):
+    return torch.empty(int(n), device=like.device, dtype=torch.float32)
+
+
+def _check(x, name='x'):
+    if not x.is_cuda or x.dtype != torch.float32:
+        raise RuntimeError(f'encx: {name} must be a float32 tensor on the GPU '
+                           f'(got {x.dtype} on {x.device}); the HIP path has no CPU fallback')
+    ensure_device(x.device)
+
+
+# ---------------------------------------------------------------------------- geometry
+def extra_padding_for_conv1d(length, kernel_size, stride, padding_total=0):
+    """modules/conv.py:54-61."""
+    n_frames = (length - kernel_size + padding_total) / stride + 1
+    ideal_length = (math.ceil(n_frames) - 1) * stride + (kernel_size - padding_total)
+    return ideal_length - length
+
+
+def conv_geometry(T, K, s, d, causal, pad_mode='reflect'):
+    """SConv1d.forward's padding (modules/conv.py:195-209) + pad1d's short-input zero
+    extension (:86-91). Returns (pad_left, pad_right, short_ext, T_out)."""
+    pt = (K - 1) * d - (s - 1)
+    extra = extra_padding_for_conv1d(T, K, s, pt)
+    if causal:
+        pl, pr = pt, extra
+    else:
+        r = pt // 2
+        pl, pr = pt - r, r + extra
+    e = 0
+    if pad_mode == 'reflect' and T <= max(pl, pr):
+        e = max(pl, pr) - T + 1
+    tout = (pl + T + pr - (K - 1) * d - 1) // s + 1
+    return pl, pr, e, tout
+
+
+def convtr_geometry(T, K, s, causal, trim_right_ratio=1.0):
+    """SConvTranspose1d.forward trimming (modules/conv.py:230-252) -> (trim_left, T_out)."""
+    pt = K - s
+    if causal:
+        pr = math.ceil(pt * trim_right_ratio)
+        pl = pt - pr
+    else:
+        pr = pt // 2
+        pl = pt - pr
+    return pl, (T - 1) * s + K - pl - pr
+
+
+def _weight_prep(v, g, K, s, want_f, want_p):
+    """w = v*(g/||v||) (weight_norm, conv.py:25-34) written in the kernels' operand layouts."""
+    A0, A1 = v.shape[0], v.shape[1]
+    J = -(-K // s)
+    wf = _f32(A1 * K * A0, v) if want_f else None
+    wp = _f32(A0 * J * A1 * s, v) if want_p else None
+    call('encx_weightnorm_fwd', ptr(v), ptr(g), ptr(wf), ptr(wp), A0, A1, K, s, stream())
+    return wf, wp
+
+
+def _weight_bwd(v, g, dw):
+    if g is None:
+        return dw.view_as(v), None
+    dv = torch.empty_like(v)
+    dg = torch.empty_like(g)
+    call('encx_weightnorm_bwd', ptr(v), ptr(g), ptr(dw), ptr(dv), ptr(dg), v.shape[0],
+         v[0].numel(), 0, stream())
+    return dv, dg
+
+
+# ---------------------------------------------------------------------------- Conv1d
+class Conv1dFn(torch.autograd.Function):
+    """SConv1d.forward (modules/conv.py:195-210) incl. weight_norm and a fused pre-ELU."""
+
+    @staticmethod
+    def forward(ctx, x, v, g, b, res, K, s, d, causal, pad_mode, act):
+        _check(x)
+        x = x.contiguous()
+        B, Cin, T = x.shape
+        Cout = v.shape[0]
+        pl, pr, e, tout = conv_geometry(T, K, s, d, causal, pad_mode)
+        need_dx = ctx.needs_input_grad[0]
+        if need_dx and d != 1:
+            raise NotImplementedError('encx: backward-data of dilated Conv1d (EnCodec uses d=1)')
+        wf, wp = _weight_prep(v, g, K, s, True, need_dx)
+        y = torch.empty(B, Cout, tout, device=x.device, dtype=torch.float32)
+        if res is not None:
+            res = res.contiguous()
+            assert res.shape == y.shape
+        call('encx_conv1d_fwd', ptr(x), ptr(wf), ptr(b), ptr(res), ptr(y), B, Cin, T, Cout, tout, K,
+             s, d, pl, e, PAD[pad_mode], ACT[act], stream())
+        ctx.save_for_backward(x, v, g, wp)
+        ctx.cfg = (K, s, d, pl, pr, e, tout, PAD[pad_mode], ACT[act], res is not None, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, v, g, wp = ctx.saved_tensors
+        K, s, d, pl, pr, e, tout, mode, act, has_res, has_b = ctx.cfg
+        dy = dy.contiguous()
+        B, Cin, T = x.shape
+        Cout = v.shape[0]
+        st = stream()
+        dx = dv = dg = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            side = _f32(lib.encx_conv1d_bwd_data_workspace(B, Cin, pl, pr) // 4, x)
+            call('encx_conv1d_bwd_data', ptr(dy), ptr(wp), ptr(x), ptr(dx), ptr(side), B, Cin, T,
+                 Cout, tout, K, s, pl, pr, e, mode, act, 0, st)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
+            dw = torch.empty(Cout, Cin, K, device=x.device, dtype=torch.float32)
+            db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_b else None
+            ws = _f32(lib.encx_conv1d_bwd_weight_workspace(B, Cin, Cout, tout, K) // 4 + 1, x)
+            call('encx_conv1d_bwd_weight', ptr(dy), ptr(x), ptr(dw), ptr(db), ptr(ws), B, Cin, T,
+                 Cout, tout, K, s, d, pl, e, mode, act, 0, st)
+            dv, dg = _weight_bwd(v, g, dw)
+        return dx, dv, dg, db, (dy if has_res else None), None, None, None, None, None, None
+
+
+def conv1d(x, v, g, b, K, stride=1, dilation=1, causal=True, pad_mode='reflect', act=None, res=None):
+    return Conv1dFn.apply(x, v, g, b, res, K, stride, dilation, causal, pad_mode, act)
+
+
+# ---------------------------------------------------------------------------- ConvTranspose1d
+class ConvTr1dFn(torch.autograd.Function):
+    """SConvTranspose1d.forward (modules/conv.py:230-252) incl. weight_norm (dim 0 = in
+    channels, conv.py:149) and a fused pre-ELU."""
+
+    @staticmethod
+    def forward(ctx, x, v, g, b, K, s, causal, trim_right_ratio, act):
+        _check(x)
+        x = x.contiguous()
+        B, Cin, T = x.shape
+        Cout = v.shape[1]
+        trim_left, tout = convtr_geometry(T, K, s, causal, trim_right_ratio)
+        need_dx = ctx.needs_input_grad[0]
+        wf, wp = _weight_prep(v, g, K, s, need_dx, True)
+        y = torch.empty(B, Cout, tout, device=x.device, dtype=torch.float32)
+        call('encx_convtr1d_fwd', ptr(x), ptr(wp), ptr(b), ptr(y), B, Cin, T, Cout, tout, K, s,
+             trim_left, ACT[act], stream())
+        ctx.save_for_backward(x, v, g, wf)
+        ctx.cfg = (K, s, trim_left, tout, ACT[act], b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, v, g, wf = ctx.saved_tensors
+        K, s, trim_left, tout, act, has_b = ctx.cfg
+        dy = dy.contiguous()
+        B, Cin, T = x.shape
+        Cout = v.shape[1]
+        st = stream()
+        dx = dv = dg = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            call('encx_convtr1d_bwd_data', ptr(dy), ptr(wf), ptr(x), ptr(dx), B, Cin, T, Cout, tout,
+                 K, s, trim_left, act, 0, st)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
+            dw = torch.empty(Cin, Cout, K, device=x.device, dtype=torch.float32)
+            db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_b else None
+            ws = _f32(lib.encx_convtr1d_bwd_weight_workspace(B, Cin, Cout, T, K) // 4 + 1, x)
+            call('encx_convtr1d_bwd_weight', ptr(x), ptr(dy), ptr(dw), ptr(db), ptr(ws), B, Cin, T,
+                 Cout, tout, K, s, trim_left, act, 0, st)
+            dv, dg = _weight_bwd(v, g, dw)
+        return dx, dv, dg, db, None, None, None, None, None
+
+
+def convtr1d(x, v, g, b, K, stride, causal=True, trim_right_ratio=1.0, act=None):
+    return ConvTr1dFn.apply(x, v, g, b, K, stride, causal, trim_right_ratio, act)
+
+
+# ---------------------------------------------------------------------------- normalisation
+def normalize(x):
+    """model.py:152-157 -> (x / scale, scale [B,1]). The input wave never needs a grad."""
+    _check(x)
+    x = x.contiguous()
+    B, C, T = x.shape
+    xn = torch.empty_like(x)
+    scale = torch.empty(B, device=x.device, dtype=torch.float32)
+    call('encx_normalize_fwd', ptr(x), ptr(xn), ptr(scale), B, C, T, stream())
+    return xn, scale.view(-1, 1)
+
+
+class ScaleRowsFn(torch.autograd.Function):
+    """out * scale.view(-1, 1, 1) (model.py:191-192); scale carries no grad."""
+
+    @staticmethod
+    def forward(ctx, x, scale):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        call('encx_scale_rows', ptr(x), ptr(scale), ptr(y), x.shape[0], x[0].numel(), stream())
+        ctx.save_for_backward(scale)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        scale, = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        call('encx_scale_rows', ptr(dy), ptr(scale), ptr(dx), dy.shape[0], dy[0].numel(), stream())
+        return dx, None
+
+
+# ---------------------------------------------------------------------------- losses
+class L1LossFn(torch.autograd.Function):
+    """losses.py:37 l_t = L1Loss(input_wav, output_wav); grad w.r.t. the output only."""
+
+    @staticmethod
+    def forward(ctx, x, y):
+        _check(y, 'output')
+        x, y = x.contiguous(), y.contiguous()
+        loss = torch.empty(1, device=y.device, dtype=torch.float32)
+        grad = torch.empty_like(y) if ctx.needs_input_grad[1] else None
+        ws = _f32(1024, y)
+        call('encx_l1_loss', ptr(x), ptr(y), ptr(loss), ptr(grad), ptr(ws), y.numel(), stream())
+        ctx.save_for_backward(grad)
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        grad, = ctx.saved_tensors
+        out = torch.empty_like(grad)
+        call('encx_axpby', ptr(grad), ptr(out), grad.numel(), 1.0, ptr(g.contiguous().view(1)), 0.0,
+             stream())
+        return None, out
+
+
+_MEL_CACHE = {}
+
+
+def mel_tables(device, n_fft, n_mels, sr):
+    """Device DFT (window*cos / -window*sin) + mel-basis tables for one scale, built once."""
+    key = (str(device), n_fft, n_mels, sr)
+    t = _MEL_CACHE.get(key)
+    if t is None:
+        from .audio_to_mel import mel_filterbank
+        basis = torch.from_numpy(mel_filterbank(sr, n_fft, n_mels)).to(device)
+        t = torch.empty(lib.encx_mel_tables_floats(n_fft, n_mels), device=device, dtype=torch.float32)
+        call('encx_mel_tables_init', ptr(t), ptr(basis), n_fft, n_mels, stream())
+        _MEL_CACHE[key] = (t, basis)
+        t = _MEL_CACHE[key]
+    return t[0]
+
+
+class MelLossFn(torch.autograd.Function):
+    """l_f of total_loss (losses.py:40-42): sum over n_fft = 2^5..2^11 (hop n/4, 64 mels) of
+    L1 + MSE between Audio2Mel(x) and Audio2Mel(y) (audio_to_mel.py:34-55). The gradient
+    w.r.t. y is produced by the same pass (the balancer always asks for it)."""
+
+    @staticmethod
+    def forward(ctx, x, y, sr, n_mels, scales):
+        _check(y, 'output')
+        x, y = x.contiguous(), y.contiguous()
+        B = y.shape[0] * y.shape[1]
+        T = y.shape[-1]
+        loss = torch.zeros(1, device=y.device, dtype=torch.float32)
+        grad = torch.zeros_like(y) if ctx.needs_input_grad[1] else None
+        wsn = max(lib.encx_mel_workspace_floats(B, T, n, n_mels) for n in scales)
+        ws = _f32(wsn, y)
+        for n in scales:
+            tab = mel_tables(y.device, n, n_mels, sr)
+            call('encx_mel_loss', ptr(x), ptr(y), ptr(tab), ptr(ws), ptr(loss), ptr(grad), B, T, n,
+                 n_mels, stream())
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        grad, = ctx.saved_tensors
+        out = torch.empty_like(grad)
+        call('encx_axpby', ptr(grad), ptr(out), grad.numel(), 1.0, ptr(g.contiguous().view(1)), 0.0,
+             stream())
+        return None, out, None, None, None
+
+
+def logmel(x, n_fft, n_mels, sr):
+    """Audio2Mel.forward (audio_to_mel.py:34-55) -> [B, C, n_mels * F]."""
+    _check(x)
+    x = x.contiguous()
+    shape = x.shape
+    B = shape[0] * (shape[1] if x.dim() > 2 else 1)
+    T = shape[-1]
+    F = lib.encx_mel_frames(T, n_fft)
+    out = torch.empty(B, n_mels, F, device=x.device, dtype=torch.float32)
+    ws = _f32(lib.encx_mel_workspace_floats(B, T, n_fft, n_mels), x)
+    call('encx_mel_logmel', ptr(x), ptr(mel_tables(x.device, n_fft, n_mels, sr)), ptr(ws), ptr(out),
+         B, T, n_fft, n_mels, stream())
+    if x.dim() > 2:
+        return out.reshape(shape[0], shape[1], -1)
+    return out
+
+
+# ---------------------------------------------------------------------------- RVQ
+def rvq_argmin(res, embed, direct=False):
+    """EuclideanCodebook.quantize (core_vq.py:181-189) over res [B, D, T] -> int64 [B*T]."""
+    B, D, T = res.shape
+    N = B * T
+    idx = torch.empty(N, device=res.device, dtype=torch.int64)
+    keys = torch.empty(N, device=res.device, dtype=torch.int64)
+    call('encx_rvq_argmin', ptr(res), ptr(embed), ptr(idx), ptr(keys), B, D, T, embed.shape[0],
+         int(direct), stream())
+    return idx
+
+
+def kmeans(samples, num_clusters, num_iters, seed):
+    """kmeans (core_vq.py:80-102) on the device: samples [N, D] -> (means, bins)."""
+    N, D = samples.shape
+    means = torch.empty(num_clusters, D, device=samples.device, dtype=torch.float32)
+    call('encx_sample_rows', ptr(samples), ptr(means), N, D, num_clusters, seed & (2 ** 64 - 1), stream())
+    bins = torch.zeros(num_clusters, device=samples.device, dtype=torch.int64)
+    idx = torch.empty(N, device=samples.device, dtype=torch.int64)
+    keys = torch.empty(N, device=samples.device, dtype=torch.int64)
+    for _ in range(num_iters):
+        call('encx_kmeans_step', ptr(samples), ptr(means), ptr(bins), ptr(idx), ptr(keys), N, D,
+             num_clusters, stream())
+    return means, bins
+
+
+def rvq_to_rows(res):
+    B, D, T = res.shape
+    out = torch.empty(B * T, D, device=res.device, dtype=torch.float32)
+    call('encx_bdt_to_nd', ptr(res), ptr(out), B, D, T, stream())
+    return out
+
+
+class RVQTrainFn(torch.autograd.Function):
+    """ResidualVectorQuantization.forward in train mode (core_vq.py:337-355) over
+    VectorQuantization.forward (:301-324) + the EMA codebook update (:212-237), one fused
+    pass per layer. Returns (quantized [B,D,T], codes [n_q,B,T], penalty [1]).
+    Backward: d emb = n_q * d quantized + d penalty * 2/(n_q*numel) * sum_i (x_i - q_ste_i)
+    (per-layer straight-through, Appendix A quirk 1)."""
+
+    @staticmethod
+    def forward(ctx, emb, codebooks, decay, eps):
+        _check(emb, 'emb')
+        emb = emb.contiguous()
+        B, D, T = emb.shape
+        n_q = len(codebooks)
+        numel = emb.numel()
+        st = stream()
+        res = [emb.clone(), torch.empty_like(emb)]
+        out = torch.empty_like(emb)
+        cdir = torch.empty_like(emb)
+        P = lib.encx_rvq_apply_parts(B, D, T)
+        parts = torch.empty(n_q, P, device=emb.device, dtype=torch.float32)
+        commits = torch.empty(n_q, device=emb.device, dtype=torch.float32)
+        codes = torch.empty(n_q, B * T, device=emb.device, dtype=torch.int64)
+        keys = torch.empty(B * T, device=emb.device, dtype=torch.int64)
+        for i, cb in enumerate(codebooks):
+            x = res[i % 2]
+            cb.init_embed_(x)
+            call('encx_rvq_argmin', ptr(x), ptr(cb.embed), ptr(codes[i]), ptr(keys), B, D, T,
+                 cb.embed.shape[0], 0, st)
+            # dequantize with the pre-update codebook (core_vq.py:221), then update it (:223-235)
+            call('encx_rvq_apply', ptr(x), ptr(res[(i + 1) % 2]), ptr(cb.embed), ptr(codes[i]),
+                 ptr(out), ptr(cdir), ptr(parts[i]), B, D, T, int(i == 0), 1, st)
+            if cb.training:
+                call('encx_rvq_ema', ptr(x), ptr(codes[i]), ptr(cb.cluster_size), ptr(cb.embed_avg),
+                     ptr(cb.embed), B, D, T, cb.embed.shape[0], float(decay), float(eps), st)
+            call('encx_reduce_sum', ptr(parts[i]), P, 1.0 / numel, ptr(commits[i:i + 1]), 0, st)
+        penalty = torch.empty(1, device=emb.device, dtype=torch.float32)
+        call('encx_reduce_sum', ptr(commits), n_q, 1.0 / n_q, ptr(penalty), 0, st)
+        ctx.save_for_backward(cdir)
+        ctx.n_q, ctx.numel = n_q, numel
+        ctx.mark_non_differentiable(codes)
+        return out, codes.view(n_q, B, T), penalty
+
+    @staticmethod
+    def backward(ctx, dq, dcodes, dpen):
+        cdir, = ctx.saved_tensors
+        n_q, numel = ctx.n_q, ctx.numel
+        if dq is None:
+            dq = torch.zeros_like(cdir)
+        dq = dq.contiguous()
+        demb = torch.empty_like(cdir)
+        if dpen is None:
+            call('encx_lincomb', ptr(dq), ptr(cdir), ptr(demb), demb.numel(), float(n_q), None, 0.0,
+                 stream())
+        else:
+            call('encx_lincomb', ptr(dq), ptr(cdir), ptr(demb), demb.numel(), float(n_q),
+                 ptr(dpen.contiguous().view(1)), 2.0 / (n_q * numel), stream())
+        return demb, None, None, None
+
+
+def rvq_encode(emb, embeds):
+    """ResidualVectorQuantization.encode (core_vq.py:357-367): residual -= exact q."""
+    _check(emb, 'emb')
+    emb = emb.contiguous()
+    B, D, T = emb.shape
+    res = emb.clone()
+    codes = torch.empty(len(embeds), B * T, device=emb.device, dtype=torch.int64)
+    keys = torch.empty(B * T, device=emb.device, dtype=torch.int64)
+    for i, E in enumerate(embeds):
+        call('encx_rvq_argmin', ptr(res), ptr(E), ptr(codes[i]), ptr(keys), B, D, T, E.shape[0], 0,
+             stream())
+        call('encx_rvq_apply', ptr(res), ptr(res), ptr(E), ptr(codes[i]), None, None, None, B, D, T,
+             0, 0, stream())
+    return codes.view(len(embeds), B, T)
+
+
+def rvq_decode(codes, embeds):
+    """ResidualVectorQuantization.decode (core_vq.py:369-375)."""
+    n_q, B, T = codes.shape
+    D = embeds[0].shape[1]
+    out = torch.empty(B, D, T, device=codes.device, dtype=torch.float32)
+    codes = codes.contiguous()
+    for i in range(n_q):
+        call('encx_rvq_gather', ptr(embeds[i]), ptr(codes[i]), ptr(out), B, D, T, int(i > 0), stream())
+    return out

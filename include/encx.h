@@ -1,0 +1,230 @@
+/* encx.h -- C ABI of libencx.so, the MI355X (gfx950) hot path of EnCodec training.
+ *
+ * Drop-in boundary. The reference (Madhudorai/encodec-pytorch) has no FFI: its hot path sits
+ * behind PyTorch nn.Module.forward methods and ATen kernels. Each entry point
+ * below replaces the device work of one such reference interface, cited as file:line.
+ *
+ * Conventions:
+ *  - plain device pointers (fp32 unless noted), int64 sizes, contiguous row-major tensors;
+ *  - the CALLER owns all memory (PyTorch's caching allocator); workspaces are caller-provided
+ *    after a *_workspace query; the library never allocates or frees;
+ *  - every call is stream-ordered on the given hipStream_t (pass torch's current stream) and
+ *    never synchronises, so a caller may capture it into a hipGraph;
+ *  - return 0 on success, a hipError_t value, or ENCX_EINVAL for a shape/argument error;
+ *    encx_strerror() turns a code into text. No exceptions cross the ABI;
+ *  - deterministic: no floating-point atomics; split reductions are summed in a fixed order.
+ */
+#ifndef ENCX_H
+#define ENCX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* encx_stream_t; /* == hipStream_t */
+
+#define ENCX_OK 0
+#define ENCX_EINVAL 9001
+
+#define ENCX_PAD_ZERO 0
+#define ENCX_PAD_REFLECT 1
+#define ENCX_ACT_NONE 0
+#define ENCX_ACT_ELU 1
+
+/* ---------------------------------------------------------------- library */
+int encx_version(void);
+const char* encx_strerror(int code);
+/* Select the device; cheap, idempotent. */
+int encx_init(int device);
+/* Kernel timing for bench.py's roofline: while enabled, every launch of the named kernel
+ * family is bracketed by hipEvents on its own stream together with its algorithmic FLOPs and
+ * bytes. family: 0 = all conv/GEMM MFMA kernels. */
+int encx_prof_enable(int on);
+int encx_prof_read(double* total_ms, double* total_flops, double* total_bytes, int64_t* launches);
+
+/* ---------------------------------------------------------------- weight norm
+ * torch.nn.utils.weight_norm(dim=0) installed by modules/conv.py:25-34 (apply_parametrization_norm):
+ * w = v * (g / ||v||_row). v is [A0][A1][K] (Conv1d: [Cout][Cin][K]; ConvTranspose1d: [Cin][Cout][K]).
+ * Writes the GEMM operand layouts the conv kernels read:
+ *   wf [A1][K][A0]            (conv forward / conv-transpose backward-data)
+ *   wp [A0][J][A1*s + r] = w[a0][a1][r + s*j], J = ceil(K/s)   (polyphase transposed kernels)
+ * Either output may be NULL. `g` may be NULL for an un-normalised weight (w = v). */
+int encx_weightnorm_fwd(const float* v, const float* g, float* wf, float* wp, int64_t A0,
+                        int64_t A1, int64_t K, int64_t stride, encx_stream_t stream);
+/* Backward of w = v*(g/||v||): dg = (dw.v)/||v||, dv = (g/||v||)(dw - (dw.v/||v||^2) v).
+ * rows = A0, cols = A1*K. accumulate: 0 overwrite, 1 add into dv/dg. */
+int encx_weightnorm_bwd(const float* v, const float* g, const float* dw, float* dv, float* dg,
+                        int64_t rows, int64_t cols, int accumulate, encx_stream_t stream);
+
+/* ---------------------------------------------------------------- Conv1d
+ * SConv1d.forward (modules/conv.py:195-210): pad1d (:79-96, reflect or zero, `short_ext` =
+ * the zero extension of a too-short reflect input, :86-91), then Conv1d (NormConv1d :119-122).
+ * y[b,co,t] = bias[co] + sum_{ci,k} W[co,ci,k] act(xpad[b,ci,t*s+k*d]) (+ residual[b,co,t]).
+ * pre_act = ENCX_ACT_ELU fuses the nn.ELU that precedes the conv in the SEANet stacks
+ * (modules/seanet.py:49,124,136,204,223). residual may alias y (SEANetResnetBlock sum, :63). */
+int encx_conv1d_fwd(const float* x, const float* wf, const float* bias, const float* residual,
+                    float* y, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                    int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
+                    int64_t short_ext, int pad_mode, int pre_act, encx_stream_t stream);
+/* d loss / d x of the above (with the pad folded back and the act' applied):
+ * dx = [accumulate ? dx : 0] + act'(x) * fold(W^T * dy). `x` is the pre-activation input
+ * (read only when pre_act != NONE). side: workspace of encx_conv1d_bwd_data_workspace bytes. */
+int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float* dx,
+                         float* side, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
+                         int64_t Tout, int64_t K, int64_t stride, int64_t pad_left,
+                         int64_t pad_right, int64_t short_ext, int pad_mode, int pre_act,
+                         int accumulate, encx_stream_t stream);
+size_t encx_conv1d_bwd_data_workspace(int64_t B, int64_t Cin, int64_t pad_left, int64_t pad_right);
+/* dW[co,ci,k] = sum_{b,t} dy[b,co,t] act(xpad[b,ci,t*s+k*d]); db[co] = sum dy (db may be NULL).
+ * dw is [Cout][Cin][K]; accumulate as above. ws: encx_conv1d_bwd_weight_workspace bytes. */
+int encx_conv1d_bwd_weight(const float* dy, const float* x, float* dw, float* db, float* ws,
+                           int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                           int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
+                           int64_t short_ext, int pad_mode, int pre_act, int accumulate,
+                           encx_stream_t stream);
+size_t encx_conv1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout,
+                                        int64_t K);
+
+/* ---------------------------------------------------------------- ConvTranspose1d
+ * SConvTranspose1d.forward (modules/conv.py:230-252): ConvTranspose1d then unpad1d (:99-105).
+ * y[b,co,j] = bias[co] + sum_{ci,t,k: t*s+k = j+trim_left} Wt[ci,co,k] act(x[b,ci,t]),
+ * j in [0,Tout). Polyphase: for each output phase r = (j+trim_left) mod s only the taps
+ * k = r + s*q contribute, so the work is a dense GEMM over (co,r) x (b,u) x (ci,q). */
+int encx_convtr1d_fwd(const float* x, const float* wp, const float* bias, float* y, int64_t B,
+                      int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout, int64_t K,
+                      int64_t stride, int64_t trim_left, int pre_act, encx_stream_t stream);
+int encx_convtr1d_bwd_data(const float* dy, const float* wf, const float* x, float* dx,
+                           int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                           int64_t K, int64_t stride, int64_t trim_left, int pre_act,
+                           int accumulate, encx_stream_t stream);
+/* dWt[ci,co,k] = sum_{b,t} act(x[b,ci,t]) dy[b,co,t*s+k-trim_left]; db[co] = sum dy. */
+int encx_convtr1d_bwd_weight(const float* x, const float* dy, float* dw, float* db, float* ws,
+                             int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                             int64_t K, int64_t stride, int64_t trim_left, int pre_act,
+                             int accumulate, encx_stream_t stream);
+size_t encx_convtr1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tin,
+                                          int64_t K);
+
+/* ---------------------------------------------------------------- elementwise / reductions */
+/* db[c] = [acc ? db : 0] + sum_{b,t} dy[b,c,t] (the bias grads of every conv); ws: workspace
+ * of encx_channel_sum_workspace(C) bytes. */
+size_t encx_channel_sum_workspace(int64_t C);
+int encx_channel_sum(const float* dy, float* db, float* ws, int64_t B, int64_t C, int64_t T,
+                     int accumulate, encx_stream_t stream);
+/* EncodecModel._encode_frame normalisation (model.py:152-157): scale[b] = 1e-8 +
+ * sqrt(mean_t (mean_c x)^2); xn = x / scale. */
+int encx_normalize_fwd(const float* x, float* xn, float* scale, int64_t B, int64_t C, int64_t T,
+                       encx_stream_t stream);
+/* y[b,c,t] = x[b,c,t] * scale[b] (model.py:191-192 out * scale; also its backward) */
+int encx_scale_rows(const float* x, const float* scale, float* y, int64_t B, int64_t CT,
+                    encx_stream_t stream);
+/* y = alpha * x (+ beta * y); alpha read from device scalar alpha_dev when non-NULL */
+int encx_axpby(const float* x, float* y, int64_t n, float alpha, const float* alpha_dev,
+               float beta, encx_stream_t stream);
+/* l_t = mean |x - y| (losses.py:37) into loss[0]; grad = sign(y - x)/n (may be NULL). ws:
+ * >= 1024 floats. */
+int encx_l1_loss(const float* x, const float* y, float* loss, float* grad, float* ws, int64_t n,
+                 encx_stream_t stream);
+
+/* ---------------------------------------------------------------- RVQ (quantization/core_vq.py)
+ * res is the encoder-layout residual [B][D][Tf] (the reference rearranges 'b d n -> b n d',
+ * core_vq.py:303; the kernels index it in place). N = B*Tf frames.
+ * Nearest code, EuclideanCodebook.quantize (core_vq.py:181-189): idx[n] = argmax_k
+ * -((|x_n|^2 - 2 x_n.e_k) + |e_k|^2), first index on ties. direct != 0 selects kmeans' form
+ * -sum_d (x_n,d - e_k,d)^2 (core_vq.py:86-89). keys: workspace of N uint64. */
+int encx_rvq_argmin(const float* res, const float* embed, int64_t* idx, uint64_t* keys,
+                    int64_t B, int64_t D, int64_t Tf, int64_t Kc, int direct,
+                    encx_stream_t stream);
+/* One VectorQuantization layer after its argmin (core_vq.py:301-324, :346-349), x = layer input:
+ * q = embed[idx]; q_ste = ste ? x + (q - x) : q; res_out = x - q_ste (may alias x);
+ * out (+)= q_ste; commit_dir (+)= x - q_ste; commit_part[blk] = partial sums of (q_ste - x)^2
+ * (reduce with encx_reduce_sum). first != 0 initialises out / commit_dir; out, commit_dir and
+ * commit_part may be NULL (eval-mode encode, core_vq.py:357-367, uses ste = 0). */
+int encx_rvq_apply(const float* x, float* res_out, const float* embed, const int64_t* idx,
+                   float* out, float* commit_dir, float* commit_part, int64_t B, int64_t D,
+                   int64_t Tf, int first, int ste, encx_stream_t stream);
+/* ResidualVectorQuantization.decode (core_vq.py:369-375) one layer: out (+)= embed[idx]. */
+int encx_rvq_gather(const float* embed, const int64_t* idx, float* out, int64_t B, int64_t D,
+                    int64_t Tf, int accumulate, encx_stream_t stream);
+int64_t encx_rvq_apply_parts(int64_t B, int64_t D, int64_t Tf);
+/* EMA codebook update (core_vq.py:227-235): counts/sums of the frames assigned to each code,
+ * cluster_size = d*cs + (1-d)*count; embed_avg = d*ea + (1-d)*sum; embed = embed_avg /
+ * laplace(cluster_size)*sum(cluster_size). x = the layer input (pre-update residual),
+ * layout [B][D][Tf]. Deterministic (fixed summation order per code). */
+int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float* embed_avg,
+                 float* embed, int64_t B, int64_t D, int64_t Tf, int64_t Kc, float decay,
+                 float eps, encx_stream_t stream);
+/* One kmeans iteration (core_vq.py:85-100): means <- bucket means where bins > 0.
+ * samples [N][D] row-major; means [Kc][D] in/out; bins int64 [Kc] out. */
+int encx_kmeans_step(const float* samples, float* means, int64_t* bins, int64_t* idx,
+                     uint64_t* keys, int64_t N, int64_t D, int64_t Kc, encx_stream_t stream);
+/* sample_vectors (core_vq.py:69-77) for kmeans' init: rows of a uniform random permutation
+ * (num <= N) or uniform draws with replacement, from a counter-based hash of `seed`. */
+int encx_sample_rows(const float* samples, float* out, int64_t N, int64_t D, int64_t num,
+                     uint64_t seed, encx_stream_t stream);
+/* out_rows[n][d] = res[b][d][t] (n = b*Tf + t): the 'b d n -> (b n) d' rearrange */
+int encx_bdt_to_nd(const float* res, float* out, int64_t B, int64_t D, int64_t Tf,
+                   encx_stream_t stream);
+/* out[0] = scale * sum(parts[0..n)) in a fixed order (+ out[0] if accumulate) */
+int encx_reduce_sum(const float* parts, int64_t n, float scale, float* out, int accumulate,
+                    encx_stream_t stream);
+
+/* ---------------------------------------------------------------- multi-scale mel loss
+ * Audio2Mel (audio_to_mel.py:34-55) + the l_f term of total_loss (losses.py:40-42):
+ * logmel = log10(clamp(mel_basis @ |STFT(reflect_pad(wav))|^2, 1e-5)), n_fft = win = n,
+ * hop = n/4, hann window. encx_mel_spec writes logmel [B*F][64] and (optionally) the raw
+ * spectrum (re, im) [B*F][2*nb] for the backward. tables: encx_mel_tables layout. */
+size_t encx_mel_tables_floats(int64_t n_fft, int64_t n_mels);
+/* window*cos / window*sin DFT tables + mel basis, built on the device from the mel basis
+ * uploaded by the caller (host restatement of librosa.filters.mel). */
+int encx_mel_tables_init(float* tables, const float* mel_basis, int64_t n_fft, int64_t n_mels,
+                         encx_stream_t stream);
+size_t encx_mel_workspace_floats(int64_t B, int64_t T, int64_t n_fft, int64_t n_mels);
+/* Forward of one scale for the pair (x = target, y = output): loss_part[0] += (L1 + MSE)
+ * between logmel(x) and logmel(y); if grad != NULL, grad (+)= d(L1+MSE)/dy (always added:
+ * zero it before the first scale). */
+int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws, float* loss,
+                  float* grad, int64_t B, int64_t T, int64_t n_fft, int64_t n_mels,
+                  encx_stream_t stream);
+
+/* Audio2Mel.forward (audio_to_mel.py:34-55) alone: out [B][n_mels][F] log-mel spectrogram
+ * (the reference's [B*C, 64, F] before its final reshape). ws: encx_mel_workspace_floats. */
+int encx_mel_logmel(const float* x, const float* tables, float* ws, float* out, int64_t B,
+                    int64_t T, int64_t n_fft, int64_t n_mels, encx_stream_t stream);
+/* frame count of one scale: (T + 2p - n)/h + 1 with h = n/4, p = (n-h)/2 */
+int64_t encx_mel_frames(int64_t T, int64_t n_fft);
+
+/* ---------------------------------------------------------------- step-level (train.hip) */
+/* out = a*x + (bdev ? bdev[0]*bscale : bscale) * z  -- the RVQ backward (core_vq.py:309,319):
+ * d emb = n_q * d quantized + d penalty * 2/(n_q*numel) * sum_i (x_i - q_ste_i). */
+int encx_lincomb(const float* x, const float* z, float* out, int64_t n, float a, const float* bdev,
+                 float bscale, encx_stream_t stream);
+/* Balancer (balancer.py:83-118) on the device. item_norm_mean: out[0] = mean_b ||g_b||_2
+ * (grad.norm(dim=1..).mean(), :88-90); ws: encx_item_norm_workspace(B) bytes. */
+size_t encx_item_norm_workspace(int64_t B);
+int encx_item_norm_mean(const float* g, float* out, float* ws, int64_t B, int64_t L,
+                        encx_stream_t stream);
+/* averager EMA (:10-28) in fp64: total = total*beta + norm; fix = fix*beta + 1; avg = total/fix;
+ * red = [avg*count .., count] for the average_metrics all-reduce (distrib.py:112-124). */
+int encx_balancer_update(const float* norms, double* total, double* fix, double* avg, float* red,
+                         int nl, double beta, float count, encx_stream_t stream);
+/* scales[k] = ratio[k]*total_norm/(eps + avg_k); avg_k from `avg`, or red[k]/red[nl] when
+ * from_red (after the all-reduce). */
+int encx_balancer_scales(const double* avg, const float* red, const double* ratio, float* scales,
+                         int nl, double total_norm, double eps, int from_red,
+                         encx_stream_t stream);
+/* out = g0*s0 + g1*s1 + g2*s2 + g3*s3 (g1..g3 may be NULL), the balanced output grad (:110-118) */
+int encx_balancer_combine(const float* g0, const float* g1, const float* g2, const float* g3,
+                          const float* scales, float* out, int64_t n, encx_stream_t stream);
+/* torch.optim.Adam step (amsgrad off, no weight decay) over flat fp32 buffers; step >= 1 is the
+ * step count after increment (train_multi_gpu.py:295-296 betas (0.5, 0.9)). */
+int encx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                   double beta2, double eps, int64_t step, encx_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ENCX_H */

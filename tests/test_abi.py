@@ -1,0 +1,101 @@
+"""CPU checks of the C-ABI boundary and the host layer (no GPU compute)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _lib():
+    from encx._lib import lib
+    return lib.load()
+
+
+def test_library_exports_every_header_symbol():
+    from encx._lib import parse_header, LIB_PATH
+    assert os.path.exists(LIB_PATH), 'build first: __graft_entry__.build()'
+    sigs = parse_header()
+    src = open(os.path.join(ROOT, 'include', 'encx.h')).read()
+    declared = set(re.findall(r'\b(encx_\w+)\s*\(', re.sub(r'/\*.*?\*/', '', src, flags=re.S)))
+    assert declared == set(sigs), declared ^ set(sigs)
+    lib = ctypes.CDLL(LIB_PATH)
+    missing = [n for n in sigs if not hasattr(lib, n)]
+    assert not missing, missing
+    assert len(sigs) >= 40
+
+
+def test_host_only_queries():
+    lib = _lib()
+    assert lib.encx_version() == 1
+    assert b'invalid' in lib.encx_strerror(9001)
+    assert lib.encx_mel_frames(24000, 2048) == 46
+    assert lib.encx_mel_frames(24000, 32) == 3000
+    assert lib.encx_rvq_apply_parts(32, 128, 75) == 1024
+    assert lib.encx_conv1d_bwd_weight_workspace(32, 32, 16, 24000, 3) > 0
+    assert lib.encx_mel_tables_floats(32, 64) == 32 * 34 + 2 * 17 * 64
+    # argument validation happens before any device call
+    assert lib.encx_conv1d_fwd(None, None, None, None, None, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, None) == 9001
+
+
+def test_ops_refuse_cpu_tensors():
+    from encx import ops
+    x = torch.zeros(1, 1, 100)
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        ops.normalize(x)
+
+
+def test_geometry_matches_oracle():
+    from encx import ops
+    from oracle import encodec_oracle as O
+    for T in (5, 30, 97, 480, 4800, 24000):
+        for K, s in ((7, 1), (3, 1), (1, 1), (4, 2), (8, 4), (10, 5), (16, 8)):
+            for causal in (True, False):
+                pl, pr, e, tout = ops.conv_geometry(T, K, s, 1, causal)
+                assert (pl, pr) == O.conv_padding(T, K, s, 1, causal)
+                x = torch.zeros(1, 1, T)
+                xp = O.pad1d(x, (pl, pr), 'reflect') if max(pl, pr) < T + e else None
+                if xp is not None:
+                    assert xp.shape[-1] == pl + T + pr
+                    assert tout == (xp.shape[-1] - K) // s + 1
+
+
+def test_state_dict_keys_and_count_match_reference():
+    from encx.model import EncodecModel
+    d = np.load(os.path.join(ROOT, 'tests', 'golden', 'g7_step.npz'))
+    keys = {k[6:] for k in d.files if k.startswith('gen/p/')}
+    m = EncodecModel._get_model([1.5], 24000, 1, causal=True, model_norm='weight_norm', audio_normalize=True)
+    assert set(m.state_dict()) == keys
+    m = EncodecModel._get_model([1.5, 3., 6., 12., 24.], 24000, 1, causal=True, model_norm='weight_norm')
+    assert sum(p.numel() for p in m.parameters()) == 14851810
+
+
+def test_product_mel_filterbank_matches_fixture():
+    from encx.audio_to_mel import mel_filterbank
+    d = np.load(os.path.join(ROOT, 'tests', 'golden', 'g4_mel.npz'))
+    for i in range(5, 12):
+        n = 2 ** i
+        np.testing.assert_array_equal(mel_filterbank(24000, n, 64), d[f'melbasis{n}'])
+
+
+def test_scheduler_matches_fixture():
+    from encx.scheduler import WarmupCosineLrScheduler
+    d = np.load(os.path.join(ROOT, 'tests', 'golden', 'g8_sched.npz'))
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=3e-4)
+    s = WarmupCosineLrScheduler(opt, max_iter=400, eta_ratio=0.1, warmup_iter=50, warmup_ratio=1e-4)
+    lrs = []
+    for _ in range(400):
+        lrs.append(opt.param_groups[0]['lr'])
+        opt.step()
+        s.step()
+    np.testing.assert_allclose(lrs, d['lr'], rtol=1e-12)
+
+
+def test_bandwidth_rule():
+    from encx.quantization import ResidualVectorQuantizer
+    q = ResidualVectorQuantizer(dimension=128, n_q=32, bins=1024)
+    assert [q.get_num_quantizers_for_bandwidth(75, b) for b in (1.5, 3., 6., 12., 24.)] == [2, 4, 8, 16, 32]

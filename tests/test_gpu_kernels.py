@@ -1,0 +1,286 @@
+"""GPU parity of the HIP kernels (through the libencx C ABI) against the golden fixtures and the
+CPU oracle. Run on an MI355X: pytest -m gpu."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import encodec_oracle as O
+from fixtures import load, T, model_state, codebooks_from_stats, g3_codebooks, certified
+from synth import synth_state, synth_wave
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def G(a):
+    return T(a).to(DEV)
+
+
+def close(a, b, rtol=1e-5, atol=1e-6, what=''):
+    a = a.detach().float().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    b = b.detach().float().cpu().numpy() if torch.is_tensor(b) else np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    err = np.abs(a - b)
+    tol = atol + rtol * np.abs(b)
+    bad = err > tol
+    assert not bad.any(), f'{what}: {bad.sum()}/{bad.size} off, max abs err {err.max():.3e}, ' \
+                          f'max rel {(err / (np.abs(b) + 1e-30)).max():.3e}'
+
+
+# --------------------------------------------------------------------------- conv fixtures
+CASES = [
+    ('c_k7_1to8', 'conv', 1, 8, 7, 1, True, False, 480),
+    ('c_k3_16to8_elu', 'conv', 16, 8, 3, 1, True, True, 480),
+    ('c_k1_8to16_elu', 'conv', 8, 16, 1, 1, True, True, 480),
+    ('c_k1_16to16', 'conv', 16, 16, 1, 1, True, False, 480),
+    ('c_k4s2_16to32_elu', 'conv', 16, 32, 4, 2, True, True, 480),
+    ('c_k10s5_16to32_elu', 'conv', 16, 32, 10, 5, True, True, 480),
+    ('c_k16s8_32to64_elu', 'conv', 32, 64, 16, 8, True, True, 480),
+    ('c_k7_64to16_elu', 'conv', 64, 16, 7, 1, True, True, 30),
+    ('c_k7_short_reflect', 'conv', 8, 8, 7, 1, True, False, 5),
+    ('c_k7s1_nc', 'conv', 8, 8, 7, 1, False, False, 100),
+    ('c_k10s5_nc_odd', 'conv', 8, 16, 10, 5, False, True, 97),
+    ('t_k4s2_32to16_elu', 'convtr', 32, 16, 4, 2, True, True, 240),
+    ('t_k10s5_32to16_elu', 'convtr', 32, 16, 10, 5, True, True, 96),
+    ('t_k16s8_64to32_elu', 'convtr', 64, 32, 16, 8, True, True, 60),
+    ('t_k8s4_nc', 'convtr', 16, 8, 8, 4, False, False, 50),
+]
+
+
+def _case_params(ci, kind, cin, cout, K):
+    pre = 'convtr.convtr' if kind == 'convtr' else 'conv.conv'
+    wshape = (cin, cout, K) if kind == 'convtr' else (cout, cin, K)
+    shapes = {pre + '.bias': (cout,), pre + '.weight_g': (wshape[0], 1, 1), pre + '.weight_v': wshape}
+    st = synth_state(shapes, 100 + ci)
+    return (G(st[pre + '.weight_v']).requires_grad_(True), G(st[pre + '.weight_g']).requires_grad_(True),
+            G(st[pre + '.bias']).requires_grad_(True))
+
+
+@pytest.mark.parametrize('ci', range(len(CASES)))
+def test_conv_fixture(ci):
+    from encx import ops
+    d = load('g2_convs.npz')
+    name, kind, cin, cout, K, s, causal, pre_elu, Tn = CASES[ci]
+    v, g, b = _case_params(ci, kind, cin, cout, K)
+    x = G(d[name + '/x']).requires_grad_(True)
+    act = 'elu' if pre_elu else None
+    if kind == 'conv':
+        y = ops.conv1d(x, v, g, b, K, s, 1, causal, 'reflect', act)
+    else:
+        y = ops.convtr1d(x, v, g, b, K, s, causal, 1.0, act)
+    close(y, d[name + '/y'], 1e-5, 1e-5, name + ' y')
+    y.backward(G(d[name + '/gy']))
+    close(x.grad, d[name + '/dx'], 1e-4, 1e-5, name + ' dx')
+    close(v.grad, d[name + '/dv'], 1e-4, 1e-5, name + ' dv')
+    close(g.grad, d[name + '/dg'], 1e-4, 1e-5, name + ' dg')
+    close(b.grad, d[name + '/db'], 1e-4, 1e-4, name + ' db')
+
+
+# the real SEANet layer shapes (B=2, shorter T) against the oracle, fwd + all grads
+MODEL_LAYERS = [
+    # kind, cin, cout, K, s, pre_elu, T_in
+    ('conv', 1, 32, 7, 1, False, 4800), ('conv', 32, 16, 3, 1, True, 4800),
+    ('conv', 16, 32, 1, 1, True, 4800), ('conv', 32, 32, 1, 1, False, 4800),
+    ('conv', 32, 64, 4, 2, True, 4800), ('conv', 64, 128, 8, 4, True, 2400),
+    ('conv', 128, 256, 10, 5, True, 600), ('conv', 256, 512, 16, 8, True, 120),
+    ('conv', 512, 128, 7, 1, True, 15), ('conv', 128, 512, 7, 1, False, 15),
+    ('conv', 256, 128, 3, 1, True, 120), ('conv', 128, 256, 1, 1, True, 120),
+    ('conv', 32, 1, 7, 1, True, 4800),
+    ('convtr', 512, 256, 16, 8, True, 15), ('convtr', 256, 128, 10, 5, True, 120),
+    ('convtr', 128, 64, 8, 4, True, 600), ('convtr', 64, 32, 4, 2, True, 2400),
+]
+
+
+@pytest.mark.parametrize('li', range(len(MODEL_LAYERS)))
+def test_conv_model_shapes_vs_oracle(li):
+    from encx import ops
+    kind, cin, cout, K, s, pre_elu, Tin = MODEL_LAYERS[li]
+    v0, g0, b0 = _case_params(500 + li, kind, cin, cout, K)
+    x0 = synth_wave((2, cin, Tin), 900 + li, amp=1.0)
+    act = 'elu' if pre_elu else None
+    x = G(x0).requires_grad_(True)
+    if kind == 'conv':
+        y = ops.conv1d(x, v0, g0, b0, K, s, 1, True, 'reflect', act)
+    else:
+        y = ops.convtr1d(x, v0, g0, b0, K, s, True, 1.0, act)
+    gy = synth_wave(tuple(y.shape), 950 + li, amp=1.0)
+    y.backward(G(gy))
+    # oracle on CPU
+    pre = 'convtr.convtr' if kind == 'convtr' else 'conv.conv'
+    p = {'m.' + pre + '.weight_v': v0.detach().cpu().clone().requires_grad_(True),
+         'm.' + pre + '.weight_g': g0.detach().cpu().clone().requires_grad_(True),
+         'm.' + pre + '.bias': b0.detach().cpu().clone().requires_grad_(True)}
+    xc = T(x0).requires_grad_(True)
+    xin = F.elu(xc) if pre_elu else xc
+    yc = O.sconv1d(xin, p, 'm', K, s) if kind == 'conv' else O.sconvtr1d(xin, p, 'm', K, s)
+    yc.backward(T(gy))
+    tag = f'{kind} {cin}->{cout} K{K} s{s}'
+    close(y, yc, 1e-4, 1e-5, tag + ' y')
+    close(x.grad, xc.grad, 2e-4, 1e-5, tag + ' dx')
+    close(v0.grad, p['m.' + pre + '.weight_v'].grad, 2e-4, 1e-4, tag + ' dv')
+    close(g0.grad, p['m.' + pre + '.weight_g'].grad, 2e-4, 1e-4, tag + ' dg')
+    close(b0.grad, p['m.' + pre + '.bias'].grad, 2e-4, 1e-3, tag + ' db')
+
+
+# --------------------------------------------------------------------------- RVQ
+class _CB:
+    def __init__(self, d):
+        for k, v in d.items():
+            setattr(self, k, v)
+        self.training = True
+        self.decay, self.epsilon = 0.99, 1e-5
+
+    def init_embed_(self, x):
+        pass
+
+
+def test_rvq_train_fixture():
+    from encx import ops
+    d = load('g3_rvq.npz')
+    cbs = [_CB({k: v.to(DEV).contiguous() for k, v in cb.items()}) for cb in g3_codebooks(d)]
+    emb = G(d['emb']).requires_grad_(True)
+    q, codes, pen = ops.RVQTrainFn.apply(emb, cbs, 0.99, 1e-5)
+    assert (codes.cpu().numpy() == d['codes']).all()
+    close(q, d['quantized'], 1e-6, 1e-6, 'quantized')
+    close(pen, d['penalty'], 1e-5, 1e-7, 'penalty')
+    torch.autograd.backward([q, pen], [G(d['gq']), torch.ones(1, device=DEV)])
+    close(emb.grad, d['demb'], 1e-5, 1e-6, 'demb')
+    for i in range(2):
+        close(cbs[i].cluster_size, d[f'cluster_size{i}'], 1e-6, 1e-7, f'cluster_size{i}')
+        close(cbs[i].embed_avg, d[f'embed_avg{i}'], 1e-5, 1e-6, f'embed_avg{i}')
+        close(cbs[i].embed, d[f'embed{i}'], 1e-5, 1e-6, f'embed{i}')
+
+
+def test_rvq_argmin_full_size_certified():
+    from encx import ops
+    r = np.random.Generator(np.random.PCG64(7))
+    emb = r.standard_normal((32, 128, 75)).astype(np.float32)
+    E = r.standard_normal((1024, 128)).astype(np.float32)
+    idx = ops.rvq_argmin(G(emb), G(E)).cpu().numpy()
+    x = emb.transpose(0, 2, 1).reshape(-1, 128).astype(np.float64)
+    dist = (x ** 2).sum(1)[:, None] - 2 * x @ E.T.astype(np.float64) + (E.astype(np.float64) ** 2).sum(1)[None]
+    srt = np.sort(dist, 1)
+    gap = srt[:, 1] - srt[:, 0]
+    cert = certified(gap, float((x ** 2).sum(1).max()), float((E.astype(np.float64) ** 2).sum(1).max()))
+    ref = O.codebook_quantize(T(emb.transpose(0, 2, 1).reshape(-1, 128)), T(E)).numpy()
+    assert cert.mean() > 0.99
+    assert (idx[cert] == ref[cert]).all()
+    assert (idx[cert] == dist.argmin(1)[cert]).all()
+
+
+def test_rvq_argmin_ties_first_index():
+    from encx import ops
+    E = np.zeros((1024, 128), np.float32)
+    E[5] = 1.0
+    E[700] = 1.0  # exact duplicate of code 5 -> tie, first index wins
+    x = np.ones((1, 128, 3), np.float32)
+    idx = ops.rvq_argmin(G(x), G(E)).cpu().numpy()
+    assert (idx == 5).all()
+
+
+def test_kmeans_fixture():
+    from encx._lib import call, ptr, stream
+    d = load('g3_rvq.npz')
+    samples = G(d['km_samples'])
+    means = samples[T(d['km_init']).to(DEV)].contiguous()
+    bins = torch.zeros(64, dtype=torch.int64, device=DEV)
+    idx = torch.empty(600, dtype=torch.int64, device=DEV)
+    keys = torch.empty(600, dtype=torch.int64, device=DEV)
+    for _ in range(10):
+        call('encx_kmeans_step', ptr(samples), ptr(means), ptr(bins), ptr(idx), ptr(keys), 600, 128, 64, stream())
+    close(means, d['km_means'], 1e-5, 1e-6, 'kmeans means')
+    assert (bins.cpu().numpy() == d['km_bins']).all()
+
+
+def test_sample_rows_is_a_permutation_prefix():
+    from encx import ops
+    from encx._lib import call, ptr, stream
+    s = torch.arange(600 * 4, dtype=torch.float32, device=DEV).view(600, 4)
+    out = torch.empty(256, 4, device=DEV)
+    call('encx_sample_rows', ptr(s), ptr(out), 600, 4, 256, 12345, stream())
+    rows = (out[:, 0] / 4).long().cpu().numpy()
+    assert len(set(rows.tolist())) == 256 and rows.min() >= 0 and rows.max() < 600
+    means, bins = ops.kmeans(G(synth_wave((300, 8), 3, amp=1.0)), 16, 5, 99)
+    assert int(bins.sum()) == 300
+
+
+# --------------------------------------------------------------------------- mel / losses
+def test_mel_fixture():
+    from encx import ops
+    d = load('g4_mel.npz')
+    x = G(d['x'])
+    for i in range(5, 12):
+        n = 2 ** i
+        close(ops.logmel(x, n, 64, 24000), d[f'mel{n}'], 1e-4, 2e-4, f'logmel {n}')
+
+
+def test_losses_fixture():
+    from encx import losses
+    d = load('g4_mel.npz')
+    x = G(d['x'])
+    y = G(d['y']).requires_grad_(True)
+    lt, lf = losses.reconstruction_losses(x, y)
+    close(lt.view(1), d['l_t'].reshape(1), 1e-5, 1e-7, 'l_t')
+    close(lf.view(1), d['l_f'].reshape(1), 1e-5, 1e-6, 'l_f')
+    gf, = torch.autograd.grad(lf, [y])
+    gt, = torch.autograd.grad(lt, [y])
+    close(gt, d['dlt_dy'], 1e-6, 1e-9, 'dl_t/dy')
+    close(gf, d['dlf_dy'], 2e-3, 2e-7, 'dl_f/dy')
+
+
+def test_mel_loss_full_size_vs_oracle():
+    from encx import losses
+    x0 = synth_wave((4, 1, 24000), 11)
+    y0 = synth_wave((4, 1, 24000), 12)
+    y = G(y0).requires_grad_(True)
+    lt, lf = losses.reconstruction_losses(G(x0), y)
+    gf, = torch.autograd.grad(lf, [y])
+    yc = T(y0).requires_grad_(True)
+    lfc = O.loss_f(T(x0), yc)
+    gfc, = torch.autograd.grad(lfc, [yc])
+    close(lf.view(1), lfc.detach().view(1), 1e-5, 1e-6, 'l_f full')
+    close(gf, gfc, 5e-3, 1e-8, 'dl_f/dy full')
+
+
+def test_balancer_fixture():
+    from encx.balancer import Balancer
+    d = load('g6_balancer.npz')
+    b = Balancer({'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3})
+    for it in range(3):
+        grads = {k: G(d[f'it{it}_{k}']) for k in ('l_t', 'l_f', 'l_g', 'l_feat')}
+        close(b.combine(grads), d[f'it{it}_out'], 1e-5, 1e-9, f'balancer it{it}')
+    b = Balancer({'1': 1, '2': 1}, rescale_grads=False)
+    out = b.combine({'1': torch.full((1, 1), -1.0, device=DEV), '2': torch.full((1, 1), 100.0, device=DEV)})
+    assert float(out) == 99.0
+    b = Balancer({'1': 1, '2': 1})
+    out = b.combine({'1': torch.full((1, 1), -1.0, device=DEV), '2': torch.full((1, 1), 100.0, device=DEV)})
+    assert abs(float(out)) < 1e-6
+
+
+def test_adam_vs_oracle():
+    from encx.optim import FlatAdam
+    r = np.random.Generator(np.random.PCG64(5))
+    p0 = {'a': r.standard_normal((33, 7)).astype(np.float32), 'b': r.standard_normal((100,)).astype(np.float32)}
+    ps = [torch.nn.Parameter(G(p0['a'])), torch.nn.Parameter(G(p0['b']))]
+    opt = FlatAdam(ps, lr=3e-4, betas=(0.5, 0.9))
+    pc = {k: T(v).clone() for k, v in p0.items()}
+    st = {}
+    for it in range(3):
+        gs = {k: r.standard_normal(v.shape).astype(np.float32) for k, v in p0.items()}
+        opt.zero_grad()
+        ps[0].grad.copy_(G(gs['a']))
+        ps[1].grad.copy_(G(gs['b']))
+        opt.step()
+        O.adam_step(pc, {k: T(v) for k, v in gs.items()}, st, 3e-4)
+    close(ps[0], pc['a'], 1e-6, 1e-7, 'adam a')
+    close(ps[1], pc['b'], 1e-6, 1e-7, 'adam b')
+
+
+def test_normalize_and_scale():
+    from encx import ops
+    x0 = synth_wave((3, 1, 1000), 21, amp=0.3)
+    xn, sc = ops.normalize(G(x0))
+    xr, scr = O.normalize(T(x0))
+    close(xn, xr, 1e-6, 1e-7, 'xn')
+    close(sc, scr, 1e-6, 1e-9, 'scale')

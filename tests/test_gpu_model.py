@@ -1,0 +1,147 @@
+"""GPU parity of the whole model / train step (encx EncodecModel + Trainer) against the golden
+fixtures generated from the reference and against the CPU oracle at full size."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import encodec_oracle as O
+from fixtures import load, T, model_state, codebooks_from_stats, certified
+from synth import synth_wave
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def G(a):
+    return T(a).to(DEV)
+
+
+def rel(a, b):
+    a = a.detach().double().cpu() if torch.is_tensor(a) else torch.as_tensor(a, dtype=torch.float64)
+    b = b.detach().double().cpu() if torch.is_tensor(b) else torch.as_tensor(b, dtype=torch.float64)
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+def build(target_bandwidths, audio_normalize, seed, stats, cb_seed, n_used):
+    from encx.model import EncodecModel
+    m = EncodecModel._get_model(list(target_bandwidths), 24000, 1, causal=True, model_norm='weight_norm',
+                                audio_normalize=audio_normalize)
+    cfg = O.Config(target_bandwidths=target_bandwidths, audio_normalize=audio_normalize)
+    p = model_state(cfg, seed)
+    cbs = codebooks_from_stats(stats, cb_seed, n_used, cfg.n_q)
+    sd = dict(p)
+    for i, cb in enumerate(cbs):
+        for k, v in cb.items():
+            sd[f'quantizer.vq.layers.{i}._codebook.{k}'] = v
+    m.load_state_dict(sd)
+    return m.to(DEV), p, cbs, cfg
+
+
+def test_eval_model_fixture():
+    d = load('g1_eval24k.npz')
+    m, p, cbs, cfg = build((1.5, 3., 6., 12., 24.), False, 1, d['stats'], 77, 2)
+    m.eval()
+    m.set_target_bandwidth(1.5)
+    x = G(d['x'])
+    with torch.no_grad():
+        emb = m.encoder(x)
+        codes = m.encode(x)[0][0]
+        y = m(x)
+    assert rel(emb, d['emb']) < 1e-4, rel(emb, d['emb'])
+    ref = d['codes'].astype(np.int64)
+    e2 = max(float((cb['embed'] ** 2).sum(1).max()) for cb in cbs[:2])
+    cert = certified(d['gaps'], float((emb.cpu() ** 2).sum(1).max()), e2)
+    mine = codes.cpu().numpy()
+    assert (mine[0][cert] == ref[0][cert]).all()
+    if (mine == ref).all():
+        assert rel(y, d['y']) < 1e-3, rel(y, d['y'])
+
+
+def test_train_step_gen_fixture():
+    from encx.train import Trainer
+    d = load('g7_step.npz')
+    m, p, cbs, cfg = build((1.5,), True, 71, d['gen/stats'], 73, 2)
+    tr = Trainer(m, None, lr=3e-4, scheduler=False, weights={'l_t': 0.1, 'l_f': 1})
+    x = G(d['gen/x'])
+    for it in range(2):
+        out = tr.step(x)
+        for k in ('l_t', 'l_f'):
+            np.testing.assert_allclose(float(out[k]), float(d[f'gen/it{it}_{k}'].reshape(-1)[0]), rtol=1e-4)
+        np.testing.assert_allclose(float(out['loss_w']), float(d[f'gen/it{it}_loss_w'].reshape(-1)[0]),
+                                   rtol=5e-3, atol=1e-6)
+    sd = m.state_dict()
+    worst = 0.0
+    for k, v in sd.items():
+        ref = d['gen/p/' + k]
+        mine = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        err = np.abs(mine - ref) / (np.abs(ref) + 1e-3)
+        worst = max(worst, float(err.max()))
+        assert (err < 2e-3).all(), (k, mine, ref)
+    print('worst param checksum rel err', worst)
+
+
+def test_full_size_forward_vs_oracle():
+    """Config-2 shapes (B=32, 1 s @ 24 kHz, n_q=8): encoder/decoder parity at full size,
+    codes bit-exact on every fp64-certified frame."""
+    torch.manual_seed(0)
+    from encx.model import EncodecModel
+    cfg = O.Config(target_bandwidths=(6.0,), audio_normalize=True)
+    p = model_state(cfg, 5)
+    m = EncodecModel._get_model([6.0], 24000, 1, causal=True, model_norm='weight_norm', audio_normalize=True)
+    x0 = synth_wave((32, 1, 24000), 1234)
+    xn, _ = O.normalize(T(x0))
+    with torch.no_grad():
+        emb_ref = O.run_plan(xn, p, cfg.enc_plan)
+    e = emb_ref.permute(0, 2, 1).reshape(-1, 128).double()
+    stats = np.zeros((8, 2, 128), np.float32)
+    for i in range(8):
+        stats[i, 0] = e.mean(0).float().numpy() * (1 if i == 0 else 0)
+        stats[i, 1] = e.std(0).float().numpy() * (0.6 ** i)
+    cbs = codebooks_from_stats(stats, 9, 8, cfg.n_q)
+    sd = dict(p)
+    for i, cb in enumerate(cbs):
+        for k, v in cb.items():
+            sd[f'quantizer.vq.layers.{i}._codebook.{k}'] = v
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    from encx import ops
+    x = G(x0)
+    with torch.no_grad():
+        emb = m.encoder(ops.normalize(x)[0])
+    assert rel(emb, emb_ref) < 2e-4, rel(emb, emb_ref)
+    # RVQ layer 0 codes: bit-exact on certified frames
+    idx = ops.rvq_argmin(emb.contiguous(), m.quantizer.vq.layers[0]._codebook.embed).cpu().numpy()
+    xr = emb_ref.permute(0, 2, 1).reshape(-1, 128).double()
+    E = cbs[0]['embed'].double()
+    dist = (xr ** 2).sum(1, keepdim=True) - 2 * xr @ E.t() + (E ** 2).sum(1)[None]
+    s = torch.sort(dist, 1).values
+    cert = certified((s[:, 1] - s[:, 0]).numpy(), float((xr ** 2).sum(1).max()), float((E ** 2).sum(1).max()))
+    ref_idx = O.codebook_quantize(emb_ref.permute(0, 2, 1).reshape(-1, 128), cbs[0]['embed']).numpy()
+    assert cert.mean() > 0.9, cert.mean()
+    assert (idx[cert] == ref_idx[cert]).all()
+    # decoder on the same latent
+    with torch.no_grad():
+        y = m.decoder(emb)
+        y_ref = O.run_plan(emb_ref, p, cfg.dec_plan)
+    assert rel(y, y_ref) < 1e-3, rel(y, y_ref)
+
+
+def test_full_size_train_steps_run():
+    """Fresh model (kmeans init on the first batch), 3 config-2 steps at full size."""
+    torch.manual_seed(0)
+    from encx.model import EncodecModel
+    from encx.train import Trainer
+    m = EncodecModel._get_model([6.0], 24000, 1, causal=True, model_norm='weight_norm',
+                                audio_normalize=True).to(DEV)
+    tr = Trainer(m, None, lr=3e-4, warmup_iter=10)
+    x = G(synth_wave((32, 1, 24000), 77))
+    hist = []
+    for _ in range(3):
+        out = tr.step(x)
+        hist.append({k: float(v) for k, v in out.items()})
+    for h in hist:
+        assert all(np.isfinite(v) for v in h.values()), h
+    cb = m.quantizer.vq.layers[0]._codebook
+    assert float(cb.inited) == 1.0 and torch.isfinite(cb.embed).all()
+    assert torch.isfinite(tr.opt.flat).all()
+    assert hist[-1]['l_f'] < hist[0]['l_f'] * 1.05
