@@ -12,9 +12,13 @@
 //                folded back and act' applied in the epilogue; pad positions go to a side
 //                buffer that conv_fold_edges adds in a fixed order).
 //   conv_wgrad   dW[a][(c,k)] = sum_{b,t} L[b][a][t] * R[b][c][t*s + k*d - pl], split over
-//                (b, t) ranges into a workspace and summed by wgrad_reduce in a fixed order.
-// Plus VALU kernels for the 1-channel ends of the stack (Cout = 1 forward, tiny wgrads),
-// where a 32-wide MFMA tile would be >90% padding.
+//                (b, t) ranges into a workspace and summed by wgrad_reduce in a fixed order;
+//                for narrow weights (Cin*K <= 32) the 4 waves split the t range of one 32x32
+//                tile instead of tiling N.
+// Low-rate layers (T = 75 / 600 at B = 32) would launch fewer workgroups than the chip has
+// CUs, so conv_fwd / conv_poly split the channel reduction (split-K) into a workspace and a
+// fixed-order reduce kernel applies the epilogue: deterministic, no float atomics.
+// Plus VALU kernels for the 1-channel ends of the stack (Cout = 1 forward, tiny wgrads).
 #include "common.h"
 #include "prof.h"
 
@@ -30,10 +34,13 @@ struct FwdArgs {
     const float* res;
     float* y;
     const float* xact;  // epilogue act' source (backward-data use), or null
+    float* part;        // split-K partials [KS][B][Cout][Tout]
     int B, Cin, Tin, Cout, Tout, K, s, d, pl, e, mode, act;
     int epi_act, accumulate;
-    int CK;  // channels per LDS chunk (even)
-    int Up;  // LDS words per (ci, phase) row
+    int CK;   // channels per LDS chunk (even)
+    int Up;   // LDS words per (ci, phase) row
+    int KS;   // channel splits
+    int cps;  // channels per split (multiple of CK)
 };
 
 // y = [acc ? y : 0] + act'(xact) * (v + bias) + res
@@ -54,9 +61,11 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     float* Ws = smem + CK * S * Up;         // [K][CK][BM]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
-    const int t0 = blockIdx.x * BN, co0 = blockIdx.y * BM, b = blockIdx.z;
+    const int t0 = blockIdx.x * BN, co0 = blockIdx.y * BM;
+    const int b = blockIdx.z / a.KS, ks = blockIdx.z - (blockIdx.z / a.KS) * a.KS;
     const float* xb = a.x + (int64_t)b * a.Cin * a.Tin;
     const int span = S * Up;
+    const int cbeg = ks * a.cps, cend = min(a.Cin, cbeg + a.cps);
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -64,7 +73,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
-    for (int c0 = 0; c0 < a.Cin; c0 += CK) {
+    for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
         // stage activated input window, phase-major
         for (int i = tid; i < CK * span; i += NT) {
@@ -72,7 +81,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
             int u = q / S, ph = q - u * S;
             int c = c0 + cl;
             float v = 0.f;
-            if (c < a.Cin) {
+            if (c < cend) {
                 int m = pad_src(t0 * S + q, a.pl, a.Tin, a.e, a.mode);
                 if (m >= 0) v = act_apply(a.act, xb[(int64_t)c * a.Tin + m]);
             }
@@ -84,7 +93,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
             int cl = r % CK, k = r / CK;
             int c = c0 + cl, co = co0 + col;
             float v = 0.f;
-            if (c < a.Cin && co < a.Cout) v = a.wf[((int64_t)c * K + k) * a.Cout + co];
+            if (c < cend && co < a.Cout) v = a.wf[((int64_t)c * K + k) * a.Cout + co];
             Ws[(k * CK + cl) * BM + col] = v;
         }
         __syncthreads();
@@ -106,7 +115,6 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
             }
         }
     }
-    // epilogue: bias (+ residual), coalesced along t
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -115,10 +123,23 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int co = co0 + wm0 + i * 32 + mfma_row(r, lane);
-                if (co < a.Cout && t < a.Tout)
-                    fwd_store(a, ((int64_t)b * a.Cout + co) * a.Tout + t, co, acc[i][j][r]);
+                if (co < a.Cout && t < a.Tout) {
+                    const int64_t o = ((int64_t)b * a.Cout + co) * a.Tout + t;
+                    if (a.KS > 1) a.part[(int64_t)ks * a.B * a.Cout * a.Tout + o] = acc[i][j][r];
+                    else fwd_store(a, o, co, acc[i][j][r]);
+                }
             }
         }
+}
+
+__global__ void conv_fwd_reduce(FwdArgs a) {
+    const int64_t n = (int64_t)a.B * a.Cout * a.Tout;
+    int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n) return;
+    float v = 0.f;
+    for (int ks = 0; ks < a.KS; ++ks) v += a.part[(int64_t)ks * n + o];
+    const int co = (int)((o / a.Tout) % a.Cout);
+    fwd_store(a, o, co, v);
 }
 
 // ------------------------------------------------------------------------- polyphase
@@ -129,6 +150,7 @@ struct PolyArgs {
     const float* xact; // dgrad mode: pre-activation input for act'
     float* out;        // convtr: y [B][Co][Tout]; dgrad: dx [B][Co][Tx]
     float* side;       // dgrad: [B][Co][pl+pr]
+    float* part;       // split-K partials [KS][B][Co][Q], Q = ncols * s
     int B, Ci, Tin, Co, s, J;
     int mode;          // 0 convtr store, 1 dgrad fold
     int trim;          // convtr: trim_left
@@ -136,7 +158,27 @@ struct PolyArgs {
     int pl, pr, Tx;    // dgrad: pads, unpadded length
     int act, in_act, accumulate;
     int CK, Ub;        // chunk channels, LDS row length (BN + J - 1 [+pad])
+    int KS, cps, Q;
 };
+
+ENCX_DEV void poly_store(const PolyArgs& a, int b, int o, int qpos, float v) {
+    if (a.mode == 0) {
+        const int p = qpos - a.trim;
+        if (p >= 0 && p < a.Tout)
+            a.out[((int64_t)b * a.Co + o) * a.Tout + p] = v + (a.bias ? a.bias[o] : 0.f);
+    } else {
+        const int m = qpos - a.pl;
+        if (m >= 0 && m < a.Tx) {
+            const int64_t idx = ((int64_t)b * a.Co + o) * a.Tx + m;
+            float g = v;
+            if (a.act != ENCX_ACT_NONE) g *= act_grad(a.act, a.xact[idx]);
+            a.out[idx] = a.accumulate ? a.out[idx] + g : g;
+        } else if (qpos >= 0 && qpos < a.pl + a.Tx + a.pr) {
+            const int slot = m < 0 ? qpos : a.pl + (m - a.Tx);
+            a.side[((int64_t)b * a.Co + o) * (a.pl + a.pr) + slot] = v;
+        }
+    }
+}
 
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
@@ -148,8 +190,10 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
     float* As = smem + CK * Ub;     // [J][CK][BM]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
-    const int u0 = blockIdx.x * BN, m0 = blockIdx.y * BM, b = blockIdx.z;
+    const int u0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int b = blockIdx.z / a.KS, ks = blockIdx.z - (blockIdx.z / a.KS) * a.KS;
     const float* ib = a.in + (int64_t)b * a.Ci * a.Tin;
+    const int cbeg = ks * a.cps, cend = min(a.Ci, cbeg + a.cps);
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -158,13 +202,13 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
     const int wlen = BN + J - 1;
-    for (int c0 = 0; c0 < a.Ci; c0 += CK) {
+    for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
         for (int i = tid; i < CK * wlen; i += NT) {
             int cl = i / wlen, w = i - cl * wlen;
             int c = c0 + cl, t = u0 - (J - 1) + w;
             float v = 0.f;
-            if (c < a.Ci && t >= 0 && t < a.Tin) v = act_apply(a.in_act, ib[(int64_t)c * a.Tin + t]);
+            if (c < cend && t >= 0 && t < a.Tin) v = act_apply(a.in_act, ib[(int64_t)c * a.Tin + t]);
             Xs[cl * Ub + w] = v;
         }
         for (int i = tid; i < J * CK * BM; i += NT) {
@@ -172,7 +216,7 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
             int cl = r % CK, q = r / CK;
             int c = c0 + cl, row = m0 + col;
             float v = 0.f;
-            if (c < a.Ci && row < M) v = a.wp[((int64_t)c * J + q) * M + row];
+            if (c < cend && row < M) v = a.wp[((int64_t)c * J + q) * M + row];
             As[(q * CK + cl) * BM + col] = v;
         }
         __syncthreads();
@@ -204,25 +248,25 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
                 if (row >= M) continue;
                 const int o = row / S, rr = row - o * S;
                 const int qpos = u * S + rr;
-                const float v = acc[i][j][r];
-                if (a.mode == 0) {
-                    const int p = qpos - a.trim;
-                    if (p >= 0 && p < a.Tout)
-                        a.out[((int64_t)b * a.Co + o) * a.Tout + p] = v + (a.bias ? a.bias[o] : 0.f);
+                if (a.KS > 1) {
+                    if (qpos < a.Q)
+                        a.part[(((int64_t)ks * a.B + b) * a.Co + o) * a.Q + qpos] = acc[i][j][r];
                 } else {
-                    const int m = qpos - a.pl;
-                    if (m >= 0 && m < a.Tx) {
-                        const int64_t idx = ((int64_t)b * a.Co + o) * a.Tx + m;
-                        float g = v;
-                        if (a.act != ENCX_ACT_NONE) g *= act_grad(a.act, a.xact[idx]);
-                        a.out[idx] = a.accumulate ? a.out[idx] + g : g;
-                    } else if (qpos >= 0 && qpos < a.pl + a.Tx + a.pr) {
-                        const int slot = m < 0 ? qpos : a.pl + (m - a.Tx);
-                        a.side[((int64_t)b * a.Co + o) * (a.pl + a.pr) + slot] = v;
-                    }
+                    poly_store(a, b, o, qpos, acc[i][j][r]);
                 }
             }
         }
+}
+
+__global__ void conv_poly_reduce(PolyArgs a) {
+    const int64_t n = (int64_t)a.B * a.Co * a.Q;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = 0.f;
+    for (int ks = 0; ks < a.KS; ++ks) v += a.part[(int64_t)ks * n + i];
+    const int qpos = (int)(i % a.Q);
+    const int64_t bo = i / a.Q;
+    poly_store(a, (int)(bo / a.Co), (int)(bo % a.Co), qpos, v);
 }
 
 // Add the gradients that landed on pad positions back onto their reflect sources, in slot
@@ -256,15 +300,18 @@ struct WgArgs {
     int NCmax;       // R window rows
 };
 
-template <int BM, int BN, int WM, int WN>
+// WK > 1: the WK waves share one (32*TM) x (32*TN) tile and split each chunk's t range
+template <int BM, int BN, int WM, int WN, int WK>
 __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    static_assert(WM * WN * WK == 4, "4 waves");
     extern __shared__ float smem[];
     const int BT = a.BT, WLp = a.WLp, K = a.K, N = a.C * a.K;
     float* Ls = smem;              // [BT][BM]
     float* Rs = smem + BT * BM;    // [NCmax][WLp]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int wk = wave % WK, wmn = wave / WK;
+    const int wm0 = (wmn / WN) * TM * 32, wn0 = (wmn % WN) * TN * 32;
     const int a0 = blockIdx.y * BM, n0 = blockIdx.x * BN, split = blockIdx.z;
     const int c_first = n0 / K;
     const int nchunks_t = (a.Tl + BT - 1) / BT;
@@ -287,6 +334,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     const int it_beg = split * a.per_split;
     const int it_end = min(a.items, it_beg + a.per_split);
     const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
+    const int tw = BT / WK;  // t per wave per chunk
     for (int it = it_beg; it < it_end; ++it) {
         const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
         const float* Lb = a.L + (int64_t)b * a.A * a.Tl;
@@ -310,7 +358,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
             Rs[cr * WLp + w] = v;
         }
         __syncthreads();
-        for (int tp = 0; tp < BT; tp += 2) {
+        for (int tp = wk * tw; tp < (wk + 1) * tw; tp += 2) {
             const int tl = tp + h;
             float av[TM], bv[TN];
 #pragma unroll
@@ -322,6 +370,29 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
         }
+    }
+    if (WK > 1) {  // combine the waves' partial tiles in wave order (deterministic)
+        __syncthreads();
+        float* red = smem;  // [WK][TM*TN*16][64]
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    red[((wk * TM * TN + i * TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+        __syncthreads();
+        if (wk != 0) return;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float v = red[((i * TN + j) * 16 + r) * 64 + lane];
+                    for (int w = 1; w < WK; ++w) v += red[((w * TM * TN + i * TN + j) * 16 + r) * 64 + lane];
+                    acc[i][j][r] = v;
+                }
     }
     float* wsb = a.ws + (int64_t)split * a.A * N;
 #pragma unroll
@@ -346,7 +417,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
     const int split = blockIdx.x, tid = threadIdx.x;
     const int nchunks_t = (a.Tl + BT - 1) / BT;
     const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // AN <= 4 * NT
+    float acc = 0.f;  // AN <= NT
     const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
     for (int it = it_beg; it < it_end; ++it) {
         const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
@@ -363,32 +434,35 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
             Rs[c * a.WLp + w] = m >= 0 ? act_apply(a.actR, Rb[(int64_t)c * a.Tr + m]) : 0.f;
         }
         __syncthreads();
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-            int o = tid + z * NT;
-            if (o < AN) {
-                int aa = o / N, n = o - aa * N, c = n / K, k = n - c * K;
-                const float* lp = Ls + aa * BT;
-                const float* rp = Rs + c * a.WLp + k * a.d;
-                float sacc = acc[z];
-                for (int tl = 0; tl < BT; ++tl) sacc = fmaf(lp[tl], rp[tl * a.s], sacc);
-                acc[z] = sacc;
+        if (tid < AN) {
+            int aa = tid / N, n = tid - aa * N, c = n / K, k = n - c * K;
+            const float* lp = Ls + aa * BT;
+            const float* rp = Rs + c * a.WLp + k * a.d;
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 independent chains
+            for (int tl = 0; tl < BT; tl += 4) {
+                s0 = fmaf(lp[tl], rp[tl * a.s], s0);
+                s1 = fmaf(lp[tl + 1], rp[(tl + 1) * a.s], s1);
+                s2 = fmaf(lp[tl + 2], rp[(tl + 2) * a.s], s2);
+                s3 = fmaf(lp[tl + 3], rp[(tl + 3) * a.s], s3);
             }
+            acc += (s0 + s1) + (s2 + s3);
         }
     }
-#pragma unroll
-    for (int z = 0; z < 4; ++z) {
-        int o = tid + z * NT;
-        if (o < AN) a.ws[(int64_t)split * AN + o] = acc[z];
-    }
+    if (tid < AN) a.ws[(int64_t)split * AN + tid] = acc;
 }
 
-__global__ void wgrad_reduce(const float* ws, float* dw, int64_t AN, int S, int accumulate) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= AN) return;
+// dw[i] = [acc ? dw : 0] + sum_s ws[s][i]: SL lanes per output, each summing a strided slice
+// of the splits, then a fixed xor-tree across the SL lanes (deterministic).
+__global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, float* dw, int64_t AN, int S,
+                                                    int SL, int accumulate) {
+    const int per_block = 256 / SL;
+    const int sl = threadIdx.x % SL;
+    const int64_t i = (int64_t)blockIdx.x * per_block + threadIdx.x / SL;
     float v = 0.f;
-    for (int sidx = 0; sidx < S; ++sidx) v += ws[(int64_t)sidx * AN + i];
-    dw[i] = accumulate ? dw[i] + v : v;
+    if (i < AN)
+        for (int s = sl; s < S; s += SL) v += ws[(int64_t)s * AN + i];
+    for (int o = SL >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (sl == 0 && i < AN) dw[i] = accumulate ? dw[i] + v : v;
 }
 
 // VALU forward for Cout <= 4 (decoder's final 32 -> 1 conv): thread per output sample.
@@ -433,110 +507,180 @@ __global__ __launch_bounds__(NT) void conv_fwd_small_kernel(FwdArgs a) {
             fwd_store(a, ((int64_t)b * a.Cout + co) * a.Tout + t, co, acc[co]);
 }
 
-// ------------------------------------------------------------------------- launch helpers
-template <int BM, int BN, int WM, int WN>
-int launch_fwd(const FwdArgs& a, hipStream_t st) {
-    dim3 grid(cdiv(a.Tout, BN), cdiv(a.Cout, BM), a.B);
-    size_t lds = (size_t)(a.CK * a.s * a.Up + a.K * a.CK * BM) * sizeof(float);
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
-    return 0;
-}
-
-template <int BM, int BN, int WM, int WN>
-int launch_poly(const PolyArgs& a, int ncols, hipStream_t st) {
-    dim3 grid(cdiv(ncols, BN), cdiv((int64_t)a.Co * a.s, BM), a.B);
-    size_t lds = (size_t)(a.CK * a.Ub + a.J * a.CK * BM) * sizeof(float);
-    hipLaunchKernelGGL((conv_poly_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
-    return 0;
-}
-
-template <int BM, int BN, int WM, int WN>
-int launch_wg(const WgArgs& a, int splits, hipStream_t st) {
-    dim3 grid(cdiv((int64_t)a.C * a.K, BN), cdiv(a.A, BM), splits);
-    size_t lds = (size_t)(a.BT * BM + a.NCmax * a.WLp) * sizeof(float);
-    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
-    return 0;
-}
-
+// ------------------------------------------------------------------------- planning
 static int even_up(int v) { return (v + 1) & ~1; }
 
-// tile-shape choice: M rows (output channels / polyphase rows), N columns (time)
 enum Tile { T32x128, T64x64, T64x128, T128x32, T128x64, T128x128 };
 static Tile pick_tile(int64_t M, int64_t N) {
-    if (N <= 48) return T128x32;
+    if (N <= 96) return T128x32;
     if (M <= 32) return T32x128;
-    if (M <= 64) return N <= 96 ? T64x64 : T64x128;
-    if (N <= 96) return T128x64;
+    if (M <= 64) return T64x128;
     return T128x128;
 }
 static int tile_bm(Tile t) { return (t == T32x128) ? 32 : (t == T64x64 || t == T64x128) ? 64 : 128; }
+static int tile_bn(Tile t) { return (t == T128x32) ? 32 : (t == T64x64 || t == T128x64) ? 64 : 128; }
 
-int conv_fwd_dispatch(FwdArgs a, hipStream_t st) {
-    // chunk size: ~64 reduction elements per LDS stage
-    int ck = 64 / a.K;
-    if (ck < 2) ck = 2;
-    ck = even_up(ck);
-    if (ck > even_up(a.Cin)) ck = even_up(a.Cin);
-    a.CK = ck;
-    Tile t = pick_tile(a.Cout, a.Tout);
-    int BN = (t == T128x32) ? 32 : (t == T64x64 || t == T128x64) ? 64 : 128;
-    a.Up = BN + ((a.K - 1) * a.d) / a.s + 1;
-    if ((a.Up & 31) == 0) a.Up += 1;
-    switch (t) {
-        case T32x128: return launch_fwd<32, 128, 1, 4>(a, st);
-        case T64x64: return launch_fwd<64, 64, 2, 2>(a, st);
-        case T64x128: return launch_fwd<64, 128, 2, 2>(a, st);
-        case T128x32: return launch_fwd<128, 32, 4, 1>(a, st);
-        case T128x64: return launch_fwd<128, 64, 2, 2>(a, st);
-        default: return launch_fwd<128, 128, 2, 2>(a, st);
+// split the channel reduction when the plain grid would underfill the 256 CUs
+static void plan_split(int64_t blocks, int C, int CK, int* KS, int* cps) {
+    int nch = (C + CK - 1) / CK;
+    int ks = 1;
+    if (blocks < 1024 && nch >= 4) {
+        ks = (int)cdiv(1024, blocks);
+        if (ks > nch / 2) ks = nch / 2;
+        if (ks > 16) ks = 16;
+        if (ks < 1) ks = 1;
     }
+    int per = (int)cdiv(nch, ks);
+    *cps = per * CK;
+    *KS = (int)cdiv(C, *cps);
 }
 
-int poly_dispatch(PolyArgs a, int ncols, hipStream_t st) {
-    int ck = 64 / a.J;
+struct FwdPlan { Tile t; int CK, Up, KS, cps; bool small; };
+static FwdPlan plan_fwd(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K, int64_t s,
+                        int64_t d) {
+    FwdPlan p;
+    p.small = Cout <= 4;
+    int ck = (int)(64 / K);
     if (ck < 2) ck = 2;
     ck = even_up(ck);
-    if (ck > even_up(a.Ci)) ck = even_up(a.Ci);
-    a.CK = ck;
-    Tile t = pick_tile((int64_t)a.Co * a.s, ncols);
-    int BN = (t == T128x32) ? 32 : (t == T64x64 || t == T128x64) ? 64 : 128;
-    a.Ub = BN + a.J - 1;
-    if ((a.Ub & 31) == 0) a.Ub += 1;
-    switch (t) {
-        case T32x128: return launch_poly<32, 128, 1, 4>(a, ncols, st);
-        case T64x64: return launch_poly<64, 64, 2, 2>(a, ncols, st);
-        case T64x128: return launch_poly<64, 128, 2, 2>(a, ncols, st);
-        case T128x32: return launch_poly<128, 32, 4, 1>(a, ncols, st);
-        case T128x64: return launch_poly<128, 64, 2, 2>(a, ncols, st);
-        default: return launch_poly<128, 128, 2, 2>(a, ncols, st);
+    if (ck > even_up((int)Cin)) ck = even_up((int)Cin);
+    p.CK = ck;
+    p.t = pick_tile(Cout, Tout);
+    int BN = tile_bn(p.t);
+    p.Up = BN + (int)(((K - 1) * d) / s) + 1;
+    if ((p.Up & 31) == 0) p.Up += 1;
+    int64_t blocks = cdiv(Tout, BN) * cdiv(Cout, tile_bm(p.t)) * B;
+    p.KS = 1;
+    p.cps = (int)Cin;
+    if (!p.small) plan_split(blocks, (int)Cin, ck, &p.KS, &p.cps);
+    return p;
+}
+
+struct PolyPlan { Tile t; int CK, Ub, KS, cps; };
+static PolyPlan plan_poly(int64_t B, int64_t Ci, int64_t M, int64_t ncols, int64_t J) {
+    PolyPlan p;
+    int ck = (int)(64 / J);
+    if (ck < 2) ck = 2;
+    ck = even_up(ck);
+    if (ck > even_up((int)Ci)) ck = even_up((int)Ci);
+    p.CK = ck;
+    p.t = pick_tile(M, ncols);
+    int BN = tile_bn(p.t);
+    p.Ub = BN + (int)J - 1;
+    if ((p.Ub & 31) == 0) p.Ub += 1;
+    int64_t blocks = cdiv(ncols, BN) * cdiv(M, tile_bm(p.t)) * B;
+    plan_split(blocks, (int)Ci, ck, &p.KS, &p.cps);
+    return p;
+}
+
+// ------------------------------------------------------------------------- launch helpers
+template <int BM, int BN, int WM, int WN>
+void launch_fwd(const FwdArgs& a, hipStream_t st) {
+    dim3 grid(cdiv(a.Tout, BN), cdiv(a.Cout, BM), a.B * a.KS);
+    size_t lds = (size_t)(a.CK * a.s * a.Up + a.K * a.CK * BM) * sizeof(float);
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_poly(const PolyArgs& a, int ncols, hipStream_t st) {
+    dim3 grid(cdiv(ncols, BN), cdiv((int64_t)a.Co * a.s, BM), a.B * a.KS);
+    size_t lds = (size_t)(a.CK * a.Ub + a.J * a.CK * BM) * sizeof(float);
+    hipLaunchKernelGGL((conv_poly_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+}
+
+int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
+    FwdPlan p = plan_fwd(a.B, a.Cin, a.Cout, a.Tout, a.K, a.s, a.d);
+    if (p.small) {
+        int ck = 64 / a.K;
+        if (ck < 1) ck = 1;
+        if (ck > a.Cin) ck = a.Cin;
+        a.CK = ck;
+        a.KS = 1;
+        a.cps = a.Cin;
+        const int WL = (NT - 1) * a.s + (a.K - 1) * a.d + 1;
+        size_t lds = (size_t)(ck * WL + a.Cout * ck * a.K) * sizeof(float);
+        ENCX_REQUIRE(lds <= 160 * 1024);
+        hipLaunchKernelGGL(conv_fwd_small_kernel, dim3(cdiv(a.Tout, NT), 1, a.B), dim3(NT), lds, st, a);
+        ENCX_CHECK_LAUNCH();
+        return 0;
     }
+    a.CK = p.CK; a.Up = p.Up; a.KS = p.KS; a.cps = p.cps; a.part = ws;
+    ENCX_REQUIRE(a.KS == 1 || ws);
+    switch (p.t) {
+        case T32x128: launch_fwd<32, 128, 1, 4>(a, st); break;
+        case T64x64: launch_fwd<64, 64, 2, 2>(a, st); break;
+        case T64x128: launch_fwd<64, 128, 2, 2>(a, st); break;
+        case T128x32: launch_fwd<128, 32, 4, 1>(a, st); break;
+        case T128x64: launch_fwd<128, 64, 2, 2>(a, st); break;
+        default: launch_fwd<128, 128, 2, 2>(a, st); break;
+    }
+    ENCX_CHECK_LAUNCH();
+    if (a.KS > 1) {
+        int64_t n = (int64_t)a.B * a.Cout * a.Tout;
+        hipLaunchKernelGGL(conv_fwd_reduce, dim3(cdiv(n, 256)), dim3(256), 0, st, a);
+        ENCX_CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K, int64_t s, int64_t d) {
+    FwdPlan p = plan_fwd(B, Cin, Cout, Tout, K, s, d);
+    return (p.small || p.KS == 1) ? 0 : (size_t)p.KS * B * Cout * Tout * sizeof(float);
+}
+
+int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
+    PolyPlan p = plan_poly(a.B, a.Ci, (int64_t)a.Co * a.s, ncols, a.J);
+    a.CK = p.CK; a.Ub = p.Ub; a.KS = p.KS; a.cps = p.cps; a.Q = ncols * a.s; a.part = ws;
+    ENCX_REQUIRE(a.KS == 1 || ws);
+    switch (p.t) {
+        case T32x128: launch_poly<32, 128, 1, 4>(a, ncols, st); break;
+        case T64x64: launch_poly<64, 64, 2, 2>(a, ncols, st); break;
+        case T64x128: launch_poly<64, 128, 2, 2>(a, ncols, st); break;
+        case T128x32: launch_poly<128, 32, 4, 1>(a, ncols, st); break;
+        case T128x64: launch_poly<128, 64, 2, 2>(a, ncols, st); break;
+        default: launch_poly<128, 128, 2, 2>(a, ncols, st); break;
+    }
+    ENCX_CHECK_LAUNCH();
+    if (a.KS > 1) {
+        int64_t n = (int64_t)a.B * a.Co * a.Q;
+        hipLaunchKernelGGL(conv_poly_reduce, dim3(cdiv(n, 256)), dim3(256), 0, st, a);
+        ENCX_CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+size_t poly_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int64_t J) {
+    PolyPlan p = plan_poly(B, Ci, Co * s, ncols, J);
+    return p.KS == 1 ? 0 : (size_t)p.KS * B * Co * ncols * s * sizeof(float);
 }
 
 // wgrad planning shared by the launcher and the workspace query
 struct WgPlan {
-    bool small;
+    int kind;  // 0 VALU small, 1 narrow (32x32, waves split t), 2 tiled
     int BM, BN, BT, splits, items, per_split, tiles;
 };
 static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
     WgPlan p;
     const int64_t N = C * K;
-    p.small = (A * N <= 4 * NT);
-    p.BT = p.small ? 256 : 32;
-    if (!p.small) {
-        Tile t = (A <= 32) ? T32x128 : (A <= 64 ? T64x128 : T128x128);
-        p.BM = tile_bm(t);
-        p.BN = (t == T32x128) ? 128 : 128;
-        p.tiles = (int)(cdiv(N, p.BN) * cdiv(A, p.BM));
+    if (A * N <= NT) {
+        p.kind = 0; p.BT = 256; p.BM = p.BN = 0; p.tiles = 1;
+    } else if (N <= 32 && A <= 64) {
+        p.kind = 1; p.BT = 64; p.BM = A <= 32 ? 32 : 64; p.BN = 32;
+        p.tiles = (int)cdiv(A, p.BM);
     } else {
-        p.BM = p.BN = 0;
-        p.tiles = 1;
+        p.kind = 2; p.BT = 32;
+        Tile t = (A <= 32) ? T32x128 : (A <= 64 ? T64x128 : T128x128);
+        p.BM = tile_bm(t); p.BN = 128;
+        p.tiles = (int)(cdiv(N, p.BN) * cdiv(A, p.BM));
     }
     p.items = (int)(B * cdiv(Tl, p.BT));
-    int64_t want = cdiv(2048, p.tiles);
-    int64_t cap = (64ll << 20) / (4 * A * N);  // <= 64 MB of partials
+    int64_t want = cdiv(1024, p.tiles);                 // ~1024 workgroups in flight
+    int64_t cap = (64ll << 20) / (4 * A * N);           // <= 64 MB of partials
+    int64_t minper = cdiv(p.items, (int64_t)p.items >= 8 ? 8 : 1);
+    (void)minper;
     if (cap < 1) cap = 1;
     int64_t sp = want < cap ? want : cap;
-    if (sp > p.items) sp = p.items;
+    if (sp > p.items / 4) sp = p.items / 4;              // >= 4 chunks of t per workgroup
     if (sp < 1) sp = 1;
     p.per_split = (int)cdiv(p.items, sp);
     p.splits = (int)cdiv(p.items, p.per_split);
@@ -547,6 +691,15 @@ static int wlp_for(int WL, int K) {
     // row stride == K (mod 32) so 32 consecutive (c,k) columns hit 32 distinct banks
     int r = ((K % 32) - (WL % 32) + 32) % 32;
     return WL + r;
+}
+
+template <int BM, int BN, int WM, int WN, int WK>
+void launch_wg(const WgArgs& a, int splits, hipStream_t st) {
+    dim3 grid(cdiv((int64_t)a.C * a.K, BN), cdiv(a.A, BM), splits);
+    size_t lds = (size_t)(a.BT * BM + a.NCmax * a.WLp) * sizeof(float);
+    size_t red = (size_t)WK * (BM / WM / 32) * (BN / WN / 32) * 16 * 64 * sizeof(float);
+    if (WK > 1 && red > lds) lds = red;
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, WK>), grid, dim3(NT), lds, st, a);
 }
 
 int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, int64_t A,
@@ -560,7 +713,7 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
     a.actR = actR; a.BT = p.BT; a.items = p.items; a.per_split = p.per_split;
     const int WL = (p.BT - 1) * a.s + (a.K - 1) * a.d + 1;
     const int64_t AN = A * C * K;
-    if (p.small) {
+    if (p.kind == 0) {
         a.WLp = WL;
         a.NCmax = (int)C;
         size_t lds = (size_t)(A * p.BT + C * WL) * sizeof(float);
@@ -570,13 +723,18 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
         a.WLp = wlp_for(WL, a.K);
         a.NCmax = (int)((p.BN + a.K - 1) / a.K + 1);
         if (a.NCmax > C) a.NCmax = (int)C;
-        if (p.BM == 32) launch_wg<32, 128, 1, 4>(a, p.splits, st);
-        else if (p.BM == 64) launch_wg<64, 128, 2, 2>(a, p.splits, st);
-        else launch_wg<128, 128, 2, 2>(a, p.splits, st);
+        if (p.kind == 1) {
+            if (p.BM == 32) launch_wg<32, 32, 1, 1, 4>(a, p.splits, st);
+            else launch_wg<64, 32, 2, 1, 2>(a, p.splits, st);
+        } else if (p.BM == 32) launch_wg<32, 128, 1, 4, 1>(a, p.splits, st);
+        else if (p.BM == 64) launch_wg<64, 128, 2, 2, 1>(a, p.splits, st);
+        else launch_wg<128, 128, 2, 2, 1>(a, p.splits, st);
     }
     ENCX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(wgrad_reduce, dim3(cdiv(AN, 256)), dim3(256), 0, st, ws, dw, AN, p.splits,
-                       accumulate);
+    int SL = 1;
+    while (SL < 64 && SL * 16 < p.splits) SL <<= 1;
+    hipLaunchKernelGGL(wgrad_reduce, dim3(cdiv(AN, 256 / SL)), dim3(256), 0, st, ws, dw, AN, p.splits,
+                       SL, accumulate);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
@@ -586,58 +744,57 @@ size_t wgrad_ws_bytes(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
     return (size_t)p.splits * A * C * K * sizeof(float);
 }
 
+static size_t maxz(size_t a, size_t b) { return a > b ? a : b; }
+
 }  // namespace
 
 // ============================================================================ C ABI
 extern "C" {
 
-static int conv_fwd_impl(FwdArgs a, hipStream_t st) {
-    if (a.Cout <= 4) {
-        int ck = 64 / a.K;
-        if (ck < 1) ck = 1;
-        if (ck > a.Cin) ck = a.Cin;
-        a.CK = ck;
-        const int WL = (NT - 1) * a.s + (a.K - 1) * a.d + 1;
-        size_t lds = (size_t)(ck * WL + a.Cout * ck * a.K) * sizeof(float);
-        ENCX_REQUIRE(lds <= 160 * 1024);
-        hipLaunchKernelGGL(conv_fwd_small_kernel, dim3(cdiv(a.Tout, NT), 1, a.B), dim3(NT), lds, st, a);
-    } else {
-        conv_fwd_dispatch(a, st);
-    }
-    ENCX_CHECK_LAUNCH();
-    return 0;
+size_t encx_conv1d_fwd_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K,
+                                 int64_t stride, int64_t dilation) {
+    return conv_fwd_ws(B, Cin, Cout, Tout, K, stride, dilation);
 }
 
 int encx_conv1d_fwd(const float* x, const float* wf, const float* bias, const float* residual,
-                    float* y, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
-                    int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
+                    float* y, float* ws, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
+                    int64_t Tout, int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
                     int64_t short_ext, int pad_mode, int pre_act, encx_stream_t stream) {
     ENCX_REQUIRE(x && wf && y && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0);
     ENCX_REQUIRE(K > 0 && stride > 0 && dilation > 0 && pad_left >= 0 && short_ext >= 0);
     hipStream_t st = (hipStream_t)stream;
     FwdArgs a;
-    a.x = x; a.wf = wf; a.bias = bias; a.res = residual; a.y = y; a.xact = nullptr;
+    a.x = x; a.wf = wf; a.bias = bias; a.res = residual; a.y = y; a.xact = nullptr; a.part = nullptr;
     a.B = (int)B; a.Cin = (int)Cin; a.Tin = (int)Tin; a.Cout = (int)Cout; a.Tout = (int)Tout;
     a.K = (int)K; a.s = (int)stride; a.d = (int)dilation; a.pl = (int)pad_left; a.e = (int)short_ext;
     a.mode = pad_mode; a.act = pre_act; a.epi_act = ENCX_ACT_NONE; a.accumulate = 0;
     encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
                        4.0 * (B * Cin * Tin + B * Cout * Tout * (residual ? 2 : 1) + Cin * K * Cout));
-    return conv_fwd_impl(a, st);
+    return conv_fwd_run(a, ws, st);
 }
 
-size_t encx_conv1d_bwd_data_workspace(int64_t B, int64_t Cin, int64_t pad_left, int64_t pad_right) {
-    return (size_t)(B * Cin * (pad_left + pad_right) + 1) * sizeof(float);
+size_t encx_conv1d_bwd_data_workspace(int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
+                                      int64_t Tout, int64_t K, int64_t stride, int64_t pad_left,
+                                      int64_t pad_right) {
+    const int64_t Tpad = pad_left + Tin + pad_right;
+    const int64_t ncols = cdiv(Tpad, stride);
+    size_t side = (size_t)(B * Cin * (pad_left + pad_right) + 1) * sizeof(float);
+    side = (side + 255) & ~(size_t)255;
+    return side + poly_ws(B, Cout, Cin, stride, ncols, cdiv(K, stride));
 }
 
-int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float* dx,
-                         float* side, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
-                         int64_t Tout, int64_t K, int64_t stride, int64_t pad_left,
-                         int64_t pad_right, int64_t short_ext, int pad_mode, int pre_act,
-                         int accumulate, encx_stream_t stream) {
-    ENCX_REQUIRE(dy && wp && dx && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0);
+int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float* dx, float* ws,
+                         int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                         int64_t K, int64_t stride, int64_t pad_left, int64_t pad_right,
+                         int64_t short_ext, int pad_mode, int pre_act, int accumulate,
+                         encx_stream_t stream) {
+    ENCX_REQUIRE(dy && wp && dx && ws && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0);
     ENCX_REQUIRE(pre_act == ENCX_ACT_NONE || x);
-    ENCX_REQUIRE((pad_left + pad_right) == 0 || side);
     hipStream_t st = (hipStream_t)stream;
+    size_t side_b = (size_t)(B * Cin * (pad_left + pad_right) + 1) * sizeof(float);
+    side_b = (side_b + 255) & ~(size_t)255;
+    float* side = ws;
+    float* part = (float*)((char*)ws + side_b);
     PolyArgs a;
     a.in = dy; a.wp = wp; a.bias = nullptr; a.xact = x; a.out = dx; a.side = side;
     a.B = (int)B; a.Ci = (int)Cout; a.Tin = (int)Tout; a.Co = (int)Cin; a.s = (int)stride;
@@ -648,8 +805,8 @@ int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float
     const int ncols = (int)cdiv(Tpad, stride);
     encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
                        4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout));
-    poly_dispatch(a, ncols, st);
-    ENCX_CHECK_LAUNCH();
+    int rc = poly_run(a, ncols, part, st);
+    if (rc) return rc;
     if (pad_left + pad_right > 0 && pad_mode == ENCX_PAD_REFLECT) {
         int rows = (int)(B * Cin);
         hipLaunchKernelGGL(conv_fold_edges, dim3(cdiv(rows, 256)), dim3(256), 0, st, side, x, dx,
@@ -677,12 +834,16 @@ int encx_conv1d_bwd_weight(const float* dy, const float* x, float* dw, float* db
 
 size_t encx_conv1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout,
                                         int64_t K) {
-    size_t a = wgrad_ws_bytes(B, Cout, Tout, Cin, K), b = encx_channel_sum_workspace(Cout);
-    return a > b ? a : b;
+    return maxz(wgrad_ws_bytes(B, Cout, Tout, Cin, K), encx_channel_sum_workspace(Cout));
 }
 
-int encx_convtr1d_fwd(const float* x, const float* wp, const float* bias, float* y, int64_t B,
-                      int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout, int64_t K,
+size_t encx_convtr1d_fwd_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K,
+                                   int64_t stride, int64_t trim_left) {
+    return poly_ws(B, Cin, Cout, stride, cdiv(Tout + trim_left, stride), cdiv(K, stride));
+}
+
+int encx_convtr1d_fwd(const float* x, const float* wp, const float* bias, float* y, float* ws,
+                      int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout, int64_t K,
                       int64_t stride, int64_t trim_left, int pre_act, encx_stream_t stream) {
     ENCX_REQUIRE(x && wp && y && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0);
     hipStream_t st = (hipStream_t)stream;
@@ -693,12 +854,15 @@ int encx_convtr1d_fwd(const float* x, const float* wp, const float* bias, float*
     a.pl = a.pr = a.Tx = 0; a.act = ENCX_ACT_NONE; a.in_act = pre_act; a.accumulate = 0;
     const int ncols = (int)cdiv(Tout + trim_left, stride);
     encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K, 4.0 * (B * Cin * Tin + B * Cout * Tout + Cin * K * Cout));
-    poly_dispatch(a, ncols, st);
-    ENCX_CHECK_LAUNCH();
-    return 0;
+    return poly_run(a, ncols, ws, st);
 }
 
-int encx_convtr1d_bwd_data(const float* dy, const float* wf, const float* x, float* dx,
+size_t encx_convtr1d_bwd_data_workspace(int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
+                                        int64_t K, int64_t stride) {
+    return conv_fwd_ws(B, Cout, Cin, Tin, K, stride, 1);
+}
+
+int encx_convtr1d_bwd_data(const float* dy, const float* wf, const float* x, float* dx, float* ws,
                            int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
                            int64_t K, int64_t stride, int64_t trim_left, int pre_act,
                            int accumulate, encx_stream_t stream) {
@@ -708,14 +872,14 @@ int encx_convtr1d_bwd_data(const float* dy, const float* wf, const float* x, flo
     ENCX_REQUIRE(pre_act == ENCX_ACT_NONE || x);
     hipStream_t st = (hipStream_t)stream;
     FwdArgs a;
-    a.x = dy; a.wf = wf; a.bias = nullptr; a.res = nullptr; a.y = dx;
+    a.x = dy; a.wf = wf; a.bias = nullptr; a.res = nullptr; a.y = dx; a.part = nullptr;
     a.xact = pre_act != ENCX_ACT_NONE ? x : nullptr;
     a.B = (int)B; a.Cin = (int)Cout; a.Tin = (int)Tout; a.Cout = (int)Cin; a.Tout = (int)Tin;
     a.K = (int)K; a.s = (int)stride; a.d = 1; a.pl = (int)trim_left; a.e = 0;
     a.mode = ENCX_PAD_ZERO; a.act = ENCX_ACT_NONE; a.epi_act = pre_act; a.accumulate = accumulate;
     encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K,
                        4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout));
-    return conv_fwd_impl(a, st);
+    return conv_fwd_run(a, ws, st);
 }
 
 int encx_convtr1d_bwd_weight(const float* x, const float* dy, float* dw, float* db, float* ws,
@@ -735,8 +899,7 @@ int encx_convtr1d_bwd_weight(const float* x, const float* dy, float* dw, float* 
 
 size_t encx_convtr1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tin,
                                           int64_t K) {
-    size_t a = wgrad_ws_bytes(B, Cin, Tin, Cout, K), b = encx_channel_sum_workspace(Cout);
-    return a > b ? a : b;
+    return maxz(wgrad_ws_bytes(B, Cin, Tin, Cout, K), encx_channel_sum_workspace(Cout));
 }
 
 }  // extern "C"

@@ -71,14 +71,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
 // launch with a tile picked from the problem shape
 template <class LD, class EP>
 int gemm_launch(const LD& ld, const EP& ep, int M, int N, int Kred, hipStream_t st) {
+    // 128x128 tiles when they still give >= 2 workgroups per CU, else 64x64 (256 CUs)
+    const int64_t big = cdiv(N, 128) * cdiv(M, 128);
     if (N <= 48) {
-        hipLaunchKernelGGL((gemm_kernel<128, 32, 4, 1, 16, LD, EP>), dim3(cdiv(N, 32), cdiv(M, 128)),
+        hipLaunchKernelGGL((gemm_kernel<128, 32, 4, 1, 32, LD, EP>), dim3(cdiv(N, 32), cdiv(M, 128)),
                            dim3(256), 0, st, ld, ep, M, N, Kred);
     } else if (N <= 96) {
-        hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, 16, LD, EP>), dim3(cdiv(N, 64), cdiv(M, 128)),
+        hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, 32, LD, EP>), dim3(cdiv(N, 64), cdiv(M, 128)),
+                           dim3(256), 0, st, ld, ep, M, N, Kred);
+    } else if (big < 512) {
+        hipLaunchKernelGGL((gemm_kernel<64, 64, 2, 2, 32, LD, EP>), dim3(cdiv(N, 64), cdiv(M, 64)),
                            dim3(256), 0, st, ld, ep, M, N, Kred);
     } else {
-        hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, 16, LD, EP>), dim3(cdiv(N, 128), cdiv(M, 128)),
+        hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, 32, LD, EP>), dim3(cdiv(N, 128), cdiv(M, 128)),
                            dim3(256), 0, st, ld, ep, M, N, Kred);
     }
     ENCX_CHECK_LAUNCH();

@@ -205,30 +205,41 @@ __global__ void rvq_gather_kernel(const float* embed, const int64_t* idx, float*
 }
 
 // wave per code: counts and sums over the frames assigned to it, ascending frame order
+// 16 waves per workgroup = 16 codes; the assignment vector is staged once per workgroup in
+// LDS (as int32) and scanned 64 frames per ballot.
+constexpr int BK_WAVES = 16, BK_CHUNK = 8192;
 template <int MODE>  // 0: EMA (core_vq.py:227-229), 1: kmeans (:92-100)
-__global__ __launch_bounds__(NT) void bucket_kernel(Rows x, const int64_t* idx, int N, int D, int Kc,
-                                                    float* cs, float* ea, float* means,
-                                                    int64_t* bins, float decay, float one_m) {
-    const int lane = threadIdx.x & 63, c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= Kc) return;
+__global__ __launch_bounds__(1024) void bucket_kernel(Rows x, const int64_t* idx, int N, int D,
+                                                      int Kc, float* cs, float* ea, float* means,
+                                                      int64_t* bins, float decay, float one_m) {
+    __shared__ int sidx[BK_CHUNK];
+    const int lane = threadIdx.x & 63, c = blockIdx.x * BK_WAVES + (threadIdx.x >> 6);
     float acc[4] = {0.f, 0.f, 0.f, 0.f};  // D <= 256
     int count = 0;
-    for (int n0 = 0; n0 < N; n0 += 64) {
-        const int n = n0 + lane;
-        const bool m = n < N && idx[n] == c;
-        uint64_t mask = __ballot(m);
-        while (mask) {
-            const int j = __ffsll((long long)mask) - 1;
-            mask &= mask - 1;
-            const int nn = n0 + j;
+    for (int base = 0; base < N; base += BK_CHUNK) {
+        const int nn_end = min(N - base, BK_CHUNK);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nn_end; i += blockDim.x) sidx[i] = (int)idx[base + i];
+        __syncthreads();
+        if (c >= Kc) continue;
+        for (int n0 = 0; n0 < nn_end; n0 += 64) {
+            const int n = n0 + lane;
+            const bool m = n < nn_end && sidx[n] == c;
+            uint64_t mask = __ballot(m);
+            while (mask) {
+                const int j = __ffsll((long long)mask) - 1;
+                mask &= mask - 1;
+                const int nn = base + n0 + j;
 #pragma unroll
-            for (int z = 0; z < 4; ++z) {
-                int d = lane + 64 * z;
-                if (d < D) acc[z] += x.at(nn, d);
+                for (int z = 0; z < 4; ++z) {
+                    int d = lane + 64 * z;
+                    if (d < D) acc[z] += x.at(nn, d);
+                }
+                ++count;
             }
-            ++count;
         }
     }
+    if (c >= Kc) return;
     if (MODE == 0) {
         if (lane == 0) cs[c] = fmaf((float)count, one_m, cs[c] * decay);
 #pragma unroll
@@ -367,7 +378,7 @@ int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float*
     ENCX_REQUIRE(x && idx && cluster_size && embed_avg && embed && D <= 256 && Kc > 0);
     hipStream_t st = (hipStream_t)stream;
     const float one_m = (float)(1.0 - (double)decay);
-    hipLaunchKernelGGL(bucket_kernel<0>, dim3(cdiv(Kc, 4)), dim3(NT), 0, st, bdt_rows(x, B, D, Tf),
+    hipLaunchKernelGGL(bucket_kernel<0>, dim3(cdiv(Kc, BK_WAVES)), dim3(64 * BK_WAVES), 0, st, bdt_rows(x, B, D, Tf),
                        idx, (int)(B * Tf), (int)D, (int)Kc, cluster_size, embed_avg, nullptr, nullptr,
                        decay, one_m);
     ENCX_CHECK_LAUNCH();
@@ -385,7 +396,7 @@ int encx_kmeans_step(const float* samples, float* means, int64_t* bins, int64_t*
     Rows r = nd_rows(samples, N, D);
     int rc = argmin_run(r, means, idx, keys, (int)N, (int)D, (int)Kc, 1, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(bucket_kernel<1>, dim3(cdiv(Kc, 4)), dim3(NT), 0, st, r, idx, (int)N, (int)D,
+    hipLaunchKernelGGL(bucket_kernel<1>, dim3(cdiv(Kc, BK_WAVES)), dim3(64 * BK_WAVES), 0, st, r, idx, (int)N, (int)D,
                        (int)Kc, nullptr, nullptr, means, bins, 0.f, 0.f);
     ENCX_CHECK_LAUNCH();
     return 0;

@@ -121,7 +121,8 @@ class EncodecModel(nn.Module):
             loss_w = None
             for emb, scale in frames:
                 qv = self.quantizer(emb, self.frame_rate, bw)
-                loss_w = qv.penalty if loss_w is None else loss_w + qv.penalty
+                pen = qv.penalty.reshape(1)  # loss_w = tensor([0.]) + penalty (model.py:199,208)
+                loss_w = pen if loss_w is None else loss_w + pen
                 codes.append((qv.quantized, scale))
             self.last_codes = [qv.codes]
             return self.decode(codes)[:, :, :x.shape[-1]], loss_w, frames

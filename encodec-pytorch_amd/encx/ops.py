@@ -19,6 +19,13 @@ def _f32(n, like):
     return torch.empty(int(n), device=like.device, dtype=torch.float32)
 
 
+def _ws(nbytes, like):
+    """Caller-owned workspace (PyTorch caching allocator); None when the kernel needs none."""
+    if nbytes == 0:
+        return None
+    return torch.empty((nbytes + 3) // 4, device=like.device, dtype=torch.float32)
+
+
 def _check(x, name='x'):
     if not x.is_cuda or x.dtype != torch.float32:
         raise RuntimeError(f'encx: {name} must be a float32 tensor on the GPU '
@@ -102,8 +109,9 @@ class Conv1dFn(torch.autograd.Function):
         if res is not None:
             res = res.contiguous()
             assert res.shape == y.shape
-        call('encx_conv1d_fwd', ptr(x), ptr(wf), ptr(b), ptr(res), ptr(y), B, Cin, T, Cout, tout, K,
-             s, d, pl, e, PAD[pad_mode], ACT[act], stream())
+        ws = _ws(lib.encx_conv1d_fwd_workspace(B, Cin, Cout, tout, K, s, d), x)
+        call('encx_conv1d_fwd', ptr(x), ptr(wf), ptr(b), ptr(res), ptr(y), ptr(ws), B, Cin, T, Cout,
+             tout, K, s, d, pl, e, PAD[pad_mode], ACT[act], stream())
         ctx.save_for_backward(x, v, g, wp)
         ctx.cfg = (K, s, d, pl, pr, e, tout, PAD[pad_mode], ACT[act], res is not None, b is not None)
         return y
@@ -119,8 +127,8 @@ class Conv1dFn(torch.autograd.Function):
         dx = dv = dg = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            side = _f32(lib.encx_conv1d_bwd_data_workspace(B, Cin, pl, pr) // 4, x)
-            call('encx_conv1d_bwd_data', ptr(dy), ptr(wp), ptr(x), ptr(dx), ptr(side), B, Cin, T,
+            ws = _ws(lib.encx_conv1d_bwd_data_workspace(B, Cin, T, Cout, tout, K, s, pl, pr), x)
+            call('encx_conv1d_bwd_data', ptr(dy), ptr(wp), ptr(x), ptr(dx), ptr(ws), B, Cin, T,
                  Cout, tout, K, s, pl, pr, e, mode, act, 0, st)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
             dw = torch.empty(Cout, Cin, K, device=x.device, dtype=torch.float32)
@@ -151,8 +159,9 @@ class ConvTr1dFn(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         wf, wp = _weight_prep(v, g, K, s, need_dx, True)
         y = torch.empty(B, Cout, tout, device=x.device, dtype=torch.float32)
-        call('encx_convtr1d_fwd', ptr(x), ptr(wp), ptr(b), ptr(y), B, Cin, T, Cout, tout, K, s,
-             trim_left, ACT[act], stream())
+        ws = _ws(lib.encx_convtr1d_fwd_workspace(B, Cin, Cout, tout, K, s, trim_left), x)
+        call('encx_convtr1d_fwd', ptr(x), ptr(wp), ptr(b), ptr(y), ptr(ws), B, Cin, T, Cout, tout, K,
+             s, trim_left, ACT[act], stream())
         ctx.save_for_backward(x, v, g, wf)
         ctx.cfg = (K, s, trim_left, tout, ACT[act], b is not None)
         return y
@@ -168,8 +177,9 @@ class ConvTr1dFn(torch.autograd.Function):
         dx = dv = dg = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            call('encx_convtr1d_bwd_data', ptr(dy), ptr(wf), ptr(x), ptr(dx), B, Cin, T, Cout, tout,
-                 K, s, trim_left, act, 0, st)
+            ws = _ws(lib.encx_convtr1d_bwd_data_workspace(B, Cin, T, Cout, K, s), x)
+            call('encx_convtr1d_bwd_data', ptr(dy), ptr(wf), ptr(x), ptr(dx), ptr(ws), B, Cin, T,
+                 Cout, tout, K, s, trim_left, act, 0, st)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
             dw = torch.empty(Cin, Cout, K, device=x.device, dtype=torch.float32)
             db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_b else None
@@ -378,7 +388,7 @@ class RVQTrainFn(torch.autograd.Function):
         ctx.save_for_backward(cdir)
         ctx.n_q, ctx.numel = n_q, numel
         ctx.mark_non_differentiable(codes)
-        return out, codes.view(n_q, B, T), penalty
+        return out, codes.view(n_q, B, T), penalty.view(())
 
     @staticmethod
     def backward(ctx, dq, dcodes, dpen):

@@ -64,20 +64,25 @@ int encx_weightnorm_bwd(const float* v, const float* g, const float* dw, float* 
  * the zero extension of a too-short reflect input, :86-91), then Conv1d (NormConv1d :119-122).
  * y[b,co,t] = bias[co] + sum_{ci,k} W[co,ci,k] act(xpad[b,ci,t*s+k*d]) (+ residual[b,co,t]).
  * pre_act = ENCX_ACT_ELU fuses the nn.ELU that precedes the conv in the SEANet stacks
- * (modules/seanet.py:49,124,136,204,223). residual may alias y (SEANetResnetBlock sum, :63). */
+ * (modules/seanet.py:49,124,136,204,223). residual may alias y (SEANetResnetBlock sum, :63).
+ * ws: encx_conv1d_fwd_workspace bytes (split-K partials of low-rate layers; may be 0). */
+size_t encx_conv1d_fwd_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K,
+                                 int64_t stride, int64_t dilation);
 int encx_conv1d_fwd(const float* x, const float* wf, const float* bias, const float* residual,
-                    float* y, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
-                    int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
+                    float* y, float* ws, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
+                    int64_t Tout, int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
                     int64_t short_ext, int pad_mode, int pre_act, encx_stream_t stream);
 /* d loss / d x of the above (with the pad folded back and the act' applied):
  * dx = [accumulate ? dx : 0] + act'(x) * fold(W^T * dy). `x` is the pre-activation input
- * (read only when pre_act != NONE). side: workspace of encx_conv1d_bwd_data_workspace bytes. */
-int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float* dx,
-                         float* side, int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
-                         int64_t Tout, int64_t K, int64_t stride, int64_t pad_left,
-                         int64_t pad_right, int64_t short_ext, int pad_mode, int pre_act,
-                         int accumulate, encx_stream_t stream);
-size_t encx_conv1d_bwd_data_workspace(int64_t B, int64_t Cin, int64_t pad_left, int64_t pad_right);
+ * (read only when pre_act != NONE). ws: encx_conv1d_bwd_data_workspace bytes. */
+size_t encx_conv1d_bwd_data_workspace(int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
+                                      int64_t Tout, int64_t K, int64_t stride, int64_t pad_left,
+                                      int64_t pad_right);
+int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float* dx, float* ws,
+                         int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                         int64_t K, int64_t stride, int64_t pad_left, int64_t pad_right,
+                         int64_t short_ext, int pad_mode, int pre_act, int accumulate,
+                         encx_stream_t stream);
 /* dW[co,ci,k] = sum_{b,t} dy[b,co,t] act(xpad[b,ci,t*s+k*d]); db[co] = sum dy (db may be NULL).
  * dw is [Cout][Cin][K]; accumulate as above. ws: encx_conv1d_bwd_weight_workspace bytes. */
 int encx_conv1d_bwd_weight(const float* dy, const float* x, float* dw, float* db, float* ws,
@@ -92,11 +97,17 @@ size_t encx_conv1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, in
  * SConvTranspose1d.forward (modules/conv.py:230-252): ConvTranspose1d then unpad1d (:99-105).
  * y[b,co,j] = bias[co] + sum_{ci,t,k: t*s+k = j+trim_left} Wt[ci,co,k] act(x[b,ci,t]),
  * j in [0,Tout). Polyphase: for each output phase r = (j+trim_left) mod s only the taps
- * k = r + s*q contribute, so the work is a dense GEMM over (co,r) x (b,u) x (ci,q). */
-int encx_convtr1d_fwd(const float* x, const float* wp, const float* bias, float* y, int64_t B,
-                      int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout, int64_t K,
+ * k = r + s*q contribute, so the work is a dense GEMM over (co,r) x (b,u) x (ci,q).
+ * ws: encx_convtr1d_fwd_workspace bytes. */
+size_t encx_convtr1d_fwd_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K,
+                                   int64_t stride, int64_t trim_left);
+int encx_convtr1d_fwd(const float* x, const float* wp, const float* bias, float* y, float* ws,
+                      int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout, int64_t K,
                       int64_t stride, int64_t trim_left, int pre_act, encx_stream_t stream);
-int encx_convtr1d_bwd_data(const float* dy, const float* wf, const float* x, float* dx,
+/* dx = [accumulate ? dx : 0] + act'(x) * sum_{co,k} Wt[ci,co,k] dy[co, t*s+k-trim_left]. */
+size_t encx_convtr1d_bwd_data_workspace(int64_t B, int64_t Cin, int64_t Tin, int64_t Cout,
+                                        int64_t K, int64_t stride);
+int encx_convtr1d_bwd_data(const float* dy, const float* wf, const float* x, float* dx, float* ws,
                            int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
                            int64_t K, int64_t stride, int64_t trim_left, int pre_act,
                            int accumulate, encx_stream_t stream);

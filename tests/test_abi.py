@@ -38,7 +38,7 @@ def test_host_only_queries():
     assert lib.encx_conv1d_bwd_weight_workspace(32, 32, 16, 24000, 3) > 0
     assert lib.encx_mel_tables_floats(32, 64) == 32 * 34 + 2 * 17 * 64
     # argument validation happens before any device call
-    assert lib.encx_conv1d_fwd(None, None, None, None, None, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, None) == 9001
+    assert lib.encx_conv1d_fwd(*([None] * 6 + [0] * 12 + [None])) == 9001
 
 
 def test_ops_refuse_cpu_tensors():
