@@ -510,6 +510,18 @@ __global__ __launch_bounds__(NT) void conv_fwd_small_kernel(FwdArgs a) {
 // ------------------------------------------------------------------------- planning
 static int even_up(int v) { return (v + 1) & ~1; }
 
+// channels per LDS stage: ~64 reduction elements, even, and preferably dividing C exactly
+// (a ragged last chunk is zero-padded MFMA work)
+static int pick_ck(int C, int taps) {
+    int cap = 64 / taps;
+    if (cap < 2) cap = 2;
+    cap = even_up(cap);
+    if (cap >= C) return even_up(C);
+    for (int ck = cap & ~1; ck >= 2; ck -= 2)
+        if (C % ck == 0 && ck * 2 >= cap) return ck;
+    return cap & ~1;
+}
+
 enum Tile { T32x128, T64x64, T64x128, T128x32, T128x64, T128x128 };
 static Tile pick_tile(int64_t M, int64_t N) {
     if (N <= 96) return T128x32;
@@ -540,10 +552,7 @@ static FwdPlan plan_fwd(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int6
                         int64_t d) {
     FwdPlan p;
     p.small = Cout <= 4;
-    int ck = (int)(64 / K);
-    if (ck < 2) ck = 2;
-    ck = even_up(ck);
-    if (ck > even_up((int)Cin)) ck = even_up((int)Cin);
+    const int ck = pick_ck((int)Cin, (int)K);
     p.CK = ck;
     p.t = pick_tile(Cout, Tout);
     int BN = tile_bn(p.t);
@@ -559,10 +568,7 @@ static FwdPlan plan_fwd(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int6
 struct PolyPlan { Tile t; int CK, Ub, KS, cps; };
 static PolyPlan plan_poly(int64_t B, int64_t Ci, int64_t M, int64_t ncols, int64_t J) {
     PolyPlan p;
-    int ck = (int)(64 / J);
-    if (ck < 2) ck = 2;
-    ck = even_up(ck);
-    if (ck > even_up((int)Ci)) ck = even_up((int)Ci);
+    const int ck = pick_ck((int)Ci, (int)J);
     p.CK = ck;
     p.t = pick_tile(M, ncols);
     int BN = tile_bn(p.t);

@@ -90,6 +90,34 @@ def _weight_bwd(v, g, dw):
     return dv, dg
 
 
+def _direct(p):
+    return p is None or (getattr(p, '_encx_flat', False) and p.grad is not None)
+
+
+def _param_grads(v, g, b, dw, bias_src, Bn, C, T):
+    """dw (natural layout) + the bias-grad source -> grads of (v, g, b). For parameters that
+    live in a FlatAdam buffer the kernels accumulate straight into the (pre-zeroed) flat grad
+    views and autograd gets None: no separate accumulation pass over the weights."""
+    st = stream()
+    if _direct(v) and _direct(g) and _direct(b):
+        if g is None:
+            call('encx_axpby', ptr(dw), ptr(v.grad), dw.numel(), 1.0, None, 1.0, st)
+        else:
+            call('encx_weightnorm_bwd', ptr(v), ptr(g), ptr(dw), ptr(v.grad), ptr(g.grad),
+                 v.shape[0], v[0].numel(), 1, st)
+        if b is not None:
+            ws = _f32(lib.encx_channel_sum_workspace(C) // 4, dw)
+            call('encx_channel_sum', ptr(bias_src), ptr(b.grad), ptr(ws), Bn, C, T, 1, st)
+        return None, None, None
+    dv, dg = _weight_bwd(v, g, dw)
+    db = None
+    if b is not None:
+        db = torch.empty(C, device=dw.device, dtype=torch.float32)
+        ws = _f32(lib.encx_channel_sum_workspace(C) // 4, dw)
+        call('encx_channel_sum', ptr(bias_src), ptr(db), ptr(ws), Bn, C, T, 0, st)
+    return dv, dg, db
+
+
 # ---------------------------------------------------------------------------- Conv1d
 class Conv1dFn(torch.autograd.Function):
     """SConv1d.forward (modules/conv.py:195-210) incl. weight_norm and a fused pre-ELU."""
@@ -112,13 +140,15 @@ class Conv1dFn(torch.autograd.Function):
         ws = _ws(lib.encx_conv1d_fwd_workspace(B, Cin, Cout, tout, K, s, d), x)
         call('encx_conv1d_fwd', ptr(x), ptr(wf), ptr(b), ptr(res), ptr(y), ptr(ws), B, Cin, T, Cout,
              tout, K, s, d, pl, e, PAD[pad_mode], ACT[act], stream())
-        ctx.save_for_backward(x, v, g, wp)
+        ctx.save_for_backward(x, wp)
+        ctx.params = (v, g, b)
         ctx.cfg = (K, s, d, pl, pr, e, tout, PAD[pad_mode], ACT[act], res is not None, b is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, v, g, wp = ctx.saved_tensors
+        x, wp = ctx.saved_tensors
+        v, g, b = ctx.params
         K, s, d, pl, pr, e, tout, mode, act, has_res, has_b = ctx.cfg
         dy = dy.contiguous()
         B, Cin, T = x.shape
@@ -132,11 +162,10 @@ class Conv1dFn(torch.autograd.Function):
                  Cout, tout, K, s, pl, pr, e, mode, act, 0, st)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
             dw = torch.empty(Cout, Cin, K, device=x.device, dtype=torch.float32)
-            db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_b else None
             ws = _f32(lib.encx_conv1d_bwd_weight_workspace(B, Cin, Cout, tout, K) // 4 + 1, x)
-            call('encx_conv1d_bwd_weight', ptr(dy), ptr(x), ptr(dw), ptr(db), ptr(ws), B, Cin, T,
+            call('encx_conv1d_bwd_weight', ptr(dy), ptr(x), ptr(dw), None, ptr(ws), B, Cin, T,
                  Cout, tout, K, s, d, pl, e, mode, act, 0, st)
-            dv, dg = _weight_bwd(v, g, dw)
+            dv, dg, db = _param_grads(v, g, b, dw, dy, B, Cout, tout)
         return dx, dv, dg, db, (dy if has_res else None), None, None, None, None, None, None
 
 
@@ -162,13 +191,15 @@ class ConvTr1dFn(torch.autograd.Function):
         ws = _ws(lib.encx_convtr1d_fwd_workspace(B, Cin, Cout, tout, K, s, trim_left), x)
         call('encx_convtr1d_fwd', ptr(x), ptr(wp), ptr(b), ptr(y), ptr(ws), B, Cin, T, Cout, tout, K,
              s, trim_left, ACT[act], stream())
-        ctx.save_for_backward(x, v, g, wf)
+        ctx.save_for_backward(x, wf)
+        ctx.params = (v, g, b)
         ctx.cfg = (K, s, trim_left, tout, ACT[act], b is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, v, g, wf = ctx.saved_tensors
+        x, wf = ctx.saved_tensors
+        v, g, b = ctx.params
         K, s, trim_left, tout, act, has_b = ctx.cfg
         dy = dy.contiguous()
         B, Cin, T = x.shape
@@ -182,11 +213,10 @@ class ConvTr1dFn(torch.autograd.Function):
                  Cout, tout, K, s, trim_left, act, 0, st)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
             dw = torch.empty(Cin, Cout, K, device=x.device, dtype=torch.float32)
-            db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_b else None
             ws = _f32(lib.encx_convtr1d_bwd_weight_workspace(B, Cin, Cout, T, K) // 4 + 1, x)
-            call('encx_convtr1d_bwd_weight', ptr(x), ptr(dy), ptr(dw), ptr(db), ptr(ws), B, Cin, T,
+            call('encx_convtr1d_bwd_weight', ptr(x), ptr(dy), ptr(dw), None, ptr(ws), B, Cin, T,
                  Cout, tout, K, s, trim_left, act, 0, st)
-            dv, dg = _weight_bwd(v, g, dw)
+            dv, dg, db = _param_grads(v, g, b, dw, dy, B, Cout, tout)
         return dx, dv, dg, db, None, None, None, None, None
 
 

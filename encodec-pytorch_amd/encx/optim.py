@@ -33,6 +33,7 @@ class FlatAdam(torch.optim.Optimizer):
             p.data = v
             g = self.flat_grad[o:o + k].view_as(p)
             p.grad = g
+            p._encx_flat = True  # encx ops accumulate this param's grad in place
             self._views.append((p, g))
             o += k
 
