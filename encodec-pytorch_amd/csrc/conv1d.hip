@@ -20,11 +20,13 @@
 // fixed-order reduce kernel applies the epilogue: deterministic, no float atomics.
 // Plus VALU kernels for the 1-channel ends of the stack (Cout = 1 forward, tiny wgrads).
 #include "common.h"
+#include "gemm.h"
 #include "prof.h"
 
 namespace {
 
 constexpr int NT = 256;  // threads per workgroup (4 waves)
+constexpr int FLAT_T = 128;  // layers with T_out <= this run as one (b, t)-flattened GEMM
 
 // ------------------------------------------------------------------------- conv forward
 struct FwdArgs {
@@ -507,6 +509,57 @@ __global__ __launch_bounds__(NT) void conv_fwd_small_kernel(FwdArgs a) {
             fwd_store(a, ((int64_t)b * a.Cout + co) * a.Tout + t, co, acc[co]);
 }
 
+// ------------------------------------------------------------------------- low-rate layers
+// At T = 75 (B = 32) a per-item time tile is mostly padding and the weights are re-staged for
+// every 32 columns. These layers run instead as one GEMM over the flattened (b, t) columns
+// (N = B*T = 2400) with an im2col B operand gathered from L2 while staging, split over the
+// reduction into fixed slabs (conv_fwd_reduce / conv_poly_reduce apply the epilogue).
+struct LdConvFlat {
+    static constexpr bool A_K_FAST = false, B_N_FAST = true;
+    FwdArgs p;
+    ENCX_DEV float a(int m, int k) const { return p.wf[(int64_t)k * p.Cout + m]; }
+    ENCX_DEV float b(int k, int n) const {
+        const int ci = k / p.K, tap = k - ci * p.K;
+        const int bb = n / p.Tout, t = n - bb * p.Tout;
+        const int m = pad_src(t * p.s + tap * p.d, p.pl, p.Tin, p.e, p.mode);
+        return m >= 0 ? act_apply(p.act, p.x[((int64_t)bb * p.Cin + ci) * p.Tin + m]) : 0.f;
+    }
+};
+struct EpConvFlat {
+    FwdArgs p;
+    int slabs;
+    ENCX_DEV void operator()(int co, int n, float v) const {
+        const int bb = n / p.Tout, t = n - bb * p.Tout;
+        const int64_t o = ((int64_t)bb * p.Cout + co) * p.Tout + t;
+        if (slabs > 1) p.part[(int64_t)blockIdx.z * p.B * p.Cout * p.Tout + o] = v;
+        else fwd_store(p, o, co, v);
+    }
+};
+struct LdPolyFlat {
+    static constexpr bool A_K_FAST = false, B_N_FAST = true;
+    PolyArgs p;
+    int M, ncols;
+    ENCX_DEV float a(int m, int k) const { return p.wp[(int64_t)k * M + m]; }
+    ENCX_DEV float b(int k, int n) const {
+        const int i = k / p.J, q = k - i * p.J;
+        const int bb = n / ncols, u = n - bb * ncols, t = u - q;
+        return (t >= 0 && t < p.Tin) ? act_apply(p.in_act, p.in[((int64_t)bb * p.Ci + i) * p.Tin + t]) : 0.f;
+    }
+};
+struct EpPolyFlat {
+    PolyArgs p;
+    int ncols, slabs;
+    ENCX_DEV void operator()(int row, int n, float v) const {
+        const int o = row / p.s, rr = row - o * p.s;
+        const int bb = n / ncols, u = n - bb * ncols, qpos = u * p.s + rr;
+        if (slabs > 1) {
+            if (qpos < p.Q) p.part[(((int64_t)blockIdx.z * p.B + bb) * p.Co + o) * p.Q + qpos] = v;
+        } else {
+            poly_store(p, bb, o, qpos, v);
+        }
+    }
+};
+
 // ------------------------------------------------------------------------- planning
 static int even_up(int v) { return (v + 1) & ~1; }
 
@@ -594,7 +647,29 @@ void launch_poly(const PolyArgs& a, int ncols, hipStream_t st) {
     hipLaunchKernelGGL((conv_poly_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
 }
 
+static bool fwd_flat(int64_t Cout, int64_t Tout) { return Cout > 4 && Tout <= FLAT_T; }
+static int fwd_flat_slabs(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K) {
+    const int Kred = (int)(Cin * K);
+    return gemm_slabs(Kred, gemm_splits((int)Cout, (int)(B * Tout), Kred));
+}
+
 int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
+    if (fwd_flat(a.Cout, a.Tout)) {
+        const int Kred = a.Cin * a.K, N = a.B * a.Tout;
+        const int splits = gemm_splits(a.Cout, N, Kred);
+        const int slabs = gemm_slabs(Kred, splits);
+        a.part = ws;
+        a.KS = slabs;
+        ENCX_REQUIRE(slabs == 1 || ws);
+        int rc = gemm_launch(LdConvFlat{a}, EpConvFlat{a, slabs}, a.Cout, N, Kred, st, splits);
+        if (rc) return rc;
+        if (slabs > 1) {
+            int64_t n = (int64_t)a.B * a.Cout * a.Tout;
+            hipLaunchKernelGGL(conv_fwd_reduce, dim3(cdiv(n, 256)), dim3(256), 0, st, a);
+            ENCX_CHECK_LAUNCH();
+        }
+        return 0;
+    }
     FwdPlan p = plan_fwd(a.B, a.Cin, a.Cout, a.Tout, a.K, a.s, a.d);
     if (p.small) {
         int ck = 64 / a.K;
@@ -630,11 +705,32 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
 }
 
 size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K, int64_t s, int64_t d) {
+    if (fwd_flat(Cout, Tout)) {
+        const int slabs = fwd_flat_slabs(B, Cin, Cout, Tout, K);
+        return slabs > 1 ? (size_t)slabs * B * Cout * Tout * sizeof(float) : 0;
+    }
     FwdPlan p = plan_fwd(B, Cin, Cout, Tout, K, s, d);
     return (p.small || p.KS == 1) ? 0 : (size_t)p.KS * B * Cout * Tout * sizeof(float);
 }
 
 int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
+    if (ncols <= FLAT_T) {
+        const int M = a.Co * a.s, Kred = a.Ci * a.J, N = a.B * ncols;
+        const int splits = gemm_splits(M, N, Kred);
+        const int slabs = gemm_slabs(Kred, splits);
+        a.Q = ncols * a.s;
+        a.part = ws;
+        a.KS = slabs;
+        ENCX_REQUIRE(slabs == 1 || ws);
+        int rc = gemm_launch(LdPolyFlat{a, M, ncols}, EpPolyFlat{a, ncols, slabs}, M, N, Kred, st, splits);
+        if (rc) return rc;
+        if (slabs > 1) {
+            int64_t n = (int64_t)a.B * a.Co * a.Q;
+            hipLaunchKernelGGL(conv_poly_reduce, dim3(cdiv(n, 256)), dim3(256), 0, st, a);
+            ENCX_CHECK_LAUNCH();
+        }
+        return 0;
+    }
     PolyPlan p = plan_poly(a.B, a.Ci, (int64_t)a.Co * a.s, ncols, a.J);
     a.CK = p.CK; a.Ub = p.Ub; a.KS = p.KS; a.cps = p.cps; a.Q = ncols * a.s; a.part = ws;
     ENCX_REQUIRE(a.KS == 1 || ws);
@@ -656,6 +752,11 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
 }
 
 size_t poly_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int64_t J) {
+    if (ncols <= FLAT_T) {
+        const int Kred = (int)(Ci * J);
+        const int slabs = gemm_slabs(Kred, gemm_splits((int)(Co * s), (int)(B * ncols), Kred));
+        return slabs > 1 ? (size_t)slabs * B * Co * ncols * s * sizeof(float) : 0;
+    }
     PolyPlan p = plan_poly(B, Ci, Co * s, ncols, J);
     return p.KS == 1 ? 0 : (size_t)p.KS * B * Co * ncols * s * sizeof(float);
 }

@@ -1,10 +1,13 @@
 // Generic LDS-staged fp32 MFMA GEMM skeleton, C[M][N] = sum_k A(m,k) B(k,n), with operand
-// loaders and the epilogue supplied as functors (implicit-GEMM style): the mel/STFT loss
-// kernels build their A operands (framed, reflect-padded audio; |X|^2; d mel) on the fly
-// while staging, so no im2col / intermediate tensor ever reaches HBM.
+// loaders and the epilogue supplied as functors (implicit-GEMM style): the mel/STFT loss,
+// the EMA codebook sums and the low-rate (T <= 128) conv layers build their operands on the
+// fly while staging (framed audio, |X|^2, one-hot codes, im2col windows), so no intermediate
+// tensor reaches HBM.
 //
 // Tiles: BM x BN per 256-thread workgroup (4 waves as WM x WN), BK-deep LDS stages,
-// v_mfma_f32_32x32x2_f32 (exact fp32). Loader contract:
+// v_mfma_f32_32x32x2_f32 (exact fp32). Split-K: workgroup z covers k in
+// [z*kchunk, (z+1)*kchunk); the epilogue sees blockIdx.z and writes its own partial slab.
+// Loader contract:
 //   float a(int m, int k) const; static constexpr bool A_K_FAST;  // coalescing order
 //   float b(int k, int n) const; static constexpr bool B_N_FAST;
 // Epilogue: void operator()(int m, int n, float v) const  (only for m < M, n < N).
@@ -12,34 +15,35 @@
 #include "common.h"
 
 template <int BM, int BN, int WM, int WN, int BK, class LD, class EP>
-__global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, int Kred) {
+__global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, int Kred, int kchunk) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     __shared__ float As[BK][BM + 1];
     __shared__ float Bs[BK][BN + 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int kbeg = blockIdx.z * kchunk, kend = min(Kred, kbeg + kchunk);
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
-    for (int k0 = 0; k0 < Kred; k0 += BK) {
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
         __syncthreads();
         for (int i = tid; i < BM * BK; i += 256) {
             int m, k;
             if (LD::A_K_FAST) { m = i / BK; k = i - m * BK; }
             else { k = i / BM; m = i - k * BM; }
             int gm = m0 + m, gk = k0 + k;
-            As[k][m] = (gm < M && gk < Kred) ? ld.a(gm, gk) : 0.f;
+            As[k][m] = (gm < M && gk < kend) ? ld.a(gm, gk) : 0.f;
         }
         for (int i = tid; i < BN * BK; i += 256) {
             int n, k;
             if (LD::B_N_FAST) { k = i / BN; n = i - k * BN; }
             else { n = i / BK; k = i - n * BK; }
             int gn = n0 + n, gk = k0 + k;
-            Bs[k][n] = (gn < N && gk < Kred) ? ld.b(gk, gn) : 0.f;
+            Bs[k][n] = (gn < N && gk < kend) ? ld.b(gk, gn) : 0.f;
         }
         __syncthreads();
 #pragma unroll
@@ -68,24 +72,58 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
         }
 }
 
-// launch with a tile picked from the problem shape
+struct GemmShape {
+    int BM, BN;
+    int64_t blocks;
+};
+
+// tile choice shared by gemm_launch and split-K planners: 128x128 while that still gives
+// >= 2 workgroups per CU (256 CUs), else 64x64; narrow N gets 128x32 / 128x64
+static inline GemmShape gemm_shape(int M, int N) {
+    GemmShape s;
+    if (N <= 48) { s.BM = 128; s.BN = 32; }
+    else if (N <= 96) { s.BM = 128; s.BN = 64; }
+    else if (cdiv(N, 128) * cdiv(M, 128) < 512) { s.BM = 64; s.BN = 64; }
+    else { s.BM = 128; s.BN = 128; }
+    s.blocks = cdiv(N, s.BN) * cdiv(M, s.BM);
+    return s;
+}
+
+// split count that brings the grid to ~1024 workgroups, each with >= min_k reduction depth
+static inline int gemm_splits(int M, int N, int Kred, int min_k = 256, int max_splits = 32) {
+    GemmShape s = gemm_shape(M, N);
+    int sp = (int)cdiv(1024, s.blocks);
+    int cap = Kred / min_k;
+    if (sp > cap) sp = cap;
+    if (sp > max_splits) sp = max_splits;
+    return sp < 1 ? 1 : sp;
+}
+
 template <class LD, class EP>
-int gemm_launch(const LD& ld, const EP& ep, int M, int N, int Kred, hipStream_t st) {
-    // 128x128 tiles when they still give >= 2 workgroups per CU, else 64x64 (256 CUs)
-    const int64_t big = cdiv(N, 128) * cdiv(M, 128);
-    if (N <= 48) {
-        hipLaunchKernelGGL((gemm_kernel<128, 32, 4, 1, 32, LD, EP>), dim3(cdiv(N, 32), cdiv(M, 128)),
-                           dim3(256), 0, st, ld, ep, M, N, Kred);
-    } else if (N <= 96) {
-        hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, 32, LD, EP>), dim3(cdiv(N, 64), cdiv(M, 128)),
-                           dim3(256), 0, st, ld, ep, M, N, Kred);
-    } else if (big < 512) {
-        hipLaunchKernelGGL((gemm_kernel<64, 64, 2, 2, 32, LD, EP>), dim3(cdiv(N, 64), cdiv(M, 64)),
-                           dim3(256), 0, st, ld, ep, M, N, Kred);
+int gemm_launch(const LD& ld, const EP& ep, int M, int N, int Kred, hipStream_t st, int splits = 1) {
+    GemmShape s = gemm_shape(M, N);
+    const int kchunk = splits > 1 ? (int)(cdiv(cdiv(Kred, splits), 32) * 32) : Kred;
+    const int z = (int)cdiv(Kred, kchunk);
+    if (s.BN == 32) {
+        hipLaunchKernelGGL((gemm_kernel<128, 32, 4, 1, 32, LD, EP>), dim3(cdiv(N, 32), cdiv(M, 128), z),
+                           dim3(256), 0, st, ld, ep, M, N, Kred, kchunk);
+    } else if (s.BN == 64 && s.BM == 128) {
+        hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, 32, LD, EP>), dim3(cdiv(N, 64), cdiv(M, 128), z),
+                           dim3(256), 0, st, ld, ep, M, N, Kred, kchunk);
+    } else if (s.BN == 64) {
+        hipLaunchKernelGGL((gemm_kernel<64, 64, 2, 2, 32, LD, EP>), dim3(cdiv(N, 64), cdiv(M, 64), z),
+                           dim3(256), 0, st, ld, ep, M, N, Kred, kchunk);
     } else {
-        hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, 32, LD, EP>), dim3(cdiv(N, 128), cdiv(M, 128)),
-                           dim3(256), 0, st, ld, ep, M, N, Kred);
+        hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, 32, LD, EP>), dim3(cdiv(N, 128), cdiv(M, 128), z),
+                           dim3(256), 0, st, ld, ep, M, N, Kred, kchunk);
     }
     ENCX_CHECK_LAUNCH();
     return 0;
+}
+
+// number of k-slabs gemm_launch actually uses for a requested split count
+static inline int gemm_slabs(int Kred, int splits) {
+    if (splits <= 1) return 1;
+    const int kchunk = (int)(cdiv(cdiv(Kred, splits), 32) * 32);
+    return (int)cdiv(Kred, kchunk);
 }

@@ -12,6 +12,7 @@
 //                   visited in ascending order (deterministic), used by the EMA update (:227-235)
 //                   and by kmeans (:92-100).
 #include "common.h"
+#include "gemm.h"
 
 namespace {
 
@@ -204,62 +205,64 @@ __global__ void rvq_gather_kernel(const float* embed, const int64_t* idx, float*
     out[i] = acc ? out[i] + q : q;
 }
 
-// wave per code: counts and sums over the frames assigned to it, ascending frame order
-// 16 waves per workgroup = 16 codes; the assignment vector is staged once per workgroup in
-// LDS (as int32) and scanned 64 frames per ballot.
-constexpr int BK_WAVES = 16, BK_CHUNK = 8192;
-template <int MODE>  // 0: EMA (core_vq.py:227-229), 1: kmeans (:92-100)
-__global__ __launch_bounds__(1024) void bucket_kernel(Rows x, const int64_t* idx, int N, int D,
-                                                      int Kc, float* cs, float* ea, float* means,
-                                                      int64_t* bins, float decay, float one_m) {
-    __shared__ int sidx[BK_CHUNK];
-    const int lane = threadIdx.x & 63, c = blockIdx.x * BK_WAVES + (threadIdx.x >> 6);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // D <= 256
-    int count = 0;
-    for (int base = 0; base < N; base += BK_CHUNK) {
-        const int nn_end = min(N - base, BK_CHUNK);
-        __syncthreads();
-        for (int i = threadIdx.x; i < nn_end; i += blockDim.x) sidx[i] = (int)idx[base + i];
-        __syncthreads();
-        if (c >= Kc) continue;
-        for (int n0 = 0; n0 < nn_end; n0 += 64) {
-            const int n = n0 + lane;
-            const bool m = n < nn_end && sidx[n] == c;
-            uint64_t mask = __ballot(m);
-            while (mask) {
-                const int j = __ffsll((long long)mask) - 1;
-                mask &= mask - 1;
-                const int nn = base + n0 + j;
-#pragma unroll
-                for (int z = 0; z < 4; ++z) {
-                    int d = lane + 64 * z;
-                    if (d < D) acc[z] += x.at(nn, d);
-                }
-                ++count;
-            }
-        }
+// Per-code sums of the assigned frames, the reference's own formulation
+// embed_sum = x^T @ onehot (core_vq.py:228; kmeans' scatter_add :96-97) as an MFMA GEMM
+// [Kc x N] x [N x (D+1)] whose one-hot A operand is generated from the codes while staging and
+// whose extra all-ones column yields the counts. Split over frames into fixed slabs, then
+// summed in slab order: deterministic and insensitive to how skewed the assignment is.
+struct LdOneHot {
+    static constexpr bool A_K_FAST = true, B_N_FAST = false;
+    Rows x;
+    const int64_t* idx;
+    int D;
+    ENCX_DEV float a(int c, int n) const { return idx[n] == c ? 1.f : 0.f; }
+    ENCX_DEV float b(int n, int d) const { return d < D ? x.at(n, d) : 1.f; }
+};
+struct EpSlab {
+    float* ws;
+    int Kc, W;
+    ENCX_DEV void operator()(int c, int d, float v) const {
+        ws[((int64_t)blockIdx.z * Kc + c) * W + d] = v;
     }
-    if (c >= Kc) return;
-    if (MODE == 0) {
-        if (lane == 0) cs[c] = fmaf((float)count, one_m, cs[c] * decay);
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-            int d = lane + 64 * z;
+};
+
+template <int MODE>  // 0: EMA (core_vq.py:227-229), 1: kmeans (:92-100)
+__global__ void bucket_finish(const float* ws, int S, int Kc, int D, float* cs, float* ea,
+                              float* means, int64_t* bins, float decay, float one_m) {
+    const int c = blockIdx.x, W = D + 1;
+    float cnt = 0.f;
+    for (int z = 0; z < S; ++z) cnt += ws[((int64_t)z * Kc + c) * W + D];
+    for (int d = threadIdx.x; d <= D; d += blockDim.x) {
+        float s = 0.f;
+        for (int z = 0; z < S; ++z) s += ws[((int64_t)z * Kc + c) * W + d];
+        if (MODE == 0) {
             if (d < D) {
                 float* p = ea + (int64_t)c * D + d;
-                *p = fmaf(acc[z], one_m, *p * decay);
+                *p = fmaf(s, one_m, *p * decay);
+            } else {
+                cs[c] = fmaf(s, one_m, cs[c] * decay);
             }
-        }
-    } else {
-        if (lane == 0) bins[c] = count;
-        if (count > 0) {
-#pragma unroll
-            for (int z = 0; z < 4; ++z) {
-                int d = lane + 64 * z;
-                if (d < D) means[(int64_t)c * D + d] = acc[z] / (float)count;
+        } else {
+            if (d < D) {
+                if (cnt > 0.f) means[(int64_t)c * D + d] = s / cnt;
+            } else {
+                bins[c] = (int64_t)cnt;
             }
         }
     }
+}
+
+template <int MODE>
+int bucket_run(Rows x, const int64_t* idx, int N, int D, int Kc, float* ws, float* cs, float* ea,
+               float* means, int64_t* bins, float decay, float one_m, hipStream_t st) {
+    const int splits = gemm_splits(Kc, D + 1, N);
+    const int S = gemm_slabs(N, splits);
+    int rc = gemm_launch(LdOneHot{x, idx, D}, EpSlab{ws, Kc, D + 1}, Kc, D + 1, N, st, splits);
+    if (rc) return rc;
+    hipLaunchKernelGGL(bucket_finish<MODE>, dim3(Kc), dim3(D + 1 < 64 ? 64 : 256), 0, st, ws, S, Kc, D,
+                       cs, ea, means, bins, decay, one_m);
+    ENCX_CHECK_LAUNCH();
+    return 0;
 }
 
 // embed = embed_avg / (laplace(cluster_size) * sum(cluster_size)), core_vq.py:230-235
@@ -372,16 +375,20 @@ int encx_rvq_gather(const float* embed, const int64_t* idx, float* out, int64_t 
     return 0;
 }
 
+size_t encx_rvq_bucket_workspace(int64_t N, int64_t D, int64_t Kc) {
+    const int S = gemm_slabs((int)N, gemm_splits((int)Kc, (int)D + 1, (int)N));
+    return (size_t)S * Kc * (D + 1) * sizeof(float);
+}
+
 int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float* embed_avg,
-                 float* embed, int64_t B, int64_t D, int64_t Tf, int64_t Kc, float decay,
-                 float eps, encx_stream_t stream) {
-    ENCX_REQUIRE(x && idx && cluster_size && embed_avg && embed && D <= 256 && Kc > 0);
+                 float* embed, float* ws, int64_t B, int64_t D, int64_t Tf, int64_t Kc,
+                 float decay, float eps, encx_stream_t stream) {
+    ENCX_REQUIRE(x && idx && cluster_size && embed_avg && embed && ws && D <= 256 && Kc > 0);
     hipStream_t st = (hipStream_t)stream;
     const float one_m = (float)(1.0 - (double)decay);
-    hipLaunchKernelGGL(bucket_kernel<0>, dim3(cdiv(Kc, BK_WAVES)), dim3(64 * BK_WAVES), 0, st, bdt_rows(x, B, D, Tf),
-                       idx, (int)(B * Tf), (int)D, (int)Kc, cluster_size, embed_avg, nullptr, nullptr,
-                       decay, one_m);
-    ENCX_CHECK_LAUNCH();
+    int rc = bucket_run<0>(bdt_rows(x, B, D, Tf), idx, (int)(B * Tf), (int)D, (int)Kc, ws,
+                           cluster_size, embed_avg, nullptr, nullptr, decay, one_m, st);
+    if (rc) return rc;
     hipLaunchKernelGGL(ema_normalize, dim3(Kc), dim3(D < 64 ? 64 : (D > 256 ? 256 : D)), 0, st,
                        cluster_size, embed_avg, embed, (int)D, (int)Kc, eps,
                        (float)((double)Kc * (double)eps));
@@ -390,16 +397,15 @@ int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float*
 }
 
 int encx_kmeans_step(const float* samples, float* means, int64_t* bins, int64_t* idx,
-                     uint64_t* keys, int64_t N, int64_t D, int64_t Kc, encx_stream_t stream) {
-    ENCX_REQUIRE(samples && means && bins && idx && keys && N > 0 && D > 0 && D <= 256 && Kc > 0);
+                     uint64_t* keys, float* ws, int64_t N, int64_t D, int64_t Kc,
+                     encx_stream_t stream) {
+    ENCX_REQUIRE(samples && means && bins && idx && keys && ws && N > 0 && D > 0 && D <= 256 && Kc > 0);
     hipStream_t st = (hipStream_t)stream;
     Rows r = nd_rows(samples, N, D);
     int rc = argmin_run(r, means, idx, keys, (int)N, (int)D, (int)Kc, 1, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(bucket_kernel<1>, dim3(cdiv(Kc, BK_WAVES)), dim3(64 * BK_WAVES), 0, st, r, idx, (int)N, (int)D,
-                       (int)Kc, nullptr, nullptr, means, bins, 0.f, 0.f);
-    ENCX_CHECK_LAUNCH();
-    return 0;
+    return bucket_run<1>(r, idx, (int)N, (int)D, (int)Kc, ws, nullptr, nullptr, means, bins, 0.f,
+                         0.f, st);
 }
 
 int encx_sample_rows(const float* samples, float* out, int64_t N, int64_t D, int64_t num,

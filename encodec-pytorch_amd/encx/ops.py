@@ -365,9 +365,10 @@ def kmeans(samples, num_clusters, num_iters, seed):
     bins = torch.zeros(num_clusters, device=samples.device, dtype=torch.int64)
     idx = torch.empty(N, device=samples.device, dtype=torch.int64)
     keys = torch.empty(N, device=samples.device, dtype=torch.int64)
+    ws = _ws(lib.encx_rvq_bucket_workspace(N, D, num_clusters), samples)
     for _ in range(num_iters):
-        call('encx_kmeans_step', ptr(samples), ptr(means), ptr(bins), ptr(idx), ptr(keys), N, D,
-             num_clusters, stream())
+        call('encx_kmeans_step', ptr(samples), ptr(means), ptr(bins), ptr(idx), ptr(keys), ptr(ws),
+             N, D, num_clusters, stream())
     return means, bins
 
 
@@ -401,6 +402,8 @@ class RVQTrainFn(torch.autograd.Function):
         commits = torch.empty(n_q, device=emb.device, dtype=torch.float32)
         codes = torch.empty(n_q, B * T, device=emb.device, dtype=torch.int64)
         keys = torch.empty(B * T, device=emb.device, dtype=torch.int64)
+        Kc = codebooks[0].embed.shape[0]
+        bws = _ws(lib.encx_rvq_bucket_workspace(B * T, D, Kc), emb)
         for i, cb in enumerate(codebooks):
             x = res[i % 2]
             cb.init_embed_(x)
@@ -411,7 +414,7 @@ class RVQTrainFn(torch.autograd.Function):
                  ptr(out), ptr(cdir), ptr(parts[i]), B, D, T, int(i == 0), 1, st)
             if cb.training:
                 call('encx_rvq_ema', ptr(x), ptr(codes[i]), ptr(cb.cluster_size), ptr(cb.embed_avg),
-                     ptr(cb.embed), B, D, T, cb.embed.shape[0], float(decay), float(eps), st)
+                     ptr(cb.embed), ptr(bws), B, D, T, cb.embed.shape[0], float(decay), float(eps), st)
             call('encx_reduce_sum', ptr(parts[i]), P, 1.0 / numel, ptr(commits[i:i + 1]), 0, st)
         penalty = torch.empty(1, device=emb.device, dtype=torch.float32)
         call('encx_reduce_sum', ptr(commits), n_q, 1.0 / n_q, ptr(penalty), 0, st)

@@ -165,13 +165,17 @@ int64_t encx_rvq_apply_parts(int64_t B, int64_t D, int64_t Tf);
  * cluster_size = d*cs + (1-d)*count; embed_avg = d*ea + (1-d)*sum; embed = embed_avg /
  * laplace(cluster_size)*sum(cluster_size). x = the layer input (pre-update residual),
  * layout [B][D][Tf]. Deterministic (fixed summation order per code). */
+/* The per-code sums are x^T @ onehot (core_vq.py:228) as an MFMA GEMM with the one-hot operand
+ * generated on the fly; ws: encx_rvq_bucket_workspace(N = B*Tf, D, Kc) bytes. */
+size_t encx_rvq_bucket_workspace(int64_t N, int64_t D, int64_t Kc);
 int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float* embed_avg,
-                 float* embed, int64_t B, int64_t D, int64_t Tf, int64_t Kc, float decay,
-                 float eps, encx_stream_t stream);
+                 float* embed, float* ws, int64_t B, int64_t D, int64_t Tf, int64_t Kc,
+                 float decay, float eps, encx_stream_t stream);
 /* One kmeans iteration (core_vq.py:85-100): means <- bucket means where bins > 0.
- * samples [N][D] row-major; means [Kc][D] in/out; bins int64 [Kc] out. */
+ * samples [N][D] row-major; means [Kc][D] in/out; bins int64 [Kc] out; ws as above. */
 int encx_kmeans_step(const float* samples, float* means, int64_t* bins, int64_t* idx,
-                     uint64_t* keys, int64_t N, int64_t D, int64_t Kc, encx_stream_t stream);
+                     uint64_t* keys, float* ws, int64_t N, int64_t D, int64_t Kc,
+                     encx_stream_t stream);
 /* sample_vectors (core_vq.py:69-77) for kmeans' init: rows of a uniform random permutation
  * (num <= N) or uniform draws with replacement, from a counter-based hash of `seed`. */
 int encx_sample_rows(const float* samples, float* out, int64_t N, int64_t D, int64_t num,

@@ -187,8 +187,11 @@ def test_kmeans_fixture():
     bins = torch.zeros(64, dtype=torch.int64, device=DEV)
     idx = torch.empty(600, dtype=torch.int64, device=DEV)
     keys = torch.empty(600, dtype=torch.int64, device=DEV)
+    from encx._lib import lib
+    ws = torch.empty(lib.encx_rvq_bucket_workspace(600, 128, 64) // 4 + 1, device=DEV)
     for _ in range(10):
-        call('encx_kmeans_step', ptr(samples), ptr(means), ptr(bins), ptr(idx), ptr(keys), 600, 128, 64, stream())
+        call('encx_kmeans_step', ptr(samples), ptr(means), ptr(bins), ptr(idx), ptr(keys), ptr(ws),
+             600, 128, 64, stream())
     close(means, d['km_means'], 1e-5, 1e-6, 'kmeans means')
     assert (bins.cpu().numpy() == d['km_bins']).all()
 

@@ -74,9 +74,13 @@ def test_train_step_gen_fixture():
     for k, v in sd.items():
         ref = d['gen/p/' + k]
         mine = np.array([v.double().sum().item(), v.double().abs().sum().item()])
-        err = np.abs(mine - ref) / (np.abs(ref) + 1e-3)
-        worst = max(worst, float(err.max()))
-        assert (err < 2e-3).all(), (k, mine, ref)
+        # Adam's first steps move every weight by ~lr*sign(g): an element whose grad is ~0
+        # can flip sign under fp reordering (2*lr per flip), so the signed sum gets an
+        # absolute slack of a few flips; the abs-sum must agree to 1e-4 relative
+        flips = 20 * 2 * 3e-4 * 2
+        assert abs(mine[0] - ref[0]) <= 1e-5 * ref[1] + flips, (k, mine, ref)
+        assert abs(mine[1] - ref[1]) <= 1e-4 * ref[1] + flips, (k, mine, ref)
+        worst = max(worst, abs(mine[1] - ref[1]) / max(ref[1], 1e-12))
     print('worst param checksum rel err', worst)
 
 
