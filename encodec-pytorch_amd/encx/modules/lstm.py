@@ -1,10 +1,12 @@
-"""SLSTM (modules/lstm.py of the reference).
+"""SLSTM (modules/lstm.py of the reference) on the encx LSTM kernels (csrc/lstm.hip).
 
-Phase-1 choice: the 2-layer LSTM(512) over 75 frames stays on the vendor RNN
-(MIOpen through torch.nn.LSTM); it is a 20 GFLOP/step sequential recurrence and is the next
-kernel to replace with a persistent-CU LSTM.
+The parameters stay in a torch.nn.LSTM container so the state-dict keys
+(`lstm.weight_ih_l0`, `lstm.bias_hh_l1`, ...) and the default init match the reference;
+its forward is never called: the sequence runs through encx.ops.LSTMFn.
 """
 from torch import nn
+
+from .. import ops
 
 
 class SLSTM(nn.Module):
@@ -15,9 +17,12 @@ class SLSTM(nn.Module):
         self.skip = skip
         self.lstm = nn.LSTM(dimension, dimension, num_layers)
 
+    def _weights(self):
+        w = []
+        for l in range(self.lstm.num_layers):
+            w += [getattr(self.lstm, f'{n}_l{l}')
+                  for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
+        return w
+
     def forward(self, x):
-        x = x.permute(2, 0, 1)
-        y, _ = self.lstm(x)
-        if self.skip:
-            y = y + x
-        return y.permute(1, 2, 0)
+        return ops.lstm(x, self._weights(), skip=self.skip)

@@ -465,3 +465,83 @@ def rvq_decode(codes, embeds):
     for i in range(n_q):
         call('encx_rvq_gather', ptr(embeds[i]), ptr(codes[i]), ptr(out), B, D, T, int(i > 0), stream())
     return out
+
+
+# ---------------------------------------------------------------------------- LSTM
+class LSTMFn(torch.autograd.Function):
+    """SLSTM.forward (modules/lstm.py:22-28): torch.nn.LSTM(H, H, L) over [T, B, H] + skip.
+
+    Takes x in the conv layout [B][H][T] and returns the same layout; the per-layer sequences
+    live as [B][T][.] on the device. Weights per layer: (w_ih, w_hh, b_ih, b_hh)."""
+
+    @staticmethod
+    def forward(ctx, x, skip, *weights):
+        _check(x)
+        x = x.contiguous()
+        B, H, T = x.shape
+        L = len(weights) // 4
+        if B > 64 or H % 16:
+            raise NotImplementedError('encx LSTM: batch <= 64 per GPU and hidden % 16 == 0')
+        st = stream()
+        gx = _f32(B * T * 4 * H, x)
+        inp, bct, states = x, 1, []
+        for l in range(L):
+            w_ih, w_hh, b_ih, b_hh = (w.contiguous() for w in weights[4 * l:4 * l + 4])
+            Y = torch.empty(B, T, H, device=x.device, dtype=torch.float32)
+            Cs = torch.empty_like(Y)
+            Gs = torch.empty(B, T, 4 * H, device=x.device, dtype=torch.float32)
+            call('encx_lstm_layer_fwd', ptr(inp), bct, ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh),
+                 ptr(gx), ptr(Y), ptr(Cs), ptr(Gs), B, T, H, H, st)
+            states.append((inp, bct, Y, Cs, Gs))
+            inp, bct = Y, 0
+        out = torch.empty_like(x)
+        if skip:
+            call('encx_lstm_out_skip', ptr(inp), ptr(x), ptr(out), B, T, H, st)
+        else:
+            out.copy_(inp.permute(0, 2, 1))
+        ctx.states = states
+        ctx.weights = weights
+        ctx.skip = skip
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = dout.contiguous()
+        B, H, T = dout.shape
+        weights, states = ctx.weights, ctx.states
+        L = len(weights) // 4
+        st = stream()
+        dY = torch.empty(B, T, H, device=dout.device, dtype=torch.float32)
+        call('encx_lstm_dout_t', ptr(dout), ptr(dY), B, T, H, st)
+        need_dx = ctx.needs_input_grad[0]
+        dx = (dout.clone() if ctx.skip else torch.zeros_like(dout)) if need_dx else None
+        DA = _f32(B * T * 4 * H, dout)
+        ws = _ws(lib.encx_lstm_bwd_workspace(B, T, H, H), dout)
+        grads = [None] * len(weights)
+        for l in reversed(range(L)):
+            inp, bct, Y, Cs, Gs = states[l]
+            w_ih, w_hh, b_ih, b_hh = weights[4 * l:4 * l + 4]
+            want_w = any(ctx.needs_input_grad[2 + 4 * l + i] for i in range(4))
+            direct = all(_direct(w) for w in (w_ih, w_hh, b_ih, b_hh))
+            if want_w and direct:
+                dws, acc_w = [w.grad for w in (w_ih, w_hh, b_ih, b_hh)], 1
+            elif want_w:
+                dws, acc_w = [torch.empty_like(w) for w in (w_ih, w_hh, b_ih, b_hh)], 0
+                grads[4 * l:4 * l + 4] = dws
+            else:
+                dws, acc_w = [None] * 4, 0
+            if l > 0:
+                dprev = torch.empty(B, T, H, device=dout.device, dtype=torch.float32)
+                acc_x = 0
+            else:
+                dprev, acc_x = dx, 1
+            call('encx_lstm_layer_bwd', ptr(inp), bct, ptr(w_ih.contiguous()), ptr(w_hh.contiguous()),
+                 ptr(Y), ptr(Cs), ptr(Gs), ptr(dY), ptr(DA), ptr(dprev), acc_x, ptr(dws[0]),
+                 ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), acc_w, ptr(ws), B, T, H, H, st)
+            dY = dprev
+        ctx.states = None
+        return (dx, None, *grads)
+
+
+def lstm(x, weights, skip=True):
+    return LSTMFn.apply(x, skip, *weights)

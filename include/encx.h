@@ -239,6 +239,29 @@ int encx_balancer_combine(const float* g0, const float* g1, const float* g2, con
 int encx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
                    double beta2, double eps, int64_t step, encx_stream_t stream);
 
+/* ---- SLSTM (modules/lstm.py:12-28 -> torch.nn.LSTM(dim, dim, num_layers) + skip) ----
+ * Sequence tensors are [B][T][.]; gate order i, f, g, o. B <= 64, H % 16 == 0.
+ * One layer forward: x is the layer input ([B][C][T] when x_bct, else [B][T][C]); Gx is a
+ * [B*T][4H] scratch; writes h_t (Y), c_t (Cst) [B][T][H] and gate activations Gs [B][T][4H]. */
+int encx_lstm_layer_fwd(const float* x, int x_bct, const float* w_ih, const float* w_hh,
+                        const float* b_ih, const float* b_hh, float* Gx, float* Y, float* Cst,
+                        float* Gs, int64_t B, int64_t T, int64_t C, int64_t H, encx_stream_t stream);
+size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t C, int64_t H);
+/* One layer backward from dY [B][T][H]: DA [B][T][4H] scratch; weight grads written (acc_w=0)
+ * or added (acc_w=1), the bias grad going to both db_ih and db_hh; dx in the layout of x
+ * (added when acc_x). Any of dx/dw_ih/dw_hh may be NULL to skip. */
+int encx_lstm_layer_bwd(const float* x, int x_bct, const float* w_ih, const float* w_hh,
+                        const float* Y, const float* Cst, const float* Gs, const float* dY,
+                        float* DA, float* dx, int acc_x, float* dw_ih, float* dw_hh,
+                        float* db_ih, float* db_hh, int acc_w, float* ws, int64_t B, int64_t T,
+                        int64_t C, int64_t H, encx_stream_t stream);
+/* out[b][u][t] = Y[b][t][u] + x[b][u][t]  (lstm.py:25-27 permute back + skip) */
+int encx_lstm_out_skip(const float* Y, const float* x, float* out, int64_t B, int64_t T, int64_t H,
+                       encx_stream_t stream);
+/* dY[b][t][u] = dout[b][u][t] */
+int encx_lstm_dout_t(const float* dout, float* dY, int64_t B, int64_t T, int64_t H,
+                     encx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -287,3 +287,39 @@ def test_normalize_and_scale():
     xr, scr = O.normalize(T(x0))
     close(xn, xr, 1e-6, 1e-7, 'xn')
     close(sc, scr, 1e-6, 1e-9, 'scale')
+
+
+# --------------------------------------------------------------------------- LSTM
+@pytest.mark.parametrize('B,H,Tn', [(3, 32, 7), (17, 64, 20), (32, 512, 75)])
+def test_lstm_vs_oracle(B, H, Tn):
+    """encx LSTM (csrc/lstm.hip) forward + backward against the oracle's step-by-step
+    restatement of SLSTM (modules/lstm.py:22-28) run in fp64 on the CPU."""
+    from encx import ops
+    gen = torch.Generator().manual_seed(B * 1000 + H)
+    k = 1.0 / np.sqrt(H)
+    names = ['weight_ih', 'weight_hh', 'bias_ih', 'bias_hh']
+    shapes = [(4 * H, H), (4 * H, H), (4 * H,), (4 * H,)]
+    p64, wts = {}, []
+    for l in range(2):
+        for n, s in zip(names, shapes):
+            w = (torch.rand(s, generator=gen, dtype=torch.float64) * 2 - 1) * k
+            p64[f'm.lstm.{n}_l{l}'] = w.requires_grad_(True)
+            wts.append(w.detach().float().to(DEV).requires_grad_(True))
+    x64 = torch.randn(B, H, Tn, generator=gen, dtype=torch.float64).requires_grad_(True)
+    r64 = torch.randn(B, H, Tn, generator=gen, dtype=torch.float64)
+    y64 = O.slstm(x64, p64, 'm', 2)
+    (y64 * r64).sum().backward()
+    x = x64.detach().float().to(DEV).requires_grad_(True)
+    y = ops.lstm(x, wts, skip=True)
+    (y * r64.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+
+    def rel_close(a, b, what, tol=2e-4):
+        b = b.detach()
+        scale = b.abs().max().item() + 1e-12
+        close(a, b, rtol=tol, atol=tol * scale, what=what)
+
+    rel_close(y, y64, 'y')
+    rel_close(x.grad, x64.grad, 'dx')
+    for i, (n, w) in enumerate(p64.items()):
+        rel_close(wts[i].grad, w.grad, n, tol=5e-4)
