@@ -375,14 +375,14 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     }
     if (WK > 1) {  // combine the waves' partial tiles in wave order (deterministic)
         __syncthreads();
-        float* red = smem;  // [WK][TM*TN*16][64]
+        float* red = smem;  // [WM*WN][WK][TM*TN*16][64]
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    red[((wk * TM * TN + i * TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+                    red[(((wmn * WK + wk) * TM * TN + i * TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
         __syncthreads();
         if (wk != 0) return;
 #pragma unroll
@@ -391,8 +391,9 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    float v = red[((i * TN + j) * 16 + r) * 64 + lane];
-                    for (int w = 1; w < WK; ++w) v += red[((w * TM * TN + i * TN + j) * 16 + r) * 64 + lane];
+                    float v = red[(((wmn * WK) * TM * TN + i * TN + j) * 16 + r) * 64 + lane];
+                    for (int w = 1; w < WK; ++w)
+                        v += red[(((wmn * WK + w) * TM * TN + i * TN + j) * 16 + r) * 64 + lane];
                     acc[i][j][r] = v;
                 }
     }
@@ -804,7 +805,7 @@ template <int BM, int BN, int WM, int WN, int WK>
 void launch_wg(const WgArgs& a, int splits, hipStream_t st) {
     dim3 grid(cdiv((int64_t)a.C * a.K, BN), cdiv(a.A, BM), splits);
     size_t lds = (size_t)(a.BT * BM + a.NCmax * a.WLp) * sizeof(float);
-    size_t red = (size_t)WK * (BM / WM / 32) * (BN / WN / 32) * 16 * 64 * sizeof(float);
+    size_t red = (size_t)4 * (BM / WM / 32) * (BN / WN / 32) * 16 * 64 * sizeof(float);  // all 4 waves
     if (WK > 1 && red > lds) lds = red;
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, WK>), grid, dim3(NT), lds, st, a);
 }

@@ -1,0 +1,772 @@
+// MS-STFT discriminator (msstftd.py:28-149) and its losses (losses.py:44-80) on gfx950.
+//
+//   spectrogram  torchaudio Spectrogram(normalized, center=False, power=None) as a DFT GEMM:
+//                frames gathered from the waveform while staging, [w cos | -w sin] table
+//                shared with the mel loss; the epilogue writes the cat([re, im]) and
+//                'b c w t -> b c t w' layout directly. Backward: the transposed GEMM + a
+//                fixed-order overlap-add.
+//   NormConv2d   (modules/conv.py:125-139) as three implicit GEMMs over v_mfma_f32_32x32x2_f32:
+//     fwd    Y[co][(t,f)]  = sum_{(ci,kt),kf} W * X[ci][t+kt*dt-pt][f*sf+kf-pf]; the (t, f)
+//            output positions of a batch item are flattened into one GEMM column space so
+//            narrow late layers (F = 33..65) still fill 32-wide MFMA tiles; every tile stages
+//            the input rows it touches (one window per (ci, kt) and output row) in LDS.
+//            Bias + LeakyReLU(0.2) fused in the epilogue.
+//     dgrad  polyphase along f (rows (ci, r), columns (t, u), reduction ((co, kt), q)), the
+//            output-grad mask LeakyReLU'(y) applied while staging, the input's LeakyReLU'
+//            applied in the epilogue; every dX element is written exactly once.
+//     wgrad  dW[co][((ci,kt),kf)] + the bias as a ones column, split over (b, position chunk)
+//            work items into slabs, summed in a fixed order (deterministic).
+#include "common.h"
+#include "gemm.h"
+#include "prof.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+struct C2Geo {
+    int B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf;
+};
+
+// ------------------------------------------------------------------------------- forward
+struct C2Fwd {
+    C2Geo g;
+    const float* x;
+    const float* wf;  // [(ci,kt)][kf][co]
+    const float* bias;
+    float* y;
+    int act;
+    int CK, NR, RL;
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(NT) void c2_fwd_kernel(C2Fwd a) {
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int CK = a.CK, NR = a.NR, RL = a.RL, KF = g.KF, S = g.sf;
+    const int VC = g.Ci * g.KT, XR = NR * RL;
+    float* Xs = smem;           // [CK][NR][RL]
+    float* Ws = smem + CK * XR; // [KF][CK][BM]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.z, n0 = blockIdx.x * BN, co0 = blockIdx.y * BM;
+    const int Nall = g.T2 * g.Fo, nend = min(Nall, n0 + BN);
+    const int tf = n0 / g.Fo, f0 = n0 - tf * g.Fo;
+    const int nr = (nend - 1) / g.Fo - tf + 1;
+    int boff[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+        boff[j] = 0;
+        if (n < nend) {
+            const int tr = n / g.Fo, f = n - tr * g.Fo, rs = tr - tf;
+            boff[j] = rs * RL + (f - (rs ? 0 : f0)) * S;
+        }
+    }
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    const float* xb = a.x + (int64_t)b * g.Ci * g.T2 * g.Fi;
+    for (int c0 = 0; c0 < VC; c0 += CK) {
+        __syncthreads();
+        for (int i = tid; i < CK * XR; i += NT) {
+            const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
+            const int vc = c0 + cl;
+            float v = 0.f;
+            if (vc < VC && rs < nr) {
+                const int ci = vc / g.KT, kt = vc - ci * g.KT;
+                const int row = tf + rs + kt * g.dt - g.pt;
+                const int pos = (rs ? 0 : f0) * S - g.pf + w;
+                if (row >= 0 && row < g.T2 && pos >= 0 && pos < g.Fi)
+                    v = xb[((int64_t)ci * g.T2 + row) * g.Fi + pos];
+            }
+            Xs[i] = v;
+        }
+        for (int i = tid; i < KF * CK * BM; i += NT) {
+            const int col = i % BM, r = i / BM, cl = r % CK, kf = r / CK;
+            const int vc = c0 + cl, co = co0 + col;
+            Ws[i] = (vc < VC && co < g.Co) ? a.wf[((int64_t)vc * KF + kf) * g.Co + co] : 0.f;
+        }
+        __syncthreads();
+        for (int kf = 0; kf < KF; ++kf) {
+            const float* wk = Ws + (kf * CK + h) * BM + wm0 + l32;
+            const float* xk = Xs + h * XR + kf;
+            for (int cp = 0; cp < CK; cp += 2) {
+                float av[TM], bv[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = wk[cp * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xk[cp * XR + boff[j]];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = co0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (co < g.Co && n < nend) {
+                    float v = acc[i][j][r] + (a.bias ? a.bias[co] : 0.f);
+                    if (a.act) v = lrelu(v);
+                    a.y[((int64_t)b * g.Co + co) * Nall + n] = v;
+                }
+            }
+        }
+}
+
+// ------------------------------------------------------------------------ backward data
+struct C2Dg {
+    C2Geo g;
+    const float* dy;    // [B][Co][T2][Fo]
+    const float* yact;  // post-activation output (LeakyReLU' mask of dy) or null
+    const float* wp;    // [(co,kt)][J][ci*S + r]
+    const float* xact;  // input (LeakyReLU' of the previous layer) or null
+    float* dx;          // [B][Ci][T2][Fi]
+    int J, U, CK, NR, RL, accumulate;
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int CK = a.CK, NR = a.NR, RL = a.RL, J = a.J, U = a.U, S = g.sf;
+    const int VC = g.Co * g.KT, XR = NR * RL, M = g.Ci * S;
+    float* Xs = smem;            // [CK][NR][RL]
+    float* As = smem + CK * XR;  // [J][CK][BM]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.z, n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int Nall = g.T2 * U, nend = min(Nall, n0 + BN);
+    const int tf = n0 / U, u0 = n0 - tf * U;
+    const int nr = (nend - 1) / U - tf + 1;
+    int boff[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+        boff[j] = J - 1;  // in-range LDS reads for masked columns
+        if (n < nend) {
+            const int tr = n / U, u = n - tr * U, rs = tr - tf;
+            boff[j] = rs * RL + (u - (rs ? 0 : u0)) + (J - 1);
+        }
+    }
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    const int64_t plane = (int64_t)g.T2 * g.Fo;
+    const float* dyb = a.dy + (int64_t)b * g.Co * plane;
+    const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane : nullptr;
+    for (int c0 = 0; c0 < VC; c0 += CK) {
+        __syncthreads();
+        for (int i = tid; i < CK * XR; i += NT) {
+            const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
+            const int vc = c0 + cl;
+            float v = 0.f;
+            if (vc < VC && rs < nr) {
+                const int co = vc / g.KT, kt = vc - co * g.KT;
+                const int row = tf + rs + g.pt - kt * g.dt;        // output row feeding this x row
+                const int pos = (rs ? 0 : u0) - (J - 1) + w;     // output column f = u - q
+                if (row >= 0 && row < g.T2 && pos >= 0 && pos < g.Fo) {
+                    const int64_t o = (int64_t)co * plane + (int64_t)row * g.Fo + pos;
+                    v = dyb[o];
+                    if (yab) v *= lrelu_grad(yab[o]);
+                }
+            }
+            Xs[i] = v;
+        }
+        for (int i = tid; i < J * CK * BM; i += NT) {
+            const int col = i % BM, r = i / BM, cl = r % CK, q = r / CK;
+            const int vc = c0 + cl, row = m0 + col;
+            As[i] = (vc < VC && row < M) ? a.wp[((int64_t)vc * J + q) * M + row] : 0.f;
+        }
+        __syncthreads();
+        for (int q = 0; q < J; ++q) {
+            const float* aq = As + (q * CK + h) * BM + wm0 + l32;
+            const float* xq = Xs + h * XR - q;
+            for (int cp = 0; cp < CK; cp += 2) {
+                float av[TM], bv[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = aq[cp * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xq[cp * XR + boff[j]];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 32 + l32;
+            if (n >= nend) continue;
+            const int tr = n / U, u = n - tr * U;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (m >= M) continue;
+                const int ci = m / S, rr = m - ci * S;
+                const int f = u * S + rr - g.pf;
+                if (f < 0 || f >= g.Fi) continue;
+                const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
+                float v = acc[i][j][r];
+                if (a.xact) v *= lrelu_grad(a.xact[o]);
+                a.dx[o] = a.accumulate ? a.dx[o] + v : v;
+            }
+        }
+}
+
+// ------------------------------------------------------------------------ weight grad
+struct C2Wg {
+    C2Geo g;
+    const float* dy;
+    const float* yact;
+    const float* x;
+    float* ws;  // [S][Co][N], N = VC*KF + 1 (bias column last)
+    int BT, NR, RL, NCmax, items, per_split, chunks;
+};
+
+template <int BM, int BN, int WM, int WN, int WK>
+__global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    static_assert(WM * WN * WK == 4, "4 waves");
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int BT = a.BT, NR = a.NR, RL = a.RL, KF = g.KF, S = g.sf;
+    const int VC = g.Ci * g.KT, Nw = VC * KF, N = Nw + 1, XR = NR * RL;
+    float* Ls = smem;                                 // [BT][BM]
+    float* Rs = Ls + BT * BM;                         // [NCmax][NR][RL]
+    int* poff = (int*)(Rs + a.NCmax * XR);            // [BT]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wk = wave % WK, wmn = wave / WK;
+    const int wm0 = (wmn / WN) * TM * 32, wn0 = (wmn % WN) * TN * 32;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int co0 = blockIdx.y * BM, n0 = blockIdx.x * BN, split = blockIdx.z;
+    const int c_first = n0 / KF;
+    const int Nall = g.T2 * g.Fo;
+    const int64_t plane_y = (int64_t)Nall, plane_x = (int64_t)g.T2 * g.Fi;
+    int cbase[TN];
+    bool isb[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+        const int vc = n / KF, kf = n - vc * KF;
+        isb[j] = n == Nw;
+        cbase[j] = (n < Nw) ? (vc - c_first) * XR + kf : 0;
+    }
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
+    const int tw = BT / WK;
+    for (int it = it_beg; it < it_end; ++it) {
+        const int b = it / a.chunks, p0 = (it - b * a.chunks) * BT;
+        const int pend = min(Nall, p0 + BT);
+        const int tf = p0 / g.Fo, f0 = p0 - tf * g.Fo;
+        const int nr = (pend - 1) / g.Fo - tf + 1;
+        const float* dyb = a.dy + (int64_t)b * g.Co * plane_y;
+        const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane_y : nullptr;
+        const float* xb = a.x + (int64_t)b * g.Ci * plane_x;
+        __syncthreads();
+        for (int i = tid; i < BT * BM; i += NT) {
+            const int tl = i % BT, col = i / BT, p = p0 + tl, co = co0 + col;
+            float v = 0.f;
+            if (p < pend && co < g.Co) {
+                const int64_t o = (int64_t)co * plane_y + p;
+                v = dyb[o];
+                if (yab) v *= lrelu_grad(yab[o]);
+            }
+            Ls[tl * BM + col] = v;
+        }
+        for (int i = tid; i < a.NCmax * XR; i += NT) {
+            const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
+            const int vc = c_first + cl;
+            float v = 0.f;
+            if (vc < VC && rs < nr) {
+                const int ci = vc / g.KT, kt = vc - ci * g.KT;
+                const int row = tf + rs + kt * g.dt - g.pt;
+                const int pos = (rs ? 0 : f0) * S - g.pf + w;
+                if (row >= 0 && row < g.T2 && pos >= 0 && pos < g.Fi)
+                    v = xb[(int64_t)ci * plane_x + (int64_t)row * g.Fi + pos];
+            }
+            Rs[i] = v;
+        }
+        for (int tl = tid; tl < BT; tl += NT) {
+            const int p = p0 + tl;
+            int off = 0;
+            if (p < pend) {
+                const int tr = p / g.Fo, f = p - tr * g.Fo, rs = tr - tf;
+                off = rs * RL + (f - (rs ? 0 : f0)) * S;
+            }
+            poff[tl] = off;
+        }
+        __syncthreads();
+        for (int tp = wk * tw; tp < (wk + 1) * tw; tp += 2) {
+            const int tl = tp + h;
+            const int po = poff[tl];
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) av[i] = Ls[tl * BM + wm0 + i * 32 + l32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bv[j] = isb[j] ? 1.f : Rs[cbase[j] + po];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+        }
+    }
+    if (WK > 1) {
+        __syncthreads();
+        float* red = smem;  // [WM*WN][WK][TM*TN*16][64]
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    red[(((wmn * WK + wk) * TM * TN + i * TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+        __syncthreads();
+        if (wk != 0) return;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float v = red[(((wmn * WK) * TM * TN + i * TN + j) * 16 + r) * 64 + lane];
+                    for (int w = 1; w < WK; ++w)
+                        v += red[(((wmn * WK + w) * TM * TN + i * TN + j) * 16 + r) * 64 + lane];
+                    acc[i][j][r] = v;
+                }
+    }
+    float* wsb = a.ws + (int64_t)split * g.Co * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = co0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (co < g.Co && n < N) wsb[(int64_t)co * N + n] = acc[i][j][r];
+            }
+        }
+}
+
+// dw[co][n] (+)= sum_s ws[s][co][n] for n < Nw; db[co] (+)= sum_s ws[s][co][Nw]. Fixed order.
+__global__ void c2_wg_reduce(const float* ws, int S, int Co, int N, float* dw, float* db, int acc_w,
+                             int acc_b) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Co * N) return;
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += ws[(int64_t)s * Co * N + i];
+    const int co = (int)(i / N), n = (int)(i - (int64_t)co * N);
+    const int Nw = N - 1;
+    if (n < Nw) {
+        if (dw) {
+            float* p = dw + (int64_t)co * Nw + n;
+            *p = acc_w ? *p + v : v;
+        }
+    } else if (db) {
+        db[co] = acc_b ? db[co] + v : v;
+    }
+}
+
+// wp[(co,kt)][q][ci*S + r] = W[co][ci][kt][q*S + r] from wf[((ci,kt))*KF + kf][co]
+__global__ void c2_wpoly_kernel(const float* wf, float* wp, int Co, int Ci, int KT, int KF, int S, int J) {
+    const int64_t total = (int64_t)Co * KT * J * Ci * S;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int M = Ci * S;
+    const int m = (int)(i % M);
+    const int64_t rq = i / M;
+    const int q = (int)(rq % J), vc = (int)(rq / J);
+    const int co = vc / KT, kt = vc - co * KT;
+    const int ci = m / S, r = m - ci * S, kf = q * S + r;
+    wp[i] = kf < KF ? wf[(((int64_t)ci * KT + kt) * KF + kf) * Co + co] : 0.f;
+}
+
+// ---------------------------------------------------------------------------- spectrogram
+struct LdSpecD {  // A(m = (bc, fr), k) = x[bc][fr*hop + k]; B = DFT table [n][2nb]
+    static constexpr bool A_K_FAST = true, B_N_FAST = true;
+    const float* x;
+    const float* bt;
+    int T, Fr, hop, nb2;
+    ENCX_DEV float a(int m, int k) const {
+        const int bc = m / Fr, fr = m - bc * Fr;
+        return x[(int64_t)bc * T + (int64_t)fr * hop + k];
+    }
+    ENCX_DEV float b(int k, int n) const { return bt[(int64_t)k * nb2 + n]; }
+};
+struct EpSpecD {  // z[b][ch][fr][k], ch = c (re) or C + c (im)
+    float* z;
+    int C, Fr, nb;
+    float inv;
+    ENCX_DEV void operator()(int m, int n, float v) const {
+        const int bc = m / Fr, fr = m - bc * Fr, b = bc / C, c = bc - b * C;
+        const int im = n >= nb, k = im ? n - nb : n, ch = im ? C + c : c;
+        z[(((int64_t)b * 2 * C + ch) * Fr + fr) * nb + k] = v * inv;
+    }
+};
+struct LdSpecDB {  // A(m = (bc, fr), col) = dz at col; B(col, t) = bt[t][col]
+    static constexpr bool A_K_FAST = true, B_N_FAST = false;
+    const float* dz;
+    const float* bt;
+    int C, Fr, nb, nb2;
+    float inv;
+    ENCX_DEV float a(int m, int col) const {
+        const int bc = m / Fr, fr = m - bc * Fr, b = bc / C, c = bc - b * C;
+        const int im = col >= nb, k = im ? col - nb : col, ch = im ? C + c : c;
+        return dz[(((int64_t)b * 2 * C + ch) * Fr + fr) * nb + k] * inv;
+    }
+    ENCX_DEV float b(int col, int t) const { return bt[(int64_t)t * nb2 + col]; }
+};
+struct EpFrames {
+    float* out;
+    int n;
+    ENCX_DEV void operator()(int m, int t, float v) const { out[(int64_t)m * n + t] = v; }
+};
+// dx[bc][t] (+)= sum_{fr: 0 <= t - fr*hop < n} frames[bc*Fr + fr][t - fr*hop], fr ascending
+__global__ void spec_overlap_add(const float* frames, float* dx, int BC, int T, int Fr, int n, int hop,
+                                 int acc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)BC * T) return;
+    const int bc = (int)(i / T), t = (int)(i - (int64_t)bc * T);
+    int lo = t - n + 1;
+    lo = lo <= 0 ? 0 : (lo + hop - 1) / hop;
+    const int hi = min(Fr - 1, t / hop);
+    float s = 0.f;
+    for (int fr = lo; fr <= hi; ++fr) s += frames[((int64_t)bc * Fr + fr) * n + (t - fr * hop)];
+    dx[i] = acc ? dx[i] + s : s;
+}
+
+// ---------------------------------------------------------------------------- losses
+// sums[0] += sum relu(1 + s*x) over n (s = -1: generator / real term, +1: fake term)
+__global__ __launch_bounds__(256) void hinge_kernel(const float* x, int64_t n, float s, float* parts) {
+    __shared__ float red[16];
+    float acc = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        acc += fmaxf(1.f + s * x[i], 0.f);
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) parts[blockIdx.x] = acc;
+}
+// parts[b] = (sum |fr - ff|, sum |fr|) over a grid-stride slice
+__global__ __launch_bounds__(256) void feat_kernel(const float* fr, const float* ff, int64_t n, float* parts) {
+    __shared__ float red[16];
+    float s1 = 0.f, s2 = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float r = fr[i];
+        s1 += fabsf(r - ff[i]);
+        s2 += fabsf(r);
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (threadIdx.x == 0) {
+        parts[2 * blockIdx.x] = s1;
+        parts[2 * blockIdx.x + 1] = s2;
+    }
+}
+constexpr int LP = 512;  // partial blocks of the loss reductions
+// out[0] (+)= scale * sum(parts[0::stride]) / (stride == 2 ? sum(parts[1::2]) : n)
+__global__ __launch_bounds__(256) void loss_finish(const float* parts, int np, int stride, double n,
+                                                   float scale, float* out, float* denom, int acc) {
+    __shared__ float red[16];
+    float a = 0.f, d = 0.f;
+    for (int i = threadIdx.x; i < np; i += 256) {
+        a += parts[i * stride];
+        if (stride == 2) d += parts[i * stride + 1];
+    }
+    a = block_sum(a, red);
+    d = block_sum(d, red);
+    if (threadIdx.x == 0) {
+        const float den = stride == 2 ? d : (float)n;
+        const float v = scale * (a / den);
+        out[0] = acc ? out[0] + v : v;
+        if (denom) denom[0] = den;
+    }
+}
+// grad of scale * mean(relu(1 + s*x)): scale * s / n where 1 + s*x > 0; g0 = upstream scalar
+__global__ void hinge_grad_kernel(const float* x, int64_t n, float s, float scale, const float* g0,
+                                  float* dx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float g = (g0 ? g0[0] : 1.f) * scale * s / (float)n;
+    dx[i] = (1.f + s * x[i] > 0.f) ? g : 0.f;
+}
+// grad wrt ff of scale * sum|fr - ff| / sum|fr| (the reference's l1 / mean|fr| ratio)
+__global__ void feat_grad_kernel(const float* fr, const float* ff, int64_t n, float scale,
+                                 const float* denom, const float* g0, float* dff) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float g = (g0 ? g0[0] : 1.f) * scale / denom[0];
+    const float d = ff[i] - fr[i];
+    dff[i] = d > 0.f ? g : (d < 0.f ? -g : 0.f);
+}
+
+// ---------------------------------------------------------------------------- planning
+static int c2_rows(int BN, int len) { return (len + BN - 2) / len + 1; }
+
+template <int BM, int BN, int WM, int WN>
+int launch_fwd(C2Fwd a, hipStream_t st) {
+    const size_t lds = ((size_t)a.CK * a.NR * a.RL + (size_t)a.g.KF * a.CK * BM) * sizeof(float);
+    dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.g.Fo, BN), (unsigned)cdiv(a.g.Co, BM), (unsigned)a.g.B);
+    hipLaunchKernelGGL((c2_fwd_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+template <int BM, int BN, int WM, int WN>
+int launch_dgrad(C2Dg a, hipStream_t st) {
+    const size_t lds = ((size_t)a.CK * a.NR * a.RL + (size_t)a.J * a.CK * BM) * sizeof(float);
+    dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.U, BN), (unsigned)cdiv(a.g.Ci * a.g.sf, BM), (unsigned)a.g.B);
+    hipLaunchKernelGGL((c2_dgrad_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+// channels per LDS chunk: even, <= VC rounded up to even, LDS <= budget floats
+static int c2_ck(int VC, int per_ch, int budget = 12288) {
+    int ck = budget / per_ch;
+    if (ck > 32) ck = 32;
+    int vce = (VC + 1) & ~1;
+    if (ck > vce) ck = vce;
+    ck &= ~1;
+    if (ck < 2) ck = 2;
+    // prefer an exact (even) divisor of VC near ck
+    for (int c = ck; c >= 2; c -= 2)
+        if (VC % c == 0 && c * 2 >= ck) return c;
+    return ck;
+}
+
+struct WgPlan2 {
+    int BT, NR, RL, NCmax, chunks, items, splits, per_split, narrow;
+};
+static WgPlan2 plan_wg2(const C2Geo& g) {
+    WgPlan2 p;
+    p.BT = 64;
+    const int Nall = g.T2 * g.Fo;
+    p.NR = c2_rows(p.BT, g.Fo);
+    p.RL = (min(p.BT, g.Fo) - 1) * g.sf + g.KF;
+    const int N = g.Ci * g.KT * g.KF + 1;
+    p.narrow = N <= 64;
+    const int BN = p.narrow ? 64 : 128;
+    p.NCmax = (BN - 1) / g.KF + 2;
+    p.chunks = (int)cdiv(Nall, p.BT);
+    p.items = g.B * p.chunks;
+    const int tiles = (int)(cdiv(N, BN) * cdiv(g.Co, 32));
+    int sp = (int)cdiv(1024, tiles);
+    if (sp > p.items) sp = p.items;
+    p.per_split = (int)cdiv(p.items, sp);
+    p.splits = (int)cdiv(p.items, p.per_split);
+    return p;
+}
+
+static bool geo_ok(const C2Geo& g) {
+    return g.B > 0 && g.Ci > 0 && g.T2 > 0 && g.Fi > 0 && g.Co > 0 && g.Fo > 0 && g.KT > 0 && g.KF > 0 &&
+           g.sf > 0 && g.dt > 0 && g.pt >= 0 && g.pf >= 0 &&
+           g.Fo == (g.Fi + 2 * g.pf - g.KF) / g.sf + 1 && g.T2 + 2 * g.pt - g.dt * (g.KT - 1) == g.T2;
+}
+
+}  // namespace
+
+extern "C" {
+
+/* NormConv2d geometry as used by DiscriminatorSTFT (msstftd.py:67-84): input [B][Ci][T2][Fi]
+ * (time frames x freq bins), kernel (KT, KF), stride (1, sf), dilation (dt, 1), zero padding
+ * (pt, pf) with T2 preserved; Fo = (Fi + 2 pf - KF)/sf + 1. */
+int encx_conv2d_wpoly(const float* wf, float* wp, int64_t Co, int64_t Ci, int64_t KT, int64_t KF, int64_t sf,
+                      encx_stream_t stream) {
+    ENCX_REQUIRE(wf && wp && Co > 0 && Ci > 0 && KT > 0 && KF > 0 && sf > 0);
+    const int J = (int)cdiv(KF, sf);
+    const int64_t total = Co * KT * J * Ci * sf;
+    hipLaunchKernelGGL(c2_wpoly_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, wf,
+                       wp, (int)Co, (int)Ci, (int)KT, (int)KF, (int)sf, J);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y, int64_t B, int64_t Ci,
+                    int64_t T2, int64_t Fi, int64_t Co, int64_t Fo, int64_t KT, int64_t KF, int64_t sf,
+                    int64_t dt, int64_t pt, int64_t pf, int act, encx_stream_t stream) {
+    ENCX_REQUIRE(x && wf && y);
+    C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
+    ENCX_REQUIRE(geo_ok(g));
+    hipStream_t st = (hipStream_t)stream;
+    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + B * Co * T2 * Fo));
+    C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
+    constexpr int BN = 128;
+    a.NR = c2_rows(BN, (int)Fo);
+    a.RL = (min(BN, (int)Fo) - 1) * (int)sf + (int)KF;
+    a.CK = c2_ck((int)(Ci * KT), a.NR * a.RL + (int)KF * 32);
+    if (Co <= 32) return launch_fwd<32, 128, 1, 4>(a, st);
+    a.CK = c2_ck((int)(Ci * KT), a.NR * a.RL + (int)KF * 64);
+    return launch_fwd<64, 128, 2, 2>(a, st);
+}
+
+int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
+                         int accumulate, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
+                         int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
+                         encx_stream_t stream) {
+    ENCX_REQUIRE(dy && wp && dx);
+    C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
+    ENCX_REQUIRE(geo_ok(g));
+    hipStream_t st = (hipStream_t)stream;
+    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo));
+    C2Dg a{g, dy, yact, wp, xact, dx, 0, 0, 0, 0, 0, accumulate};
+    constexpr int BN = 128;
+    a.J = (int)cdiv(KF, sf);
+    a.U = (int)((Fi - 1 + pf) / sf + 1);
+    a.NR = c2_rows(BN, a.U);
+    a.RL = min(BN, a.U) - 1 + a.J;
+    const int M = (int)(Ci * sf);
+    if (M <= 32) {
+        a.CK = c2_ck((int)(Co * KT), a.NR * a.RL + a.J * 32);
+        return launch_dgrad<32, 128, 1, 4>(a, st);
+    }
+    a.CK = c2_ck((int)(Co * KT), a.NR * a.RL + a.J * 64);
+    return launch_dgrad<64, 128, 2, 2>(a, st);
+}
+
+size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
+                                        int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf) {
+    C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
+    WgPlan2 p = plan_wg2(g);
+    return (size_t)p.splits * Co * (Ci * KT * KF + 1) * sizeof(float);
+}
+
+/* dw [Co][Ci][KT][KF] and db [Co] (either may be NULL) of the layer whose output grad is dy,
+ * masked by LeakyReLU'(yact) when yact != NULL. acc_w / acc_b: add into dw / db. */
+int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, float* dw, float* db,
+                           int acc_w, int acc_b, float* ws, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co,
+                           int64_t Fo, int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
+                           encx_stream_t stream) {
+    ENCX_REQUIRE(dy && x && ws);
+    C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
+    ENCX_REQUIRE(geo_ok(g));
+    hipStream_t st = (hipStream_t)stream;
+    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo));
+    WgPlan2 p = plan_wg2(g);
+    C2Wg a{g, dy, yact, x, ws, p.BT, p.NR, p.RL, p.NCmax, p.items, p.per_split, p.chunks};
+    const int N = (int)(Ci * KT * KF + 1);
+    const size_t lds = ((size_t)p.BT * 32 + (size_t)p.NCmax * p.NR * p.RL) * sizeof(float) + p.BT * sizeof(int);
+    if (p.narrow) {
+        const size_t red = (size_t)4 * 16 * 64 * sizeof(float);  // all 4 waves' tiles
+        hipLaunchKernelGGL((c2_wgrad_kernel<32, 64, 1, 2, 2>), dim3((unsigned)cdiv(N, 64), (unsigned)cdiv(Co, 32), p.splits),
+                           dim3(NT), lds > red ? lds : red, st, a);
+    } else {
+        hipLaunchKernelGGL((c2_wgrad_kernel<32, 128, 1, 4, 1>), dim3((unsigned)cdiv(N, 128), (unsigned)cdiv(Co, 32), p.splits),
+                           dim3(NT), lds, st, a);
+    }
+    ENCX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 256)), dim3(256), 0, st, ws, p.splits, (int)Co, N,
+                       dw, db, acc_w, acc_b);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+/* Spectrogram of DiscriminatorSTFT (msstftd.py:62-64, 97-99): x [B][C][T] -> z [B][2C][Fr][nb]
+ * (channels re_0..re_{C-1}, im_0..im_{C-1}), Fr = (T - n)/hop + 1, nb = n/2 + 1, scaled by
+ * 1/sqrt(sum w^2) (normalized=True). tables: the mel-table layout of n (encx_mel_tables_init). */
+int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B, int64_t C, int64_t T,
+                       int64_t n_fft, int64_t hop, encx_stream_t stream) {
+    ENCX_REQUIRE(x && tables && z && T >= n_fft && hop > 0);
+    hipStream_t st = (hipStream_t)stream;
+    const int Fr = (int)((T - n_fft) / hop + 1), nb = (int)(n_fft / 2 + 1);
+    const float inv = (float)(1.0 / sqrt(3.0 * (double)n_fft / 8.0));  // sum of periodic hann^2 = 3n/8
+    const int M = (int)(B * C * Fr), N = 2 * nb, K = (int)n_fft;
+    encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * (B * C * T + (int64_t)M * N));
+    return gemm_launch(LdSpecD{x, tables, (int)T, Fr, (int)hop, N}, EpSpecD{z, (int)C, Fr, nb, inv}, M, N, K, st);
+}
+
+size_t encx_disc_spec_bwd_workspace(int64_t B, int64_t C, int64_t T, int64_t n_fft, int64_t hop) {
+    const int64_t Fr = (T - n_fft) / hop + 1;
+    return (size_t)(B * C * Fr * n_fft) * sizeof(float);
+}
+
+/* dx (+)= d spectrogram^T dz (accumulate: add into dx). ws: encx_disc_spec_bwd_workspace. */
+int encx_disc_spec_bwd(const float* dz, const float* tables, float* dx, float* ws, int accumulate, int64_t B,
+                       int64_t C, int64_t T, int64_t n_fft, int64_t hop, encx_stream_t stream) {
+    ENCX_REQUIRE(dz && tables && dx && ws && T >= n_fft && hop > 0);
+    hipStream_t st = (hipStream_t)stream;
+    const int Fr = (int)((T - n_fft) / hop + 1), nb = (int)(n_fft / 2 + 1);
+    const float inv = (float)(1.0 / sqrt(3.0 * (double)n_fft / 8.0));
+    const int M = (int)(B * C * Fr), N = (int)n_fft, K = 2 * nb;
+    {
+        encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * ((int64_t)M * K + (int64_t)M * N));
+        int rc = gemm_launch(LdSpecDB{dz, tables, (int)C, Fr, nb, K, inv}, EpFrames{ws, N}, M, N, K, st);
+        if (rc) return rc;
+    }
+    const int64_t tot = B * C * T;
+    hipLaunchKernelGGL(spec_overlap_add, dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, st, ws, dx, (int)(B * C),
+                       (int)T, Fr, (int)n_fft, (int)hop, accumulate);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+size_t encx_disc_loss_workspace(void) { return (size_t)2 * LP * sizeof(float); }
+
+/* out[0] (+)= scale * mean(relu(1 + s*x)) over n elements (losses.py:48, 78-79). */
+int encx_hinge_loss(const float* x, int64_t n, double s, double scale, float* out, int accumulate, float* ws,
+                    encx_stream_t stream) {
+    ENCX_REQUIRE(x && out && ws && n > 0);
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = (int)min((int64_t)LP, cdiv(n, 256));
+    hipLaunchKernelGGL(hinge_kernel, dim3(nb), dim3(256), 0, st, x, n, (float)s, ws);
+    hipLaunchKernelGGL(loss_finish, dim3(1), dim3(256), 0, st, ws, nb, 1, (double)n, (float)scale, out,
+                       (float*)nullptr, accumulate);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+/* out[0] (+)= scale * mean|fr - ff| / mean|fr| (losses.py:53); denom[0] = sum|fr| for the
+ * backward. */
+int encx_feat_loss(const float* fr, const float* ff, int64_t n, double scale, float* out, float* denom,
+                   int accumulate, float* ws, encx_stream_t stream) {
+    ENCX_REQUIRE(fr && ff && out && ws && n > 0);
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = (int)min((int64_t)LP, cdiv(n, 256));
+    hipLaunchKernelGGL(feat_kernel, dim3(nb), dim3(256), 0, st, fr, ff, n, ws);
+    hipLaunchKernelGGL(loss_finish, dim3(1), dim3(256), 0, st, ws, nb, 2, (double)n, (float)scale, out, denom,
+                       accumulate);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+/* dx = g0[0] * scale * s / n * [1 + s*x > 0]  (g0 may be NULL: 1) */
+int encx_hinge_loss_bwd(const float* x, int64_t n, double s, double scale, const float* g0, float* dx,
+                        encx_stream_t stream) {
+    ENCX_REQUIRE(x && dx && n > 0);
+    hipLaunchKernelGGL(hinge_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, x, n,
+                       (float)s, (float)scale, g0, dx);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+/* dff = g0[0] * scale * sign(ff - fr) / denom[0] */
+int encx_feat_loss_bwd(const float* fr, const float* ff, int64_t n, double scale, const float* denom,
+                       const float* g0, float* dff, encx_stream_t stream) {
+    ENCX_REQUIRE(fr && ff && denom && dff && n > 0);
+    hipLaunchKernelGGL(feat_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, fr, ff, n,
+                       (float)scale, denom, g0, dff);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

@@ -88,6 +88,34 @@ class NormConvTranspose1d(nn.Module):
         self.kernel_size, self.stride = kernel_size, stride
 
 
+class NormConv2d(nn.Module):
+    """modules/conv.py:125-139: Conv2d with weight norm (or none), the DiscriminatorSTFT layer.
+    forward(x, act) also applies the LeakyReLU(0.2) that follows every inner layer of the
+    discriminator (msstftd.py:100-103); param_grads=False runs the layer as a function of its
+    input only (the generator step differentiates the discriminator w.r.t. audio, never its
+    weights)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, dilation=1, padding=0,
+                 bias=True, norm='none', norm_kwargs={}):
+        super().__init__()
+        assert norm in CONV_NORMALIZATIONS
+        pair = lambda v: tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+        self.kernel_size, self.stride = pair(kernel_size), pair(stride)
+        self.dilation, self.padding = pair(dilation), pair(padding)
+        self.conv = _ConvParams((out_channels, in_channels) + self.kernel_size, out_channels, norm, bias)
+        self.norm = nn.Identity()
+        self.norm_type = norm
+
+    def forward(self, x, act=False, param_grads=True):
+        v, g = self.conv.wv()
+        b = self.conv.bias
+        if not param_grads:
+            v = v.detach()
+            g = g.detach() if g is not None else None
+            b = b.detach() if b is not None else None
+        return ops.conv2d(x, v, g, b, self.kernel_size, self.stride, self.dilation, self.padding, act)
+
+
 class SConv1d(nn.Module):
     """modules/conv.py:175-210: causal / asymmetric reflect padding + conv, one HIP launch."""
 

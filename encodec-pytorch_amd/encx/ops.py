@@ -545,3 +545,175 @@ class LSTMFn(torch.autograd.Function):
 
 def lstm(x, weights, skip=True):
     return LSTMFn.apply(x, skip, *weights)
+
+
+# ---------------------------------------------------------------------------- MS-STFT disc
+def conv2d_geometry(Fi, kernel, stride, dilation, padding):
+    (KT, KF), (st, sf), (dt, df), (pt, pf) = kernel, stride, dilation, padding
+    if st != 1 or df != 1 or 2 * pt != dt * (KT - 1):
+        raise NotImplementedError('encx conv2d: the DiscriminatorSTFT geometry (time stride 1, '
+                                  'freq dilation 1, time-preserving padding)')
+    Fo = (Fi + 2 * pf - KF) // sf + 1
+    return KT, KF, sf, dt, pt, pf, Fo
+
+
+class Conv2dFn(torch.autograd.Function):
+    """NormConv2d.forward (modules/conv.py:136-139) + the LeakyReLU(0.2) that follows it in
+    DiscriminatorSTFT.forward (msstftd.py:100-103) when act. Returns the post-activation map
+    (the fmap entry); its sign is the pre-activation's, so it also serves as the LeakyReLU'
+    mask in the backward."""
+
+    @staticmethod
+    def forward(ctx, x, v, g, b, geo, act):
+        _check(x)
+        x = x.contiguous()
+        B, Ci, T2, Fi = x.shape
+        Co = v.shape[0]
+        KT, KF, sf, dt, pt, pf, Fo = geo
+        st = stream()
+        wf = _f32(Co * Ci * KT * KF, x)
+        call('encx_weightnorm_fwd', ptr(v), ptr(g), ptr(wf), None, Co, Ci * KT, KF, 1, st)
+        y = torch.empty(B, Co, T2, Fo, device=x.device, dtype=torch.float32)
+        call('encx_conv2d_fwd', ptr(x), ptr(wf), ptr(b), ptr(y), B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt,
+             pf, int(act), st)
+        ctx.save_for_backward(x, y, wf)
+        ctx.params = (v, g, b)
+        ctx.geo, ctx.act = geo, act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, wf = ctx.saved_tensors
+        v, g, b = ctx.params
+        KT, KF, sf, dt, pt, pf, Fo = ctx.geo
+        dy = dy.contiguous()
+        B, Ci, T2, Fi = x.shape
+        Co = v.shape[0]
+        st = stream()
+        yact = y if ctx.act else None
+        dims = (B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf)
+        dx = dv = dg = db = None
+        if ctx.needs_input_grad[0]:
+            J = -(-KF // sf)
+            wp = _f32(Co * KT * J * Ci * sf, x)
+            call('encx_conv2d_wpoly', ptr(wf), ptr(wp), Co, Ci, KT, KF, sf, st)
+            dx = torch.empty_like(x)
+            call('encx_conv2d_bwd_data', ptr(dy), ptr(yact), ptr(wp), None, ptr(dx), 0, *dims, st)
+        if any(ctx.needs_input_grad[1:4]):
+            ws = _ws(lib.encx_conv2d_bwd_weight_workspace(*dims), x)
+            direct = _direct(v) and _direct(g) and _direct(b)
+            if direct and g is None:   # plain weight: straight into the flat grad views
+                call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(v.grad), ptr(b.grad), 1, 1,
+                     ptr(ws), *dims, st)
+            elif direct:
+                dw = torch.empty(v.shape, device=x.device, dtype=torch.float32)
+                call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(dw), ptr(b.grad), 0, 1,
+                     ptr(ws), *dims, st)
+                call('encx_weightnorm_bwd', ptr(v), ptr(g), ptr(dw), ptr(v.grad), ptr(g.grad), Co,
+                     v[0].numel(), 1, st)
+            else:
+                dw = torch.empty(v.shape, device=x.device, dtype=torch.float32)
+                db = torch.empty(Co, device=x.device, dtype=torch.float32) if b is not None else None
+                call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(dw), ptr(db), 0, 0,
+                     ptr(ws), *dims, st)
+                dv, dg = _weight_bwd(v, g, dw)
+        return dx, dv, dg, db, None, None
+
+
+def conv2d(x, v, g, b, kernel, stride=(1, 1), dilation=(1, 1), padding=(0, 0), act=False):
+    geo = conv2d_geometry(x.shape[-1], kernel, stride, dilation, padding)
+    return Conv2dFn.apply(x, v, g, b, geo, act)
+
+
+class DiscSpecFn(torch.autograd.Function):
+    """torchaudio Spectrogram(normalized=True, center=False, power=None) + cat([re, im], 1) +
+    'b c w t -> b c t w' of DiscriminatorSTFT.forward (msstftd.py:62-64, 97-99)."""
+
+    @staticmethod
+    def forward(ctx, x, n_fft, hop, sr):
+        _check(x)
+        x = x.contiguous()
+        B, C, T = x.shape
+        tab = mel_tables(x.device, n_fft, 64, sr)
+        Fr = (T - n_fft) // hop + 1
+        z = torch.empty(B, 2 * C, Fr, n_fft // 2 + 1, device=x.device, dtype=torch.float32)
+        call('encx_disc_spec_fwd', ptr(x), ptr(tab), ptr(z), B, C, T, n_fft, hop, stream())
+        ctx.cfg = (B, C, T, n_fft, hop)
+        ctx.tab = tab
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        B, C, T, n_fft, hop = ctx.cfg
+        dz = dz.contiguous()
+        dx = torch.empty(B, C, T, device=dz.device, dtype=torch.float32)
+        ws = _ws(lib.encx_disc_spec_bwd_workspace(B, C, T, n_fft, hop), dz)
+        call('encx_disc_spec_bwd', ptr(dz), ptr(ctx.tab), ptr(dx), ptr(ws), 0, B, C, T, n_fft, hop, stream())
+        return dx, None, None, None
+
+
+class HingeFn(torch.autograd.Function):
+    """scale * sum_i mean(relu(1 + s_i * x_i)) over a list of logits (losses.py:48, 78-79)."""
+
+    @staticmethod
+    def forward(ctx, signs, scale, *xs):
+        out = torch.zeros(1, device=xs[0].device, dtype=torch.float32)
+        ws = _ws(lib.encx_disc_loss_workspace(), out)
+        xs = [x.contiguous() for x in xs]
+        for s, x in zip(signs, xs):
+            _check(x)
+            call('encx_hinge_loss', ptr(x), x.numel(), float(s), float(scale), ptr(out), 1, ptr(ws), stream())
+        ctx.save_for_backward(*xs)
+        ctx.signs, ctx.scale = signs, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        grads = []
+        for i, (s, x) in enumerate(zip(ctx.signs, ctx.saved_tensors)):
+            if not ctx.needs_input_grad[2 + i]:
+                grads.append(None)
+                continue
+            dx = torch.empty_like(x)
+            call('encx_hinge_loss_bwd', ptr(x), x.numel(), float(s), float(ctx.scale), ptr(g), ptr(dx), stream())
+            grads.append(dx)
+        return (None, None, *grads)
+
+
+class FeatFn(torch.autograd.Function):
+    """scale * sum_i l1(fr_i, ff_i) / mean|fr_i| (losses.py:53): the relative feature-matching
+    loss. Gradients flow to the fake maps; the real maps are treated as constants (in the
+    reference they only reach the discriminator's parameters, which the generator step's
+    balancer never differentiates)."""
+
+    @staticmethod
+    def forward(ctx, scale, n_pairs, *maps):
+        frs, ffs = maps[:n_pairs], maps[n_pairs:]
+        out = torch.zeros(1, device=ffs[0].device, dtype=torch.float32)
+        denom = torch.empty(n_pairs, device=out.device, dtype=torch.float32)
+        ws = _ws(lib.encx_disc_loss_workspace(), out)
+        frs = [f.contiguous() for f in frs]
+        ffs = [f.contiguous() for f in ffs]
+        for i, (fr, ff) in enumerate(zip(frs, ffs)):
+            _check(ff)
+            call('encx_feat_loss', ptr(fr), ptr(ff), ff.numel(), float(scale), ptr(out), ptr(denom[i:i + 1]),
+                 1, ptr(ws), stream())
+        ctx.save_for_backward(denom, *frs, *ffs)
+        ctx.scale, ctx.n = scale, n_pairs
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        denom, *maps = ctx.saved_tensors
+        n = ctx.n
+        frs, ffs = maps[:n], maps[n:]
+        grads = [None] * (2 * n)
+        for i, (fr, ff) in enumerate(zip(frs, ffs)):
+            if ctx.needs_input_grad[2 + n + i]:
+                d = torch.empty_like(ff)
+                call('encx_feat_loss_bwd', ptr(fr), ptr(ff), ff.numel(), float(ctx.scale), ptr(denom[i:i + 1]),
+                     ptr(g), ptr(d), stream())
+                grads[n + i] = d
+        return (None, None, *grads)

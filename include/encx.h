@@ -262,6 +262,52 @@ int encx_lstm_out_skip(const float* Y, const float* x, float* out, int64_t B, in
 int encx_lstm_dout_t(const float* dout, float* dY, int64_t B, int64_t T, int64_t H,
                      encx_stream_t stream);
 
+/* ---- MS-STFT discriminator (msstftd.py:28-149) ----
+ * NormConv2d (modules/conv.py:125-139) as used by DiscriminatorSTFT: input [B][Ci][T2][Fi]
+ * (frames x bins), kernel (KT, KF), stride (1, sf), dilation (dt, 1), zero padding (pt, pf)
+ * with T2 preserved, Fo = (Fi + 2 pf - KF)/sf + 1. Weights in the wf layout written by
+ * encx_weightnorm_fwd(v, g, wf, NULL, Co, Ci*KT, KF, 1, .) (g may be NULL: plain weight).
+ * act = 1 fuses LeakyReLU(0.2) (msstftd.py:101-102) into the output. */
+int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y, int64_t B, int64_t Ci,
+                    int64_t T2, int64_t Fi, int64_t Co, int64_t Fo, int64_t KT, int64_t KF, int64_t sf,
+                    int64_t dt, int64_t pt, int64_t pf, int act, encx_stream_t stream);
+/* polyphase weight layout for the backward-data: wp[(co,kt)][ceil(KF/sf)][ci*sf + r] */
+int encx_conv2d_wpoly(const float* wf, float* wp, int64_t Co, int64_t Ci, int64_t KT, int64_t KF, int64_t sf,
+                      encx_stream_t stream);
+/* dx (+)= d/dx, from dy masked by LeakyReLU'(yact) (yact NULL: no output activation) and
+ * multiplied by LeakyReLU'(xact) (xact NULL: the input had no activation). */
+int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
+                         int accumulate, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
+                         int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
+                         encx_stream_t stream);
+size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
+                                        int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf);
+/* dw [Co][Ci][KT][KF] and db [Co] (either may be NULL), written or added (acc_w / acc_b). */
+int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, float* dw, float* db,
+                           int acc_w, int acc_b, float* ws, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co,
+                           int64_t Fo, int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
+                           encx_stream_t stream);
+/* Spectrogram(n_fft, hop, win=n_fft, hann, normalized=True, center=False, power=None) of
+ * x [B][C][T], written as cat([re, im], 1) in 'b c t w' layout: z [B][2C][Fr][n/2+1]
+ * (msstftd.py:97-99). tables: the mel-table buffer of this n_fft (encx_mel_tables_init). */
+int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B, int64_t C, int64_t T,
+                       int64_t n_fft, int64_t hop, encx_stream_t stream);
+size_t encx_disc_spec_bwd_workspace(int64_t B, int64_t C, int64_t T, int64_t n_fft, int64_t hop);
+int encx_disc_spec_bwd(const float* dz, const float* tables, float* dx, float* ws, int accumulate, int64_t B,
+                       int64_t C, int64_t T, int64_t n_fft, int64_t hop, encx_stream_t stream);
+/* Hinge / relative feature-matching losses (losses.py:44-56, 65-80). ws: workspace bytes. */
+size_t encx_disc_loss_workspace(void);
+/* out[0] (+)= scale * mean(relu(1 + s*x)) */
+int encx_hinge_loss(const float* x, int64_t n, double s, double scale, float* out, int accumulate, float* ws,
+                    encx_stream_t stream);
+int encx_hinge_loss_bwd(const float* x, int64_t n, double s, double scale, const float* g0, float* dx,
+                        encx_stream_t stream);
+/* out[0] (+)= scale * mean|fr - ff| / mean|fr|; denom[0] = sum|fr| for the backward */
+int encx_feat_loss(const float* fr, const float* ff, int64_t n, double scale, float* out, float* denom,
+                   int accumulate, float* ws, encx_stream_t stream);
+int encx_feat_loss_bwd(const float* fr, const float* ff, int64_t n, double scale, const float* denom,
+                       const float* g0, float* dff, encx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,152 @@
+"""GPU parity of the MS-STFT discriminator path (csrc/disc.hip through the C ABI): the G5
+fixture generated from the reference, the fp64 oracle at 1 s clips (forward, input grad,
+weight grads), the adversarial / feature / discriminator losses, and the GAN train step."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import encodec_oracle as O
+from fixtures import load, T, disc_state, model_state, codebooks_from_stats
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+def make_disc(seed):
+    from encx.msstftd import MultiScaleSTFTDiscriminator
+    d = MultiScaleSTFTDiscriminator(filters=32)
+    p = disc_state(seed)
+    missing, unexpected = d.load_state_dict(p, strict=False)
+    assert not unexpected and all(k.endswith('spec_transform.window') for k in missing)
+    return d.to(DEV), p
+
+
+def test_disc_fixture():
+    """G5: logits, feature maps and d/dx of sum(logits*w) + sum(mean(fmap)) (msstftd.py:131-149)."""
+    d = load('g5_disc.npz')
+    disc, _ = make_disc(51)
+    x = T(d['x']).to(DEV).requires_grad_(True)
+    logits, fmaps = disc(x)
+    r = np.random.Generator(np.random.PCG64(53))
+    f = 0
+    for k, lg in enumerate(logits):
+        assert rel(lg, T(d[f'logits{k}'])) < 1e-4, k
+        wl = T(r.standard_normal(size=tuple(lg.shape)).astype(np.float32)).to(DEV)
+        f = f + (lg * wl).sum()
+        for j, fm in enumerate(fmaps[k]):
+            assert tuple(fm.shape) == tuple(d[f'fmap{k}_{j}_shape'])
+            np.testing.assert_allclose(fm.double().sum().item(), d[f'fmap{k}_{j}_sum'], rtol=1e-4)
+            np.testing.assert_allclose(fm.double().pow(2).sum().item(), d[f'fmap{k}_{j}_sq'], rtol=1e-4)
+            assert rel(fm.reshape(-1)[:256], T(d[f'fmap{k}_{j}_head'])) < 1e-4
+            f = f + fm.mean()
+    f.backward()
+    assert rel(x.grad, T(d['dx'])) < 1e-3
+
+
+@pytest.mark.parametrize('B,Tn', [(2, 24000), (3, 7001)])
+def test_disc_vs_oracle_fp64(B, Tn):
+    """Full 1 s clips (all three scales at their real sizes) and a ragged length: every
+    parameter grad and the input grad against the oracle in fp64."""
+    disc, p = make_disc(7)
+    g = torch.Generator().manual_seed(B * 31 + Tn)
+    x64 = (0.1 * torch.randn(B, 1, Tn, generator=g, dtype=torch.float64)).requires_grad_(True)
+    p64 = {k: v.double().requires_grad_(True) for k, v in p.items()}
+    lg64, fm64 = O.msstft_forward(x64, p64)
+    ws = [torch.randn(l.shape, generator=g, dtype=torch.float64) for l in lg64]
+    wf = [[torch.randn(f.shape, generator=g, dtype=torch.float64) for f in fm] for fm in fm64]
+    f64 = sum((l * w).sum() for l, w in zip(lg64, ws)) + \
+        sum((f * w).sum() for fm, wm in zip(fm64, wf) for f, w in zip(fm, wm))
+    f64.backward()
+
+    x = x64.detach().float().to(DEV).requires_grad_(True)
+    lg, fm = disc(x)
+    for a, b in zip(lg, lg64):
+        assert rel(a, b) < 1e-4
+    for fa, fb in zip(fm, fm64):
+        for a, b in zip(fa, fb):
+            assert rel(a, b) < 1e-4
+    f = sum((l * w.float().to(DEV)).sum() for l, w in zip(lg, ws)) + \
+        sum((f_ * w.float().to(DEV)).sum() for fa, wm in zip(fm, wf) for f_, w in zip(fa, wm))
+    f.backward()
+    torch.cuda.synchronize()
+    assert rel(x.grad, x64.grad) < 1e-3
+    params = dict(disc.named_parameters())
+    worst, where = 0.0, ''
+    for k, v in p64.items():
+        e = rel(params[k].grad, v.grad)
+        if e > worst:
+            worst, where = e, k
+    print(f'worst disc grad rel err {worst:.3e} at {where}')
+    assert worst < 1e-3, (worst, where)
+
+
+def test_gan_losses_vs_oracle():
+    """l_g / l_feat (losses.py:44-56, incl. the double division by K) and disc_loss (:65-80)
+    values, and the generator-side grads d l_g / dy, d l_feat / dy through the discriminator."""
+    from encx.losses import total_loss, disc_loss
+    disc, p = make_disc(9)
+    g = torch.Generator().manual_seed(5)
+    x64 = 0.1 * torch.randn(2, 1, 24000, generator=g, dtype=torch.float64)
+    y64 = (x64 + 0.05 * torch.randn(2, 1, 24000, generator=g, dtype=torch.float64)).requires_grad_(True)
+    p64 = {k: v.double() for k, v in p.items()}
+    lr64, fr64 = O.msstft_forward(x64, p64)
+    lf64, ff64 = O.msstft_forward(y64, p64)
+    ref = O.total_loss(fr64, lf64, ff64, x64, y64)
+    gg64, = torch.autograd.grad(ref['l_g'].sum(), [y64], retain_graph=True)
+    gf64, = torch.autograd.grad(ref['l_feat'].sum(), [y64], retain_graph=True)
+    ld64 = O.disc_loss(lr64, [l.detach() for l in lf64])
+
+    x = x64.float().to(DEV)
+    y = y64.detach().float().to(DEV).requires_grad_(True)
+    lr, fr = disc(x, param_grads=False)
+    lf, ff = disc(y, param_grads=False)
+    out = total_loss(fr, lf, ff, x, y)
+    for k in ('l_g', 'l_feat'):
+        np.testing.assert_allclose(out[k].item(), ref[k].item(), rtol=1e-4)
+    gg, = torch.autograd.grad(out['l_g'], [y], retain_graph=True)
+    gf, = torch.autograd.grad(out['l_feat'], [y], retain_graph=True)
+    assert rel(gg, gg64) < 1e-3
+    assert rel(gf, gf64) < 2e-3
+    ld = disc_loss(lr, [l.detach() for l in lf])
+    np.testing.assert_allclose(ld.item(), ld64.item(), rtol=1e-5)
+
+
+def test_train_step_gan_fixture():
+    """G7 GAN: two full train steps (generator with the 4-loss balancer, then the
+    discriminator update) against the reference's losses and parameter checksums."""
+    from encx.train import Trainer
+    from encx.model import EncodecModel
+    d = load('g7_step.npz')
+    cfg = O.Config(target_bandwidths=(1.5,), audio_normalize=True)
+    m = EncodecModel._get_model([1.5], 24000, 1, causal=True, model_norm='weight_norm', audio_normalize=True)
+    p = model_state(cfg, 71)
+    cbs = codebooks_from_stats(d['gan/stats'], 73, 2, cfg.n_q)
+    sd = dict(p)
+    for i, cb in enumerate(cbs):
+        for k, v in cb.items():
+            sd[f'quantizer.vq.layers.{i}._codebook.{k}'] = v
+    m.load_state_dict(sd)
+    m = m.to(DEV)
+    disc, _ = make_disc(74)
+    tr = Trainer(m, disc, lr=3e-4, disc_lr=3e-4, scheduler=False)
+    x = T(d['gan/x']).to(DEV)
+    for it in range(2):
+        out = tr.step(x)
+        for k in ('l_t', 'l_f', 'l_g', 'l_feat'):
+            np.testing.assert_allclose(float(out[k]), float(d[f'gan/it{it}_{k}'].reshape(-1)[0]), rtol=2e-4)
+        np.testing.assert_allclose(float(out['l_d']), float(d[f'gan/it{it}_l_d'].reshape(-1)[0]), rtol=1e-4)
+    dsd = disc.state_dict()
+    flips = 20 * 2 * 3e-4 * 2
+    for k, v in dsd.items():
+        if k.endswith('spec_transform.window'):
+            continue
+        ref = d['gan/d/' + k]
+        mine = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        assert abs(mine[1] - ref[1]) <= 1e-4 * ref[1] + flips, (k, mine, ref)
+        assert abs(mine[0] - ref[0]) <= 1e-5 * ref[1] + flips, (k, mine, ref)

@@ -149,3 +149,43 @@ def test_full_size_train_steps_run():
     assert float(cb.inited) == 1.0 and torch.isfinite(cb.embed).all()
     assert torch.isfinite(tr.opt.flat).all()
     assert hist[-1]['l_f'] < hist[0]['l_f'] * 1.05
+
+
+def test_train_grads_vs_oracle_fp64():
+    """Element-level check of the whole generator backward (balanced l_t + l_f + commit, ONE
+    backward as in Trainer.step) against the oracle run in fp64, on the G7 fixture's model,
+    codebooks and clip. Adam is left out so near-zero grads cannot hide behind sign flips."""
+    from encx.losses import total_loss
+    from encx.train import Trainer
+    d = load('g7_step.npz')
+    m, p, cbs, cfg = build((1.5,), True, 71, d['gen/stats'], 73, 2)
+    tr = Trainer(m, None, lr=3e-4, scheduler=False, weights={'l_t': 0.1, 'l_f': 1})
+    x = G(d['gen/x'])
+    m.train()
+    tr.opt.zero_grad()
+    y, loss_w, _ = m(x)
+    codes = m.last_codes[0]
+    losses = total_loss(None, None, None, x, y, 24000)
+    out_grad = tr.balancer.compute(losses, y)
+    torch.autograd.backward([y, loss_w], [out_grad, torch.ones_like(loss_w)])
+    torch.cuda.synchronize()
+
+    x64 = T(d['gen/x']).double()
+    p64 = {k: v.double().requires_grad_(True) for k, v in p.items()}
+    cbs64 = [{k: v.double() for k, v in cb.items()} for cb in cbs]
+    y64, lw64, codes64, _, _ = O.encodec_forward_train(x64, p64, cbs64, cfg, 1.5)
+    l64 = {'l_t': O.loss_t(x64, y64), 'l_f': O.loss_f(x64, y64, 24000)}
+    g64 = {k: torch.autograd.grad(l, [y64], retain_graph=True)[0] for k, l in l64.items()}
+    og = O.Balancer({'l_t': 0.1, 'l_f': 1}).combine(g64)
+    torch.autograd.backward([y64, lw64], [og, torch.ones_like(lw64)])
+
+    assert torch.equal(codes.cpu().long(), torch.as_tensor(codes64).long().reshape(codes.shape))
+    assert rel(y, y64) < 1e-4
+    worst, where = 0.0, ''
+    params = dict(m.named_parameters())
+    for k, v in p64.items():
+        e = rel(params[k].grad, v.grad)
+        if e > worst:
+            worst, where = e, k
+    print(f'worst grad rel err {worst:.3e} at {where}')
+    assert worst < 1e-3, (worst, where)
