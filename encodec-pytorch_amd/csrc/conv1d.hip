@@ -28,6 +28,11 @@ namespace {
 constexpr int NT = 256;  // threads per workgroup (4 waves)
 constexpr int FLAT_T = 128;  // layers with T_out <= this run as one (b, t)-flattened GEMM
 
+// LDS staging: position lanes per channel lane for a window of `len` positions (QP | NT)
+constexpr int SPX = 5;  // window positions per thread in the forward staging (span <= SPX * NT)
+constexpr int SPXW = 3;  // ... and in the weight-grad R window (WL <= SPXW * NT)
+ENCX_DEV int stage_lanes(int len) { return len > 128 ? NT : (len > 64 ? 128 : 64); }
+
 // ------------------------------------------------------------------------- conv forward
 struct FwdArgs {
     const float* x;
@@ -75,29 +80,44 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
+    // staging lanes: each thread owns up to SPX window positions (their pad source and LDS slot
+    // are chunk-invariant, computed once) and walks the chunk's channels
+    const int QP = stage_lanes(span), CP = NT / QP;
+    const int qlane = tid % QP, clane = tid / QP;
+    int xm[SPX], xo[SPX];
+#pragma unroll
+    for (int k = 0; k < SPX; ++k) {
+        const int q = qlane + k * QP;
+        xo[k] = -1;
+        xm[k] = -1;
+        if (q < span) {
+            const int u = q / S, ph = q - u * S;
+            xo[k] = ph * Up + u;
+            xm[k] = pad_src(t0 * S + q, a.pl, a.Tin, a.e, a.mode);
+        }
+    }
+    constexpr int RSTEP = NT / BM;
+    const int wcol = tid % BM, wr0 = tid / BM;
+    const bool wco = co0 + wcol < a.Cout;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
         // stage activated input window, phase-major
-        for (int i = tid; i < CK * span; i += NT) {
-            int cl = i / span, q = i - cl * span;
-            int u = q / S, ph = q - u * S;
-            int c = c0 + cl;
-            float v = 0.f;
-            if (c < cend) {
-                int m = pad_src(t0 * S + q, a.pl, a.Tin, a.e, a.mode);
-                if (m >= 0) v = act_apply(a.act, xb[(int64_t)c * a.Tin + m]);
-            }
-            Xs[(cl * S + ph) * Up + u] = v;
+        for (int cl = clane; cl < CK; cl += CP) {
+            const int c = c0 + cl;
+            const bool cv = c < cend;
+            const float* xr = xb + (int64_t)c * a.Tin;
+            float* xs = Xs + cl * span;
+#pragma unroll
+            for (int k = 0; k < SPX; ++k)
+                if (xo[k] >= 0) xs[xo[k]] = (cv && xm[k] >= 0) ? act_apply(a.act, xr[xm[k]]) : 0.f;
         }
         // stage weights [k][ci][co]
-        for (int i = tid; i < K * CK * BM; i += NT) {
-            int col = i % BM, r = i / BM;
-            int cl = r % CK, k = r / CK;
-            int c = c0 + cl, co = co0 + col;
-            float v = 0.f;
-            if (c < cend && co < a.Cout) v = a.wf[((int64_t)c * K + k) * a.Cout + co];
-            Ws[(k * CK + cl) * BM + col] = v;
-        }
+        for (int k = 0; k < K; ++k)
+            for (int cl = wr0; cl < CK; cl += RSTEP) {
+                const int c = c0 + cl;
+                Ws[(k * CK + cl) * BM + wcol] =
+                    (c < cend && wco) ? a.wf[((int64_t)c * K + k) * a.Cout + co0 + wcol] : 0.f;
+            }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
         for (int k = 0; k < K; ++k) {
@@ -204,23 +224,35 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
     const int wlen = BN + J - 1;
+    const int QP = stage_lanes(wlen), CP = NT / QP;
+    const int qlane = tid % QP, clane = tid / QP;
+    int xm[2], xo[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int w = qlane + k * QP, t = u0 - (J - 1) + w;
+        xo[k] = w < wlen ? w : -1;
+        xm[k] = (t >= 0 && t < a.Tin) ? t : -1;
+    }
+    constexpr int RSTEP = NT / BM;
+    const int wcol = tid % BM, wr0 = tid / BM;
+    const bool wrow = m0 + wcol < M;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
-        for (int i = tid; i < CK * wlen; i += NT) {
-            int cl = i / wlen, w = i - cl * wlen;
-            int c = c0 + cl, t = u0 - (J - 1) + w;
-            float v = 0.f;
-            if (c < cend && t >= 0 && t < a.Tin) v = act_apply(a.in_act, ib[(int64_t)c * a.Tin + t]);
-            Xs[cl * Ub + w] = v;
+        for (int cl = clane; cl < CK; cl += CP) {
+            const int c = c0 + cl;
+            const bool cv = c < cend;
+            const float* ir = ib + (int64_t)c * a.Tin;
+            float* xs = Xs + cl * Ub;
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (xo[k] >= 0) xs[xo[k]] = (cv && xm[k] >= 0) ? act_apply(a.in_act, ir[xm[k]]) : 0.f;
         }
-        for (int i = tid; i < J * CK * BM; i += NT) {
-            int col = i % BM, r = i / BM;
-            int cl = r % CK, q = r / CK;
-            int c = c0 + cl, row = m0 + col;
-            float v = 0.f;
-            if (c < cend && row < M) v = a.wp[((int64_t)c * J + q) * M + row];
-            As[(q * CK + cl) * BM + col] = v;
-        }
+        for (int q = 0; q < J; ++q)
+            for (int cl = wr0; cl < CK; cl += RSTEP) {
+                const int c = c0 + cl;
+                As[(q * CK + cl) * BM + wcol] =
+                    (c < cend && wrow) ? a.wp[((int64_t)c * J + q) * M + m0 + wcol] : 0.f;
+            }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
         for (int q = 0; q < J; ++q) {
@@ -337,27 +369,35 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     const int it_end = min(a.items, it_beg + a.per_split);
     const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
     const int tw = BT / WK;  // t per wave per chunk
+    const int lgBT = __builtin_ctz(BT);  // BT is a power of two
+    const int QP = stage_lanes(WL), CP = NT / QP;
+    const int qlane = tid % QP, clane = tid / QP;
     for (int it = it_beg; it < it_end; ++it) {
         const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
         const float* Lb = a.L + (int64_t)b * a.A * a.Tl;
         const float* Rb = a.R + (int64_t)b * a.C * a.Tr;
+        int rm[SPXW];
+#pragma unroll
+        for (int k = 0; k < SPXW; ++k) {
+            const int w = qlane + k * QP;
+            rm[k] = w < WL ? pad_src(tc * a.s + w, a.pl, a.Tr, a.e, a.mode) : -2;
+        }
         __syncthreads();
         for (int i = tid; i < BT * BM; i += NT) {
-            int tl = i % BT, al = i / BT;
-            int t = tc + tl, aa = a0 + al;
+            const int tl = i & (BT - 1), al = i >> lgBT;
+            const int t = tc + tl, aa = a0 + al;
             float v = 0.f;
             if (t < a.Tl && aa < a.A) v = act_apply(a.actL, Lb[(int64_t)aa * a.Tl + t]);
             Ls[tl * BM + al] = v;
         }
-        for (int i = tid; i < a.NCmax * WL; i += NT) {
-            int cr = i / WL, w = i - cr * WL;
-            int c = c_first + cr;
-            float v = 0.f;
-            if (c < a.C) {
-                int m = pad_src(tc * a.s + w, a.pl, a.Tr, a.e, a.mode);
-                if (m >= 0) v = act_apply(a.actR, Rb[(int64_t)c * a.Tr + m]);
-            }
-            Rs[cr * WLp + w] = v;
+        for (int cr = clane; cr < a.NCmax; cr += CP) {
+            const int c = c_first + cr;
+            const bool cv = c < a.C;
+            const float* rr = Rb + (int64_t)c * a.Tr;
+            float* rs = Rs + cr * WLp;
+#pragma unroll
+            for (int k = 0; k < SPXW; ++k)
+                if (rm[k] != -2) rs[qlane + k * QP] = (cv && rm[k] >= 0) ? act_apply(a.actR, rr[rm[k]]) : 0.f;
         }
         __syncthreads();
         for (int tp = wk * tw; tp < (wk + 1) * tw; tp += 2) {
@@ -688,6 +728,7 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
     }
     a.CK = p.CK; a.Up = p.Up; a.KS = p.KS; a.cps = p.cps; a.part = ws;
     ENCX_REQUIRE(a.KS == 1 || ws);
+    ENCX_REQUIRE(a.s * a.Up <= SPX * NT);  // staging positions per thread
     switch (p.t) {
         case T32x128: launch_fwd<32, 128, 1, 4>(a, st); break;
         case T64x64: launch_fwd<64, 64, 2, 2>(a, st); break;
@@ -828,6 +869,7 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
         if (lds > 160 * 1024) return ENCX_EINVAL;
         hipLaunchKernelGGL(conv_wgrad_small_kernel, dim3(p.splits), dim3(NT), lds, st, a);
     } else {
+        if (WL > SPXW * NT) return ENCX_EINVAL;
         a.WLp = wlp_for(WL, a.K);
         a.NCmax = (int)((p.BN + a.K - 1) / a.K + 1);
         if (a.NCmax > C) a.NCmax = (int)C;

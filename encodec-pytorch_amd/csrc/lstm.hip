@@ -43,6 +43,17 @@ __global__ __launch_bounds__(256) void lstm_fwd_step(const float* Gx, const floa
     const int col = lane & 15, kk = lane >> 4;
     const int NG = H >> 4;
     const int j = (col >> 2) * H + u0 + (col & 3);  // gate column of this lane
+    // the gate phase's own operands (B*UNITS <= 256 threads), fetched before the MFMA chain
+    const int pb = tid / UNITS, pu = u0 + (tid - pb * UNITS);
+    const bool pact = tid < B * UNITS && pu < H;
+    const int64_t po = ((int64_t)pb * T + t) * H + pu;
+    float gxv[4] = {0.f, 0.f, 0.f, 0.f}, cpv = 0.f;
+    if (pact) {
+        const float* gx = Gx + ((int64_t)pb * T + t) * 4 * H;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) gxv[g] = gx[g * H + pu];
+        if (t > 0) cpv = C[po - H];
+    }
     float4 wv[G], hv[RT][G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -70,94 +81,92 @@ __global__ __launch_bounds__(256) void lstm_fwd_step(const float* Gx, const floa
 #pragma unroll
         for (int q = 0; q < 4; ++q) red[wave][r * 16 + kk * 4 + q][col] = acc[r][q];
     __syncthreads();
-    for (int p = tid; p < B * UNITS; p += 256) {
-        const int b = p / UNITS, uu = p - b * UNITS, u = u0 + uu;
-        if (u >= H) continue;
+    if (pact) {
+        const int uu = pu - u0;
         float pre[4];
-        const float* gx = Gx + ((int64_t)b * T + t) * 4 * H;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int cc = g * 4 + uu;
-            pre[g] = gx[g * H + u] + (((red[0][b][cc] + red[1][b][cc]) + red[2][b][cc]) + red[3][b][cc]);
+            pre[g] = gxv[g] + (((red[0][pb][cc] + red[1][pb][cc]) + red[2][pb][cc]) + red[3][pb][cc]);
         }
         const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanhf(pre[2]), og = sigm(pre[3]);
-        const int64_t o = ((int64_t)b * T + t) * H + u;
-        const float cp = t > 0 ? C[o - H] : 0.f;
-        const float c = fg * cp + ig * gg;
-        C[o] = c;
-        Y[o] = og * tanhf(c);
-        float* gs = Gs + ((int64_t)b * T + t) * 4 * H;
-        gs[u] = ig;
-        gs[H + u] = fg;
-        gs[2 * H + u] = gg;
-        gs[3 * H + u] = og;
+        const float c = fg * cpv + ig * gg;
+        C[po] = c;
+        Y[po] = og * tanhf(c);
+        float* gs = Gs + ((int64_t)pb * T + t) * 4 * H;
+        gs[pu] = ig;
+        gs[H + pu] = fg;
+        gs[2 * H + pu] = gg;
+        gs[3 * H + pu] = og;
     }
 }
 
 // ------------------------------------------------------------------------- backward step
-// One launch per frame t, workgroup = 16 hidden units u (all batch rows), 16 waves:
-//   1. dh_rec[b][u] = sum_j DA[b][t+1][j] W_hh[j][u]  (MFMA, waves interleave the 4H/16
-//      k-groups; B operand from W_hh^T so it loads as float4)
-//   2. dh = dY[t] + dh_rec; dc = dh o (1 - tanh^2 c) + dcn; da_{i,f,g,o} -> DA[b][t];
-//      dcn <- dc f   (only the block's own units, so no grid-wide dependency inside a launch)
-template <int G, int RT>
-__global__ __launch_bounds__(1024) void lstm_bwd_step(const float* dY, float* DA, const float* WhhT,
-                                                      float* dcn, const float* C, const float* Gs,
-                                                      int B, int T, int H, int t) {
-    __shared__ float red[16][64][17];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int c0 = blockIdx.x * 16, col = lane & 15, kk = lane >> 4;
-    const int K = 4 * H, NG = K >> 4;
+// Per frame t (descending) two launches:
+//   E(t): dh = dY[t] + sum_s P[s] (the recurrent grad from frame t+1, split partials summed in
+//         a fixed order); dc = dh o (1 - tanh^2 c) + dcn; da_{i,f,g,o} -> DA[b][t]; dcn <- dc f
+//   G(t): P[s][b][u] = sum_{j in split s} DA[b][t][j] W_hh[j][u]  (MFMA 16x16x4; the 4H
+//         reduction split over blockIdx.y so the grid covers ~256 CUs instead of H/16)
+__global__ void lstm_bwd_elem(const float* dY, const float* P, int ns, float* dcn, const float* C,
+                              const float* Gs, float* DA, int B, int T, int H, int t) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= B * H) return;
+    const int b = p / H, u = p - b * H;
     const bool rec = t < T - 1;
-    if (rec) {
-        float4 wv[G], av[RT][G];
+    float dhr = 0.f;
+    if (rec)
+        for (int s = 0; s < ns; ++s) dhr += P[(int64_t)s * B * H + p];
+    const int64_t o = ((int64_t)b * T + t) * H + u;
+    const float dh = dY[o] + dhr;
+    const float* gs = Gs + ((int64_t)b * T + t) * 4 * H;
+    const float ig = gs[u], fg = gs[H + u], gg = gs[2 * H + u], og = gs[3 * H + u];
+    const float c = C[o], cp = t > 0 ? C[o - H] : 0.f, tc = tanhf(c);
+    const float dc = dh * og * (1.f - tc * tc) + (rec ? dcn[p] : 0.f);
+    float* da = DA + ((int64_t)b * T + t) * 4 * H;
+    da[u] = dc * gg * ig * (1.f - ig);
+    da[H + u] = dc * cp * fg * (1.f - fg);
+    da[2 * H + u] = dc * ig * (1.f - gg * gg);
+    da[3 * H + u] = dh * tc * og * (1.f - og);
+    dcn[p] = dc * fg;
+}
+
+template <int G, int RT>
+__global__ __launch_bounds__(256) void lstm_bwd_gemm(const float* DA, const float* WhhT, float* P, int B,
+                                                     int T, int H, int t, int gper) {
+    __shared__ float red[4][64][17];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c0 = blockIdx.x * 16, s = blockIdx.y, col = lane & 15, kk = lane >> 4;
+    const int K = 4 * H, g0 = s * gper;
+    float4 wv[G], av[RT][G];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int gi = wave + 16 * g;
-            wv[g] = gi < NG ? ld4(WhhT + (int64_t)(c0 + col) * K + gi * 16 + 4 * kk)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g = 0; g < G; ++g) {
+        const int gl = wave + 4 * g, gi = g0 + gl;
+        const bool ok = gl < gper;
+        wv[g] = ok ? ld4(WhhT + (int64_t)(c0 + col) * K + gi * 16 + 4 * kk) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-            for (int r = 0; r < RT; ++r) {
-                const int row = r * 16 + col;
-                av[r][g] = (row < B && gi < NG) ? ld4(DA + ((int64_t)row * T + (t + 1)) * K + gi * 16 + 4 * kk)
-                                                : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+        for (int r = 0; r < RT; ++r) {
+            const int row = r * 16 + col;
+            av[r][g] = (ok && row < B) ? ld4(DA + ((int64_t)row * T + t) * K + gi * 16 + 4 * kk)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        f32x4v acc[RT];
-#pragma unroll
-        for (int r = 0; r < RT; ++r) acc[r] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int r = 0; r < RT; ++r) acc[r] = mfma16(at4(av[r][g], s), at4(wv[g], s), acc[r]);
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) red[wave][r * 16 + kk * 4 + q][col] = acc[r][q];
     }
-    __syncthreads();
-    for (int p = tid; p < B * 16; p += 1024) {
-        const int b = p >> 4, cc = p & 15, u = c0 + cc;
-        float dhr = 0.f;
-        if (rec) {
+    f32x4v acc[RT];
 #pragma unroll
-            for (int w = 0; w < 16; ++w) dhr += red[w][b][cc];
-        }
-        const int64_t o = ((int64_t)b * T + t) * H + u;
-        const float dh = dY[o] + dhr;
-        const float* gs = Gs + ((int64_t)b * T + t) * 4 * H;
-        const float ig = gs[u], fg = gs[H + u], gg = gs[2 * H + u], og = gs[3 * H + u];
-        const float c = C[o], cp = t > 0 ? C[o - H] : 0.f, tc = tanhf(c);
-        const int bu = b * H + u;
-        const float dc = dh * og * (1.f - tc * tc) + (rec ? dcn[bu] : 0.f);
-        float* da = DA + ((int64_t)b * T + t) * K;
-        da[u] = dc * gg * ig * (1.f - ig);
-        da[H + u] = dc * cp * fg * (1.f - fg);
-        da[2 * H + u] = dc * ig * (1.f - gg * gg);
-        da[3 * H + u] = dh * tc * og * (1.f - og);
-        dcn[bu] = dc * fg;
+    for (int r = 0; r < RT; ++r) acc[r] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < RT; ++r) acc[r] = mfma16(at4(av[r][g], q), at4(wv[g], q), acc[r]);
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[wave][r * 16 + kk * 4 + q][col] = acc[r][q];
+    __syncthreads();
+    for (int p = tid; p < B * 16; p += 256) {
+        const int b = p >> 4, cc = p & 15;
+        P[((int64_t)s * B + b) * H + c0 + cc] = ((red[0][b][cc] + red[1][b][cc]) + red[2][b][cc]) + red[3][b][cc];
     }
 }
 
@@ -194,21 +203,29 @@ static void fwd_step(int G, int RT, dim3 grid, hipStream_t st, const float* Gx, 
     else fwd_step_rt<16>(RT, grid, st, Gx, Whh, Y, C, Gs, B, T, H, t);
 }
 template <int G>
-static void bwd_step_rt(int RT, dim3 grid, hipStream_t st, const float* dY, float* DA, const float* WhhT,
-                        float* dcn, const float* C, const float* Gs, int B, int T, int H, int t) {
+static void bwd_gemm_rt(int RT, dim3 grid, hipStream_t st, const float* DA, const float* WhhT, float* P, int B,
+                        int T, int H, int t, int gper) {
     switch (RT) {
-        case 1: hipLaunchKernelGGL((lstm_bwd_step<G, 1>), grid, dim3(1024), 0, st, dY, DA, WhhT, dcn, C, Gs, B, T, H, t); break;
-        case 2: hipLaunchKernelGGL((lstm_bwd_step<G, 2>), grid, dim3(1024), 0, st, dY, DA, WhhT, dcn, C, Gs, B, T, H, t); break;
-        case 3: hipLaunchKernelGGL((lstm_bwd_step<G, 3>), grid, dim3(1024), 0, st, dY, DA, WhhT, dcn, C, Gs, B, T, H, t); break;
-        default: hipLaunchKernelGGL((lstm_bwd_step<G, 4>), grid, dim3(1024), 0, st, dY, DA, WhhT, dcn, C, Gs, B, T, H, t); break;
+        case 1: hipLaunchKernelGGL((lstm_bwd_gemm<G, 1>), grid, dim3(256), 0, st, DA, WhhT, P, B, T, H, t, gper); break;
+        case 2: hipLaunchKernelGGL((lstm_bwd_gemm<G, 2>), grid, dim3(256), 0, st, DA, WhhT, P, B, T, H, t, gper); break;
+        case 3: hipLaunchKernelGGL((lstm_bwd_gemm<G, 3>), grid, dim3(256), 0, st, DA, WhhT, P, B, T, H, t, gper); break;
+        default: hipLaunchKernelGGL((lstm_bwd_gemm<G, 4>), grid, dim3(256), 0, st, DA, WhhT, P, B, T, H, t, gper); break;
     }
 }
-static void bwd_step(int G, int RT, dim3 grid, hipStream_t st, const float* dY, float* DA, const float* WhhT,
-                     float* dcn, const float* C, const float* Gs, int B, int T, int H, int t) {
-    if (G <= 1) bwd_step_rt<1>(RT, grid, st, dY, DA, WhhT, dcn, C, Gs, B, T, H, t);
-    else if (G <= 2) bwd_step_rt<2>(RT, grid, st, dY, DA, WhhT, dcn, C, Gs, B, T, H, t);
-    else if (G <= 4) bwd_step_rt<4>(RT, grid, st, dY, DA, WhhT, dcn, C, Gs, B, T, H, t);
-    else bwd_step_rt<8>(RT, grid, st, dY, DA, WhhT, dcn, C, Gs, B, T, H, t);
+static void bwd_gemm(int G, int RT, dim3 grid, hipStream_t st, const float* DA, const float* WhhT, float* P, int B,
+                     int T, int H, int t, int gper) {
+    if (G <= 1) bwd_gemm_rt<1>(RT, grid, st, DA, WhhT, P, B, T, H, t, gper);
+    else if (G <= 2) bwd_gemm_rt<2>(RT, grid, st, DA, WhhT, P, B, T, H, t, gper);
+    else if (G <= 4) bwd_gemm_rt<4>(RT, grid, st, DA, WhhT, P, B, T, H, t, gper);
+    else bwd_gemm_rt<8>(RT, grid, st, DA, WhhT, P, B, T, H, t, gper);
+}
+// k-splits of the recurrent backward GEMM: <= 8, dividing the H/4 k-groups, >= 4 groups each
+static int bwd_splits(int64_t H) {
+    const int groups = (int)(H / 4);
+    int ns = groups / 4 < 8 ? groups / 4 : 8;
+    if (ns < 1) ns = 1;
+    while (groups % ns) --ns;
+    return ns;
 }
 
 // ------------------------------------------------------------------------- GEMM operands
@@ -358,7 +375,7 @@ size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t C, int64_t H) {
     const int s1 = gemm_slabs(M, gemm_splits(N4, (int)H + 1, M));
     const int s2 = gemm_slabs(M, gemm_splits(N4, (int)C, M));
     size_t a = (size_t)s1 * N4 * (H + 1), b = (size_t)s2 * N4 * C;
-    return ((a > b ? a : b) + B * H + 4 * H * H) * sizeof(float);
+    return ((a > b ? a : b) + B * H + 4 * H * H + (size_t)bwd_splits(H) * B * H) * sizeof(float);
 }
 
 /* One layer backward. dY [B][T][H] (the grad of this layer's output sequence), states from
@@ -376,12 +393,19 @@ int encx_lstm_layer_bwd(const float* x, int x_bct, const float* w_ih, const floa
     const int M = (int)(B * T), N4 = (int)(4 * H);
     float* dcn = ws;
     float* whhT = ws + B * H;
-    float* slabs = whhT + 4 * H * H;
+    float* P = whhT + 4 * H * H;
+    const int ns = bwd_splits(H);
+    float* slabs = P + (int64_t)ns * B * H;
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)cdiv(H, 32), (unsigned)cdiv(4 * H, 32)), dim3(32, 8), 0, st,
                        w_hh, whhT, (int)(4 * H), (int)H);
-    const int RT = (int)cdiv(B, 16), G = (int)cdiv(H / 4, 16);
-    for (int t = (int)T - 1; t >= 0; --t)
-        bwd_step(G, RT, dim3((unsigned)(H / 16)), st, dY, DA, whhT, dcn, Cst, Gs, (int)B, (int)T, (int)H, t);
+    const int RT = (int)cdiv(B, 16), gper = (int)(H / 4) / ns, G = (int)cdiv(gper, 4);
+    const int BH = (int)(B * H);
+    for (int t = (int)T - 1; t >= 0; --t) {
+        hipLaunchKernelGGL(lstm_bwd_elem, dim3((unsigned)cdiv(BH, 256)), dim3(256), 0, st, dY, P, ns, dcn, Cst, Gs,
+                           DA, (int)B, (int)T, (int)H, t);
+        if (t > 0)
+            bwd_gemm(G, RT, dim3((unsigned)(H / 16), (unsigned)ns), st, DA, whhT, P, (int)B, (int)T, (int)H, t, gper);
+    }
     ENCX_CHECK_LAUNCH();
     int rc;
     if (dw_hh) {

@@ -86,9 +86,34 @@ def test_disc_vs_oracle_fp64(B, Tn):
     assert worst < 1e-3, (worst, where)
 
 
+def masked_msstft(x, p, fmaps_mine):
+    """The oracle's MS-STFT forward in fp64 with every LeakyReLU slope taken from the sign of
+    OUR feature maps: a pre-activation within fp32 rounding of 0 can land on either side, and
+    the generator-side seed (uniform over the logits) is what makes such flips visible in
+    d l / dy; with the masks shared, the backward is linear and must agree to fp32 accuracy."""
+    import torch.nn.functional as F
+    logits = []
+    for k, (n, h) in enumerate(zip(O.DISC_CFG['n_ffts'], O.DISC_CFG['hops'])):
+        pre = f'discriminators.{k}'
+        z = O.spectrogram(x, n, h, n)
+        z = torch.cat([z.real, z.imag], dim=1).permute(0, 1, 3, 2)
+        masks = [torch.where(f.detach().cpu() > 0, 1.0, 0.2).double() for f in fmaps_mine[k]]
+        z = F.conv2d(z, p[pre + '.convs.0.conv.weight'], p[pre + '.convs.0.conv.bias'], padding=(1, 4)) * masks[0]
+        for i, d in enumerate((1, 2, 4)):
+            q = f'{pre}.convs.{i + 1}.conv'
+            w = O.weight_norm(p[q + '.weight_v'], p[q + '.weight_g'])
+            z = F.conv2d(z, w, p[q + '.bias'], stride=(1, 2), dilation=(d, 1), padding=(d, 4)) * masks[i + 1]
+        q = f'{pre}.convs.4.conv'
+        z = F.conv2d(z, O.weight_norm(p[q + '.weight_v'], p[q + '.weight_g']), p[q + '.bias'], padding=(1, 1)) * masks[4]
+        q = f'{pre}.conv_post.conv'
+        logits.append(F.conv2d(z, O.weight_norm(p[q + '.weight_v'], p[q + '.weight_g']), p[q + '.bias'], padding=(1, 1)))
+    return logits
+
+
 def test_gan_losses_vs_oracle():
     """l_g / l_feat (losses.py:44-56, incl. the double division by K) and disc_loss (:65-80)
-    values, and the generator-side grads d l_g / dy, d l_feat / dy through the discriminator."""
+    values against the oracle; the generator-side grads d l_g / dy and d l_feat / dy through
+    the discriminator against the fp64 oracle evaluated with our LeakyReLU masks."""
     from encx.losses import total_loss, disc_loss
     disc, p = make_disc(9)
     g = torch.Generator().manual_seed(5)
@@ -98,8 +123,6 @@ def test_gan_losses_vs_oracle():
     lr64, fr64 = O.msstft_forward(x64, p64)
     lf64, ff64 = O.msstft_forward(y64, p64)
     ref = O.total_loss(fr64, lf64, ff64, x64, y64)
-    gg64, = torch.autograd.grad(ref['l_g'].sum(), [y64], retain_graph=True)
-    gf64, = torch.autograd.grad(ref['l_feat'].sum(), [y64], retain_graph=True)
     ld64 = O.disc_loss(lr64, [l.detach() for l in lf64])
 
     x = x64.float().to(DEV)
@@ -111,10 +134,25 @@ def test_gan_losses_vs_oracle():
         np.testing.assert_allclose(out[k].item(), ref[k].item(), rtol=1e-4)
     gg, = torch.autograd.grad(out['l_g'], [y], retain_graph=True)
     gf, = torch.autograd.grad(out['l_feat'], [y], retain_graph=True)
-    assert rel(gg, gg64) < 1e-3
-    assert rel(gf, gf64) < 2e-3
     ld = disc_loss(lr, [l.detach() for l in lf])
     np.testing.assert_allclose(ld.item(), ld64.item(), rtol=1e-5)
+
+    # sign disagreements with fp64 only where the fp64 activation is ~0
+    flips = 0
+    for fa, fb in zip(ff, ff64):
+        for a, b in zip(fa, fb):
+            bad = (a.detach().cpu() > 0) != (b.detach() > 0)
+            flips += int(bad.sum())
+            if bad.any():
+                assert float(b.detach()[bad].abs().max()) < 1e-5 * float(b.detach().abs().max())
+    lfm = masked_msstft(y64, p64, ff)
+    K = len(lfm)
+    lg_m = sum(torch.relu(1 - l).mean() for l in lfm) / (K * K)
+    gg64, = torch.autograd.grad(lg_m, [y64], retain_graph=True)
+    gf64, = torch.autograd.grad(ref['l_feat'].sum(), [y64], retain_graph=True)
+    print(f'mask flips {flips}; d l_g/dy rel {rel(gg, gg64):.2e}; d l_feat/dy rel {rel(gf, gf64):.2e}')
+    assert rel(gg, gg64) < 1e-4
+    assert rel(gf, gf64) < 2e-3  # sign(ff - fr) kinks: elements with ff ~ fr
 
 
 def test_train_step_gan_fixture():
@@ -150,3 +188,41 @@ def test_train_step_gan_fixture():
         mine = np.array([v.double().sum().item(), v.double().abs().sum().item()])
         assert abs(mine[1] - ref[1]) <= 1e-4 * ref[1] + flips, (k, mine, ref)
         assert abs(mine[0] - ref[0]) <= 1e-5 * ref[1] + flips, (k, mine, ref)
+
+
+# (Ci, Co, kernel, stride, dilation, padding) of the DiscriminatorSTFT layers (msstftd.py:67-84)
+LAYERS = [(2, 32, (3, 9), (1, 1), (1, 1), (1, 4)),
+          (32, 32, (3, 9), (1, 2), (1, 1), (1, 4)),
+          (32, 32, (3, 9), (1, 2), (2, 1), (2, 4)),
+          (32, 32, (3, 9), (1, 2), (4, 1), (4, 4)),
+          (32, 32, (3, 3), (1, 1), (1, 1), (1, 1)),
+          (32, 1, (3, 3), (1, 1), (1, 1), (1, 1))]
+
+
+@pytest.mark.parametrize('li', range(len(LAYERS)))
+@pytest.mark.parametrize('T2,Fi', [(7, 33), (23, 65), (5, 129), (3, 513)])
+def test_conv2d_vs_torch_fp64(li, T2, Fi):
+    """One NormConv2d (+ LeakyReLU except conv_post): output, input grad and weight/bias
+    grads against torch.nn.functional.conv2d in fp64, with a random output grad."""
+    import torch.nn.functional as F
+    from encx import ops
+    Ci, Co, k, s, d, pad = LAYERS[li]
+    act = li < 5
+    g = torch.Generator().manual_seed(li * 100 + T2)
+    x64 = torch.randn(2, Ci, T2, Fi, generator=g, dtype=torch.float64).requires_grad_(True)
+    v64 = (0.2 * torch.randn((Co, Ci) + k, generator=g, dtype=torch.float64)).requires_grad_(True)
+    b64 = (0.1 * torch.randn(Co, generator=g, dtype=torch.float64)).requires_grad_(True)
+    y64 = F.conv2d(x64, v64, b64, stride=s, dilation=d, padding=pad)
+    if act:
+        y64 = F.leaky_relu(y64, 0.2)
+    dy64 = torch.randn(y64.shape, generator=g, dtype=torch.float64)
+    y64.backward(dy64)
+    x = x64.detach().float().to(DEV).requires_grad_(True)
+    v = v64.detach().float().to(DEV).requires_grad_(True)
+    b = b64.detach().float().to(DEV).requires_grad_(True)
+    y = ops.conv2d(x, v, None, b, k, s, d, pad, act)
+    y.backward(dy64.float().to(DEV))
+    assert rel(y, y64) < 1e-5
+    assert rel(x.grad, x64.grad) < 1e-5, rel(x.grad, x64.grad)
+    assert rel(v.grad, v64.grad) < 1e-5, rel(v.grad, v64.grad)
+    assert rel(b.grad, b64.grad) < 1e-5, rel(b.grad, b64.grad)
