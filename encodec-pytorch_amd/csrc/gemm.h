@@ -29,23 +29,52 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        __syncthreads();
-        for (int i = tid; i < BM * BK; i += 256) {
+    // register-prefetch pipeline: the next BK slice's operands are fetched (through the
+    // loaders) while the current slice runs on the MFMA units
+    constexpr int EA = BM * BK / 256, EB = BN * BK / 256;
+    static_assert(EA * 256 == BM * BK && EB * 256 == BN * BK, "tile/thread mismatch");
+    float ra[EA], rb[EB];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int e = 0; e < EA; ++e) {
+            const int i = tid + e * 256;
             int m, k;
             if (LD::A_K_FAST) { m = i / BK; k = i - m * BK; }
             else { k = i / BM; m = i - k * BM; }
-            int gm = m0 + m, gk = k0 + k;
-            As[k][m] = (gm < M && gk < kend) ? ld.a(gm, gk) : 0.f;
+            const int gm = m0 + m, gk = k0 + k;
+            ra[e] = (gm < M && gk < kend) ? ld.a(gm, gk) : 0.f;
         }
-        for (int i = tid; i < BN * BK; i += 256) {
+#pragma unroll
+        for (int e = 0; e < EB; ++e) {
+            const int i = tid + e * 256;
             int n, k;
             if (LD::B_N_FAST) { k = i / BN; n = i - k * BN; }
             else { n = i / BK; k = i - n * BK; }
-            int gn = n0 + n, gk = k0 + k;
-            Bs[k][n] = (gn < N && gk < kend) ? ld.b(gk, gn) : 0.f;
+            const int gn = n0 + n, gk = k0 + k;
+            rb[e] = (gn < N && gk < kend) ? ld.b(gk, gn) : 0.f;
+        }
+    };
+    if (kbeg < kend) fetch(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < EA; ++e) {
+            const int i = tid + e * 256;
+            int m, k;
+            if (LD::A_K_FAST) { m = i / BK; k = i - m * BK; }
+            else { k = i / BM; m = i - k * BM; }
+            As[k][m] = ra[e];
+        }
+#pragma unroll
+        for (int e = 0; e < EB; ++e) {
+            const int i = tid + e * 256;
+            int n, k;
+            if (LD::B_N_FAST) { k = i / BN; n = i - k * BN; }
+            else { n = i / BK; k = i - n * BK; }
+            Bs[k][n] = rb[e];
         }
         __syncthreads();
+        if (k0 + BK < kend) fetch(k0 + BK);
 #pragma unroll
         for (int kp = 0; kp < BK; kp += 2) {
             float av[TM], bv[TN];

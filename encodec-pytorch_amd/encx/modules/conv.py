@@ -65,8 +65,9 @@ class NormConv1d(nn.Module):
         if norm == 'time_group_norm':
             if causal:
                 raise ValueError("GroupNorm doesn't support causal evaluation.")
-            raise NotImplementedError('encx: time_group_norm (48 kHz model) is a next-round row')
-        self.norm = nn.Identity()
+            self.norm = nn.GroupNorm(1, out_channels, **norm_kwargs)  # conv.py:45-49 (params only)
+        else:
+            self.norm = nn.Identity()
         self.norm_type = norm
         self.in_channels, self.out_channels = in_channels, out_channels
         self.kernel_size, self.stride, self.dilation = kernel_size, stride, dilation
@@ -81,8 +82,11 @@ class NormConvTranspose1d(nn.Module):
         assert norm in CONV_NORMALIZATIONS
         self.convtr = _ConvParams((in_channels, out_channels, kernel_size), out_channels, norm)
         if norm == 'time_group_norm':
-            raise NotImplementedError('encx: time_group_norm (48 kHz model) is a next-round row')
-        self.norm = nn.Identity()
+            if causal:
+                raise ValueError("GroupNorm doesn't support causal evaluation.")
+            self.norm = nn.GroupNorm(1, out_channels, **norm_kwargs)
+        else:
+            self.norm = nn.Identity()
         self.norm_type = norm
         self.in_channels, self.out_channels = in_channels, out_channels
         self.kernel_size, self.stride = kernel_size, stride
@@ -133,8 +137,15 @@ class SConv1d(nn.Module):
     def forward(self, x, act=None, res=None):
         c = self.conv
         v, g = c.conv.wv()
-        return ops.conv1d(x, v, g, c.conv.bias, c.kernel_size, c.stride, c.dilation, self.causal,
-                          self.pad_mode, act, res)
+        if c.norm_type != 'time_group_norm':
+            return ops.conv1d(x, v, g, c.conv.bias, c.kernel_size, c.stride, c.dilation, self.causal,
+                              self.pad_mode, act, res)
+        # conv -> GroupNorm(1, C) (NormConv1d.forward, conv.py:119-122); a residual is added
+        # after the norm, so it is not fused into the conv epilogue here
+        y = ops.conv1d(x, v, g, c.conv.bias, c.kernel_size, c.stride, c.dilation, self.causal,
+                       self.pad_mode, act, None)
+        y = ops.group_norm(y, c.norm.weight, c.norm.bias, c.norm.eps)
+        return y if res is None else ops.add(y, res)
 
 
 class SConvTranspose1d(nn.Module):
@@ -155,5 +166,8 @@ class SConvTranspose1d(nn.Module):
     def forward(self, x, act=None):
         c = self.convtr
         v, g = c.convtr.wv()
-        return ops.convtr1d(x, v, g, c.convtr.bias, c.kernel_size, c.stride, self.causal,
-                            self.trim_right_ratio, act)
+        y = ops.convtr1d(x, v, g, c.convtr.bias, c.kernel_size, c.stride, self.causal,
+                         self.trim_right_ratio, act)
+        if c.norm_type == 'time_group_norm':  # NormConvTranspose1d.forward, conv.py:153-156
+            y = ops.group_norm(y, c.norm.weight, c.norm.bias, c.norm.eps)
+        return y

@@ -717,3 +717,109 @@ class FeatFn(torch.autograd.Function):
                      ptr(g), ptr(d), stream())
                 grads[n + i] = d
         return (None, None, *grads)
+
+
+# ---------------------------------------------------------------------------- 48 kHz model
+class AddFn(torch.autograd.Function):
+    """x + y (SEANetResnetBlock's shortcut sum, seanet.py:63, where it cannot ride in a conv
+    epilogue)."""
+
+    @staticmethod
+    def forward(ctx, x, y):
+        _check(x)
+        x, y = x.contiguous(), y.contiguous()
+        out = torch.empty_like(x)
+        call('encx_lincomb', ptr(x), ptr(y), ptr(out), x.numel(), 1.0, None, 1.0, stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def add(x, y):
+    return AddFn.apply(x, y)
+
+
+class GroupNormFn(torch.autograd.Function):
+    """nn.GroupNorm(1, C) of norm='time_group_norm' (modules/conv.py:45-49)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        _check(x)
+        x = x.contiguous()
+        B, C, T = x.shape
+        y = torch.empty_like(x)
+        stats = _f32(2 * B, x)
+        ws = _ws(lib.encx_groupnorm_workspace(B, C), x)
+        call('encx_groupnorm_fwd', ptr(x), ptr(gamma), ptr(beta), ptr(y), ptr(stats), ptr(ws), B, C, T,
+             float(eps), stream())
+        ctx.save_for_backward(x, stats)
+        ctx.params = (gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, stats = ctx.saved_tensors
+        gamma, beta = ctx.params
+        dy = dy.contiguous()
+        B, C, T = x.shape
+        ws = _ws(lib.encx_groupnorm_workspace(B, C), x)
+        coef = _f32(2 * B, x)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        want_p = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        if want_p and _direct(gamma) and _direct(beta):
+            dg, db, acc, ret = (gamma.grad if gamma is not None else None,
+                                beta.grad if beta is not None else None, 1, False)
+        elif want_p:
+            dg = torch.empty_like(gamma) if gamma is not None else None
+            db = torch.empty_like(beta) if beta is not None else None
+            acc, ret = 0, True
+        else:
+            dg = db = None
+            acc, ret = 0, False
+        call('encx_groupnorm_bwd', ptr(dy), ptr(x), ptr(gamma), ptr(stats), ptr(dx), ptr(dg), ptr(db), 0, acc,
+             ptr(ws), ptr(coef), B, C, T, stream())
+        return dx, (dg if ret else None), (db if ret else None), None
+
+
+def group_norm(x, gamma, beta, eps=1e-5):
+    return GroupNormFn.apply(x, gamma, beta, eps)
+
+
+class OverlapAddFn(torch.autograd.Function):
+    """_linear_overlap_add (utils.py:22-61): triangle-weighted sum of decoded segments."""
+
+    @staticmethod
+    def forward(ctx, stride, *frames):
+        import ctypes
+        frames = [f.contiguous() for f in frames]
+        for f in frames:
+            _check(f)
+        shape = frames[0].shape[:-1]
+        BC = int(np.prod(shape))
+        lens = [f.shape[-1] for f in frames]
+        total = stride * (len(frames) - 1) + lens[-1]
+        out = torch.empty(*shape, total, device=frames[0].device, dtype=torch.float32)
+        parr = (ctypes.c_void_p * len(frames))(*[f.data_ptr() for f in frames])
+        larr = (ctypes.c_int64 * len(frames))(*lens)
+        call('encx_overlap_add', parr, larr, len(frames), stride, BC, ptr(out), stream())
+        ctx.cfg = (stride, lens, BC, total, shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        stride, lens, BC, total, shape = ctx.cfg
+        dout = dout.contiguous()
+        grads = []
+        for k, L in enumerate(lens):
+            d = torch.empty(*shape, L, device=dout.device, dtype=torch.float32)
+            call('encx_overlap_add_bwd', ptr(dout), len(lens), stride, lens[0], BC, total, k, L, ptr(d), stream())
+            grads.append(d)
+        return (None, *grads)
+
+
+def linear_overlap_add(frames, stride):
+    if len(frames) == 1:
+        return frames[0]
+    return OverlapAddFn.apply(stride, *frames)

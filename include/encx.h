@@ -308,6 +308,25 @@ int encx_feat_loss(const float* fr, const float* ff, int64_t n, double scale, fl
 int encx_feat_loss_bwd(const float* fr, const float* ff, int64_t n, double scale, const float* denom,
                        const float* g0, float* dff, encx_stream_t stream);
 
+/* ---- 48 kHz model (config 5) ----
+ * GroupNorm(1, C) of norm='time_group_norm' (modules/conv.py:45-49, applied after the conv at
+ * :121/:155): y = (x - mean_b) * rstd_b * gamma[c] + beta[c] over x [B][C][T]; stats [2B]
+ * (mean, rstd) is written for the backward; ws: encx_groupnorm_workspace bytes (fp64 rows). */
+size_t encx_groupnorm_workspace(int64_t B, int64_t C);
+int encx_groupnorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* stats, void* ws,
+                       int64_t B, int64_t C, int64_t T, double eps, encx_stream_t stream);
+/* dx (+)= d/dx (acc_x), dgamma / dbeta (+)= (acc_params; either may be NULL); coef: [2B] scratch */
+int encx_groupnorm_bwd(const float* dy, const float* x, const float* gamma, const float* stats, float* dx,
+                       float* dgamma, float* dbeta, int acc_x, int acc_params, void* ws, float* coef, int64_t B,
+                       int64_t C, int64_t T, encx_stream_t stream);
+/* _linear_overlap_add (utils.py:22-61) of nf <= 32 decoded segments [BC][len_k] (host arrays of
+ * device pointers / lengths; all but the last of equal length) at `stride` -> out [BC][total]. */
+int encx_overlap_add(const float* const* frames, const int64_t* lengths, int nf, int64_t stride, int64_t BC,
+                     float* out, encx_stream_t stream);
+/* d frame_k = w * dout[k*stride + j] / sum_w (L0 = the first segment's length) */
+int encx_overlap_add_bwd(const float* dout, int nf, int64_t stride, int64_t L0, int64_t BC, int64_t total, int k,
+                         int64_t len, float* dframe, encx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
