@@ -30,7 +30,8 @@ constexpr int FLAT_T = 128;  // layers with T_out <= this run as one (b, t)-flat
 
 // LDS staging: position lanes per channel lane for a window of `len` positions (QP | NT)
 constexpr int SPX = 5;  // window positions per thread in the forward staging (span <= SPX * NT)
-constexpr int SPXW = 3;  // ... and in the weight-grad R window (WL <= SPXW * NT)
+constexpr int SPXW = 3;
+constexpr int SB = 4;  // staging batch: channels (or rows) whose loads are issued before their LDS writes  // ... and in the weight-grad R window (WL <= SPXW * NT)
 ENCX_DEV int stage_lanes(int len) { return len > 128 ? NT : (len > 64 ? 128 : 64); }
 
 // ------------------------------------------------------------------------- conv forward
@@ -66,9 +67,11 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     const int CK = a.CK, S = a.s, Up = a.Up, K = a.K;
     float* Xs = smem;                       // [CK][S][Up]
     float* Ws = smem + CK * S * Up;         // [K][CK][BM]
+    float* Bsm = Ws + K * CK * BM;          // [BM] bias of the block's rows
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
     const int t0 = blockIdx.x * BN, co0 = blockIdx.y * BM;
+    if (tid < BM) Bsm[tid] = (a.bias && co0 + tid < a.Cout) ? a.bias[co0 + tid] : 0.f;
     const int b = blockIdx.z / a.KS, ks = blockIdx.z - (blockIdx.z / a.KS) * a.KS;
     const float* xb = a.x + (int64_t)b * a.Cin * a.Tin;
     const int span = S * Up;
@@ -101,23 +104,42 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     const bool wco = co0 + wcol < a.Cout;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
-        // stage activated input window, phase-major
-        for (int cl = clane; cl < CK; cl += CP) {
-            const int c = c0 + cl;
-            const bool cv = c < cend;
-            const float* xr = xb + (int64_t)c * a.Tin;
-            float* xs = Xs + cl * span;
+        // stage activated input window, phase-major; loads are issued in batches of SB
+        // channels before any LDS write so their latencies overlap
+        for (int cb = clane; cb < CK; cb += SB * CP) {
+            float v[SB][SPX];
 #pragma unroll
-            for (int k = 0; k < SPX; ++k)
-                if (xo[k] >= 0) xs[xo[k]] = (cv && xm[k] >= 0) ? act_apply(a.act, xr[xm[k]]) : 0.f;
+            for (int j = 0; j < SB; ++j) {
+                const int cl = cb + j * CP, c = c0 + cl;
+                const bool cv = cl < CK && c < cend;
+                const float* xr = xb + (int64_t)c * a.Tin;
+#pragma unroll
+                for (int k = 0; k < SPX; ++k) v[j][k] = (cv && xm[k] >= 0) ? xr[xm[k]] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int cl = cb + j * CP;
+                if (cl >= CK) continue;
+                float* xs = Xs + cl * span;
+#pragma unroll
+                for (int k = 0; k < SPX; ++k)
+                    if (xo[k] >= 0) xs[xo[k]] = act_apply(a.act, v[j][k]);
+            }
         }
         // stage weights [k][ci][co]
-        for (int k = 0; k < K; ++k)
-            for (int cl = wr0; cl < CK; cl += RSTEP) {
-                const int c = c0 + cl;
-                Ws[(k * CK + cl) * BM + wcol] =
-                    (c < cend && wco) ? a.wf[((int64_t)c * K + k) * a.Cout + co0 + wcol] : 0.f;
+        for (int r0 = wr0; r0 < K * CK; r0 += SB * RSTEP) {
+            float v[SB];
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int r = r0 + j * RSTEP, k = r / CK, cl = r - k * CK, c = c0 + cl;
+                v[j] = (r < K * CK && c < cend && wco) ? a.wf[((int64_t)c * K + k) * a.Cout + co0 + wcol] : 0.f;
             }
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int r = r0 + j * RSTEP;
+                if (r < K * CK) Ws[r * BM + wcol] = v[j];
+            }
+        }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
         for (int k = 0; k < K; ++k) {
@@ -137,18 +159,37 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
             }
         }
     }
+    // epilogue: bias from LDS (staged at entry); residual / act' source / accumulated y are
+    // loaded for 8 rows at a time before those rows are stored, so each group's loads overlap
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int t = t0 + wn0 + j * 32 + (lane & 31);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int co = co0 + wm0 + i * 32 + mfma_row(r, lane);
-                if (co < a.Cout && t < a.Tout) {
+            for (int r0 = 0; r0 < 16; r0 += 8) {
+                float e0[8], e1[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int co = co0 + wm0 + i * 32 + mfma_row(r0 + q, lane);
+                    const bool ok = co < a.Cout && t < a.Tout && a.KS == 1;
                     const int64_t o = ((int64_t)b * a.Cout + co) * a.Tout + t;
-                    if (a.KS > 1) a.part[(int64_t)ks * a.B * a.Cout * a.Tout + o] = acc[i][j][r];
-                    else fwd_store(a, o, co, acc[i][j][r]);
+                    e0[q] = (ok && a.xact) ? a.xact[o] : 0.f;
+                    e1[q] = ok ? ((a.res ? a.res[o] : 0.f) + (a.accumulate ? a.y[o] : 0.f)) : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int cl = wm0 + i * 32 + mfma_row(r0 + q, lane), co = co0 + cl;
+                    if (co >= a.Cout || t >= a.Tout) continue;
+                    const int64_t o = ((int64_t)b * a.Cout + co) * a.Tout + t;
+                    const float v = acc[i][j][r0 + q];
+                    if (a.KS > 1) {
+                        a.part[(int64_t)ks * a.B * a.Cout * a.Tout + o] = v;
+                    } else {
+                        float w = v + Bsm[cl];
+                        if (a.xact) w *= act_grad(a.epi_act, e0[q]);
+                        a.y[o] = w + e1[q];
+                    }
                 }
             }
         }
@@ -210,9 +251,11 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
     const int M = a.Co * S;
     float* Xs = smem;               // [CK][Ub]
     float* As = smem + CK * Ub;     // [J][CK][BM]
+    float* Bsm = As + J * CK * BM;  // [BM] per-row bias (ConvTranspose1d mode)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
     const int u0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    if (tid < BM) Bsm[tid] = (a.mode == 0 && a.bias && m0 + tid < M) ? a.bias[(m0 + tid) / S] : 0.f;
     const int b = blockIdx.z / a.KS, ks = blockIdx.z - (blockIdx.z / a.KS) * a.KS;
     const float* ib = a.in + (int64_t)b * a.Ci * a.Tin;
     const int cbeg = ks * a.cps, cend = min(a.Ci, cbeg + a.cps);
@@ -238,21 +281,39 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
     const bool wrow = m0 + wcol < M;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
-        for (int cl = clane; cl < CK; cl += CP) {
-            const int c = c0 + cl;
-            const bool cv = c < cend;
-            const float* ir = ib + (int64_t)c * a.Tin;
-            float* xs = Xs + cl * Ub;
+        for (int cb = clane; cb < CK; cb += SB * CP) {
+            float v[SB][2];
 #pragma unroll
-            for (int k = 0; k < 2; ++k)
-                if (xo[k] >= 0) xs[xo[k]] = (cv && xm[k] >= 0) ? act_apply(a.in_act, ir[xm[k]]) : 0.f;
-        }
-        for (int q = 0; q < J; ++q)
-            for (int cl = wr0; cl < CK; cl += RSTEP) {
-                const int c = c0 + cl;
-                As[(q * CK + cl) * BM + wcol] =
-                    (c < cend && wrow) ? a.wp[((int64_t)c * J + q) * M + m0 + wcol] : 0.f;
+            for (int j = 0; j < SB; ++j) {
+                const int cl = cb + j * CP, c = c0 + cl;
+                const bool cv = cl < CK && c < cend;
+                const float* ir = ib + (int64_t)c * a.Tin;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) v[j][k] = (cv && xm[k] >= 0) ? ir[xm[k]] : 0.f;
             }
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int cl = cb + j * CP;
+                if (cl >= CK) continue;
+                float* xs = Xs + cl * Ub;
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+                    if (xo[k] >= 0) xs[xo[k]] = act_apply(a.in_act, v[j][k]);
+            }
+        }
+        for (int r0 = wr0; r0 < J * CK; r0 += SB * RSTEP) {
+            float v[SB];
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int r = r0 + j * RSTEP, q = r / CK, cl = r - q * CK, c = c0 + cl;
+                v[j] = (r < J * CK && c < cend && wrow) ? a.wp[((int64_t)c * J + q) * M + m0 + wcol] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int r = r0 + j * RSTEP;
+                if (r < J * CK) As[r * BM + wcol] = v[j];
+            }
+        }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
         for (int q = 0; q < J; ++q) {
@@ -276,17 +337,50 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int u = u0 + wn0 + j * 32 + (lane & 31);
+            if (a.KS > 1) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
-                if (row >= M) continue;
-                const int o = row / S, rr = row - o * S;
-                const int qpos = u * S + rr;
-                if (a.KS > 1) {
-                    if (qpos < a.Q)
-                        a.part[(((int64_t)ks * a.B + b) * a.Co + o) * a.Q + qpos] = acc[i][j][r];
-                } else {
-                    poly_store(a, b, o, qpos, acc[i][j][r]);
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                    if (row >= M) continue;
+                    const int o = row / S, rr = row - o * S, qpos = u * S + rr;
+                    if (qpos < a.Q) a.part[(((int64_t)ks * a.B + b) * a.Co + o) * a.Q + qpos] = acc[i][j][r];
+                }
+                continue;
+            }
+            // mode 0 (ConvTranspose1d): bias from LDS; mode 1 (backward-data): act' source and
+            // accumulated value loaded for 8 rows at a time ahead of their stores
+#pragma unroll
+            for (int r0 = 0; r0 < 16; r0 += 8) {
+                float e0[8], e1[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int row = m0 + wm0 + i * 32 + mfma_row(r0 + q, lane);
+                    const int o = row / S, m = u * S + (row - o * S) - a.pl;
+                    const bool ok = a.mode == 1 && row < M && m >= 0 && m < a.Tx;
+                    const int64_t idx = ((int64_t)b * a.Co + o) * a.Tx + m;
+                    e0[q] = (ok && a.act != ENCX_ACT_NONE) ? a.xact[idx] : 0.f;
+                    e1[q] = (ok && a.accumulate) ? a.out[idx] : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int rl = wm0 + i * 32 + mfma_row(r0 + q, lane), row = m0 + rl;
+                    if (row >= M) continue;
+                    const int o = row / S, qpos = u * S + (row - o * S);
+                    const float v = acc[i][j][r0 + q];
+                    if (a.mode == 0) {
+                        const int p = qpos - a.trim;
+                        if (p >= 0 && p < a.Tout) a.out[((int64_t)b * a.Co + o) * a.Tout + p] = v + Bsm[rl];
+                    } else {
+                        const int m = qpos - a.pl;
+                        if (m >= 0 && m < a.Tx) {
+                            float g = v;
+                            if (a.act != ENCX_ACT_NONE) g *= act_grad(a.act, e0[q]);
+                            a.out[((int64_t)b * a.Co + o) * a.Tx + m] = g + e1[q];
+                        } else if (qpos >= 0 && qpos < a.pl + a.Tx + a.pr) {
+                            const int slot = m < 0 ? qpos : a.pl + (m - a.Tx);
+                            a.side[((int64_t)b * a.Co + o) * (a.pl + a.pr) + slot] = v;
+                        }
+                    }
                 }
             }
         }
@@ -383,21 +477,39 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
             rm[k] = w < WL ? pad_src(tc * a.s + w, a.pl, a.Tr, a.e, a.mode) : -2;
         }
         __syncthreads();
-        for (int i = tid; i < BT * BM; i += NT) {
-            const int tl = i & (BT - 1), al = i >> lgBT;
-            const int t = tc + tl, aa = a0 + al;
-            float v = 0.f;
-            if (t < a.Tl && aa < a.A) v = act_apply(a.actL, Lb[(int64_t)aa * a.Tl + t]);
-            Ls[tl * BM + al] = v;
-        }
-        for (int cr = clane; cr < a.NCmax; cr += CP) {
-            const int c = c_first + cr;
-            const bool cv = c < a.C;
-            const float* rr = Rb + (int64_t)c * a.Tr;
-            float* rs = Rs + cr * WLp;
+        for (int i0 = tid; i0 < BT * BM; i0 += SB * NT) {
+            float v[SB];
 #pragma unroll
-            for (int k = 0; k < SPXW; ++k)
-                if (rm[k] != -2) rs[qlane + k * QP] = (cv && rm[k] >= 0) ? act_apply(a.actR, rr[rm[k]]) : 0.f;
+            for (int j = 0; j < SB; ++j) {
+                const int i = i0 + j * NT, tl = i & (BT - 1), al = i >> lgBT;
+                const int t = tc + tl, aa = a0 + al;
+                v[j] = (i < BT * BM && t < a.Tl && aa < a.A) ? Lb[(int64_t)aa * a.Tl + t] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int i = i0 + j * NT, tl = i & (BT - 1), al = i >> lgBT;
+                if (i < BT * BM) Ls[tl * BM + al] = act_apply(a.actL, v[j]);
+            }
+        }
+        for (int cb = clane; cb < a.NCmax; cb += SB * CP) {
+            float v[SB][SPXW];
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int cr = cb + j * CP, c = c_first + cr;
+                const bool cv = cr < a.NCmax && c < a.C;
+                const float* rr = Rb + (int64_t)c * a.Tr;
+#pragma unroll
+                for (int k = 0; k < SPXW; ++k) v[j][k] = (cv && rm[k] >= 0) ? rr[rm[k]] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int cr = cb + j * CP;
+                if (cr >= a.NCmax) continue;
+                float* rs = Rs + cr * WLp;
+#pragma unroll
+                for (int k = 0; k < SPXW; ++k)
+                    if (rm[k] != -2) rs[qlane + k * QP] = act_apply(a.actR, v[j][k]);
+            }
         }
         __syncthreads();
         for (int tp = wk * tw; tp < (wk + 1) * tw; tp += 2) {
@@ -567,13 +679,33 @@ struct LdConvFlat {
     }
 };
 struct EpConvFlat {
+    static constexpr int NPRE = 4;  // gemm.h two-phase epilogue: bias, act' source, residual, y
     FwdArgs p;
     int slabs;
-    ENCX_DEV void operator()(int co, int n, float v) const {
+    ENCX_DEV void pre(int co, int n, float* l) const {
         const int bb = n / p.Tout, t = n - bb * p.Tout;
         const int64_t o = ((int64_t)bb * p.Cout + co) * p.Tout + t;
-        if (slabs > 1) p.part[(int64_t)blockIdx.z * p.B * p.Cout * p.Tout + o] = v;
-        else fwd_store(p, o, co, v);
+        const bool fin = slabs == 1;
+        l[0] = (fin && p.bias) ? p.bias[co] : 0.f;
+        l[1] = (fin && p.xact) ? p.xact[o] : 0.f;
+        l[2] = (fin && p.res) ? p.res[o] : 0.f;
+        l[3] = (fin && p.accumulate) ? p.y[o] : 0.f;
+    }
+    ENCX_DEV void post(int co, int n, float v, const float* l) const {
+        const int bb = n / p.Tout, t = n - bb * p.Tout;
+        const int64_t o = ((int64_t)bb * p.Cout + co) * p.Tout + t;
+        if (slabs > 1) {
+            p.part[(int64_t)blockIdx.z * p.B * p.Cout * p.Tout + o] = v;
+            return;
+        }
+        v += l[0];
+        if (p.xact) v *= act_grad(p.epi_act, l[1]);
+        p.y[o] = v + l[2] + l[3];
+    }
+    ENCX_DEV void operator()(int co, int n, float v) const {
+        float l[NPRE];
+        pre(co, n, l);
+        post(co, n, v, l);
     }
 };
 struct LdPolyFlat {
@@ -588,16 +720,51 @@ struct LdPolyFlat {
     }
 };
 struct EpPolyFlat {
+    static constexpr int NPRE = 2;  // bias or act' source, accumulated value
     PolyArgs p;
     int ncols, slabs;
-    ENCX_DEV void operator()(int row, int n, float v) const {
+    ENCX_DEV void pre(int row, int n, float* l) const {
+        const int o = row / p.s, rr = row - o * p.s;
+        const int bb = n / ncols, u = n - bb * ncols, qpos = u * p.s + rr;
+        l[0] = l[1] = 0.f;
+        if (slabs > 1) return;
+        if (p.mode == 0) {
+            l[0] = p.bias ? p.bias[o] : 0.f;
+        } else {
+            const int m = qpos - p.pl;
+            if (m >= 0 && m < p.Tx) {
+                const int64_t idx = ((int64_t)bb * p.Co + o) * p.Tx + m;
+                if (p.act != ENCX_ACT_NONE) l[0] = p.xact[idx];
+                if (p.accumulate) l[1] = p.out[idx];
+            }
+        }
+    }
+    ENCX_DEV void post(int row, int n, float v, const float* l) const {
         const int o = row / p.s, rr = row - o * p.s;
         const int bb = n / ncols, u = n - bb * ncols, qpos = u * p.s + rr;
         if (slabs > 1) {
             if (qpos < p.Q) p.part[(((int64_t)blockIdx.z * p.B + bb) * p.Co + o) * p.Q + qpos] = v;
-        } else {
-            poly_store(p, bb, o, qpos, v);
+            return;
         }
+        if (p.mode == 0) {
+            const int q = qpos - p.trim;
+            if (q >= 0 && q < p.Tout) p.out[((int64_t)bb * p.Co + o) * p.Tout + q] = v + l[0];
+        } else {
+            const int m = qpos - p.pl;
+            if (m >= 0 && m < p.Tx) {
+                float g = v;
+                if (p.act != ENCX_ACT_NONE) g *= act_grad(p.act, l[0]);
+                p.out[((int64_t)bb * p.Co + o) * p.Tx + m] = g + l[1];
+            } else if (qpos >= 0 && qpos < p.pl + p.Tx + p.pr) {
+                const int slot = m < 0 ? qpos : p.pl + (m - p.Tx);
+                p.side[((int64_t)bb * p.Co + o) * (p.pl + p.pr) + slot] = v;
+            }
+        }
+    }
+    ENCX_DEV void operator()(int row, int n, float v) const {
+        float l[NPRE];
+        pre(row, n, l);
+        post(row, n, v, l);
     }
 };
 
@@ -677,14 +844,14 @@ static PolyPlan plan_poly(int64_t B, int64_t Ci, int64_t M, int64_t ncols, int64
 template <int BM, int BN, int WM, int WN>
 void launch_fwd(const FwdArgs& a, hipStream_t st) {
     dim3 grid(cdiv(a.Tout, BN), cdiv(a.Cout, BM), a.B * a.KS);
-    size_t lds = (size_t)(a.CK * a.s * a.Up + a.K * a.CK * BM) * sizeof(float);
+    size_t lds = (size_t)(a.CK * a.s * a.Up + a.K * a.CK * BM + BM) * sizeof(float);
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
 }
 
 template <int BM, int BN, int WM, int WN>
 void launch_poly(const PolyArgs& a, int ncols, hipStream_t st) {
     dim3 grid(cdiv(ncols, BN), cdiv((int64_t)a.Co * a.s, BM), a.B * a.KS);
-    size_t lds = (size_t)(a.CK * a.Ub + a.J * a.CK * BM) * sizeof(float);
+    size_t lds = (size_t)(a.CK * a.Ub + a.J * a.CK * BM + BM) * sizeof(float);
     hipLaunchKernelGGL((conv_poly_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
 }
 

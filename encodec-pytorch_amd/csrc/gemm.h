@@ -14,6 +14,13 @@
 #pragma once
 #include "common.h"
 
+// epilogue functors that load operands declare `static constexpr int NPRE` floats per element
+// and split into pre(m, n, float*) / post(m, n, v, const float*)
+template <class EP, class = void>
+struct ep_npre { static constexpr int value = 0; };
+template <class EP>
+struct ep_npre<EP, decltype((void)EP::NPRE)> { static constexpr int value = EP::NPRE; };
+
 template <int BM, int BN, int WM, int WN, int BK, class LD, class EP>
 __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, int Kred, int kchunk) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -93,10 +100,29 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int n = n0 + wn0 + j * 32 + l32;
+            if constexpr (ep_npre<EP>::value > 0) {
+                // two-phase epilogue: all of the tile's operand loads, then all of its stores
+                constexpr int NP = ep_npre<EP>::value;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm0 + i * 32 + mfma_row(r, lane);
-                if (m < M && n < N) ep(m, n, acc[i][j][r]);
+                for (int r0 = 0; r0 < 16; r0 += 8) {  // 8 rows' loads in flight together
+                    float pl[8][NP];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int m = m0 + wm0 + i * 32 + mfma_row(r0 + q, lane);
+                        if (m < M && n < N) ep.pre(m, n, pl[q]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int m = m0 + wm0 + i * 32 + mfma_row(r0 + q, lane);
+                        if (m < M && n < N) ep.post(m, n, acc[i][j][r0 + q], pl[q]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                    if (m < M && n < N) ep(m, n, acc[i][j][r]);
+                }
             }
         }
 }
