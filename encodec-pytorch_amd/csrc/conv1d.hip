@@ -60,7 +60,8 @@ ENCX_DEV void fwd_store(const FwdArgs& a, int64_t o, int co, float v) {
     a.y[o] = v;
 }
 
-template <int BM, int BN, int WM, int WN>
+// EPI = 0: bias-only epilogue (no operand loads); EPI = 1: act' source / residual / accumulate
+template <int BM, int BN, int WM, int WN, int EPI>
 __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     extern __shared__ float smem[];
@@ -171,6 +172,8 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
                 float e0[8], e1[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
+                    e0[q] = e1[q] = 0.f;
+                    if (EPI == 0) continue;
                     const int co = co0 + wm0 + i * 32 + mfma_row(r0 + q, lane);
                     const bool ok = co < a.Cout && t < a.Tout && a.KS == 1;
                     const int64_t o = ((int64_t)b * a.Cout + co) * a.Tout + t;
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
                         a.part[(int64_t)ks * a.B * a.Cout * a.Tout + o] = v;
                     } else {
                         float w = v + Bsm[cl];
-                        if (a.xact) w *= act_grad(a.epi_act, e0[q]);
+                        if (EPI && a.xact) w *= act_grad(a.epi_act, e0[q]);
                         a.y[o] = w + e1[q];
                     }
                 }
@@ -679,7 +682,6 @@ struct LdConvFlat {
     }
 };
 struct EpConvFlat {
-    static constexpr int NPRE = 4;  // gemm.h two-phase epilogue: bias, act' source, residual, y
     FwdArgs p;
     int slabs;
     ENCX_DEV void pre(int co, int n, float* l) const {
@@ -703,7 +705,7 @@ struct EpConvFlat {
         p.y[o] = v + l[2] + l[3];
     }
     ENCX_DEV void operator()(int co, int n, float v) const {
-        float l[NPRE];
+        float l[4];
         pre(co, n, l);
         post(co, n, v, l);
     }
@@ -720,7 +722,6 @@ struct LdPolyFlat {
     }
 };
 struct EpPolyFlat {
-    static constexpr int NPRE = 2;  // bias or act' source, accumulated value
     PolyArgs p;
     int ncols, slabs;
     ENCX_DEV void pre(int row, int n, float* l) const {
@@ -762,7 +763,7 @@ struct EpPolyFlat {
         }
     }
     ENCX_DEV void operator()(int row, int n, float v) const {
-        float l[NPRE];
+        float l[2];
         pre(row, n, l);
         post(row, n, v, l);
     }
@@ -845,7 +846,10 @@ template <int BM, int BN, int WM, int WN>
 void launch_fwd(const FwdArgs& a, hipStream_t st) {
     dim3 grid(cdiv(a.Tout, BN), cdiv(a.Cout, BM), a.B * a.KS);
     size_t lds = (size_t)(a.CK * a.s * a.Up + a.K * a.CK * BM + BM) * sizeof(float);
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    if (a.KS == 1 && (a.xact || a.res || a.accumulate))
+        hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, 1>), grid, dim3(NT), lds, st, a);
+    else
+        hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, 0>), grid, dim3(NT), lds, st, a);
 }
 
 template <int BM, int BN, int WM, int WN>
