@@ -24,12 +24,19 @@ MI355X_FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) p
 MI355X_HBM_PEAK_GBS = 8000.0
 
 
+WORKLOADS = {
+    'gen': 'config 2: 24 kHz mono SEANet + RVQ n_q=8, generator-only (l_t, l_f via Balancer, commit loss, Adam)',
+    'gan': 'config 3: 24 kHz mono full GAN (MS-STFT disc + Balancer)',
+    '48k': 'config 5: 48 kHz stereo, non-causal time_group_norm, 1 s segments, n_q=16, full GAN',
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', choices=['gen', 'gan'], default='gen')
+    ap.add_argument('--config', choices=['gen', 'gan', '48k'], default='gen')
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
@@ -38,31 +45,36 @@ def parse():
 
 def cpu_baseline(config, threads):
     """The CPU oracle's train step (oracle/encodec_oracle.py, the reference algorithm restated on
-    torch-CPU) on a bounded sample: batches of 8 clips with initialised codebooks, 1 warm-up
+    torch-CPU) on a bounded sample: 8 clips (2 stereo clips for 48k) with initialised codebooks, 1 warm-up
     step, then timed steps until at least 12 s of wall time have passed (>= 2 steps)."""
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
     from oracle import encodec_oracle as O
-    from fixtures import model_state, codebooks_from_stats, disc_state
+    from fixtures import model_state, codebooks_from_stats, disc_state, cfg48k
     from synth import synth_wave
     torch.set_num_threads(threads)
-    cfg = O.Config(target_bandwidths=(6.0,), audio_normalize=True)
+    if config == '48k':
+        cfg = cfg48k(target_bandwidths=(24.0,), segment=1.0)
+        bw, B, shape, lr = 24.0, 2, (2, 2, 48000), 1e-4
+    else:
+        cfg = O.Config(target_bandwidths=(6.0,), audio_normalize=True)
+        bw, B, shape, lr = 6.0, 8, (8, 1, 24000), 3e-4
     p = model_state(cfg, 3)
-    stats = np.zeros((8, 2, 128), np.float32)
+    stats = np.zeros((cfg.n_q, 2, 128), np.float32)
     stats[:, 1] = 0.05
-    cbs = codebooks_from_stats(stats, 4, 8, cfg.n_q)
-    gan = config == 'gan'
-    dp = disc_state(5) if gan else None
-    w = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3} if gan else {'l_t': 0.1, 'l_f': 1}
+    cbs = codebooks_from_stats(stats, 4, cfg.n_q, cfg.n_q)
+    gan = config in ('gan', '48k')
+    dp = disc_state(5, cfg.channels, cfg.channels) if gan else None
+    lg = 4 if config == '48k' else 3
+    w = {'l_t': 0.1, 'l_f': 1, 'l_g': lg, 'l_feat': lg} if gan else {'l_t': 0.1, 'l_f': 1}
     bal = O.Balancer(w)
     st, dst = {}, {}
-    B = 8
-    x = torch.from_numpy(synth_wave((B, 1, 24000), 99))
-    O.train_step(x, p, cbs, cfg, 6.0, bal, st, 3e-4, dp, dst, 3e-4)
+    x = torch.from_numpy(synth_wave(shape, 99))
+    O.train_step(x, p, cbs, cfg, bw, bal, st, lr, dp, dst, lr)
     t0 = time.perf_counter()
     n = 0
     while n < 2 or (time.perf_counter() - t0 < 12.0 and n < 200):
-        O.train_step(x, p, cbs, cfg, 6.0, bal, st, 3e-4, dp, dst, 3e-4)
+        O.train_step(x, p, cbs, cfg, bw, bal, st, lr, dp, dst, lr)
         n += 1
     dt = time.perf_counter() - t0
     return {'value': B * n / dt, 'unit': 'audio-seconds/sec', 'cores': threads, 'kind': 'port',
@@ -85,16 +97,28 @@ def main():
     from encx._lib import lib
 
     torch.manual_seed(3401 + rank)
-    model = EncodecModel._get_model([6.0], 24000, 1, causal=True, model_norm='weight_norm',
-                                    audio_normalize=True, name='my_encodec').to(dev)
-    disc = None
-    if args.config == 'gan':
-        from encx.msstftd import MultiScaleSTFTDiscriminator
-        disc = MultiScaleSTFTDiscriminator(filters=32).to(dev)
-    trainer = Trainer(model, disc, lr=3e-4, disc_lr=3e-4, max_iter=100000, warmup_iter=500)
     B = args.batch
     g = np.random.Generator(np.random.PCG64(1234 + rank))
-    batches = [torch.from_numpy((0.1 * g.standard_normal((B, 1, 24000))).astype(np.float32)).to(dev)
+    if args.config == '48k':
+        # config 5 (scripts/train.sbatch:18-33): 48 kHz stereo, non-causal, time_group_norm,
+        # 1 s segments (48000 + 480 samples per clip), n_q 16, lr 1e-4, l_g = l_feat = 4
+        model = EncodecModel._get_model([24.0], 48000, 2, causal=False, model_norm='time_group_norm',
+                                        audio_normalize=True, segment=1.0, name='encodec_48khz').to(dev)
+        from encx.msstftd import MultiScaleSTFTDiscriminator
+        disc = MultiScaleSTFTDiscriminator(filters=32, in_channels=2, out_channels=2).to(dev)
+        trainer = Trainer(model, disc, lr=1e-4, disc_lr=1e-4, max_iter=100000, warmup_iter=500,
+                          weights={'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4}, sample_rate=48000)
+        shape = (B, 2, 48000)
+    else:
+        model = EncodecModel._get_model([6.0], 24000, 1, causal=True, model_norm='weight_norm',
+                                        audio_normalize=True, name='my_encodec').to(dev)
+        disc = None
+        if args.config == 'gan':
+            from encx.msstftd import MultiScaleSTFTDiscriminator
+            disc = MultiScaleSTFTDiscriminator(filters=32).to(dev)
+        trainer = Trainer(model, disc, lr=3e-4, disc_lr=3e-4, max_iter=100000, warmup_iter=500)
+        shape = (B, 1, 24000)
+    batches = [torch.from_numpy((0.1 * g.standard_normal(shape)).astype(np.float32)).to(dev)
                for _ in range(4)]
 
     for i in range(args.warmup):
@@ -140,10 +164,9 @@ def main():
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt * 1e3 / args.steps, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
             'data': 'synthetic (0.1*N(0,1) clips, random-init weights)',
-            'config': {'workload': ('config 2: 24 kHz mono SEANet + RVQ n_q=8, generator-only (l_t, l_f '
-                                    'via Balancer, commit loss, Adam)') if args.config == 'gen' else
-                       'config 3: 24 kHz mono full GAN (MS-STFT disc + Balancer)',
-                       'global_batch': B * world, 'clip_seconds': 1.0, 'sample_rate': 24000,
+            'config': {'workload': WORKLOADS[args.config],
+                       'global_batch': B * world, 'clip_seconds': 1.0,
+                       'sample_rate': 48000 if args.config == '48k' else 24000,
                        'parallelism': f'dp{world}'},
             'roofline': roof,
         }

@@ -1,4 +1,6 @@
 // Library entry points: version, error strings, device selection, launch profiling.
+#include <stdarg.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <atomic>
@@ -17,20 +19,32 @@ struct ProfState {
     hipEvent_t ev1[kMaxSlots];
     double flops[kMaxSlots];
     double bytes[kMaxSlots];
+    char tags[kMaxSlots][64];
     bool created = false;
 };
 ProfState g_prof;
 std::atomic<bool> g_prof_on{false};
 }  // namespace
 
-encx_prof_scope::encx_prof_scope(hipStream_t s, double f, double b) : st(s), slot(-1) {
+encx_prof_scope::encx_prof_scope(hipStream_t s, double f, double b, const char* kind) : st(s), slot(-1) {
     if (!g_prof_on.load(std::memory_order_relaxed)) return;
     std::lock_guard<std::mutex> g(g_prof.mu);
     if (!g_prof.on || g_prof.next >= kMaxSlots) return;
     slot = g_prof.next++;
     g_prof.flops[slot] = f;
     g_prof.bytes[slot] = b;
+    snprintf(g_prof.tags[slot], sizeof(g_prof.tags[slot]), "%s", kind ? kind : "");
     (void)hipEventRecord(g_prof.ev0[slot], st);
+}
+
+void encx_prof_scope::tag(const char* fmt, ...) {
+    if (slot < 0) return;
+    char* t = g_prof.tags[slot];
+    size_t n = strlen(t);
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(t + n, sizeof(g_prof.tags[slot]) - n, fmt, ap);
+    va_end(ap);
 }
 
 encx_prof_scope::~encx_prof_scope() {
@@ -84,6 +98,21 @@ int encx_prof_read(double* total_ms, double* total_flops, double* total_bytes, i
     if (total_flops) *total_flops = fl;
     if (total_bytes) *total_bytes = by;
     if (launches) *launches = g_prof.next;
+    return 0;
+}
+
+int encx_prof_slot(int64_t i, double* ms, double* flops, double* bytes, const char** tag) {
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    if (i < 0 || i >= g_prof.next) return ENCX_EINVAL;
+    hipError_t e = hipEventSynchronize(g_prof.ev1[i]);
+    if (e != hipSuccess) return (int)e;
+    float t = 0.f;
+    e = hipEventElapsedTime(&t, g_prof.ev0[i], g_prof.ev1[i]);
+    if (e != hipSuccess) return (int)e;
+    if (ms) *ms = t;
+    if (flops) *flops = g_prof.flops[i];
+    if (bytes) *bytes = g_prof.bytes[i];
+    if (tag) *tag = g_prof.tags[i];
     return 0;
 }
 

@@ -1090,7 +1090,8 @@ int encx_conv1d_fwd(const float* x, const float* wf, const float* bias, const fl
     a.K = (int)K; a.s = (int)stride; a.d = (int)dilation; a.pl = (int)pad_left; a.e = (int)short_ext;
     a.mode = pad_mode; a.act = pre_act; a.epi_act = ENCX_ACT_NONE; a.accumulate = 0;
     encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
-                       4.0 * (B * Cin * Tin + B * Cout * Tout * (residual ? 2 : 1) + Cin * K * Cout));
+                       4.0 * (B * Cin * Tin + B * Cout * Tout * (residual ? 2 : 1) + Cin * K * Cout), "conv_fwd");
+    ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
     return conv_fwd_run(a, ws, st);
 }
 
@@ -1125,7 +1126,8 @@ int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float
     const int64_t Tpad = pad_left + Tin + pad_right;
     const int ncols = (int)cdiv(Tpad, stride);
     encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
-                       4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout));
+                       4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout), "conv_dgrad");
+    ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
     int rc = poly_run(a, ncols, part, st);
     if (rc) return rc;
     if (pad_left + pad_right > 0 && pad_mode == ENCX_PAD_REFLECT) {
@@ -1145,7 +1147,8 @@ int encx_conv1d_bwd_weight(const float* dy, const float* x, float* dw, float* db
                            encx_stream_t stream) {
     ENCX_REQUIRE(dy && x && dw && ws && B > 0);
     hipStream_t st = (hipStream_t)stream;
-    encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K, 4.0 * (B * Cout * Tout + B * Cin * Tin + Cin * K * Cout));
+    encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K, 4.0 * (B * Cout * Tout + B * Cin * Tin + Cin * K * Cout), "conv_wgrad");
+    ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
     int rc = wgrad_run(dy, x, dw, ws, B, Cout, Tout, Cin, Tin, K, stride, dilation, pad_left,
                        short_ext, pad_mode, ENCX_ACT_NONE, pre_act, accumulate, st);
     if (rc) return rc;
@@ -1174,7 +1177,8 @@ int encx_convtr1d_fwd(const float* x, const float* wp, const float* bias, float*
     a.J = (int)cdiv(K, stride); a.mode = 0; a.trim = (int)trim_left; a.Tout = (int)Tout;
     a.pl = a.pr = a.Tx = 0; a.act = ENCX_ACT_NONE; a.in_act = pre_act; a.accumulate = 0;
     const int ncols = (int)cdiv(Tout + trim_left, stride);
-    encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K, 4.0 * (B * Cin * Tin + B * Cout * Tout + Cin * K * Cout));
+    encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K, 4.0 * (B * Cin * Tin + B * Cout * Tout + Cin * K * Cout), "convtr_fwd");
+    ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
     return poly_run(a, ncols, ws, st);
 }
 
@@ -1199,7 +1203,8 @@ int encx_convtr1d_bwd_data(const float* dy, const float* wf, const float* x, flo
     a.K = (int)K; a.s = (int)stride; a.d = 1; a.pl = (int)trim_left; a.e = 0;
     a.mode = ENCX_PAD_ZERO; a.act = ENCX_ACT_NONE; a.epi_act = pre_act; a.accumulate = accumulate;
     encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K,
-                       4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout));
+                       4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout), "convtr_dgrad");
+    ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
     return conv_fwd_run(a, ws, st);
 }
 
@@ -1209,7 +1214,8 @@ int encx_convtr1d_bwd_weight(const float* x, const float* dy, float* dw, float* 
                              int accumulate, encx_stream_t stream) {
     ENCX_REQUIRE(x && dy && dw && ws && B > 0);
     hipStream_t st = (hipStream_t)stream;
-    encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K, 4.0 * (B * Cout * Tout + B * Cin * Tin + Cin * K * Cout));
+    encx_prof_scope ps(st, 2.0 * B * Cin * Tin * Cout * K, 4.0 * (B * Cout * Tout + B * Cin * Tin + Cin * K * Cout), "convtr_wgrad");
+    ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
     // L = act(x) [ci][t], R = dy [co][t*s + k - trim_left] zero-padded
     int rc = wgrad_run(x, dy, dw, ws, B, Cin, Tin, Cout, Tout, K, stride, 1, trim_left, 0,
                        ENCX_PAD_ZERO, pre_act, ENCX_ACT_NONE, accumulate, st);

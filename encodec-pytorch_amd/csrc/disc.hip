@@ -609,7 +609,8 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
     ENCX_REQUIRE(geo_ok(g));
     hipStream_t st = (hipStream_t)stream;
-    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + B * Co * T2 * Fo));
+    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + B * Co * T2 * Fo), "c2_fwd");
+    ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
     constexpr int BN = 128;
     a.NR = c2_rows(BN, (int)Fo);
@@ -628,7 +629,8 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
     C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
     ENCX_REQUIRE(geo_ok(g));
     hipStream_t st = (hipStream_t)stream;
-    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo));
+    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo), "c2_dgrad");
+    ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     C2Dg a{g, dy, yact, wp, xact, dx, 0, 0, 0, 0, 0, accumulate};
     constexpr int BN = 128;
     a.J = (int)cdiv(KF, sf);
@@ -661,7 +663,8 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
     C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
     ENCX_REQUIRE(geo_ok(g));
     hipStream_t st = (hipStream_t)stream;
-    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo));
+    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo), "c2_wgrad");
+    ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     WgPlan2 p = plan_wg2(g);
     C2Wg a{g, dy, yact, x, ws, p.BT, p.NR, p.RL, p.NCmax, p.items, p.per_split, p.chunks};
     const int N = (int)(Ci * KT * KF + 1);
@@ -691,7 +694,8 @@ int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B,
     const int Fr = (int)((T - n_fft) / hop + 1), nb = (int)(n_fft / 2 + 1);
     const float inv = (float)(1.0 / sqrt(3.0 * (double)n_fft / 8.0));  // sum of periodic hann^2 = 3n/8
     const int M = (int)(B * C * Fr), N = 2 * nb, K = (int)n_fft;
-    encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * (B * C * T + (int64_t)M * N));
+    encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * (B * C * T + (int64_t)M * N), "spec_fwd");
+    ps.tag(" n%ld", (long)n_fft);
     return gemm_launch(LdSpecD{x, tables, (int)T, Fr, (int)hop, N}, EpSpecD{z, (int)C, Fr, nb, inv}, M, N, K, st);
 }
 
@@ -709,7 +713,8 @@ int encx_disc_spec_bwd(const float* dz, const float* tables, float* dx, float* w
     const float inv = (float)(1.0 / sqrt(3.0 * (double)n_fft / 8.0));
     const int M = (int)(B * C * Fr), N = (int)n_fft, K = 2 * nb;
     {
-        encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * ((int64_t)M * K + (int64_t)M * N));
+        encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * ((int64_t)M * K + (int64_t)M * N), "spec_bwd");
+        ps.tag(" n%ld", (long)n_fft);
         int rc = gemm_launch(LdSpecDB{dz, tables, (int)C, Fr, nb, K, inv}, EpFrames{ws, N}, M, N, K, st);
         if (rc) return rc;
     }

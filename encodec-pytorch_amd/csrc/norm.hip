@@ -57,26 +57,28 @@ __global__ void gn_finish_stats(const double* rows, float* stats, int B, int C, 
     stats[2 * b + 1] = (float)(1.0 / sqrt(var + eps));
 }
 
+// y[row][t] = norm(x[row][tl + t]) for t < Ty (the statistics cover all T positions)
 __global__ void gn_apply(const float* x, const float* stats, const float* gamma, const float* beta, float* y,
-                         int C, int T, int64_t n) {
+                         int C, int T, int tl, int Ty, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int64_t row = i / T;
+    const int64_t row = i / Ty;
+    const int t = (int)(i - row * Ty) + tl;
     const int b = (int)(row / C), c = (int)(row - (int64_t)b * C);
-    const float xh = (x[i] - stats[2 * b]) * stats[2 * b + 1];
+    const float xh = (x[row * T + t] - stats[2 * b]) * stats[2 * b + 1];
     y[i] = xh * (gamma ? gamma[c] : 1.f) + (beta ? beta[c] : 0.f);
 }
 
-// rows[(b*C + c)*2 + {0,1}] = (sum dy, sum dy * xhat) over t
+// rows[(b*C + c)*2 + {0,1}] = (sum dy, sum dy * xhat) over the window (dy is 0 outside it)
 __global__ __launch_bounds__(NT) void gn_row_bwd(const float* dy, const float* x, const float* stats,
-                                                 double* rows, int C, int T) {
+                                                 double* rows, int C, int T, int tl, int Ty) {
     __shared__ double red[4];
     const int b = blockIdx.x / C;
     const float mean = stats[2 * b], rstd = stats[2 * b + 1];
-    const float* dr = dy + (int64_t)blockIdx.x * T;
-    const float* xr = x + (int64_t)blockIdx.x * T;
+    const float* dr = dy + (int64_t)blockIdx.x * Ty;
+    const float* xr = x + (int64_t)blockIdx.x * T + tl;
     double s = 0.0, q = 0.0;
-    for (int t = threadIdx.x; t < T; t += NT) {
+    for (int t = threadIdx.x; t < Ty; t += NT) {
         const double g = dr[t];
         s += g;
         q += g * (double)((xr[t] - mean) * rstd);
@@ -116,16 +118,18 @@ __global__ void gn_finish_bwd(const double* rows, const float* gamma, float* coe
     }
 }
 
-// dx = rstd * (dy*gamma - mean(g) - xhat * mean(g*xhat))
+// dx = rstd * (dy*gamma - mean(g) - xhat * mean(g*xhat)), dy = 0 outside the window
 __global__ void gn_dx(const float* dy, const float* x, const float* stats, const float* coef, const float* gamma,
-                      float* dx, int C, int T, int64_t n, int acc) {
+                      float* dx, int C, int T, int tl, int Ty, int64_t n, int acc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t row = i / T;
+    const int t = (int)(i - row * T) - tl;
     const int b = (int)(row / C), c = (int)(row - (int64_t)b * C);
     const float mean = stats[2 * b], rstd = stats[2 * b + 1];
     const float xh = (x[i] - mean) * rstd;
-    const float g = dy[i] * (gamma ? gamma[c] : 1.f);
+    const float d = (t >= 0 && t < Ty) ? dy[row * Ty + t] : 0.f;
+    const float g = d * (gamma ? gamma[c] : 1.f);
     const float v = rstd * (g - coef[2 * b] - xh * coef[2 * b + 1]);
     dx[i] = acc ? dx[i] + v : v;
 }
@@ -179,34 +183,38 @@ extern "C" {
 size_t encx_groupnorm_workspace(int64_t B, int64_t C) { return (size_t)(2 * B * C) * sizeof(double); }
 
 int encx_groupnorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* stats, void* ws,
-                       int64_t B, int64_t C, int64_t T, double eps, encx_stream_t stream) {
+                       int64_t B, int64_t C, int64_t T, int64_t trim_left, int64_t Ty, double eps,
+                       encx_stream_t stream) {
     ENCX_REQUIRE(x && y && stats && ws && B > 0 && C > 0 && T > 0);
+    ENCX_REQUIRE(trim_left >= 0 && Ty > 0 && trim_left + Ty <= T);
     hipStream_t st = (hipStream_t)stream;
     double* rows = (double*)ws;
     hipLaunchKernelGGL(gn_row_stats, dim3((unsigned)(B * C)), dim3(NT), 0, st, x, rows, (int)T);
     hipLaunchKernelGGL(gn_finish_stats, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, st, rows, stats, (int)B, (int)C,
                        (int)T, eps);
-    const int64_t n = B * C * T;
+    const int64_t n = B * C * Ty;
     hipLaunchKernelGGL(gn_apply, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, x, stats, gamma, beta, y, (int)C,
-                       (int)T, n);
+                       (int)T, (int)trim_left, (int)Ty, n);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
 
 int encx_groupnorm_bwd(const float* dy, const float* x, const float* gamma, const float* stats, float* dx,
                        float* dgamma, float* dbeta, int acc_x, int acc_params, void* ws, float* coef, int64_t B,
-                       int64_t C, int64_t T, encx_stream_t stream) {
+                       int64_t C, int64_t T, int64_t trim_left, int64_t Ty, encx_stream_t stream) {
     ENCX_REQUIRE(dy && x && stats && ws && coef && B > 0 && C > 0 && T > 0);
+    ENCX_REQUIRE(trim_left >= 0 && Ty > 0 && trim_left + Ty <= T);
     hipStream_t st = (hipStream_t)stream;
     double* rows = (double*)ws;
-    hipLaunchKernelGGL(gn_row_bwd, dim3((unsigned)(B * C)), dim3(NT), 0, st, dy, x, stats, rows, (int)C, (int)T);
+    hipLaunchKernelGGL(gn_row_bwd, dim3((unsigned)(B * C)), dim3(NT), 0, st, dy, x, stats, rows, (int)C, (int)T,
+                       (int)trim_left, (int)Ty);
     const int64_t m = B > C ? B : C;
     hipLaunchKernelGGL(gn_finish_bwd, dim3((unsigned)cdiv(m, 64)), dim3(64), 0, st, rows, gamma, coef, dgamma, dbeta,
                        (int)B, (int)C, (int)T, acc_params);
     if (dx) {
         const int64_t n = B * C * T;
         hipLaunchKernelGGL(gn_dx, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, dy, x, stats, coef, gamma, dx,
-                           (int)C, (int)T, n, acc_x);
+                           (int)C, (int)T, (int)trim_left, (int)Ty, n, acc_x);
     }
     ENCX_CHECK_LAUNCH();
     return 0;

@@ -7,6 +7,8 @@
 struct encx_prof_scope {
     hipStream_t st;
     int slot;
-    encx_prof_scope(hipStream_t s, double flops, double bytes);
+    encx_prof_scope(hipStream_t s, double flops, double bytes, const char* kind = "");
     ~encx_prof_scope();
+    // per-launch label (shape) for the per-slot table; printf-style, only formatted when on
+    void tag(const char* fmt, ...);
 };

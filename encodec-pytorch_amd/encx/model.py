@@ -84,12 +84,12 @@ class EncodecModel(nn.Module):
         return codes.transpose(0, 1), scale
 
     def decode(self, encoded_frames: tp.List[EncodedFrame]) -> torch.Tensor:
-        """model.py:170-181."""
+        """model.py:170-181: per-segment decode, then the triangle-weighted overlap-add."""
         if self.segment_length is None:
             assert len(encoded_frames) == 1
             return self._decode_frame(encoded_frames[0])
-        raise NotImplementedError('encx: segment overlap-add (48 kHz model, utils.py:22-61) is a '
-                                  'next-round row (SURVEY.md §8f row 3)')
+        frames = [self._decode_frame(frame) for frame in encoded_frames]
+        return ops.linear_overlap_add(frames, self.segment_stride or 1)  # utils.py:22-61
 
     def _decode_frame(self, encoded_frame: EncodedFrame) -> torch.Tensor:
         """model.py:183-193."""
@@ -155,5 +155,17 @@ class EncodecModel(nn.Module):
             raise RuntimeError('encx: pretrained checkpoints are remote-only; load a state dict instead')
         model = EncodecModel._get_model([1.5, 3., 6, 12., 24.], 24_000, 1, causal=True,
                                         model_norm='weight_norm', audio_normalize=False, name='unset')
+        model.eval()
+        return model
+
+    @staticmethod
+    def encodec_model_48khz(pretrained: bool = False, repository=None):
+        """model.py:311-329 architecture: 48 kHz stereo, non-causal, time_group_norm, 1 s
+        segments (pretrained weights are remote-only: out of scope)."""
+        if pretrained:
+            raise RuntimeError('encx: pretrained checkpoints are remote-only; load a state dict instead')
+        model = EncodecModel._get_model([3., 6., 12., 24.], 48_000, 2, causal=False,
+                                        model_norm='time_group_norm', audio_normalize=True,
+                                        segment=1., name='unset')
         model.eval()
         return model

@@ -166,8 +166,13 @@ class SConvTranspose1d(nn.Module):
     def forward(self, x, act=None):
         c = self.convtr
         v, g = c.convtr.wv()
+        if c.norm_type != 'time_group_norm':
+            return ops.convtr1d(x, v, g, c.convtr.bias, c.kernel_size, c.stride, self.causal,
+                                self.trim_right_ratio, act)
+        # NormConvTranspose1d.forward normalises the FULL transposed-conv output (conv.py:153-156)
+        # and only then does SConvTranspose1d trim it (:248-252): the GroupNorm statistics include
+        # the trimmed edge samples, so the conv runs untrimmed and the norm writes the window
         y = ops.convtr1d(x, v, g, c.convtr.bias, c.kernel_size, c.stride, self.causal,
-                         self.trim_right_ratio, act)
-        if c.norm_type == 'time_group_norm':  # NormConvTranspose1d.forward, conv.py:153-156
-            y = ops.group_norm(y, c.norm.weight, c.norm.bias, c.norm.eps)
-        return y
+                         self.trim_right_ratio, act, untrimmed=True)
+        tl, tout = ops.convtr_geometry(x.shape[-1], c.kernel_size, c.stride, self.causal, self.trim_right_ratio)
+        return ops.group_norm(y, c.norm.weight, c.norm.bias, c.norm.eps, tl, y.shape[-1] - tl - tout)

@@ -179,12 +179,15 @@ class ConvTr1dFn(torch.autograd.Function):
     channels, conv.py:149) and a fused pre-ELU."""
 
     @staticmethod
-    def forward(ctx, x, v, g, b, K, s, causal, trim_right_ratio, act):
+    def forward(ctx, x, v, g, b, K, s, causal, trim_right_ratio, act, untrimmed=False):
         _check(x)
         x = x.contiguous()
         B, Cin, T = x.shape
         Cout = v.shape[1]
-        trim_left, tout = convtr_geometry(T, K, s, causal, trim_right_ratio)
+        if untrimmed:  # full (T - 1) * s + K output; the caller trims after its norm
+            trim_left, tout = 0, (T - 1) * s + K
+        else:
+            trim_left, tout = convtr_geometry(T, K, s, causal, trim_right_ratio)
         need_dx = ctx.needs_input_grad[0]
         wf, wp = _weight_prep(v, g, K, s, need_dx, True)
         y = torch.empty(B, Cout, tout, device=x.device, dtype=torch.float32)
@@ -217,11 +220,11 @@ class ConvTr1dFn(torch.autograd.Function):
             call('encx_convtr1d_bwd_weight', ptr(x), ptr(dy), ptr(dw), None, ptr(ws), B, Cin, T,
                  Cout, tout, K, s, trim_left, act, 0, st)
             dv, dg, db = _param_grads(v, g, b, dw, dy, B, Cout, tout)
-        return dx, dv, dg, db, None, None, None, None, None
+        return dx, dv, dg, db, None, None, None, None, None, None
 
 
-def convtr1d(x, v, g, b, K, stride, causal=True, trim_right_ratio=1.0, act=None):
-    return ConvTr1dFn.apply(x, v, g, b, K, stride, causal, trim_right_ratio, act)
+def convtr1d(x, v, g, b, K, stride, causal=True, trim_right_ratio=1.0, act=None, untrimmed=False):
+    return ConvTr1dFn.apply(x, v, g, b, K, stride, causal, trim_right_ratio, act, untrimmed)
 
 
 # ---------------------------------------------------------------------------- normalisation
@@ -742,20 +745,24 @@ def add(x, y):
 
 
 class GroupNormFn(torch.autograd.Function):
-    """nn.GroupNorm(1, C) of norm='time_group_norm' (modules/conv.py:45-49)."""
+    """nn.GroupNorm(1, C) of norm='time_group_norm' (modules/conv.py:45-49). With a trim the
+    statistics cover the whole input and only x[..., trim_left : T - trim_right] is returned:
+    NormConvTranspose1d normalises before SConvTranspose1d trims (conv.py:153-156, 248-252)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps):
+    def forward(ctx, x, gamma, beta, eps, trim_left=0, trim_right=0):
         _check(x)
         x = x.contiguous()
         B, C, T = x.shape
-        y = torch.empty_like(x)
+        Ty = T - trim_left - trim_right
+        y = torch.empty(B, C, Ty, device=x.device, dtype=torch.float32)
         stats = _f32(2 * B, x)
         ws = _ws(lib.encx_groupnorm_workspace(B, C), x)
         call('encx_groupnorm_fwd', ptr(x), ptr(gamma), ptr(beta), ptr(y), ptr(stats), ptr(ws), B, C, T,
-             float(eps), stream())
+             trim_left, Ty, float(eps), stream())
         ctx.save_for_backward(x, stats)
         ctx.params = (gamma, beta)
+        ctx.win = (trim_left, Ty)
         return y
 
     @staticmethod
@@ -778,13 +785,14 @@ class GroupNormFn(torch.autograd.Function):
         else:
             dg = db = None
             acc, ret = 0, False
+        tl, Ty = ctx.win
         call('encx_groupnorm_bwd', ptr(dy), ptr(x), ptr(gamma), ptr(stats), ptr(dx), ptr(dg), ptr(db), 0, acc,
-             ptr(ws), ptr(coef), B, C, T, stream())
-        return dx, (dg if ret else None), (db if ret else None), None
+             ptr(ws), ptr(coef), B, C, T, tl, Ty, stream())
+        return dx, (dg if ret else None), (db if ret else None), None, None, None
 
 
-def group_norm(x, gamma, beta, eps=1e-5):
-    return GroupNormFn.apply(x, gamma, beta, eps)
+def group_norm(x, gamma, beta, eps=1e-5, trim_left=0, trim_right=0):
+    return GroupNormFn.apply(x, gamma, beta, eps, trim_left, trim_right)
 
 
 class OverlapAddFn(torch.autograd.Function):

@@ -44,6 +44,9 @@ int encx_init(int device);
  * bytes. family: 0 = all conv/GEMM MFMA kernels. */
 int encx_prof_enable(int on);
 int encx_prof_read(double* total_ms, double* total_flops, double* total_bytes, int64_t* launches);
+/* One recorded launch group: event time, algorithmic FLOPs / bytes and its label
+ * ("<op> <shape>"), for per-layer tables (tools/layer_table.py). */
+int encx_prof_slot(int64_t i, double* ms, double* flops, double* bytes, const char** tag);
 
 /* ---------------------------------------------------------------- weight norm
  * torch.nn.utils.weight_norm(dim=0) installed by modules/conv.py:25-34 (apply_parametrization_norm):
@@ -310,15 +313,20 @@ int encx_feat_loss_bwd(const float* fr, const float* ff, int64_t n, double scale
 
 /* ---- 48 kHz model (config 5) ----
  * GroupNorm(1, C) of norm='time_group_norm' (modules/conv.py:45-49, applied after the conv at
- * :121/:155): y = (x - mean_b) * rstd_b * gamma[c] + beta[c] over x [B][C][T]; stats [2B]
- * (mean, rstd) is written for the backward; ws: encx_groupnorm_workspace bytes (fp64 rows). */
+ * :121/:155): y = (x - mean_b) * rstd_b * gamma[c] + beta[c] with the statistics over all of
+ * x [B][C][T]; only the window [trim_left, trim_left + Ty) is written, y [B][C][Ty] (the
+ * ConvTranspose1d normalises BEFORE SConvTranspose1d trims, conv.py:153-156 then :248-252;
+ * Conv1d passes trim_left 0, Ty = T). stats [2B] (mean, rstd) is written for the backward;
+ * ws: encx_groupnorm_workspace bytes (fp64 rows). */
 size_t encx_groupnorm_workspace(int64_t B, int64_t C);
 int encx_groupnorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* stats, void* ws,
-                       int64_t B, int64_t C, int64_t T, double eps, encx_stream_t stream);
-/* dx (+)= d/dx (acc_x), dgamma / dbeta (+)= (acc_params; either may be NULL); coef: [2B] scratch */
+                       int64_t B, int64_t C, int64_t T, int64_t trim_left, int64_t Ty, double eps,
+                       encx_stream_t stream);
+/* dy [B][C][Ty] (zero outside the window) -> dx [B][C][T] (+)= (acc_x), dgamma / dbeta (+)=
+ * (acc_params; either may be NULL); coef: [2B] scratch */
 int encx_groupnorm_bwd(const float* dy, const float* x, const float* gamma, const float* stats, float* dx,
                        float* dgamma, float* dbeta, int acc_x, int acc_params, void* ws, float* coef, int64_t B,
-                       int64_t C, int64_t T, encx_stream_t stream);
+                       int64_t C, int64_t T, int64_t trim_left, int64_t Ty, encx_stream_t stream);
 /* _linear_overlap_add (utils.py:22-61) of nf <= 32 decoded segments [BC][len_k] (host arrays of
  * device pointers / lengths; all but the last of equal length) at `stride` -> out [BC][total]. */
 int encx_overlap_add(const float* const* frames, const int64_t* lengths, int nf, int64_t stride, int64_t BC,

@@ -26,9 +26,19 @@ def model_state(cfg, seed):
     return {k: T(v) for k, v in synth_state(model_param_shapes(cfg), seed).items()}
 
 
-def disc_state(seed):
+def disc_state(seed, in_channels=1, out_channels=1):
     from oracle.encodec_oracle import disc_param_shapes
-    return {k: T(v) for k, v in synth_state(disc_param_shapes(), seed).items()}
+    shapes = disc_param_shapes(in_channels=in_channels, out_channels=out_channels)
+    return {k: T(v) for k, v in synth_state(shapes, seed).items()}
+
+
+def cfg48k(**kw):
+    """The g9 fixture's model: config 5's 48 kHz stereo SEANet (scripts/train.sbatch:18-30:
+    non-causal, time_group_norm) with segment 0.1 s instead of 1 s (same two-frame shape)."""
+    from oracle.encodec_oracle import Config
+    return Config(sample_rate=48000, channels=2, causal=False, norm='time_group_norm',
+                  target_bandwidths=kw.pop('target_bandwidths', (3.0,)), audio_normalize=True,
+                  segment=kw.pop('segment', 0.1), **kw)
 
 
 def codebooks_from_stats(stats, seed, n_used, n_total):
@@ -62,5 +72,5 @@ def certified(gaps, x_norm2, e_norm2, factor=256):
     return gaps > factor * eps * (x_norm2 + e_norm2)
 
 
-__all__ = ['load', 'T', 'model_state', 'disc_state', 'codebooks_from_stats', 'g3_codebooks',
+__all__ = ['load', 'T', 'model_state', 'disc_state', 'cfg48k', 'codebooks_from_stats', 'g3_codebooks',
            'certified', 'synth_wave', 'rng']

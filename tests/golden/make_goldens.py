@@ -14,6 +14,8 @@ Fixture map:
   g6_balancer.npz  Balancer known-answer test (balancer.py:121-139) + a 4-loss case
   g7_step.npz      one full train step (gen-only and GAN), B 2, T 4800, n_q 2
   g8_sched.npz     WarmupCosineLrScheduler learning-rate trace
+  g9_step48k.npz   config-5 analogue: 48 kHz stereo, non-causal, time_group_norm, segment 0.1 s
+                   (two frames: 4800 + 48 samples, linear overlap-add), gen-only and GAN steps
 """
 import os
 import sys
@@ -367,6 +369,77 @@ def g7():
     save('g7_step.npz', **out)
 
 
+G9_SEG = 0.1  # seconds: frames of 4800 samples at stride 4752 -> 4800 + 48 (the 48000 + 480 of 1 s)
+
+
+def one_step_48k(gan):
+    m = R.model.EncodecModel._get_model([3.0], 48000, 2, causal=False, model_norm='time_group_norm',
+                                        audio_normalize=True, segment=G9_SEG, name='encodec_48khz')
+    load_synth(m, 91)
+    x = t(synth_wave((2, 2, 4800), 92))
+    with torch.no_grad():
+        emb = m.encoder(x / (1e-8 + x.mean(1, keepdim=True).pow(2).mean(2, keepdim=True).sqrt()))
+    e = emb.permute(0, 2, 1).reshape(-1, 128).double()
+    stats = np.zeros((2, 2, 128), np.float32)
+    stats[0, 0] = e.mean(0).float().numpy()
+    stats[0, 1] = e.std(0).float().numpy()
+    stats[1, 1] = 0.5 * stats[0, 1]
+    fill_codebooks(m, stats, 93, 2)
+    d = R.msstftd.MultiScaleSTFTDiscriminator(filters=32, in_channels=2, out_channels=2)
+    load_synth(d, 94)
+    opt = torch.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=1e-4, betas=(0.5, 0.9))
+    optd = torch.optim.Adam([p for p in d.parameters() if p.requires_grad], lr=1e-4, betas=(0.5, 0.9))
+    # scripts/train.sbatch:32-33: l_g = l_feat = 4
+    weights = {'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4} if gan else {'l_t': 0.1, 'l_f': 1}
+    bal = R.balancer.Balancer(weights)
+    m.train()
+    d.train()
+    out = {'x': x.numpy(), 'stats': stats}
+    for it in range(2):
+        opt.zero_grad()
+        y, loss_w, frames = m(x)
+        out[f'it{it}_nframes'] = np.array(len(frames))
+        if gan:
+            lr_, fr = d(x)
+            lf_, ff = d(y)
+            losses = R.losses.total_loss(fr, lf_, ff, x, y, sample_rate=48000)
+        else:
+            l_t = torch.nn.functional.l1_loss(x, y)
+            l_f = R.losses.total_loss([[torch.ones(1)]], [torch.zeros(1)], [[torch.ones(1)]], x, y,
+                                      sample_rate=48000)['l_f']
+            losses = {'l_t': l_t, 'l_f': l_f}
+        bal.backward(losses, y, retain_graph=True)
+        loss_w.backward()
+        opt.step()
+        for k, v in losses.items():
+            out[f'it{it}_{k}'] = v.detach().numpy()
+        out[f'it{it}_loss_w'] = loss_w.detach().numpy()
+        out[f'it{it}_y'] = y.detach().numpy()
+        if gan:
+            optd.zero_grad()
+            lr2, _ = d(x)
+            lf2, _ = d(y.detach())
+            ld = R.losses.disc_loss(lr2, lf2)
+            ld.backward()
+            optd.step()
+            out[f'it{it}_l_d'] = ld.detach().numpy()
+    for k, v in m.state_dict().items():
+        if v.dtype == torch.float32:
+            out['p/' + k] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+    if gan:
+        for k, v in d.state_dict().items():
+            out['d/' + k] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+    return out
+
+
+def g9():
+    out = {}
+    for gan in (False, True):
+        o = one_step_48k(gan)
+        out.update({('gan/' if gan else 'gen/') + k: v for k, v in o.items()})
+    save('g9_step48k.npz', **out)
+
+
 def g8():
     p = torch.nn.Parameter(torch.zeros(1))
     opt = torch.optim.Adam([p], lr=3e-4)
@@ -380,7 +453,7 @@ def g8():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9']
     for w in which:
         torch.manual_seed(0)
         globals()[w]()

@@ -1,0 +1,177 @@
+"""GPU parity of the config-5 path (48 kHz stereo, non-causal, time_group_norm, segmented with
+linear overlap-add) against the reference-generated g9 fixture and the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import encodec_oracle as O
+from fixtures import load, T, model_state, disc_state, codebooks_from_stats, cfg48k
+from synth import synth_wave, rng
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def rel(a, b):
+    a = a.detach().double().cpu() if torch.is_tensor(a) else torch.as_tensor(a, dtype=torch.float64)
+    b = b.detach().double().cpu() if torch.is_tensor(b) else torch.as_tensor(b, dtype=torch.float64)
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+def build48k(d, pre):
+    from encx.model import EncodecModel
+    cfg = cfg48k()
+    m = EncodecModel._get_model([3.0], 48000, 2, causal=False, model_norm='time_group_norm',
+                                audio_normalize=True, segment=0.1)
+    p = model_state(cfg, 91)
+    cbs = codebooks_from_stats(d[pre + 'stats'], 93, 2, cfg.n_q)
+    sd = dict(p)
+    for i, cb in enumerate(cbs):
+        for k, v in cb.items():
+            sd[f'quantizer.vq.layers.{i}._codebook.{k}'] = v
+    m.load_state_dict(sd)
+    return m.to(DEV), p, cbs, cfg
+
+
+@pytest.mark.parametrize('gan', [False, True])
+def test_train_step_48k_fixture(gan):
+    """Two train steps of the 48 kHz stereo model (two segments, 4800 + 48 samples) against
+    the reference's losses and post-Adam parameter checksums (g9)."""
+    from encx.train import Trainer
+    d = load('g9_step48k.npz')
+    pre = 'gan/' if gan else 'gen/'
+    m, p, cbs, cfg = build48k(d, pre)
+    disc = None
+    weights = {'l_t': 0.1, 'l_f': 1}
+    if gan:
+        from encx.msstftd import MultiScaleSTFTDiscriminator
+        disc = MultiScaleSTFTDiscriminator(filters=32, in_channels=2, out_channels=2)
+        missing, unexpected = disc.load_state_dict(disc_state(94, 2, 2), strict=False)
+        assert not unexpected and all(k.endswith('spec_transform.window') for k in missing)
+        disc = disc.to(DEV)
+        weights = {'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4}
+    tr = Trainer(m, disc, lr=1e-4, disc_lr=1e-4, scheduler=False, weights=weights, sample_rate=48000)
+    x = T(d[pre + 'x']).to(DEV)
+    for it in range(2):
+        out = tr.step(x)
+        for k in weights:
+            np.testing.assert_allclose(float(out[k]), float(d[f'{pre}it{it}_{k}'].reshape(-1)[0]), rtol=2e-4,
+                                       err_msg=f'it{it} {k}')
+        np.testing.assert_allclose(float(out['loss_w']), float(d[f'{pre}it{it}_loss_w'].reshape(-1)[0]),
+                                   rtol=5e-3, atol=1e-6)
+        if gan:
+            np.testing.assert_allclose(float(out['l_d']), float(d[f'{pre}it{it}_l_d'].reshape(-1)[0]), rtol=1e-4)
+    flips = 20 * 2 * 1e-4 * 2
+    for k, v in m.state_dict().items():
+        ref = d[pre + 'p/' + k]
+        mine = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        # codebook buffers: the second step's codes come from weights that already differ by
+        # Adam sign flips, so a near-tie code may flip; one flip moves two embed_avg rows by
+        # 0.01 * |x| (~1e-4 of the buffer's abs-sum here)
+        r = 1e-3 if '_codebook.' in k else 1e-4
+        assert abs(mine[1] - ref[1]) <= r * ref[1] + flips, (k, mine, ref)
+        assert abs(mine[0] - ref[0]) <= r * ref[1] + flips, (k, mine, ref)
+    if gan:
+        for k, v in disc.state_dict().items():
+            if k.endswith('spec_transform.window'):
+                continue
+            ref = d['gan/d/' + k]
+            mine = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+            assert abs(mine[1] - ref[1]) <= 1e-4 * ref[1] + flips, (k, mine, ref)
+            assert abs(mine[0] - ref[0]) <= 1e-5 * ref[1] + flips, (k, mine, ref)
+
+
+def test_forward_48k_vs_oracle_fp64():
+    """Element-level: the train-mode forward output of both segments overlap-added, and the
+    input grads of every parameter under a seeded output grad, vs the oracle in fp64."""
+    d = load('g9_step48k.npz')
+    m, p, cbs, cfg = build48k(d, 'gen/')
+    m.train()
+    x = T(d['gen/x']).to(DEV)
+    y, loss_w, frames = m(x)
+    assert len(frames) == 2 and frames[1][0].shape[-1] == 1  # 48 samples -> one 150 Hz frame
+    gy = T(rng(95).standard_normal(size=tuple(y.shape)).astype(np.float32)).to(DEV)
+    torch.autograd.backward([y, loss_w], [gy, torch.ones_like(loss_w)])
+    p64 = {k: v.double().requires_grad_(True) for k, v in p.items()}
+    cbs64 = [{k: v.double() for k, v in cb.items()} for cb in cbs]
+    y64, lw64, _, _, _ = O.encodec_forward_train(T(d['gen/x']).double(), p64, cbs64, cfg, 3.0)
+    torch.autograd.backward([y64, lw64], [gy.cpu().double(), torch.ones_like(lw64)])
+    assert rel(y, y64) < 1e-4, rel(y, y64)
+    worst, where = 0.0, ''
+    params = dict(m.named_parameters())
+    for k, v in p64.items():
+        e = rel(params[k].grad, v.grad)
+        if e > worst:
+            worst, where = e, k
+    print(f'worst grad rel err {worst:.3e} at {where}')
+    assert worst < 1e-3, (worst, where)
+
+
+@pytest.mark.parametrize('B,C,T_,tl,tr', [(2, 32, 4800, 0, 0), (3, 64, 37, 0, 0), (1, 512, 1, 0, 0),
+                                          (32, 32, 48000, 0, 0), (2, 256, 128, 4, 4), (3, 64, 2404, 2, 2)])
+def test_group_norm_vs_torch_fp64(B, C, T_, tl, tr):
+    """GroupNorm(1, C) forward and backward (x, gamma, beta) vs torch in fp64, incl. T = 1
+    (the second segment's LSTM-rate layers), the full config-5 stage-1 size, and the trimmed
+    window of a non-causal ConvTranspose1d (norm over the full output, then trim)."""
+    from encx import ops
+    g = rng(B * 1000 + C + T_)
+    x = g.standard_normal(size=(B, C, T_)).astype(np.float32) * 0.3 + 0.1
+    gam = g.uniform(0.5, 1.5, size=C).astype(np.float32)
+    bet = g.uniform(-0.2, 0.2, size=C).astype(np.float32)
+    dy = g.standard_normal(size=(B, C, T_)).astype(np.float32)
+    xg = T(x).to(DEV).requires_grad_(True)
+    gg = T(gam).to(DEV).requires_grad_(True)
+    bg = T(bet).to(DEV).requires_grad_(True)
+    dy = dy[..., tl:T_ - tr]
+    y = ops.group_norm(xg, gg, bg, 1e-5, tl, tr)
+    y.backward(T(dy).to(DEV))
+    x64 = T(x).double().requires_grad_(True)
+    g64 = T(gam).double().requires_grad_(True)
+    b64 = T(bet).double().requires_grad_(True)
+    y64 = F.group_norm(x64, 1, g64, b64, 1e-5)[..., tl:T_ - tr]
+    y64.backward(T(dy).double())
+    assert rel(y, y64) < 1e-5, rel(y, y64)
+    assert rel(xg.grad, x64.grad) < 1e-4, rel(xg.grad, x64.grad)
+    assert rel(gg.grad, g64.grad) < 1e-5
+    assert rel(bg.grad, b64.grad) < 1e-5
+
+
+@pytest.mark.parametrize('lens,stride', [((48000, 640), 47520), ((4800, 320), 4752), ((100, 100, 37), 80)])
+def test_overlap_add_vs_oracle(lens, stride):
+    """utils.py:22-61 forward and its backward (autograd of the oracle restatement)."""
+    from encx import ops
+    g = rng(sum(lens))
+    fr = [g.standard_normal(size=(2, 2, L)).astype(np.float32) for L in lens]
+    fg = [T(f).to(DEV).requires_grad_(True) for f in fr]
+    out = ops.linear_overlap_add(fg, stride)
+    dout = g.standard_normal(size=tuple(out.shape)).astype(np.float32)
+    out.backward(T(dout).to(DEV))
+    f64 = [T(f).double().requires_grad_(True) for f in fr]
+    o64 = O.linear_overlap_add(f64, stride)
+    o64.backward(T(dout).double())
+    # fp32 triangle weights (j + 1) / (L0 + 1) against fp64 linspace: a few ulp
+    assert rel(out, o64) < 1e-5, rel(out, o64)
+    for a, b in zip(fg, f64):
+        assert rel(a.grad, b.grad) < 1e-5
+
+
+def test_full_size_48k_step_runs():
+    """Config-5 shapes at a reduced batch: 1 s stereo 48 kHz clips -> two segments (48000 +
+    480), n_q 16, GroupNorm everywhere, the stereo disc; losses finite after 2 steps."""
+    from encx.model import EncodecModel
+    from encx.msstftd import MultiScaleSTFTDiscriminator
+    from encx.train import Trainer
+    torch.manual_seed(0)
+    m = EncodecModel._get_model([24.0], 48000, 2, causal=False, model_norm='time_group_norm',
+                                audio_normalize=True, segment=1.0).to(DEV)
+    disc = MultiScaleSTFTDiscriminator(filters=32, in_channels=2, out_channels=2).to(DEV)
+    tr = Trainer(m, disc, lr=1e-4, disc_lr=1e-4, weights={'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4},
+                 sample_rate=48000, warmup_iter=10)
+    x = T(synth_wave((4, 2, 48000), 96)).to(DEV)
+    for _ in range(2):
+        out = tr.step(x)
+        vals = {k: float(v) for k, v in out.items()}
+        assert all(np.isfinite(v) for v in vals.values()), vals
+    assert m.quantizer.n_q == 16
+    assert all(float(m.quantizer.vq.layers[i]._codebook.inited) == 1.0 for i in range(16))

@@ -236,6 +236,65 @@ def test_oracle_train_step_fixture(gan):
                                        d['gan/d/' + k], rtol=2e-4, atol=2e-5)
 
 
+# --------------------------------------------------------------------------- G9 48 kHz stereo
+@pytest.mark.parametrize('gan', [False, True])
+def test_oracle_train_step_48k_fixture(gan):
+    """Config-5 model shape: 48 kHz stereo, non-causal, GroupNorm, two segments overlap-added
+    (model.py:122-181, utils.py:22-61); mel losses at 48 kHz; stereo discriminator."""
+    from fixtures import cfg48k
+    d = load('g9_step48k.npz')
+    pre = 'gan/' if gan else 'gen/'
+    cfg = cfg48k()
+    assert cfg.n_q == 2 and cfg.frame_rate == 150
+    assert len(O.segments(cfg, 4800)) == int(d[pre + 'it0_nframes']) == 2
+    p = model_state(cfg, 91)
+    cbs = codebooks_from_stats(d[pre + 'stats'], 93, 2, cfg.n_q)
+    dp = disc_state(94, 2, 2) if gan else None
+    weights = {'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4} if gan else {'l_t': 0.1, 'l_f': 1}
+    bal = O.Balancer(weights)
+    st, dst = {}, {}
+    x = T(d[pre + 'x'])
+    for it in range(2):
+        out = O.train_step(x, p, cbs, cfg, 3.0, bal, st, 1e-4, disc_p=dp, disc_adam_state=dst, disc_lr=1e-4)
+        for k in weights:
+            np.testing.assert_allclose(out[k], float(d[f'{pre}it{it}_{k}'].reshape(-1)[0]), rtol=2e-4)
+        np.testing.assert_allclose(out['loss_w'], float(d[f'{pre}it{it}_loss_w'].reshape(-1)[0]), rtol=2e-3, atol=1e-7)
+        if gan:
+            np.testing.assert_allclose(out['l_d'], float(d[f'{pre}it{it}_l_d'].reshape(-1)[0]), rtol=1e-5)
+    # Adam's first steps move each weight by ~lr * sign(g): a weight whose grad is ~0 can flip
+    # sign under fp reordering (2 lr per flip), so the signed sums get a few flips of slack
+    flips = 4 * 2 * 1e-4 * 2
+    for k in p:
+        ref = d[pre + 'p/' + k]
+        v = p[k].double()
+        assert abs(v.sum().item() - ref[0]) <= 2e-4 * abs(ref[0]) + flips, (k, v.sum().item(), ref)
+        np.testing.assert_allclose(v.abs().sum().item(), ref[1], rtol=2e-4, atol=2e-5, err_msg=k)
+    for i in range(2):
+        for b in ('cluster_size', 'embed', 'embed_avg'):
+            ref = d[f'{pre}p/quantizer.vq.layers.{i}._codebook.{b}']
+            v = cbs[i][b].double()
+            np.testing.assert_allclose([v.sum().item(), v.abs().sum().item()], ref, rtol=1e-4, atol=1e-4)
+    if gan:
+        for k in dp:
+            v = dp[k].double()
+            assert abs(v.sum().item() - d['gan/d/' + k][0]) <= 2e-4 * abs(d['gan/d/' + k][0]) + flips, k
+            np.testing.assert_allclose(v.abs().sum().item(), d['gan/d/' + k][1], rtol=2e-4, atol=2e-5, err_msg=k)
+
+
+def test_oracle_overlap_add_matches_reference_rule():
+    """utils.py:22-61 on hand-checkable frames: a lone frame passes through; where two frames
+    overlap the weights are the first frame's triangle, normalised."""
+    f0 = torch.ones(1, 10)
+    assert torch.allclose(O.linear_overlap_add([f0], 10), f0)
+    f1 = 3 * torch.ones(1, 4)
+    out = O.linear_overlap_add([f0, f1], 8)
+    assert out.shape[-1] == 12
+    t = torch.linspace(0, 1, 12)[1:-1]
+    w = 0.5 - (t - 0.5).abs()
+    exp = torch.cat([torch.ones(8), (w[8:10] + 3 * w[:2]) / (w[8:10] + w[:2]), 3 * torch.ones(2)])
+    assert torch.allclose(out[0], exp)
+
+
 # --------------------------------------------------------------------------- G8 scheduler
 def test_oracle_scheduler_fixture():
     d = load('g8_sched.npz')
