@@ -19,6 +19,8 @@
 // CUs, so conv_fwd / conv_poly split the channel reduction (split-K) into a workspace and a
 // fixed-order reduce kernel applies the epilogue: deterministic, no float atomics.
 // Plus VALU kernels for the 1-channel ends of the stack (Cout = 1 forward, tiny wgrads).
+#include <stdlib.h>
+
 #include "common.h"
 #include "gemm.h"
 #include "prof.h"
@@ -29,7 +31,6 @@ constexpr int NT = 256;  // threads per workgroup (4 waves)
 constexpr int FLAT_T = 128;  // layers with T_out <= this run as one (b, t)-flattened GEMM
 
 // LDS staging: position lanes per channel lane for a window of `len` positions (QP | NT)
-constexpr int SPX = 5;  // window positions per thread in the forward staging (span <= SPX * NT)
 constexpr int SPXW = 3;
 constexpr int SB = 4;  // staging batch: channels (or rows) whose loads are issued before their LDS writes  // ... and in the weight-grad R window (WL <= SPXW * NT)
 ENCX_DEV int stage_lanes(int len) { return len > 128 ? NT : (len > 64 ? 128 : 64); }
@@ -45,6 +46,7 @@ struct FwdArgs {
     float* part;        // split-K partials [KS][B][Cout][Tout]
     int B, Cin, Tin, Cout, Tout, K, s, d, pl, e, mode, act;
     int epi_act, accumulate;
+    int vec;  // x rows and wf rows 16-B aligned: float4 staging loads
     int CK;   // channels per LDS chunk (even)
     int Up;   // LDS words per (ci, phase) row
     int KS;   // channel splits
@@ -60,14 +62,18 @@ ENCX_DEV void fwd_store(const FwdArgs& a, int64_t o, int co, float v) {
     a.y[o] = v;
 }
 
-// EPI = 0: bias-only epilogue (no operand loads); EPI = 1: act' source / residual / accumulate
+// Epilogue operands are compile-time (EPI bits): runtime-null operand pointers tested per
+// element compile to exec-masked branches around every load and cost ~3x on the HBM-bound
+// layers. EPI_RES: + residual; EPI_XACT: * act'(xact); EPI_ACC: + y; EPI_PART: split-K
+// partial store (no bias, no operands).
+enum { EPI_RES = 1, EPI_XACT = 2, EPI_ACC = 4, EPI_PART = 8 };
 template <int BM, int BN, int WM, int WN, int EPI>
 __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     extern __shared__ float smem[];
     const int CK = a.CK, S = a.s, Up = a.Up, K = a.K;
     float* Xs = smem;                       // [CK][S][Up]
-    float* Ws = smem + CK * S * Up;         // [K][CK][BM]
+    float* Ws = smem + ((CK * S * Up + 3) & ~3);  // [K][CK][BM], 16-B aligned
     float* Bsm = Ws + K * CK * BM;          // [BM] bias of the block's rows
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
@@ -84,62 +90,64 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
-    // staging lanes: each thread owns up to SPX window positions (their pad source and LDS slot
-    // are chunk-invariant, computed once) and walks the chunk's channels
-    const int QP = stage_lanes(span), CP = NT / QP;
-    const int qlane = tid % QP, clane = tid / QP;
-    int xm[SPX], xo[SPX];
-#pragma unroll
-    for (int k = 0; k < SPX; ++k) {
-        const int q = qlane + k * QP;
-        xo[k] = -1;
-        xm[k] = -1;
-        if (q < span) {
-            const int u = q / S, ph = q - u * S;
-            xo[k] = ph * Up + u;
-            xm[k] = pad_src(t0 * S + q, a.pl, a.Tin, a.e, a.mode);
-        }
-    }
-    constexpr int RSTEP = NT / BM;
-    const int wcol = tid % BM, wr0 = tid / BM;
-    const bool wco = co0 + wcol < a.Cout;
+    // The chunk's window of every channel row is [wb, wb + span) in input coordinates
+    // (wb = t0*S - pl), staged as 4-position items from the 4-aligned floor of wb: one float4
+    // load per interior item (VEC: rows 16-B aligned), per-element pad_src only for the items
+    // that straddle a row end. The loop is kept simple (one item per iteration): unrolled,
+    // predicated staging compiles to divergent branch ladders that cost more than the loads.
+    const int wb = t0 * S - a.pl;
+    const int ab = wb & ~3, woff = wb - ab;
+    const int nv = (woff + span + 3) >> 2;
+    const int nitems = CK * nv;
+    const int BM4 = BM / 4, nw = K * CK * BM4;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
-        // stage activated input window, phase-major; loads are issued in batches of SB
-        // channels before any LDS write so their latencies overlap
-        for (int cb = clane; cb < CK; cb += SB * CP) {
-            float v[SB][SPX];
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int cl = cb + j * CP, c = c0 + cl;
-                const bool cv = cl < CK && c < cend;
+        for (int it = tid; it < nitems; it += NT) {
+            const int cl = it / nv, vi = it - cl * nv, c = c0 + cl;
+            const int p = ab + 4 * vi;
+            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (c < cend) {
                 const float* xr = xb + (int64_t)c * a.Tin;
-#pragma unroll
-                for (int k = 0; k < SPX; ++k) v[j][k] = (cv && xm[k] >= 0) ? xr[xm[k]] : 0.f;
+                if (a.vec && p >= 0 && p + 3 < a.Tin) {
+                    v = *(const f32x4*)(xr + p);
+                } else {
+                    for (int e = 0; e < 4; ++e) {
+                        const int m = pad_src(p + e + a.pl, a.pl, a.Tin, a.e, a.mode);
+                        v[e] = m >= 0 ? xr[m] : 0.f;
+                    }
+                }
             }
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int cl = cb + j * CP;
-                if (cl >= CK) continue;
-                float* xs = Xs + cl * span;
-#pragma unroll
-                for (int k = 0; k < SPX; ++k)
-                    if (xo[k] >= 0) xs[xo[k]] = act_apply(a.act, v[j][k]);
+            float* xs = Xs + cl * span;
+            const int q0 = 4 * vi - woff;
+            if (S == 1 && q0 >= 0 && q0 + 3 < span) {
+                xs[q0] = act_apply(a.act, v[0]);
+                xs[q0 + 1] = act_apply(a.act, v[1]);
+                xs[q0 + 2] = act_apply(a.act, v[2]);
+                xs[q0 + 3] = act_apply(a.act, v[3]);
+            } else {
+                for (int e = 0; e < 4; ++e) {
+                    const int q = q0 + e;
+                    if (q >= 0 && q < span) {
+                        const int u = q / S, ph = q - u * S;
+                        xs[ph * Up + u] = act_apply(a.act, v[e]);
+                    }
+                }
             }
         }
-        // stage weights [k][ci][co]
-        for (int r0 = wr0; r0 < K * CK; r0 += SB * RSTEP) {
-            float v[SB];
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int r = r0 + j * RSTEP, k = r / CK, cl = r - k * CK, c = c0 + cl;
-                v[j] = (r < K * CK && c < cend && wco) ? a.wf[((int64_t)c * K + k) * a.Cout + co0 + wcol] : 0.f;
+        // weights [k][ci][co] from wf[ci][k][co]: BM contiguous co per row, float4 items
+        for (int it = tid; it < nw; it += NT) {
+            const int r = it / BM4, c4 = it - r * BM4, k = r / CK, cl = r - k * CK;
+            const int c = c0 + cl, co = co0 + 4 * c4;
+            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (c < cend) {
+                const float* wr = a.wf + ((int64_t)c * K + k) * a.Cout + co;
+                if (a.vec && co + 3 < a.Cout) {
+                    v = *(const f32x4*)wr;
+                } else {
+                    for (int e = 0; e < 4; ++e) v[e] = co + e < a.Cout ? wr[e] : 0.f;
+                }
             }
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int r = r0 + j * RSTEP;
-                if (r < K * CK) Ws[r * BM + wcol] = v[j];
-            }
+            *(f32x4*)(Ws + r * BM + 4 * c4) = v;
         }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
@@ -147,6 +155,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
             const int kd = k * a.d, ph = kd % S, off = kd / S;
             const float* wk = Ws + (k * CK + h) * BM + wm0 + l32;
             const float* xk = Xs + (h * S + ph) * Up + wn0 + l32 + off;
+#pragma unroll 4
             for (int cp = 0; cp < CK; cp += 2) {
                 float av[TM], bv[TN];
 #pragma unroll
@@ -160,39 +169,36 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
             }
         }
     }
-    // epilogue: bias from LDS (staged at entry); residual / act' source / accumulated y are
-    // loaded for 8 rows at a time before those rows are stored, so each group's loads overlap
+    // epilogue: bias from LDS (staged at entry); the operands of a 32 x 32 sub-tile are all
+    // loaded before its stores (y may alias them, so the compiler cannot hoist them itself)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int t = t0 + wn0 + j * 32 + (lane & 31);
+            const int64_t ob = ((int64_t)b * a.Cout + co0 + wm0 + i * 32) * a.Tout + t;
+            float e0[16], e1[16];
+            const bool tok = t < a.Tout;
 #pragma unroll
-            for (int r0 = 0; r0 < 16; r0 += 8) {
-                float e0[8], e1[8];
+            for (int r = 0; r < 16; ++r) {
+                const bool ok = tok && co0 + wm0 + i * 32 + mfma_row(r, lane) < a.Cout;
+                const int64_t o = ok ? ob + (int64_t)mfma_row(r, lane) * a.Tout : 0;
+                e0[r] = (EPI & EPI_XACT) ? a.xact[o] : 0.f;
+                e1[r] = (EPI & EPI_RES) ? a.res[o] : 0.f;
+                if (EPI & EPI_ACC) e1[r] += a.y[o];
+            }
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    e0[q] = e1[q] = 0.f;
-                    if (EPI == 0) continue;
-                    const int co = co0 + wm0 + i * 32 + mfma_row(r0 + q, lane);
-                    const bool ok = co < a.Cout && t < a.Tout && a.KS == 1;
-                    const int64_t o = ((int64_t)b * a.Cout + co) * a.Tout + t;
-                    e0[q] = (ok && a.xact) ? a.xact[o] : 0.f;
-                    e1[q] = ok ? ((a.res ? a.res[o] : 0.f) + (a.accumulate ? a.y[o] : 0.f)) : 0.f;
-                }
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int cl = wm0 + i * 32 + mfma_row(r0 + q, lane), co = co0 + cl;
-                    if (co >= a.Cout || t >= a.Tout) continue;
-                    const int64_t o = ((int64_t)b * a.Cout + co) * a.Tout + t;
-                    const float v = acc[i][j][r0 + q];
-                    if (a.KS > 1) {
-                        a.part[(int64_t)ks * a.B * a.Cout * a.Tout + o] = v;
-                    } else {
-                        float w = v + Bsm[cl];
-                        if (EPI && a.xact) w *= act_grad(a.epi_act, e0[q]);
-                        a.y[o] = w + e1[q];
-                    }
+            for (int r = 0; r < 16; ++r) {
+                const int cl = wm0 + i * 32 + mfma_row(r, lane), co = co0 + cl;
+                if (co >= a.Cout || t >= a.Tout) continue;
+                const int64_t o = ob + (int64_t)mfma_row(r, lane) * a.Tout;
+                float w = acc[i][j][r];
+                if (EPI & EPI_PART) {
+                    a.part[(int64_t)ks * a.B * a.Cout * a.Tout + o] = w;
+                } else {
+                    w += Bsm[cl];
+                    if (EPI & EPI_XACT) w *= act_grad(a.epi_act, e0[r]);
+                    a.y[o] = w + e1[r];
                 }
             }
         }
@@ -225,6 +231,7 @@ struct PolyArgs {
     int act, in_act, accumulate;
     int CK, Ub;        // chunk channels, LDS row length (BN + J - 1 [+pad])
     int KS, cps, Q;
+    int vec;           // in rows and wp rows 16-B aligned: float4 staging loads
 };
 
 ENCX_DEV void poly_store(const PolyArgs& a, int b, int o, int qpos, float v) {
@@ -246,19 +253,23 @@ ENCX_DEV void poly_store(const PolyArgs& a, int b, int o, int qpos, float v) {
     }
 }
 
-template <int BM, int BN, int WM, int WN>
+// Epilogue bits (compile-time, see conv_fwd_kernel): P_DGRAD: backward-data fold (else the
+// ConvTranspose1d store with bias and trim); P_XACT: * act'(xact); P_ACC: + out; P_PART:
+// split-K partial store.
+enum { P_DGRAD = 1, P_XACT = 2, P_ACC = 4, P_PART = 8 };
+template <int BM, int BN, int WM, int WN, int EPI>
 __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     extern __shared__ float smem[];
     const int CK = a.CK, J = a.J, Ub = a.Ub, S = a.s;
     const int M = a.Co * S;
-    float* Xs = smem;               // [CK][Ub]
-    float* As = smem + CK * Ub;     // [J][CK][BM]
-    float* Bsm = As + J * CK * BM;  // [BM] per-row bias (ConvTranspose1d mode)
+    float* Xs = smem;                               // [CK][Ub]
+    float* As = smem + ((CK * Ub + 3) & ~3);        // [J][CK][BM], 16-B aligned
+    float* Bsm = As + J * CK * BM;                  // [BM] per-row bias (ConvTranspose1d mode)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
     const int u0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-    if (tid < BM) Bsm[tid] = (a.mode == 0 && a.bias && m0 + tid < M) ? a.bias[(m0 + tid) / S] : 0.f;
+    if (tid < BM) Bsm[tid] = (!(EPI & P_DGRAD) && a.bias && m0 + tid < M) ? a.bias[(m0 + tid) / S] : 0.f;
     const int b = blockIdx.z / a.KS, ks = blockIdx.z - (blockIdx.z / a.KS) * a.KS;
     const float* ib = a.in + (int64_t)b * a.Ci * a.Tin;
     const int cbeg = ks * a.cps, cend = min(a.Ci, cbeg + a.cps);
@@ -269,59 +280,53 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
+    // input window of the tile: positions w in [0, wlen) are in[u0 - (J-1) + w] (zero outside
+    // [0, Tin)), staged as 4-position items from the 4-aligned floor (see conv_fwd_kernel)
     const int wlen = BN + J - 1;
-    const int QP = stage_lanes(wlen), CP = NT / QP;
-    const int qlane = tid % QP, clane = tid / QP;
-    int xm[2], xo[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int w = qlane + k * QP, t = u0 - (J - 1) + w;
-        xo[k] = w < wlen ? w : -1;
-        xm[k] = (t >= 0 && t < a.Tin) ? t : -1;
-    }
-    constexpr int RSTEP = NT / BM;
-    const int wcol = tid % BM, wr0 = tid / BM;
-    const bool wrow = m0 + wcol < M;
+    const int wb = u0 - (J - 1), ab = wb & ~3, woff = wb - ab;
+    const int nv = (woff + wlen + 3) >> 2, nitems = CK * nv;
+    const int BM4 = BM / 4, nw = J * CK * BM4;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
-        for (int cb = clane; cb < CK; cb += SB * CP) {
-            float v[SB][2];
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int cl = cb + j * CP, c = c0 + cl;
-                const bool cv = cl < CK && c < cend;
+        for (int it = tid; it < nitems; it += NT) {
+            const int cl = it / nv, vi = it - cl * nv, c = c0 + cl;
+            const int p = ab + 4 * vi;
+            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (c < cend) {
                 const float* ir = ib + (int64_t)c * a.Tin;
-#pragma unroll
-                for (int k = 0; k < 2; ++k) v[j][k] = (cv && xm[k] >= 0) ? ir[xm[k]] : 0.f;
+                if (a.vec && p >= 0 && p + 3 < a.Tin) {
+                    v = *(const f32x4*)(ir + p);
+                } else {
+                    for (int e = 0; e < 4; ++e) v[e] = (p + e >= 0 && p + e < a.Tin) ? ir[p + e] : 0.f;
+                }
             }
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int cl = cb + j * CP;
-                if (cl >= CK) continue;
-                float* xs = Xs + cl * Ub;
-#pragma unroll
-                for (int k = 0; k < 2; ++k)
-                    if (xo[k] >= 0) xs[xo[k]] = act_apply(a.in_act, v[j][k]);
+            float* xs = Xs + cl * Ub;
+            const int q0 = 4 * vi - woff;
+            for (int e = 0; e < 4; ++e) {
+                const int q = q0 + e;
+                if (q >= 0 && q < wlen) xs[q] = act_apply(a.in_act, v[e]);
             }
         }
-        for (int r0 = wr0; r0 < J * CK; r0 += SB * RSTEP) {
-            float v[SB];
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int r = r0 + j * RSTEP, q = r / CK, cl = r - q * CK, c = c0 + cl;
-                v[j] = (r < J * CK && c < cend && wrow) ? a.wp[((int64_t)c * J + q) * M + m0 + wcol] : 0.f;
+        for (int it = tid; it < nw; it += NT) {
+            const int r = it / BM4, c4 = it - r * BM4, q = r / CK, cl = r - q * CK;
+            const int c = c0 + cl, m = m0 + 4 * c4;
+            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (c < cend) {
+                const float* wr = a.wp + ((int64_t)c * J + q) * M + m;
+                if (a.vec && m + 3 < M) {
+                    v = *(const f32x4*)wr;
+                } else {
+                    for (int e = 0; e < 4; ++e) v[e] = m + e < M ? wr[e] : 0.f;
+                }
             }
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int r = r0 + j * RSTEP;
-                if (r < J * CK) As[r * BM + wcol] = v[j];
-            }
+            *(f32x4*)(As + r * BM + 4 * c4) = v;
         }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
         for (int q = 0; q < J; ++q) {
             const float* aq = As + (q * CK + h) * BM + wm0 + l32;
             const float* xq = Xs + h * Ub + wn0 + l32 + (J - 1) - q;
+#pragma unroll 4
             for (int cp = 0; cp < CK; cp += 2) {
                 float av[TM], bv[TN];
 #pragma unroll
@@ -340,7 +345,7 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int u = u0 + wn0 + j * 32 + (lane & 31);
-            if (a.KS > 1) {
+            if (EPI & P_PART) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
@@ -350,40 +355,40 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
                 }
                 continue;
             }
-            // mode 0 (ConvTranspose1d): bias from LDS; mode 1 (backward-data): act' source and
-            // accumulated value loaded for 8 rows at a time ahead of their stores
+            if (!(EPI & P_DGRAD)) {  // ConvTranspose1d: bias from LDS, trim
 #pragma unroll
-            for (int r0 = 0; r0 < 16; r0 += 8) {
-                float e0[8], e1[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int row = m0 + wm0 + i * 32 + mfma_row(r0 + q, lane);
-                    const int o = row / S, m = u * S + (row - o * S) - a.pl;
-                    const bool ok = a.mode == 1 && row < M && m >= 0 && m < a.Tx;
-                    const int64_t idx = ((int64_t)b * a.Co + o) * a.Tx + m;
-                    e0[q] = (ok && a.act != ENCX_ACT_NONE) ? a.xact[idx] : 0.f;
-                    e1[q] = (ok && a.accumulate) ? a.out[idx] : 0.f;
-                }
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int rl = wm0 + i * 32 + mfma_row(r0 + q, lane), row = m0 + rl;
+                for (int r = 0; r < 16; ++r) {
+                    const int rl = wm0 + i * 32 + mfma_row(r, lane), row = m0 + rl;
                     if (row >= M) continue;
-                    const int o = row / S, qpos = u * S + (row - o * S);
-                    const float v = acc[i][j][r0 + q];
-                    if (a.mode == 0) {
-                        const int p = qpos - a.trim;
-                        if (p >= 0 && p < a.Tout) a.out[((int64_t)b * a.Co + o) * a.Tout + p] = v + Bsm[rl];
-                    } else {
-                        const int m = qpos - a.pl;
-                        if (m >= 0 && m < a.Tx) {
-                            float g = v;
-                            if (a.act != ENCX_ACT_NONE) g *= act_grad(a.act, e0[q]);
-                            a.out[((int64_t)b * a.Co + o) * a.Tx + m] = g + e1[q];
-                        } else if (qpos >= 0 && qpos < a.pl + a.Tx + a.pr) {
-                            const int slot = m < 0 ? qpos : a.pl + (m - a.Tx);
-                            a.side[((int64_t)b * a.Co + o) * (a.pl + a.pr) + slot] = v;
-                        }
-                    }
+                    const int o = row / S, p = u * S + (row - o * S) - a.trim;
+                    if (p >= 0 && p < a.Tout) a.out[((int64_t)b * a.Co + o) * a.Tout + p] = acc[i][j][r] + Bsm[rl];
+                }
+                continue;
+            }
+            // backward-data: act' source / accumulated value loaded for the whole sub-tile first
+            float e0[16], e1[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                const int o = row / S, m = u * S + (row - o * S) - a.pl;
+                const bool ok = row < M && m >= 0 && m < a.Tx;
+                const int64_t idx = ok ? ((int64_t)b * a.Co + o) * a.Tx + m : 0;
+                e0[r] = (EPI & P_XACT) ? a.xact[idx] : 0.f;
+                e1[r] = (EPI & P_ACC) ? a.out[idx] : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (row >= M) continue;
+                const int o = row / S, qpos = u * S + (row - o * S), m = qpos - a.pl;
+                const float v = acc[i][j][r];
+                if (m >= 0 && m < a.Tx) {
+                    float g = v;
+                    if (EPI & P_XACT) g *= act_grad(a.act, e0[r]);
+                    a.out[((int64_t)b * a.Co + o) * a.Tx + m] = g + e1[r];
+                } else if (qpos >= 0 && qpos < a.pl + a.Tx + a.pr) {
+                    const int slot = m < 0 ? qpos : a.pl + (m - a.Tx);
+                    a.side[((int64_t)b * a.Co + o) * (a.pl + a.pr) + slot] = v;
                 }
             }
         }
@@ -843,20 +848,38 @@ static PolyPlan plan_poly(int64_t B, int64_t Ci, int64_t M, int64_t ncols, int64
 
 // ------------------------------------------------------------------------- launch helpers
 template <int BM, int BN, int WM, int WN>
-void launch_fwd(const FwdArgs& a, hipStream_t st) {
+void launch_fwd(FwdArgs a, hipStream_t st) {
     dim3 grid(cdiv(a.Tout, BN), cdiv(a.Cout, BM), a.B * a.KS);
-    size_t lds = (size_t)(a.CK * a.s * a.Up + a.K * a.CK * BM + BM) * sizeof(float);
-    if (a.KS == 1 && (a.xact || a.res || a.accumulate))
-        hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, 1>), grid, dim3(NT), lds, st, a);
-    else
-        hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, 0>), grid, dim3(NT), lds, st, a);
+    size_t lds = (size_t)(((a.CK * a.s * a.Up + 3) & ~3) + a.K * a.CK * BM + BM) * sizeof(float);
+    a.vec = (a.Tin % 4 == 0) && (a.Cout % 4 == 0) && ((uintptr_t)a.x % 16 == 0) && ((uintptr_t)a.wf % 16 == 0);
+    const int epi = a.KS > 1 ? EPI_PART
+                             : ((a.res ? EPI_RES : 0) | (a.xact ? EPI_XACT : 0) | (a.accumulate ? EPI_ACC : 0));
+#define ENCX_FWD_EPI(E) \
+    case E: hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, E>), grid, dim3(NT), lds, st, a); break
+    switch (epi) {
+        ENCX_FWD_EPI(0); ENCX_FWD_EPI(1); ENCX_FWD_EPI(2); ENCX_FWD_EPI(3); ENCX_FWD_EPI(4);
+        ENCX_FWD_EPI(5); ENCX_FWD_EPI(6); ENCX_FWD_EPI(7); ENCX_FWD_EPI(8);
+    }
+#undef ENCX_FWD_EPI
 }
 
 template <int BM, int BN, int WM, int WN>
-void launch_poly(const PolyArgs& a, int ncols, hipStream_t st) {
+void launch_poly(PolyArgs a, int ncols, hipStream_t st) {
     dim3 grid(cdiv(ncols, BN), cdiv((int64_t)a.Co * a.s, BM), a.B * a.KS);
-    size_t lds = (size_t)(a.CK * a.Ub + a.J * a.CK * BM + BM) * sizeof(float);
-    hipLaunchKernelGGL((conv_poly_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    size_t lds = (size_t)(((a.CK * a.Ub + 3) & ~3) + a.J * a.CK * BM + BM) * sizeof(float);
+    a.vec = (a.Tin % 4 == 0) && ((a.Co * a.s) % 4 == 0) && ((uintptr_t)a.in % 16 == 0) &&
+            ((uintptr_t)a.wp % 16 == 0);
+    int epi;
+    if (a.KS > 1) epi = P_PART;
+    else if (a.mode == 0) epi = 0;
+    else epi = P_DGRAD | (a.act != ENCX_ACT_NONE ? P_XACT : 0) | (a.accumulate ? P_ACC : 0);
+#define ENCX_POLY_EPI(E) \
+    case E: hipLaunchKernelGGL((conv_poly_kernel<BM, BN, WM, WN, E>), grid, dim3(NT), lds, st, a); break
+    switch (epi) {
+        ENCX_POLY_EPI(0); ENCX_POLY_EPI(1); ENCX_POLY_EPI(3); ENCX_POLY_EPI(5); ENCX_POLY_EPI(7);
+        ENCX_POLY_EPI(8);
+    }
+#undef ENCX_POLY_EPI
 }
 
 static bool fwd_flat(int64_t Cout, int64_t Tout) { return Cout > 4 && Tout <= FLAT_T; }
@@ -899,13 +922,10 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
     }
     a.CK = p.CK; a.Up = p.Up; a.KS = p.KS; a.cps = p.cps; a.part = ws;
     ENCX_REQUIRE(a.KS == 1 || ws);
-    ENCX_REQUIRE(a.s * a.Up <= SPX * NT);  // staging positions per thread
     switch (p.t) {
         case T32x128: launch_fwd<32, 128, 1, 4>(a, st); break;
-        case T64x64: launch_fwd<64, 64, 2, 2>(a, st); break;
         case T64x128: launch_fwd<64, 128, 2, 2>(a, st); break;
         case T128x32: launch_fwd<128, 32, 4, 1>(a, st); break;
-        case T128x64: launch_fwd<128, 64, 2, 2>(a, st); break;
         default: launch_fwd<128, 128, 2, 2>(a, st); break;
     }
     ENCX_CHECK_LAUNCH();
@@ -949,10 +969,8 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
     ENCX_REQUIRE(a.KS == 1 || ws);
     switch (p.t) {
         case T32x128: launch_poly<32, 128, 1, 4>(a, ncols, st); break;
-        case T64x64: launch_poly<64, 64, 2, 2>(a, ncols, st); break;
         case T64x128: launch_poly<64, 128, 2, 2>(a, ncols, st); break;
         case T128x32: launch_poly<128, 32, 4, 1>(a, ncols, st); break;
-        case T128x64: launch_poly<128, 64, 2, 2>(a, ncols, st); break;
         default: launch_poly<128, 128, 2, 2>(a, ncols, st); break;
     }
     ENCX_CHECK_LAUNCH();
