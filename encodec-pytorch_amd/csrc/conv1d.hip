@@ -31,9 +31,6 @@ constexpr int NT = 256;  // threads per workgroup (4 waves)
 constexpr int FLAT_T = 128;  // layers with T_out <= this run as one (b, t)-flattened GEMM
 
 // LDS staging: position lanes per channel lane for a window of `len` positions (QP | NT)
-constexpr int SPXW = 3;
-constexpr int SB = 4;  // staging batch: channels (or rows) whose loads are issued before their LDS writes  // ... and in the weight-grad R window (WL <= SPXW * NT)
-ENCX_DEV int stage_lanes(int len) { return len > 128 ? NT : (len > 64 ? 128 : 64); }
 
 // ------------------------------------------------------------------------- conv forward
 struct FwdArgs {
@@ -434,17 +431,20 @@ struct WgArgs {
     int per_split;   // work items per split
     int WLp;         // LDS row length of the R window
     int NCmax;       // R window rows
+    int vec;         // L / R rows 16-B aligned: float4 staging loads
 };
 
-// WK > 1: the WK waves share one (32*TM) x (32*TN) tile and split each chunk's t range
+// WK > 1: the WK waves share one (32*TM) x (32*TN) tile and split each chunk's t range.
+// L is staged as Ls[a][t] (row stride BT + 1: the MFMA A reads, 32 lanes down a column, hit
+// 32 banks; the staging writes run along t) and R as Rs[c][window]; both from float4 items.
 template <int BM, int BN, int WM, int WN, int WK>
 __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     static_assert(WM * WN * WK == 4, "4 waves");
     extern __shared__ float smem[];
-    const int BT = a.BT, WLp = a.WLp, K = a.K, N = a.C * a.K;
-    float* Ls = smem;              // [BT][BM]
-    float* Rs = smem + BT * BM;    // [NCmax][WLp]
+    const int BT = a.BT, BTp = BT + 1, WLp = a.WLp, K = a.K, N = a.C * a.K;
+    float* Ls = smem;              // [BM][BTp]
+    float* Rs = smem + BM * BTp;   // [NCmax][WLp]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wk = wave % WK, wmn = wave / WK;
     const int wm0 = (wmn / WN) * TM * 32, wn0 = (wmn % WN) * TN * 32;
@@ -471,60 +471,63 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     const int it_end = min(a.items, it_beg + a.per_split);
     const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
     const int tw = BT / WK;  // t per wave per chunk
-    const int lgBT = __builtin_ctz(BT);  // BT is a power of two
-    const int QP = stage_lanes(WL), CP = NT / QP;
-    const int qlane = tid % QP, clane = tid / QP;
+    const int BT4 = BT / 4, nl = BM * BT4;
+    // R window items: tc*s is a multiple of 4, so the window's offset from its aligned floor
+    // is the same for every chunk
+    const int woff = (4 - (a.pl & 3)) & 3;
+    const int nv = (woff + WL + 3) >> 2, nr = a.NCmax * nv;
     for (int it = it_beg; it < it_end; ++it) {
         const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
         const float* Lb = a.L + (int64_t)b * a.A * a.Tl;
         const float* Rb = a.R + (int64_t)b * a.C * a.Tr;
-        int rm[SPXW];
-#pragma unroll
-        for (int k = 0; k < SPXW; ++k) {
-            const int w = qlane + k * QP;
-            rm[k] = w < WL ? pad_src(tc * a.s + w, a.pl, a.Tr, a.e, a.mode) : -2;
-        }
         __syncthreads();
-        for (int i0 = tid; i0 < BT * BM; i0 += SB * NT) {
-            float v[SB];
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int i = i0 + j * NT, tl = i & (BT - 1), al = i >> lgBT;
-                const int t = tc + tl, aa = a0 + al;
-                v[j] = (i < BT * BM && t < a.Tl && aa < a.A) ? Lb[(int64_t)aa * a.Tl + t] : 0.f;
+        for (int i = tid; i < nl; i += NT) {
+            const int al = i / BT4, t = tc + 4 * (i - al * BT4), aa = a0 + al;
+            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (aa < a.A) {
+                const float* lr = Lb + (int64_t)aa * a.Tl;
+                if (a.vec && t + 3 < a.Tl) {
+                    v = *(const f32x4*)(lr + t);
+                } else {
+                    for (int e = 0; e < 4; ++e) v[e] = t + e < a.Tl ? lr[t + e] : 0.f;
+                }
             }
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int i = i0 + j * NT, tl = i & (BT - 1), al = i >> lgBT;
-                if (i < BT * BM) Ls[tl * BM + al] = act_apply(a.actL, v[j]);
-            }
+            float* ls = Ls + al * BTp + (t - tc);
+            ls[0] = act_apply(a.actL, v[0]);
+            ls[1] = act_apply(a.actL, v[1]);
+            ls[2] = act_apply(a.actL, v[2]);
+            ls[3] = act_apply(a.actL, v[3]);
         }
-        for (int cb = clane; cb < a.NCmax; cb += SB * CP) {
-            float v[SB][SPXW];
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int cr = cb + j * CP, c = c_first + cr;
-                const bool cv = cr < a.NCmax && c < a.C;
+        const int base = tc * a.s - a.pl - woff;  // input index of the first item's element 0
+        for (int i = tid; i < nr; i += NT) {
+            const int cr = i / nv, vi = i - cr * nv, c = c_first + cr;
+            const int p = base + 4 * vi;
+            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (c < a.C) {
                 const float* rr = Rb + (int64_t)c * a.Tr;
-#pragma unroll
-                for (int k = 0; k < SPXW; ++k) v[j][k] = (cv && rm[k] >= 0) ? rr[rm[k]] : 0.f;
+                if (a.vec && p >= 0 && p + 3 < a.Tr) {
+                    v = *(const f32x4*)(rr + p);
+                } else {
+                    for (int e = 0; e < 4; ++e) {
+                        const int m = pad_src(p + e + a.pl, a.pl, a.Tr, a.e, a.mode);
+                        v[e] = m >= 0 ? rr[m] : 0.f;
+                    }
+                }
             }
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int cr = cb + j * CP;
-                if (cr >= a.NCmax) continue;
-                float* rs = Rs + cr * WLp;
-#pragma unroll
-                for (int k = 0; k < SPXW; ++k)
-                    if (rm[k] != -2) rs[qlane + k * QP] = act_apply(a.actR, v[j][k]);
+            float* rs = Rs + cr * WLp;
+            const int q0 = 4 * vi - woff;
+            for (int e = 0; e < 4; ++e) {
+                const int q = q0 + e;
+                if (q >= 0 && q < WL) rs[q] = act_apply(a.actR, v[e]);
             }
         }
         __syncthreads();
+#pragma unroll 4
         for (int tp = wk * tw; tp < (wk + 1) * tw; tp += 2) {
             const int tl = tp + h;
             float av[TM], bv[TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) av[i] = Ls[tl * BM + wm0 + i * 32 + l32];
+            for (int i = 0; i < TM; ++i) av[i] = Ls[(wm0 + i * 32 + l32) * BTp + tl];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bv[j] = Rs[boff[j] + tl * a.s];
 #pragma unroll
@@ -1006,7 +1009,7 @@ static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K)
         p.kind = 1; p.BT = 64; p.BM = A <= 32 ? 32 : 64; p.BN = 32;
         p.tiles = (int)cdiv(A, p.BM);
     } else {
-        p.kind = 2; p.BT = 32;
+        p.kind = 2; p.BT = Tl >= 512 ? 64 : 32;  // short rows: less tail padding per chunk
         Tile t = (A <= 32) ? T32x128 : (A <= 64 ? T64x128 : T128x128);
         p.BM = tile_bm(t); p.BN = 128;
         p.tiles = (int)(cdiv(N, p.BN) * cdiv(A, p.BM));
@@ -1032,9 +1035,10 @@ static int wlp_for(int WL, int K) {
 }
 
 template <int BM, int BN, int WM, int WN, int WK>
-void launch_wg(const WgArgs& a, int splits, hipStream_t st) {
+void launch_wg(WgArgs a, int splits, hipStream_t st) {
     dim3 grid(cdiv((int64_t)a.C * a.K, BN), cdiv(a.A, BM), splits);
-    size_t lds = (size_t)(a.BT * BM + a.NCmax * a.WLp) * sizeof(float);
+    size_t lds = (size_t)((a.BT + 1) * BM + a.NCmax * a.WLp) * sizeof(float);
+    a.vec = (a.Tl % 4 == 0) && (a.Tr % 4 == 0) && ((uintptr_t)a.L % 16 == 0) && ((uintptr_t)a.R % 16 == 0);
     size_t red = (size_t)4 * (BM / WM / 32) * (BN / WN / 32) * 16 * 64 * sizeof(float);  // all 4 waves
     if (WK > 1 && red > lds) lds = red;
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, WK>), grid, dim3(NT), lds, st, a);
@@ -1058,7 +1062,6 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
         if (lds > 160 * 1024) return ENCX_EINVAL;
         hipLaunchKernelGGL(conv_wgrad_small_kernel, dim3(p.splits), dim3(NT), lds, st, a);
     } else {
-        if (WL > SPXW * NT) return ENCX_EINVAL;
         a.WLp = wlp_for(WL, a.K);
         a.NCmax = (int)((p.BN + a.K - 1) / a.K + 1);
         if (a.NCmax > C) a.NCmax = (int)C;
