@@ -82,4 +82,23 @@ ENCX_DEV float block_sum(float v, float* red /* >= 16 floats of LDS */) {
     return t;
 }
 
+// sum_{s < n} p[s * stride] in ascending s (bitwise the serial loop) with 8 loads in flight:
+// clamped addresses, values selected after the load. A plain `for (s) acc += p[s*stride]`
+// compiles to load / s_waitcnt vmcnt(0) / add per iteration, one memory round trip per term.
+ENCX_DEV float sum_strided(const float* p, int n, int64_t stride) {
+    float acc = 0.f;
+    for (int s0 = 0; s0 < n; s0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int s = s0 + q;
+            const float t = p[(int64_t)(s < n ? s : 0) * stride];
+            v[q] = s < n ? t : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q];
+    }
+    return acc;
+}
+
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

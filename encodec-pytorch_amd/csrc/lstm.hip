@@ -1,17 +1,30 @@
 // SLSTM (modules/lstm.py:12-28): nn.LSTM(H, H, num_layers) over the 75 latent frames + skip.
 //
-// Per layer the work splits into
-//   * the input projection Gx = X W_ih^T + b_ih + b_hh for ALL frames at once: one MFMA GEMM
-//     [B*T x H] x [H x 4H] on the generic skeleton (gemm.h);
-//   * the recurrence, one fused launch per frame: h_{t-1} W_hh^T on v_mfma_f32_16x16x4_f32
-//     (4 waves split the reduction, summed in LDS in wave order) + the gate nonlinearities +
-//     the cell update, writing h_t, c_t and the gate activations the backward needs;
-//   * backward: per frame an elementwise kernel (gate grads, cell-grad carry) and a small
-//     MFMA GEMM for the recurrent grad da_t W_hh; then three big GEMMs for dW_hh, dW_ih
-//     (+ the bias column) and dX over all frames.
-// Sequence tensors are [B][T][.] (row m = b*T + t). Gate order i, f, g, o (torch).
+// All L layers advance together as one diagonal wavefront: launch k moves layer l to frame
+// t = k - l (forward) or t = T-1-k+(L-1-l) (backward), so every layer's input for its frame
+// was produced by the previous launch. The recurrence costs T+L-1 dependent launches forward
+// and 2(T+L)-1 backward, instead of L*T and 2*L*T for layer-after-layer.
+//
+// Per step the whole gate pre-activation of a layer is one contraction over K = 2H:
+//   pre[b][j] = [x_l(b,t) | h_l(b,t-1)] . wcat_l[j] + bsum_l[j]
+// with wcat_l = [W_ih | W_hh] ([4H][2H], packed once per call by encx_lstm_pack) and x_l the
+// layer input (x transposed for layer 0, h_{l-1} above). The contraction runs on
+// v_mfma_f32_16x16x4_f32 with 8 waves splitting K, the partial tiles summed in LDS in wave
+// order, then the gates and cell update are fused in the same launch.
+//
+// Backward per step: an elementwise launch (gate grads of every active layer from the
+// recurrent and the upper layer's grads; the input grad of layer 0 for the frame finished one
+// step earlier) and one MFMA launch P_l = DA_l(t) . wcat_l over all layers, whose first H
+// columns are the grad of layer l's input at frame t (consumed by layer l-1, or dx for l = 0)
+// and whose last H columns are the recurrent grad of h_l(t-1). Weight grads are one GEMM per
+// layer over all frames afterwards: dwcat_l = sum_{b,t} DA_l^T [x_l | h_l(t-1) | 1].
+//
+// Sequence tensors are [L][B][T][.] (row m = b*T + t). Gate order i, f, g, o (torch).
+// All operand loads use clamped addresses with the value selected afterwards (no branches
+// around loads: a branch per load serialises the memory latency).
 #include "common.h"
 #include "gemm.h"
+#include "prof.h"
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
@@ -23,6 +36,8 @@ ENCX_DEV f32x4v mfma16(float a, float b, f32x4v c) {
 ENCX_DEV float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
 constexpr int UNITS = 4;  // hidden units per forward workgroup (16 gate columns)
+constexpr int FW = 8;     // waves per forward workgroup (K split)
+constexpr int BW = 4;     // waves per backward-GEMM workgroup
 
 // Operand fragments for v_mfma_f32_16x16x4_f32 over a 16-deep k group: lane (col = l&15,
 // kk = l>>4) supplies k = 16*grp + 4*kk + s for s = 0..3 in four consecutive MFMAs, so both
@@ -30,41 +45,58 @@ constexpr int UNITS = 4;  // hidden units per forward workgroup (16 gate columns
 // a permutation of the natural one; fp32 accumulate).
 ENCX_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 ENCX_DEV float at4(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
+ENCX_DEV float4 sel4(bool c, const float4& v) {
+    return make_float4(c ? v.x : 0.f, c ? v.y : 0.f, c ? v.z : 0.f, c ? v.w : 0.f);
+}
 
 // ------------------------------------------------------------------------- forward step
-// Workgroup: UNITS hidden units = 16 gate columns; 4 waves interleave the H/16 k-groups.
-// G = k-groups per wave, RT = 16-row batch tiles.
+// grid (H/UNITS, L); workgroup = UNITS hidden units (16 gate columns) of layer blockIdx.y.
+// G = k-groups per wave (2H/16 groups over FW waves), RT = 16-row batch tiles.
 template <int G, int RT>
-__global__ __launch_bounds__(256) void lstm_fwd_step(const float* Gx, const float* Whh, float* Y,
-                                                     float* C, float* Gs, int B, int T, int H, int t) {
-    __shared__ float red[4][64][17];
+__global__ __launch_bounds__(FW * 64) void lstm_fwd_wave(const float* xt, const float* wcat,
+                                                         const float* bsum, float* Y, float* Cst,
+                                                         float* Gs, int B, int T, int H, int k) {
+    const int l = blockIdx.y, t = k - l;
+    if (t < 0 || t >= T) return;
+    __shared__ float red[FW][64][17];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int u0 = blockIdx.x * UNITS;
     const int col = lane & 15, kk = lane >> 4;
-    const int NG = H >> 4;
+    const int K = 2 * H, NG = K >> 4;
+    const int64_t BTH = (int64_t)B * T * H;
+    const float* W = wcat + (int64_t)l * 4 * H * K;
+    const float* xin = l == 0 ? xt : Y + (int64_t)(l - 1) * BTH;  // layer input sequence
+    float* Yl = Y + (int64_t)l * BTH;
+    float* Cl = Cst + (int64_t)l * BTH;
+    const int tp = t > 0 ? t - 1 : 0;
     const int j = (col >> 2) * H + u0 + (col & 3);  // gate column of this lane
     // the gate phase's own operands (B*UNITS <= 256 threads), fetched before the MFMA chain
-    const int pb = tid / UNITS, pu = u0 + (tid - pb * UNITS);
-    const bool pact = tid < B * UNITS && pu < H;
+    const int pb0 = tid / UNITS, pu = u0 + (tid - pb0 * UNITS);
+    const bool pact = pb0 < B;
+    const int pb = pact ? pb0 : 0;
     const int64_t po = ((int64_t)pb * T + t) * H + pu;
-    float gxv[4] = {0.f, 0.f, 0.f, 0.f}, cpv = 0.f;
-    if (pact) {
-        const float* gx = Gx + ((int64_t)pb * T + t) * 4 * H;
+    float bias[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) gxv[g] = gx[g * H + pu];
-        if (t > 0) cpv = C[po - H];
-    }
+    for (int g = 0; g < 4; ++g) bias[g] = bsum[(int64_t)l * 4 * H + g * H + pu];
+    const float cpl = Cl[((int64_t)pb * T + tp) * H + pu];
+    const float cpv = t > 0 ? cpl : 0.f;
     float4 wv[G], hv[RT][G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        const int gi = wave + 4 * g;
-        wv[g] = gi < NG ? ld4(Whh + (int64_t)j * H + gi * 16 + 4 * kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int gi = wave + FW * g;
+        const bool okg = gi < NG;
+        const int kq = (okg ? gi : 0) * 16 + 4 * kk;  // first k of this lane's float4
+        wv[g] = sel4(okg, ld4(W + (int64_t)j * K + kq));
+        const bool rec = kq >= H;  // recurrent half: h_l(t-1), zero at t = 0
+        const float* src = rec ? Yl : xin;
+        const int ts = rec ? tp : t;
+        const int kc = rec ? kq - H : kq;
+        const bool keep = !rec || t > 0;
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
-            const int row = r * 16 + col;
-            hv[r][g] = (t > 0 && row < B && gi < NG)
-                           ? ld4(Y + ((int64_t)row * T + (t - 1)) * H + gi * 16 + 4 * kk)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            int row = r * 16 + col;
+            row = row < B ? row : B - 1;  // rows >= B compute garbage that is never read
+            hv[r][g] = sel4(keep, ld4(src + ((int64_t)row * T + ts) * H + kc));
         }
     }
     f32x4v acc[RT];
@@ -87,13 +119,16 @@ __global__ __launch_bounds__(256) void lstm_fwd_step(const float* Gx, const floa
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int cc = g * 4 + uu;
-            pre[g] = gxv[g] + (((red[0][pb][cc] + red[1][pb][cc]) + red[2][pb][cc]) + red[3][pb][cc]);
+            float s = red[0][pb][cc];
+#pragma unroll
+            for (int w = 1; w < FW; ++w) s += red[w][pb][cc];
+            pre[g] = s + bias[g];
         }
         const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanhf(pre[2]), og = sigm(pre[3]);
         const float c = fg * cpv + ig * gg;
-        C[po] = c;
-        Y[po] = og * tanhf(c);
-        float* gs = Gs + ((int64_t)pb * T + t) * 4 * H;
+        Cl[po] = c;
+        Yl[po] = og * tanhf(c);
+        float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)pb * T + t) * 4 * H;
         gs[pu] = ig;
         gs[H + pu] = fg;
         gs[2 * H + pu] = gg;
@@ -102,52 +137,80 @@ __global__ __launch_bounds__(256) void lstm_fwd_step(const float* Gx, const floa
 }
 
 // ------------------------------------------------------------------------- backward step
-// Per frame t (descending) two launches:
-//   E(t): dh = dY[t] + sum_s P[s] (the recurrent grad from frame t+1, split partials summed in
-//         a fixed order); dc = dh o (1 - tanh^2 c) + dcn; da_{i,f,g,o} -> DA[b][t]; dcn <- dc f
-//   G(t): P[s][b][u] = sum_{j in split s} DA[b][t][j] W_hh[j][u]  (MFMA 16x16x4; the 4H
-//         reduction split over blockIdx.y so the grid covers ~256 CUs instead of H/16)
-__global__ void lstm_bwd_elem(const float* dY, const float* P, int ns, float* dcn, const float* C,
-                              const float* Gs, float* DA, int B, int T, int H, int t) {
+// E(k), grid (cdiv(B*H, 256), L + [dx]): role l < L: layer l at frame t = T-1-k+(L-1-l):
+//   dh = (top layer: dout[b][u][t]; else sum_s P_{l+1}[s][b][u])      -- grad of h_l(t) from above
+//      + (t < T-1: sum_s P_l[s][b][H+u])                              -- recurrent, from frame t+1
+//   dc = dh o (1 - tanh^2 c) + dcn;  da_{i,f,g,o} -> DA_l[b][t];  dcn <- dc f
+// role L: dx[b][u][t0] (+)= sum_s P_0[s][b][u] for the frame t0 layer 0 finished in step k-1.
+// Partial sums over the split index s are added in ascending s (deterministic).
+__global__ __launch_bounds__(256) void lstm_bwd_elem(const float* dout, const float* P, int ns, float* dcn,
+                                                     const float* Cst, const float* Gs, float* DA, float* dx,
+                                                     int acc_x, int B, int T, int H, int L, int k) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= B * H) return;
+    const int role = blockIdx.y;
     const int b = p / H, u = p - b * H;
+    const int64_t N2 = 2 * H, SB = (int64_t)B * N2;
+    if (role == L) {
+        const int t0 = T - k + L - 1;
+        if (t0 < 0 || t0 >= T) return;
+        const float s = sum_strided(P + (int64_t)b * N2 + u, ns, SB);
+        const int64_t o = ((int64_t)b * H + u) * T + t0;
+        dx[o] = acc_x ? dx[o] + s : s;
+        return;
+    }
+    const int l = role, t = T - 1 - k + (L - 1 - l);
+    if (t < 0 || t >= T) return;
     const bool rec = t < T - 1;
-    float dhr = 0.f;
-    if (rec)
-        for (int s = 0; s < ns; ++s) dhr += P[(int64_t)s * B * H + p];
+    const int64_t BTH = (int64_t)B * T * H;
+    const bool top = l == L - 1;
+    // grad from above: dout for the top layer, else the upper layer's input-grad partials
+    const float dtop = dout[((int64_t)b * H + u) * T + t];
+    const float dup = sum_strided(P + (int64_t)(top ? l : l + 1) * ns * SB + (int64_t)b * N2 + u, ns, SB);
+    const float dhr = sum_strided(P + (int64_t)l * ns * SB + (int64_t)b * N2 + H + u, ns, SB);
+    const float dh = (top ? dtop : dup) + (rec ? dhr : 0.f);
     const int64_t o = ((int64_t)b * T + t) * H + u;
-    const float dh = dY[o] + dhr;
-    const float* gs = Gs + ((int64_t)b * T + t) * 4 * H;
+    const float* Cl = Cst + (int64_t)l * BTH;
+    const float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)b * T + t) * 4 * H;
     const float ig = gs[u], fg = gs[H + u], gg = gs[2 * H + u], og = gs[3 * H + u];
-    const float c = C[o], cp = t > 0 ? C[o - H] : 0.f, tc = tanhf(c);
-    const float dc = dh * og * (1.f - tc * tc) + (rec ? dcn[p] : 0.f);
-    float* da = DA + ((int64_t)b * T + t) * 4 * H;
+    const float c = Cl[o], cpl = Cl[t > 0 ? o - H : o], cp = t > 0 ? cpl : 0.f, tc = tanhf(c);
+    float* dcl = dcn + (int64_t)l * B * H;
+    const float dcv = dcl[p];
+    const float dc = dh * og * (1.f - tc * tc) + (rec ? dcv : 0.f);
+    float* da = DA + (int64_t)l * 4 * BTH + ((int64_t)b * T + t) * 4 * H;
     da[u] = dc * gg * ig * (1.f - ig);
     da[H + u] = dc * cp * fg * (1.f - fg);
     da[2 * H + u] = dc * ig * (1.f - gg * gg);
     da[3 * H + u] = dh * tc * og * (1.f - og);
-    dcn[p] = dc * fg;
+    dcl[p] = dc * fg;
 }
 
+// G(k), grid (2H/16, ns, L): P_l[s][b][n] = sum_{j in split s} DA_l[b][t][j] wcat_l[j][n] for the
+// frame t of layer l in step k (MFMA 16x16x4 over float4 operands from wcatT [2H][4H]; the 4H
+// reduction split over blockIdx.y so the grid covers the CUs, BW waves interleaving k-groups).
 template <int G, int RT>
-__global__ __launch_bounds__(256) void lstm_bwd_gemm(const float* DA, const float* WhhT, float* P, int B,
-                                                     int T, int H, int t, int gper) {
-    __shared__ float red[4][64][17];
+__global__ __launch_bounds__(BW * 64) void lstm_bwd_gemm(const float* DA, const float* wcatT, float* P,
+                                                         int B, int T, int H, int L, int k, int gper) {
+    const int l = blockIdx.z, t = T - 1 - k + (L - 1 - l);
+    if (t < 0 || t >= T) return;
+    __shared__ float red[BW][64][17];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c0 = blockIdx.x * 16, s = blockIdx.y, col = lane & 15, kk = lane >> 4;
-    const int K = 4 * H, g0 = s * gper;
+    const int K = 4 * H, N2 = 2 * H, g0 = s * gper, ns = gridDim.y;
+    const float* Wt = wcatT + (int64_t)l * N2 * K + (int64_t)(c0 + col) * K;
+    const float* D = DA + (int64_t)l * B * T * K;
     float4 wv[G], av[RT][G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        const int gl = wave + 4 * g, gi = g0 + gl;
+        const int gl = wave + BW * g;
         const bool ok = gl < gper;
-        wv[g] = ok ? ld4(WhhT + (int64_t)(c0 + col) * K + gi * 16 + 4 * kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int kq = (g0 + (ok ? gl : 0)) * 16 + 4 * kk;
+        wv[g] = sel4(ok, ld4(Wt + kq));
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
-            const int row = r * 16 + col;
-            av[r][g] = (ok && row < B) ? ld4(DA + ((int64_t)row * T + t) * K + gi * 16 + 4 * kk)
-                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            int row = r * 16 + col;
+            row = row < B ? row : B - 1;
+            av[r][g] = ld4(D + ((int64_t)row * T + t) * K + kq);
         }
     }
     f32x4v acc[RT];
@@ -164,14 +227,46 @@ __global__ __launch_bounds__(256) void lstm_bwd_gemm(const float* DA, const floa
 #pragma unroll
         for (int q = 0; q < 4; ++q) red[wave][r * 16 + kk * 4 + q][col] = acc[r][q];
     __syncthreads();
-    for (int p = tid; p < B * 16; p += 256) {
+    float* Pl = P + ((int64_t)l * ns + s) * B * N2;
+    for (int p = tid; p < B * 16; p += BW * 64) {
         const int b = p >> 4, cc = p & 15;
-        P[((int64_t)s * B + b) * H + c0 + cc] = ((red[0][b][cc] + red[1][b][cc]) + red[2][b][cc]) + red[3][b][cc];
+        float v = red[0][b][cc];
+#pragma unroll
+        for (int w = 1; w < BW; ++w) v += red[w][b][cc];
+        Pl[(int64_t)b * N2 + c0 + cc] = v;
     }
 }
 
-__global__ void transpose_kernel(const float* in, float* out, int R, int Cc) {  // out[c][r] = in[r][c]
+// ------------------------------------------------------------------------- layout kernels
+// wcat[j] = [w_ih[j] | w_hh[j]] ([4H][2H]), wcatT its transpose ([2H][4H]), bsum = b_ih + b_hh
+__global__ void lstm_pack_kernel(const float* wih, const float* whh, const float* bih, const float* bhh,
+                                 float* wcat, float* wcatT, float* bsum, int H) {
     __shared__ float tile[32][33];
+    const int n0 = blockIdx.x * 32, j0 = blockIdx.y * 32;  // n over 2H, j over 4H (both % 32 == 0)
+    const int N2 = 2 * H, K4 = 4 * H;
+    for (int i = threadIdx.y; i < 32; i += 8) {
+        const int jj = j0 + i, n = n0 + threadIdx.x;
+        const float v = n < H ? wih[(int64_t)jj * H + n] : whh[(int64_t)jj * H + n - H];
+        wcat[(int64_t)jj * N2 + n] = v;
+        tile[i][threadIdx.x] = v;
+    }
+    __syncthreads();
+    for (int i = threadIdx.y; i < 32; i += 8) {
+        const int n = n0 + i, jj = j0 + threadIdx.x;
+        wcatT[(int64_t)n * K4 + jj] = tile[threadIdx.x][i];
+    }
+    if (blockIdx.x == 0 && threadIdx.y == 0) {
+        const int jj = j0 + threadIdx.x;
+        bsum[jj] = bih[jj] + bhh[jj];
+    }
+}
+
+// out[z][c][r] = in[z][r][c]: in [R][Cc] per batch z
+__global__ void transpose_kernel(const float* in, float* out, int R, int Cc) {
+    __shared__ float tile[32][33];
+    const int64_t zo = (int64_t)blockIdx.z * R * Cc;
+    in += zo;
+    out += zo;
     const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
     for (int i = threadIdx.y; i < 32; i += 8) {
         const int r = r0 + i, c = c0 + threadIdx.x;
@@ -184,100 +279,35 @@ __global__ void transpose_kernel(const float* in, float* out, int R, int Cc) {  
     }
 }
 
-template <int G>
-static void fwd_step_rt(int RT, dim3 grid, hipStream_t st, const float* Gx, const float* Whh, float* Y,
-                        float* C, float* Gs, int B, int T, int H, int t) {
-    switch (RT) {
-        case 1: hipLaunchKernelGGL((lstm_fwd_step<G, 1>), grid, dim3(256), 0, st, Gx, Whh, Y, C, Gs, B, T, H, t); break;
-        case 2: hipLaunchKernelGGL((lstm_fwd_step<G, 2>), grid, dim3(256), 0, st, Gx, Whh, Y, C, Gs, B, T, H, t); break;
-        case 3: hipLaunchKernelGGL((lstm_fwd_step<G, 3>), grid, dim3(256), 0, st, Gx, Whh, Y, C, Gs, B, T, H, t); break;
-        default: hipLaunchKernelGGL((lstm_fwd_step<G, 4>), grid, dim3(256), 0, st, Gx, Whh, Y, C, Gs, B, T, H, t); break;
-    }
-}
-static void fwd_step(int G, int RT, dim3 grid, hipStream_t st, const float* Gx, const float* Whh, float* Y,
-                     float* C, float* Gs, int B, int T, int H, int t) {
-    if (G <= 1) fwd_step_rt<1>(RT, grid, st, Gx, Whh, Y, C, Gs, B, T, H, t);
-    else if (G <= 2) fwd_step_rt<2>(RT, grid, st, Gx, Whh, Y, C, Gs, B, T, H, t);
-    else if (G <= 4) fwd_step_rt<4>(RT, grid, st, Gx, Whh, Y, C, Gs, B, T, H, t);
-    else if (G <= 8) fwd_step_rt<8>(RT, grid, st, Gx, Whh, Y, C, Gs, B, T, H, t);
-    else fwd_step_rt<16>(RT, grid, st, Gx, Whh, Y, C, Gs, B, T, H, t);
-}
-template <int G>
-static void bwd_gemm_rt(int RT, dim3 grid, hipStream_t st, const float* DA, const float* WhhT, float* P, int B,
-                        int T, int H, int t, int gper) {
-    switch (RT) {
-        case 1: hipLaunchKernelGGL((lstm_bwd_gemm<G, 1>), grid, dim3(256), 0, st, DA, WhhT, P, B, T, H, t, gper); break;
-        case 2: hipLaunchKernelGGL((lstm_bwd_gemm<G, 2>), grid, dim3(256), 0, st, DA, WhhT, P, B, T, H, t, gper); break;
-        case 3: hipLaunchKernelGGL((lstm_bwd_gemm<G, 3>), grid, dim3(256), 0, st, DA, WhhT, P, B, T, H, t, gper); break;
-        default: hipLaunchKernelGGL((lstm_bwd_gemm<G, 4>), grid, dim3(256), 0, st, DA, WhhT, P, B, T, H, t, gper); break;
-    }
-}
-static void bwd_gemm(int G, int RT, dim3 grid, hipStream_t st, const float* DA, const float* WhhT, float* P, int B,
-                     int T, int H, int t, int gper) {
-    if (G <= 1) bwd_gemm_rt<1>(RT, grid, st, DA, WhhT, P, B, T, H, t, gper);
-    else if (G <= 2) bwd_gemm_rt<2>(RT, grid, st, DA, WhhT, P, B, T, H, t, gper);
-    else if (G <= 4) bwd_gemm_rt<4>(RT, grid, st, DA, WhhT, P, B, T, H, t, gper);
-    else bwd_gemm_rt<8>(RT, grid, st, DA, WhhT, P, B, T, H, t, gper);
-}
-// k-splits of the recurrent backward GEMM: <= 8, dividing the H/4 k-groups, >= 4 groups each
-static int bwd_splits(int64_t H) {
-    const int groups = (int)(H / 4);
-    int ns = groups / 4 < 8 ? groups / 4 : 8;
-    if (ns < 1) ns = 1;
-    while (groups % ns) --ns;
-    return ns;
+// out[b][u][t] = Y[b][t][u] (+ x[b][u][t]) (lstm.py:24-27 skip, back to [B][C][T])
+__global__ void lstm_out_skip(const float* Y, const float* x, float* out, int B, int T, int H, int skip) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)B * H * T) return;
+    const int t = (int)(i % T);
+    const int64_t bu = i / T;
+    const int b = (int)(bu / H), u = (int)(bu - (int64_t)b * H);
+    const float y = Y[((int64_t)b * T + t) * H + u];
+    out[i] = skip ? y + x[i] : y;
 }
 
-// ------------------------------------------------------------------------- GEMM operands
-// X operand of a layer: layer 0 reads the conv layout [B][C][T]; deeper layers [B][T][H]
-struct XRows {
-    const float* p;
-    int bct, C, T;
-    ENCX_DEV float at(int m, int c) const {
-        if (bct) {
-            const int b = m / T, t = m - b * T;
-            return p[((int64_t)b * C + c) * T + t];
-        }
-        return p[(int64_t)m * C + c];
-    }
-};
-struct LdProj {  // Gx[m][j] = sum_c X(m, c) W_ih[j][c]
-    static constexpr bool A_K_FAST = false, B_N_FAST = false;
-    XRows x;
-    const float* w;
-    int C;
-    ENCX_DEV float a(int m, int k) const { return x.at(m, k); }
-    ENCX_DEV float b(int k, int n) const { return w[(int64_t)n * C + k]; }
-};
-struct EpProj {
-    float* out;
-    const float* bih;
-    const float* bhh;
-    int N;
-    ENCX_DEV void operator()(int m, int n, float v) const {
-        out[(int64_t)m * N + n] = v + (bih[n] + bhh[n]);
-    }
-};
-// dW_hh[j][u] (u < H) and db[j] (u == H): sum_m DA[m][j] * h_{t-1}(m, u)
-struct LdWhh {
+// ------------------------------------------------------------------------- weight grads
+// dwcat_l[j][n] = sum_m DA_l[m][j] Z(m, n), Z = [x_l(m, :) | h_l(m-1, :) (0 at t = 0) | 1]
+struct LdWcat {
     static constexpr bool A_K_FAST = false, B_N_FAST = true;
     const float* DA;
-    const float* Y;
+    const float* in;
+    const float* Yl;
     int H, T;
     ENCX_DEV float a(int j, int m) const { return DA[(int64_t)m * 4 * H + j]; }
-    ENCX_DEV float b(int m, int u) const {
-        if (u == H) return 1.f;
+    ENCX_DEV float b(int m, int n) const {
+        // one load from a clamped address, the value chosen afterwards (no branch around it)
+        const bool rec = n >= H;
+        const int u = rec ? (n - H < H ? n - H : H - 1) : n;
+        const int mm = rec ? (m > 0 ? m - 1 : 0) : m;
+        const float v = (rec ? Yl : in)[(int64_t)mm * H + u];
         const int t = m % T;
-        return t > 0 ? Y[(int64_t)(m - 1) * H + u] : 0.f;
+        return n == 2 * H ? 1.f : (rec && t == 0 ? 0.f : v);
     }
-};
-struct LdWih {  // dW_ih[j][c] = sum_m DA[m][j] X(m, c)
-    static constexpr bool A_K_FAST = false, B_N_FAST = false;
-    const float* DA;
-    XRows x;
-    int H;
-    ENCX_DEV float a(int j, int m) const { return DA[(int64_t)m * 4 * H + j]; }
-    ENCX_DEV float b(int m, int c) const { return x.at(m, c); }
 };
 struct EpSlabs {  // split-K partial slabs [z][M][N]
     float* ws;
@@ -286,40 +316,17 @@ struct EpSlabs {  // split-K partial slabs [z][M][N]
         ws[((int64_t)blockIdx.z * M + m) * N + n] = v;
     }
 };
-struct LdDX {  // dX(m, c) = sum_j DA[m][j] W_ih[j][c]
-    static constexpr bool A_K_FAST = true, B_N_FAST = true;
-    const float* DA;
-    const float* w;
-    int H, C;
-    ENCX_DEV float a(int m, int j) const { return DA[(int64_t)m * 4 * H + j]; }
-    ENCX_DEV float b(int j, int c) const { return w[(int64_t)j * C + c]; }
-};
-struct EpDX {  // to [B][C][T] (+ accumulate) or [B][T][C]
-    float* out;
-    int bct, C, T, acc;
-    ENCX_DEV void operator()(int m, int c, float v) const {
-        int64_t o;
-        if (bct) {
-            const int b = m / T, t = m - b * T;
-            o = ((int64_t)b * C + c) * T + t;
-        } else {
-            o = (int64_t)m * C + c;
-        }
-        out[o] = acc ? out[o] + v : v;
-    }
-};
-
-// sum split slabs [S][M][N] into dw[M][Nw] (+= when acc); a column n == Nw (the ones column
-// of the dW_hh GEMM) is the bias grad, written to both bias vectors
-__global__ void slab_reduce(const float* ws, int S, int M, int N, int Nw, float* dw, float* db1,
-                            float* db2, int acc) {
+// sum split slabs [S][4H][2H+1] in ascending slab order into dw_ih (n < H), dw_hh (n < 2H) and
+// the bias grad (n == 2H, written to both b_ih and b_hh grads); += when acc
+__global__ void lstm_slab_reduce(const float* ws, int S, int H, float* dwi, float* dwh, float* db1, float* db2,
+                                 int acc) {
+    const int M = 4 * H, N = 2 * H + 1;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)M * N) return;
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += ws[(int64_t)z * M * N + i];
+    const float s = sum_strided(ws + i, S, (int64_t)M * N);
     const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
-    if (n < Nw) {
-        float* p = dw + (int64_t)m * Nw + n;
+    float* p = n < H ? dwi + (int64_t)m * H + n : n < 2 * H ? dwh + (int64_t)m * H + (n - H) : nullptr;
+    if (p) {
         *p = acc ? *p + s : s;
     } else {
         if (db1) db1[m] = acc ? db1[m] + s : s;
@@ -327,131 +334,148 @@ __global__ void slab_reduce(const float* ws, int S, int M, int N, int Nw, float*
     }
 }
 
-// final layer: out[b][u][t] = Y[b][t][u] + x[b][u][t] (lstm.py:24-27 skip, back to [B][C][T])
-__global__ void lstm_out_skip(const float* Y, const float* x, float* out, int B, int T, int H) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)B * H * T) return;
-    const int t = (int)(i % T);
-    const int64_t bu = i / T;
-    const int b = (int)(bu / H), u = (int)(bu - (int64_t)b * H);
-    out[i] = Y[((int64_t)b * T + t) * H + u] + x[i];
+// ------------------------------------------------------------------------- dispatch
+template <int G>
+static void fwd_rt(int RT, dim3 grid, hipStream_t st, const float* xt, const float* wcat, const float* bsum,
+                   float* Y, float* C, float* Gs, int B, int T, int H, int k) {
+    switch (RT) {
+        case 1: hipLaunchKernelGGL((lstm_fwd_wave<G, 1>), grid, dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k); break;
+        case 2: hipLaunchKernelGGL((lstm_fwd_wave<G, 2>), grid, dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k); break;
+        case 3: hipLaunchKernelGGL((lstm_fwd_wave<G, 3>), grid, dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k); break;
+        default: hipLaunchKernelGGL((lstm_fwd_wave<G, 4>), grid, dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k); break;
+    }
 }
-// dY_last[b][t][u] = dout[b][u][t]
-__global__ void lstm_dout_t(const float* dout, float* dY, int B, int T, int H) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)B * H * T) return;
-    const int t = (int)(i % T);
-    const int64_t bu = i / T;
-    const int b = (int)(bu / H), u = (int)(bu - (int64_t)b * H);
-    dY[((int64_t)b * T + t) * H + u] = dout[i];
+static void fwd_step(int G, int RT, dim3 grid, hipStream_t st, const float* xt, const float* wcat,
+                     const float* bsum, float* Y, float* C, float* Gs, int B, int T, int H, int k) {
+    if (G <= 1) fwd_rt<1>(RT, grid, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k);
+    else if (G <= 2) fwd_rt<2>(RT, grid, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k);
+    else if (G <= 4) fwd_rt<4>(RT, grid, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k);
+    else if (G <= 8) fwd_rt<8>(RT, grid, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k);
+    else fwd_rt<16>(RT, grid, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k);
+}
+template <int G>
+static void bwd_rt(int RT, dim3 grid, hipStream_t st, const float* DA, const float* wcatT, float* P, int B,
+                   int T, int H, int L, int k, int gper) {
+    switch (RT) {
+        case 1: hipLaunchKernelGGL((lstm_bwd_gemm<G, 1>), grid, dim3(BW * 64), 0, st, DA, wcatT, P, B, T, H, L, k, gper); break;
+        case 2: hipLaunchKernelGGL((lstm_bwd_gemm<G, 2>), grid, dim3(BW * 64), 0, st, DA, wcatT, P, B, T, H, L, k, gper); break;
+        case 3: hipLaunchKernelGGL((lstm_bwd_gemm<G, 3>), grid, dim3(BW * 64), 0, st, DA, wcatT, P, B, T, H, L, k, gper); break;
+        default: hipLaunchKernelGGL((lstm_bwd_gemm<G, 4>), grid, dim3(BW * 64), 0, st, DA, wcatT, P, B, T, H, L, k, gper); break;
+    }
+}
+static void bwd_gemm(int G, int RT, dim3 grid, hipStream_t st, const float* DA, const float* wcatT, float* P,
+                     int B, int T, int H, int L, int k, int gper) {
+    if (G <= 1) bwd_rt<1>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
+    else if (G <= 2) bwd_rt<2>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
+    else if (G <= 4) bwd_rt<4>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
+    else if (G <= 8) bwd_rt<8>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
+    else bwd_rt<16>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
+}
+// k-splits of the backward step GEMM (K = 4H in H/4 groups of 16): <= 4, dividing the groups,
+// >= 8 groups each
+static int bwd_splits(int64_t H) {
+    const int groups = (int)(H / 4);
+    int ns = groups / 8 < 4 ? groups / 8 : 4;
+    if (ns < 1) ns = 1;
+    while (groups % ns) --ns;
+    return ns;
+}
+static bool lstm_shape_ok(int64_t B, int64_t T, int64_t H, int64_t L) {
+    return B > 0 && B <= 64 && T > 0 && H >= 16 && (H % 16) == 0 && H <= 1024 && L >= 1 && L <= 16 &&
+           B * T * 4 * H < ((int64_t)1 << 31);
 }
 
 }  // namespace
 
 extern "C" {
 
-/* One layer forward. x: layer input ([B][C][T] if x_bct else [B][T][C]); W_ih [4H][C],
- * W_hh [4H][H]; outputs Y, Cst [B][T][H] and gate activations Gs [B][T][4H]; Gx: [B*T][4H]
- * scratch. */
-int encx_lstm_layer_fwd(const float* x, int x_bct, const float* w_ih, const float* w_hh,
-                        const float* b_ih, const float* b_hh, float* Gx, float* Y, float* Cst,
-                        float* Gs, int64_t B, int64_t T, int64_t C, int64_t H, encx_stream_t stream) {
-    ENCX_REQUIRE(x && w_ih && w_hh && b_ih && b_hh && Gx && Y && Cst && Gs);
-    ENCX_REQUIRE(B > 0 && B <= 64 && T > 0 && H > 0 && (H % 16) == 0 && H <= 1024 && C > 0);
-    hipStream_t st = (hipStream_t)stream;
-    const int M = (int)(B * T), N = (int)(4 * H);
-    int rc = gemm_launch(LdProj{XRows{x, x_bct, (int)C, (int)T}, w_ih, (int)C},
-                         EpProj{Gx, b_ih, b_hh, N}, M, N, (int)C, st);
-    if (rc) return rc;
-    const int RT = (int)cdiv(B, 16), G = (int)cdiv(H / 16, 4);
-    for (int t = 0; t < T; ++t)
-        fwd_step(G, RT, dim3((unsigned)cdiv(H, UNITS)), st, Gx, w_hh, Y, Cst, Gs, (int)B, (int)T, (int)H, t);
+int encx_lstm_pack(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, float* wcat,
+                   float* wcatT, float* bsum, int64_t H, int64_t layer, encx_stream_t stream) {
+    ENCX_REQUIRE(w_ih && w_hh && b_ih && b_hh && wcat && wcatT && bsum);
+    ENCX_REQUIRE(H >= 16 && (H % 16) == 0 && H <= 1024 && layer >= 0);
+    const int64_t wl = 8 * H * H;
+    hipLaunchKernelGGL(lstm_pack_kernel, dim3((unsigned)(2 * H / 32), (unsigned)(4 * H / 32)), dim3(32, 8), 0,
+                       (hipStream_t)stream, w_ih, w_hh, b_ih, b_hh, wcat + layer * wl, wcatT + layer * wl,
+                       bsum + layer * 4 * H, (int)H);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
 
-size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t C, int64_t H) {
-    const int M = (int)(B * T), N4 = (int)(4 * H);
-    const int s1 = gemm_slabs(M, gemm_splits(N4, (int)H + 1, M));
-    const int s2 = gemm_slabs(M, gemm_splits(N4, (int)C, M));
-    size_t a = (size_t)s1 * N4 * (H + 1), b = (size_t)s2 * N4 * C;
-    return ((a > b ? a : b) + B * H + 4 * H * H + (size_t)bwd_splits(H) * B * H) * sizeof(float);
+int encx_lstm_fwd(const float* x, const float* wcat, const float* bsum, float* xt, float* Y, float* Cst,
+                  float* Gs, float* out, int skip, int64_t B, int64_t T, int64_t H, int64_t L,
+                  encx_stream_t stream) {
+    ENCX_REQUIRE(x && wcat && bsum && xt && Y && Cst && Gs && out);
+    ENCX_REQUIRE(lstm_shape_ok(B, T, H, L));
+    hipStream_t st = (hipStream_t)stream;
+    encx_prof_scope ps(st, 2.0 * L * B * T * 4 * H * 2 * H, 4.0 * (L * 8 * H * H + B * T * H * (2 + 7 * L)),
+                       "lstm_fwd");
+    ps.tag(" H%ld L%ld T%ld", (long)H, (long)L, (long)T);
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)cdiv(T, 32), (unsigned)cdiv(H, 32), (unsigned)B),
+                       dim3(32, 8), 0, st, x, xt, (int)H, (int)T);
+    const int RT = (int)cdiv(B, 16), G = (int)cdiv(H / 8, FW);
+    const dim3 grid((unsigned)(H / UNITS), (unsigned)L);
+    for (int k = 0; k < (int)(T + L - 1); ++k)
+        fwd_step(G, RT, grid, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, k);
+    const int64_t n = B * H * T;
+    hipLaunchKernelGGL(lstm_out_skip, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, Y + (L - 1) * B * T * H, x,
+                       out, (int)B, (int)T, (int)H, skip);
+    ENCX_CHECK_LAUNCH();
+    return 0;
 }
 
-/* One layer backward. dY [B][T][H] (the grad of this layer's output sequence), states from
- * the forward; writes DA [B][T][4H] scratch, dW_ih, dW_hh, db (added to BOTH b_ih and b_hh
- * grads) with `acc_w` (1: accumulate into existing grads), dx ([B][C][T] if x_bct, then
- * accumulated when acc_x, else [B][T][C]). ws: encx_lstm_bwd_workspace bytes. */
-int encx_lstm_layer_bwd(const float* x, int x_bct, const float* w_ih, const float* w_hh,
-                        const float* Y, const float* Cst, const float* Gs, const float* dY,
-                        float* DA, float* dx, int acc_x, float* dw_ih, float* dw_hh,
-                        float* db_ih, float* db_hh, int acc_w, float* ws, int64_t B, int64_t T,
-                        int64_t C, int64_t H, encx_stream_t stream) {
-    ENCX_REQUIRE(x && w_ih && w_hh && Y && Cst && Gs && dY && DA && ws);
-    ENCX_REQUIRE(B > 0 && B <= 64 && T > 0 && H > 0 && (H % 16) == 0 && H <= 512);
+size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t L) {
+    (void)T;
+    return ((size_t)L * B * H + (size_t)L * bwd_splits(H) * B * 2 * H) * sizeof(float);
+}
+
+int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const float* Gs, float* DA, float* dx,
+                  int acc_x, float* ws, int64_t B, int64_t T, int64_t H, int64_t L, encx_stream_t stream) {
+    ENCX_REQUIRE(dout && wcatT && Cst && Gs && DA && ws);
+    ENCX_REQUIRE(lstm_shape_ok(B, T, H, L));
     hipStream_t st = (hipStream_t)stream;
-    const int M = (int)(B * T), N4 = (int)(4 * H);
+    encx_prof_scope ps(st, 2.0 * L * B * T * 4 * H * 2 * H, 4.0 * (L * 8 * H * H + B * T * H * (2 + 10 * L)),
+                       "lstm_bwd");
+    ps.tag(" H%ld L%ld T%ld", (long)H, (long)L, (long)T);
     float* dcn = ws;
-    float* whhT = ws + B * H;
-    float* P = whhT + 4 * H * H;
-    const int ns = bwd_splits(H);
-    float* slabs = P + (int64_t)ns * B * H;
-    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)cdiv(H, 32), (unsigned)cdiv(4 * H, 32)), dim3(32, 8), 0, st,
-                       w_hh, whhT, (int)(4 * H), (int)H);
-    const int RT = (int)cdiv(B, 16), gper = (int)(H / 4) / ns, G = (int)cdiv(gper, 4);
+    float* P = ws + L * B * H;
+    const int ns = bwd_splits(H), gper = (int)(H / 4) / ns, G = (int)cdiv(gper, BW), RT = (int)cdiv(B, 16);
     const int BH = (int)(B * H);
-    for (int t = (int)T - 1; t >= 0; --t) {
-        hipLaunchKernelGGL(lstm_bwd_elem, dim3((unsigned)cdiv(BH, 256)), dim3(256), 0, st, dY, P, ns, dcn, Cst, Gs,
-                           DA, (int)B, (int)T, (int)H, t);
-        if (t > 0)
-            bwd_gemm(G, RT, dim3((unsigned)(H / 16), (unsigned)ns), st, DA, whhT, P, (int)B, (int)T, (int)H, t, gper);
+    const dim3 egrid((unsigned)cdiv(BH, 256), (unsigned)(L + (dx ? 1 : 0)));
+    const dim3 ggrid((unsigned)(2 * H / 16), (unsigned)ns, (unsigned)L);
+    const int steps = (int)(T + L);
+    for (int k = 0; k < steps; ++k) {
+        hipLaunchKernelGGL(lstm_bwd_elem, egrid, dim3(256), 0, st, dout, P, ns, dcn, Cst, Gs, DA, dx, acc_x,
+                           (int)B, (int)T, (int)H, (int)L, k);
+        if (k < steps - 1) bwd_gemm(G, RT, ggrid, st, DA, wcatT, P, (int)B, (int)T, (int)H, (int)L, k, gper);
     }
-    ENCX_CHECK_LAUNCH();
-    int rc;
-    if (dw_hh) {
-        const int sp = gemm_splits(N4, (int)H + 1, M);
-        const int S = gemm_slabs(M, sp);
-        rc = gemm_launch(LdWhh{DA, Y, (int)H, (int)T}, EpSlabs{slabs, N4, (int)H + 1}, N4, (int)H + 1, M,
-                         st, sp);
-        if (rc) return rc;
-        hipLaunchKernelGGL(slab_reduce, dim3(cdiv((int64_t)N4 * (H + 1), 256)), dim3(256), 0, st, slabs,
-                           S, N4, (int)H + 1, (int)H, dw_hh, db_ih, db_hh, acc_w);
-        ENCX_CHECK_LAUNCH();
-    }
-    if (dw_ih) {
-        const int sp = gemm_splits(N4, (int)C, M);
-        const int S = gemm_slabs(M, sp);
-        rc = gemm_launch(LdWih{DA, XRows{x, x_bct, (int)C, (int)T}, (int)H}, EpSlabs{slabs, N4, (int)C},
-                         N4, (int)C, M, st, sp);
-        if (rc) return rc;
-        hipLaunchKernelGGL(slab_reduce, dim3(cdiv((int64_t)N4 * C, 256)), dim3(256), 0, st, slabs, S, N4,
-                           (int)C, (int)C, dw_ih, (float*)nullptr, (float*)nullptr, acc_w);
-        ENCX_CHECK_LAUNCH();
-    }
-    if (dx) {
-        rc = gemm_launch(LdDX{DA, w_ih, (int)H, (int)C}, EpDX{dx, x_bct, (int)C, (int)T, acc_x}, M, (int)C,
-                         N4, st);
-        if (rc) return rc;
-    }
-    return 0;
-}
-
-int encx_lstm_out_skip(const float* Y, const float* x, float* out, int64_t B, int64_t T, int64_t H,
-                       encx_stream_t stream) {
-    ENCX_REQUIRE(Y && x && out);
-    const int64_t n = B * H * T;
-    hipLaunchKernelGGL(lstm_out_skip, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, Y, x, out,
-                       (int)B, (int)T, (int)H);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
 
-int encx_lstm_dout_t(const float* dout, float* dY, int64_t B, int64_t T, int64_t H,
-                     encx_stream_t stream) {
-    ENCX_REQUIRE(dout && dY);
-    const int64_t n = B * H * T;
-    hipLaunchKernelGGL(lstm_dout_t, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, dout, dY,
-                       (int)B, (int)T, (int)H);
+size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H) {
+    const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
+    const int S = gemm_slabs(M, gemm_splits(N4, Nw, M));
+    return (size_t)S * N4 * Nw * sizeof(float);
+}
+
+int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float* dw_ih, float* dw_hh,
+                         float* db_ih, float* db_hh, int acc, float* ws, int64_t B, int64_t T, int64_t H,
+                         int64_t L, int64_t layer, encx_stream_t stream) {
+    ENCX_REQUIRE(DA && xt && Y && dw_ih && dw_hh && ws);
+    ENCX_REQUIRE(lstm_shape_ok(B, T, H, L) && layer >= 0 && layer < L);
+    hipStream_t st = (hipStream_t)stream;
+    encx_prof_scope ps(st, 2.0 * B * T * 4 * H * (2 * H + 1), 4.0 * (B * T * H * 7 + 8 * H * H), "lstm_wgrad");
+    ps.tag(" H%ld T%ld", (long)H, (long)T);
+    const int64_t BTH = B * T * H;
+    const float* in = layer == 0 ? xt : Y + (layer - 1) * BTH;
+    const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
+    const int sp = gemm_splits(N4, Nw, M);
+    const int S = gemm_slabs(M, sp);
+    int rc = gemm_launch(LdWcat{DA + layer * 4 * BTH, in, Y + layer * BTH, (int)H, (int)T}, EpSlabs{ws, N4, Nw},
+                         N4, Nw, M, st, sp);
+    if (rc) return rc;
+    hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 256)), dim3(256), 0, st, ws, S,
+                       (int)H, dw_ih, dw_hh, db_ih, db_hh, acc);
     ENCX_CHECK_LAUNCH();
     return 0;
 }

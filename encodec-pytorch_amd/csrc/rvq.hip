@@ -1,6 +1,6 @@
 // Residual vector quantizer kernels (quantization/core_vq.py).
 //
-//  rvq_argmin_mfma  EuclideanCodebook.quantize (core_vq.py:181-189). A 64-frame x 256-code tile
+//  rvq_argmin_mfma  EuclideanCodebook.quantize (core_vq.py:181-189). A 64-frame x 128-code tile
 //                   of dot products on v_mfma_f32_32x32x2_f32, then per element the reference's
 //                   own fp32 expression v = (|x|^2 - 2 x.e) + |e|^2, packed into an order-
 //                   preserving 64-bit key (dist bits << 32 | code) so that a wave min-reduction
@@ -40,80 +40,75 @@ ENCX_DEV uint64_t shfl_xor64(uint64_t v, int o) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-constexpr int AR_ROWS = 64, AR_CODES = 256, AR_DC = 32;
+// One workgroup = 64 frames x 128 codes with the whole D staged once (no chunk loop): frames
+// are loaded along t (the [B][D][T] latent is t-contiguous) into As[d][frame], codes along d
+// into Bs[d][code] (row stride 129: conflict-free transposed writes), so a workgroup does one
+// load phase, one barrier and 64 MFMA k-steps. 38 x 8 = 304 workgroups at N = 2400.
+constexpr int AR_ROWS = 64, AR_CODES = 128, AR_BS = AR_CODES + 1;
 
 __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed, uint64_t* keys,
                                                       int N, int D, int Kc) {
-    __shared__ float As[AR_DC][AR_ROWS];
-    __shared__ float Bs[AR_DC][AR_CODES + 1];
-    __shared__ float xx[AR_ROWS], ee[AR_CODES];
-    __shared__ uint64_t part[4][AR_ROWS];
+    extern __shared__ float sm[];
+    float* As = sm;                        // [D][AR_ROWS]
+    float* Bs = As + D * AR_ROWS;          // [D][AR_BS]
+    float* xx = Bs + D * AR_BS;            // [AR_ROWS]
+    float* ee = xx + AR_ROWS;              // [AR_CODES]
+    __shared__ uint64_t part[2][AR_ROWS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n0 = blockIdx.x * AR_ROWS, k0 = blockIdx.y * AR_CODES;
     const int h = lane >> 5, l32 = lane & 31;
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
-    float xs = 0.f, es = 0.f;  // running |x|^2 (tid < 64) and |e|^2 (all tids), ascending d
-    for (int d0 = 0; d0 < D; d0 += AR_DC) {
-        __syncthreads();
-        for (int i = tid; i < AR_DC * AR_ROWS; i += NT) {
-            int r = i / AR_DC, dd = i - r * AR_DC;  // d fastest: contiguous for [N][D] rows
-            int n = n0 + r, d = d0 + dd;
-            As[dd][r] = (n < N && d < D) ? x.at(n, d) : 0.f;
-        }
-        for (int i = tid; i < AR_DC * AR_CODES; i += NT) {
-            int c = i / AR_DC, dd = i - c * AR_DC;
-            int k = k0 + c, d = d0 + dd;
-            Bs[dd][c] = (k < Kc && d < D) ? embed[(int64_t)k * D + d] : 0.f;
-        }
-        __syncthreads();
-        if (tid < AR_ROWS)
-            for (int dd = 0; dd < AR_DC; ++dd) xs = fmaf(As[dd][tid], As[dd][tid], xs);
-        for (int dd = 0; dd < AR_DC; ++dd) es = fmaf(Bs[dd][tid], Bs[dd][tid], es);
-        for (int dp = 0; dp < AR_DC; dp += 2) {
-            float av[2], bv[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) av[i] = As[dp + h][i * 32 + l32];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) bv[j] = Bs[dp + h][wave * 64 + j * 32 + l32];
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
-        }
+    const int wm0 = (wave >> 1) * 32, wn0 = (wave & 1) * 64;
+    for (int i = tid; i < D * AR_ROWS; i += NT) {
+        const int d = i / AR_ROWS, r = i - d * AR_ROWS, n = n0 + r;
+        As[i] = n < N ? x.at(n, d) : 0.f;
     }
-    if (tid < AR_ROWS) xx[tid] = xs;
-    ee[tid] = es;
+    for (int i = tid; i < AR_CODES * D; i += NT) {
+        const int c = i / D, d = i - c * D, k = k0 + c;
+        Bs[d * AR_BS + c] = k < Kc ? embed[(int64_t)k * D + d] : 0.f;
+    }
     __syncthreads();
+    // |x|^2 and |e|^2 in ascending d (fmaf chain)
+    if (tid < AR_ROWS) {
+        float v = 0.f;
+        for (int d = 0; d < D; ++d) v = fmaf(As[d * AR_ROWS + tid], As[d * AR_ROWS + tid], v);
+        xx[tid] = v;
+    } else if (tid < AR_ROWS + AR_CODES) {
+        const int c = tid - AR_ROWS;
+        float v = 0.f;
+        for (int d = 0; d < D; ++d) v = fmaf(Bs[d * AR_BS + c], Bs[d * AR_BS + c], v);
+        ee[c] = v;
+    }
+    f32x16 acc[2];
+    acc[0] = acc[1] = (f32x16){0};
+    const float* ap = As + h * AR_ROWS + wm0 + l32;
+    const float* bp = Bs + h * AR_BS + wn0 + l32;
+#pragma unroll 4
+    for (int dp = 0; dp < D; dp += 2) {
+        const float av = ap[dp * AR_ROWS];
+        const float b0 = bp[dp * AR_BS], b1 = bp[dp * AR_BS + 32];
+        acc[0] = mfma32(av, b0, acc[0]);
+        acc[1] = mfma32(av, b1, acc[1]);
+    }
+    __syncthreads();  // xx / ee visible
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int r = 0; r < 16; ++r) {
+        const int row = wm0 + mfma_row(r, lane);
+        uint64_t best = ~0ull;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = i * 32 + mfma_row(r, lane);
-            uint64_t best = ~0ull;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int c = wave * 64 + j * 32 + l32;
-                const int k = k0 + c;
-                if (k < Kc) {
-                    float v = (xx[row] - 2.f * acc[i][j][r]) + ee[c];
-                    uint64_t key = ((uint64_t)ord_key(v) << 32) | (uint32_t)k;
-                    best = umin64(best, key);
-                }
+        for (int j = 0; j < 2; ++j) {
+            const int c = wn0 + j * 32 + l32, k = k0 + c;
+            if (k < Kc) {
+                const float v = (xx[row] - 2.f * acc[j][r]) + ee[c];
+                best = umin64(best, ((uint64_t)ord_key(v) << 32) | (uint32_t)k);
             }
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) best = umin64(best, shfl_xor64(best, o));
-            if (l32 == 0) part[wave][row] = best;
         }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) best = umin64(best, shfl_xor64(best, o));
+        if (l32 == 0) part[wave & 1][row] = best;
     }
     __syncthreads();
-    if (tid < AR_ROWS && n0 + tid < N) {
-        uint64_t b = umin64(umin64(part[0][tid], part[1][tid]), umin64(part[2][tid], part[3][tid]));
-        atomicMin((unsigned long long*)&keys[n0 + tid], (unsigned long long)b);
-    }
+    if (tid < AR_ROWS && n0 + tid < N)
+        atomicMin((unsigned long long*)&keys[n0 + tid], (unsigned long long)umin64(part[0][tid], part[1][tid]));
 }
 
 constexpr int DR_ROWS = 32;
@@ -321,7 +316,9 @@ int argmin_run(Rows x, const float* embed, int64_t* idx, uint64_t* keys, int N, 
                int direct, hipStream_t st) {
     hipLaunchKernelGGL(fill_u64, dim3(cdiv(N, 256)), dim3(256), 0, st, keys, ~0ull, N);
     if (!direct) {
-        hipLaunchKernelGGL(rvq_argmin_mfma, dim3(cdiv(N, AR_ROWS), cdiv(Kc, AR_CODES)), dim3(NT), 0,
+        const size_t lds = (size_t)(D * (AR_ROWS + AR_BS) + AR_ROWS + AR_CODES) * sizeof(float);
+        if (lds > 150 * 1024) return ENCX_EINVAL;
+        hipLaunchKernelGGL(rvq_argmin_mfma, dim3(cdiv(N, AR_ROWS), cdiv(Kc, AR_CODES)), dim3(NT), lds,
                            st, x, embed, keys, N, D, Kc);
     } else {
         size_t lds = (size_t)(NT * (D + 1) + DR_ROWS * D) * sizeof(float);

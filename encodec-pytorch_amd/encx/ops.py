@@ -474,8 +474,9 @@ def rvq_decode(codes, embeds):
 class LSTMFn(torch.autograd.Function):
     """SLSTM.forward (modules/lstm.py:22-28): torch.nn.LSTM(H, H, L) over [T, B, H] + skip.
 
-    Takes x in the conv layout [B][H][T] and returns the same layout; the per-layer sequences
-    live as [B][T][.] on the device. Weights per layer: (w_ih, w_hh, b_ih, b_hh)."""
+    Takes x in the conv layout [B][H][T] and returns the same layout. All L layers run as one
+    diagonal wavefront (csrc/lstm.hip); the sequences live as [L][B][T][.] on the device.
+    Weights per layer: (w_ih, w_hh, b_ih, b_hh), packed per call into [W_ih | W_hh]."""
 
     @staticmethod
     def forward(ctx, x, skip, *weights):
@@ -483,26 +484,24 @@ class LSTMFn(torch.autograd.Function):
         x = x.contiguous()
         B, H, T = x.shape
         L = len(weights) // 4
-        if B > 64 or H % 16:
-            raise NotImplementedError('encx LSTM: batch <= 64 per GPU and hidden % 16 == 0')
+        if B > 64 or H % 16 or H > 1024:
+            raise NotImplementedError('encx LSTM: batch <= 64 per GPU, hidden % 16 == 0 and <= 1024')
         st = stream()
-        gx = _f32(B * T * 4 * H, x)
-        inp, bct, states = x, 1, []
+        wcat = _f32(L * 8 * H * H, x)
+        wcatT = _f32(L * 8 * H * H, x)
+        bsum = _f32(L * 4 * H, x)
         for l in range(L):
             w_ih, w_hh, b_ih, b_hh = (w.contiguous() for w in weights[4 * l:4 * l + 4])
-            Y = torch.empty(B, T, H, device=x.device, dtype=torch.float32)
-            Cs = torch.empty_like(Y)
-            Gs = torch.empty(B, T, 4 * H, device=x.device, dtype=torch.float32)
-            call('encx_lstm_layer_fwd', ptr(inp), bct, ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh),
-                 ptr(gx), ptr(Y), ptr(Cs), ptr(Gs), B, T, H, H, st)
-            states.append((inp, bct, Y, Cs, Gs))
-            inp, bct = Y, 0
+            call('encx_lstm_pack', ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(wcat), ptr(wcatT),
+                 ptr(bsum), H, l, st)
+        xt = _f32(B * T * H, x)
+        Y = _f32(L * B * T * H, x)
+        Cs = _f32(L * B * T * H, x)
+        Gs = _f32(L * B * T * 4 * H, x)
         out = torch.empty_like(x)
-        if skip:
-            call('encx_lstm_out_skip', ptr(inp), ptr(x), ptr(out), B, T, H, st)
-        else:
-            out.copy_(inp.permute(0, 2, 1))
-        ctx.states = states
+        call('encx_lstm_fwd', ptr(x), ptr(wcat), ptr(bsum), ptr(xt), ptr(Y), ptr(Cs), ptr(Gs), ptr(out),
+             int(bool(skip)), B, T, H, L, st)
+        ctx.state = (xt, Y, Cs, Gs, wcatT)
         ctx.weights = weights
         ctx.skip = skip
         return out
@@ -511,38 +510,34 @@ class LSTMFn(torch.autograd.Function):
     def backward(ctx, dout):
         dout = dout.contiguous()
         B, H, T = dout.shape
-        weights, states = ctx.weights, ctx.states
+        weights = ctx.weights
+        xt, Y, Cs, Gs, wcatT = ctx.state
         L = len(weights) // 4
         st = stream()
-        dY = torch.empty(B, T, H, device=dout.device, dtype=torch.float32)
-        call('encx_lstm_dout_t', ptr(dout), ptr(dY), B, T, H, st)
-        need_dx = ctx.needs_input_grad[0]
-        dx = (dout.clone() if ctx.skip else torch.zeros_like(dout)) if need_dx else None
-        DA = _f32(B * T * 4 * H, dout)
-        ws = _ws(lib.encx_lstm_bwd_workspace(B, T, H, H), dout)
+        if ctx.needs_input_grad[0]:  # the skip passes dout through; the kernels add the rest
+            dx, acc_x = (dout.clone(), 1) if ctx.skip else (torch.empty_like(dout), 0)
+        else:
+            dx, acc_x = None, 0
+        DA = _f32(L * B * T * 4 * H, dout)
+        ws = _ws(lib.encx_lstm_bwd_workspace(B, T, H, L), dout)
+        call('encx_lstm_bwd', ptr(dout), ptr(wcatT), ptr(Cs), ptr(Gs), ptr(DA), ptr(dx), acc_x, ptr(ws),
+             B, T, H, L, st)
         grads = [None] * len(weights)
-        for l in reversed(range(L)):
-            inp, bct, Y, Cs, Gs = states[l]
-            w_ih, w_hh, b_ih, b_hh = weights[4 * l:4 * l + 4]
-            want_w = any(ctx.needs_input_grad[2 + 4 * l + i] for i in range(4))
-            direct = all(_direct(w) for w in (w_ih, w_hh, b_ih, b_hh))
-            if want_w and direct:
-                dws, acc_w = [w.grad for w in (w_ih, w_hh, b_ih, b_hh)], 1
-            elif want_w:
-                dws, acc_w = [torch.empty_like(w) for w in (w_ih, w_hh, b_ih, b_hh)], 0
+        wsw = None
+        for l in range(L):
+            w4 = weights[4 * l:4 * l + 4]
+            if not any(ctx.needs_input_grad[2 + 4 * l + i] for i in range(4)):
+                continue
+            if all(_direct(w) for w in w4):
+                dws, acc_w = [w.grad for w in w4], 1
+            else:
+                dws, acc_w = [torch.empty_like(w) for w in w4], 0
                 grads[4 * l:4 * l + 4] = dws
-            else:
-                dws, acc_w = [None] * 4, 0
-            if l > 0:
-                dprev = torch.empty(B, T, H, device=dout.device, dtype=torch.float32)
-                acc_x = 0
-            else:
-                dprev, acc_x = dx, 1
-            call('encx_lstm_layer_bwd', ptr(inp), bct, ptr(w_ih.contiguous()), ptr(w_hh.contiguous()),
-                 ptr(Y), ptr(Cs), ptr(Gs), ptr(dY), ptr(DA), ptr(dprev), acc_x, ptr(dws[0]),
-                 ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), acc_w, ptr(ws), B, T, H, H, st)
-            dY = dprev
-        ctx.states = None
+            if wsw is None:
+                wsw = _ws(lib.encx_lstm_bwd_weight_workspace(B, T, H), dout)
+            call('encx_lstm_bwd_weight', ptr(DA), ptr(xt), ptr(Y), ptr(dws[0]), ptr(dws[1]), ptr(dws[2]),
+                 ptr(dws[3]), acc_w, ptr(wsw), B, T, H, L, l, st)
+        ctx.state = None
         return (dx, None, *grads)
 
 

@@ -243,27 +243,31 @@ int encx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, doub
                    double beta2, double eps, int64_t step, encx_stream_t stream);
 
 /* ---- SLSTM (modules/lstm.py:12-28 -> torch.nn.LSTM(dim, dim, num_layers) + skip) ----
- * Sequence tensors are [B][T][.]; gate order i, f, g, o. B <= 64, H % 16 == 0.
- * One layer forward: x is the layer input ([B][C][T] when x_bct, else [B][T][C]); Gx is a
- * [B*T][4H] scratch; writes h_t (Y), c_t (Cst) [B][T][H] and gate activations Gs [B][T][4H]. */
-int encx_lstm_layer_fwd(const float* x, int x_bct, const float* w_ih, const float* w_hh,
-                        const float* b_ih, const float* b_hh, float* Gx, float* Y, float* Cst,
-                        float* Gs, int64_t B, int64_t T, int64_t C, int64_t H, encx_stream_t stream);
-size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t C, int64_t H);
-/* One layer backward from dY [B][T][H]: DA [B][T][4H] scratch; weight grads written (acc_w=0)
- * or added (acc_w=1), the bias grad going to both db_ih and db_hh; dx in the layout of x
- * (added when acc_x). Any of dx/dw_ih/dw_hh may be NULL to skip. */
-int encx_lstm_layer_bwd(const float* x, int x_bct, const float* w_ih, const float* w_hh,
-                        const float* Y, const float* Cst, const float* Gs, const float* dY,
-                        float* DA, float* dx, int acc_x, float* dw_ih, float* dw_hh,
-                        float* db_ih, float* db_hh, int acc_w, float* ws, int64_t B, int64_t T,
-                        int64_t C, int64_t H, encx_stream_t stream);
-/* out[b][u][t] = Y[b][t][u] + x[b][u][t]  (lstm.py:25-27 permute back + skip) */
-int encx_lstm_out_skip(const float* Y, const float* x, float* out, int64_t B, int64_t T, int64_t H,
-                       encx_stream_t stream);
-/* dY[b][t][u] = dout[b][u][t] */
-int encx_lstm_dout_t(const float* dout, float* dY, int64_t B, int64_t T, int64_t H,
-                     encx_stream_t stream);
+ * All L layers run as one diagonal wavefront (launch k advances layer l to frame k - l):
+ * T + L - 1 dependent launches forward and 2(T + L) - 1 backward. B <= 64, H % 16 == 0,
+ * H <= 1024; gate order i, f, g, o; sequence tensors are [L][B][T][.].
+ * Pack layer `layer` for the step kernels: wcat[layer] = [W_ih | W_hh] ([4H][2H]), wcatT[layer]
+ * its transpose ([2H][4H]) and bsum[layer] = b_ih + b_hh ([4H]); the buffers hold L layers. */
+int encx_lstm_pack(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, float* wcat,
+                   float* wcatT, float* bsum, int64_t H, int64_t layer, encx_stream_t stream);
+/* Forward (lstm.py:22-28): x, out [B][H][T] (conv layout), out = h_{L-1} (+ x when skip). Saves
+ * for the backward xt [B][T][H] (x transposed), Y = h and Cst = c [L][B][T][H], and the gate
+ * activations Gs [L][B][T][4H]. */
+int encx_lstm_fwd(const float* x, const float* wcat, const float* bsum, float* xt, float* Y, float* Cst,
+                  float* Gs, float* out, int skip, int64_t B, int64_t T, int64_t H, int64_t L,
+                  encx_stream_t stream);
+size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t L);
+/* Backward through time of all layers from dout [B][H][T] (the grad of the LSTM output, before
+ * the skip): the gate pre-activation grads DA [L][B][T][4H] and the input grad dx [B][H][T]
+ * (added when acc_x; NULL to skip). ws: encx_lstm_bwd_workspace bytes. */
+int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const float* Gs, float* DA, float* dx,
+                  int acc_x, float* ws, int64_t B, int64_t T, int64_t H, int64_t L, encx_stream_t stream);
+size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H);
+/* Weight grads of layer `layer` from DA: dw_ih, dw_hh [4H][H] and the bias grad (to both db_ih
+ * and db_hh; either may be NULL), written (acc = 0) or added (acc = 1). */
+int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float* dw_ih, float* dw_hh,
+                         float* db_ih, float* db_hh, int acc, float* ws, int64_t B, int64_t T, int64_t H,
+                         int64_t L, int64_t layer, encx_stream_t stream);
 
 /* ---- MS-STFT discriminator (msstftd.py:28-149) ----
  * NormConv2d (modules/conv.py:125-139) as used by DiscriminatorSTFT: input [B][Ci][T2][Fi]

@@ -296,24 +296,25 @@ def test_normalize_and_scale():
 
 
 # --------------------------------------------------------------------------- LSTM
-@pytest.mark.parametrize('B,H,Tn', [(3, 32, 7), (17, 64, 20), (32, 512, 75)])
-def test_lstm_vs_oracle(B, H, Tn):
-    """encx LSTM (csrc/lstm.hip) forward + backward against the oracle's step-by-step
-    restatement of SLSTM (modules/lstm.py:22-28) run in fp64 on the CPU."""
+@pytest.mark.parametrize('B,H,Tn,L', [(3, 32, 7, 1), (17, 64, 20, 2), (5, 48, 9, 3), (32, 512, 75, 2)])
+def test_lstm_vs_oracle(B, H, Tn, L):
+    """encx LSTM (csrc/lstm.hip, all layers as one diagonal wavefront) forward + backward
+    against the oracle's step-by-step restatement of SLSTM (modules/lstm.py:22-28) run in fp64
+    on the CPU, for 1, 2 and 3 layers."""
     from encx import ops
     gen = torch.Generator().manual_seed(B * 1000 + H)
     k = 1.0 / np.sqrt(H)
     names = ['weight_ih', 'weight_hh', 'bias_ih', 'bias_hh']
     shapes = [(4 * H, H), (4 * H, H), (4 * H,), (4 * H,)]
     p64, wts = {}, []
-    for l in range(2):
+    for l in range(L):
         for n, s in zip(names, shapes):
             w = (torch.rand(s, generator=gen, dtype=torch.float64) * 2 - 1) * k
             p64[f'm.lstm.{n}_l{l}'] = w.requires_grad_(True)
             wts.append(w.detach().float().to(DEV).requires_grad_(True))
     x64 = torch.randn(B, H, Tn, generator=gen, dtype=torch.float64).requires_grad_(True)
     r64 = torch.randn(B, H, Tn, generator=gen, dtype=torch.float64)
-    y64 = O.slstm(x64, p64, 'm', 2)
+    y64 = O.slstm(x64, p64, 'm', L)
     (y64 * r64).sum().backward()
     x = x64.detach().float().to(DEV).requires_grad_(True)
     y = ops.lstm(x, wts, skip=True)
