@@ -28,6 +28,7 @@
 namespace {
 
 constexpr int NT = 256;  // threads per workgroup (4 waves)
+constexpr int SPER = 4;  // staging items (float4) in flight per thread
 constexpr int FLAT_T = 128;  // layers with T_out <= this run as one (b, t)-flattened GEMM
 
 // LDS staging: position lanes per channel lane for a window of `len` positions (QP | NT)
@@ -99,52 +100,85 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     const int BM4 = BM / 4, nw = K * CK * BM4;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
-        for (int it = tid; it < nitems; it += NT) {
-            const int cl = it / nv, vi = it - cl * nv, c = c0 + cl;
-            const int p = ab + 4 * vi;
-            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (c < cend) {
-                const float* xr = xb + (int64_t)c * a.Tin;
-                if (a.vec && p >= 0 && p + 3 < a.Tin) {
-                    v = *(const f32x4*)(xr + p);
-                } else {
+        // SPER items per thread in flight: interior items load as float4 from a clamped address
+        // (value selected after the load), the rare items straddling a row end are patched
+        // per element afterwards, then everything goes to LDS
+        for (int it0 = 0; it0 < nitems; it0 += NT * SPER) {
+            f32x4 v[SPER];
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                const int cl = it / nv, vi = it - cl * nv, c = c0 + cl, p = ab + 4 * vi;
+                const bool ok = it < nitems && c < cend;
+                v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                if (a.vec) {
+                    const int pc = p < 0 ? 0 : (p > a.Tin - 4 ? a.Tin - 4 : p);
+                    const f32x4 t = *(const f32x4*)(xb + (int64_t)(ok ? c : cbeg) * a.Tin + pc);
+                    if (ok && p >= 0 && p + 3 < a.Tin) v[q] = t;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                const int cl = it / nv, vi = it - cl * nv, c = c0 + cl, p = ab + 4 * vi;
+                if (it < nitems && c < cend && !(a.vec && p >= 0 && p + 3 < a.Tin)) {
+                    const float* xr = xb + (int64_t)c * a.Tin;
                     for (int e = 0; e < 4; ++e) {
                         const int m = pad_src(p + e + a.pl, a.pl, a.Tin, a.e, a.mode);
-                        v[e] = m >= 0 ? xr[m] : 0.f;
+                        v[q][e] = m >= 0 ? xr[m] : 0.f;
                     }
                 }
             }
-            float* xs = Xs + cl * span;
-            const int q0 = 4 * vi - woff;
-            if (S == 1 && q0 >= 0 && q0 + 3 < span) {
-                xs[q0] = act_apply(a.act, v[0]);
-                xs[q0 + 1] = act_apply(a.act, v[1]);
-                xs[q0 + 2] = act_apply(a.act, v[2]);
-                xs[q0 + 3] = act_apply(a.act, v[3]);
-            } else {
-                for (int e = 0; e < 4; ++e) {
-                    const int q = q0 + e;
-                    if (q >= 0 && q < span) {
-                        const int u = q / S, ph = q - u * S;
-                        xs[ph * Up + u] = act_apply(a.act, v[e]);
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                if (it >= nitems) continue;
+                const int cl = it / nv, vi = it - cl * nv;
+                float* xs = Xs + cl * span;
+                const int q0 = 4 * vi - woff;
+                if (S == 1 && q0 >= 0 && q0 + 3 < span) {
+                    xs[q0] = act_apply(a.act, v[q][0]);
+                    xs[q0 + 1] = act_apply(a.act, v[q][1]);
+                    xs[q0 + 2] = act_apply(a.act, v[q][2]);
+                    xs[q0 + 3] = act_apply(a.act, v[q][3]);
+                } else {
+                    for (int e = 0; e < 4; ++e) {
+                        const int qq = q0 + e;
+                        if (qq >= 0 && qq < span) {
+                            const int u = qq / S, ph = qq - u * S;
+                            xs[ph * Up + u] = act_apply(a.act, v[q][e]);
+                        }
                     }
                 }
             }
         }
         // weights [k][ci][co] from wf[ci][k][co]: BM contiguous co per row, float4 items
-        for (int it = tid; it < nw; it += NT) {
-            const int r = it / BM4, c4 = it - r * BM4, k = r / CK, cl = r - k * CK;
-            const int c = c0 + cl, co = co0 + 4 * c4;
-            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (c < cend) {
-                const float* wr = a.wf + ((int64_t)c * K + k) * a.Cout + co;
-                if (a.vec && co + 3 < a.Cout) {
-                    v = *(const f32x4*)wr;
-                } else {
-                    for (int e = 0; e < 4; ++e) v[e] = co + e < a.Cout ? wr[e] : 0.f;
+        for (int it0 = 0; it0 < nw; it0 += NT * SPER) {
+            f32x4 v[SPER];
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                const int r = it / BM4, c4 = it - r * BM4, k = r / CK, cl = r - k * CK;
+                const int c = c0 + cl, co = co0 + 4 * c4;
+                const bool ok = it < nw && c < cend;
+                v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                if (a.vec) {
+                    const int coc = co + 3 < a.Cout ? co : a.Cout - 4;
+                    const f32x4 t = *(const f32x4*)(a.wf + ((int64_t)(ok ? c : cbeg) * K + (ok ? k : 0)) * a.Cout + coc);
+                    if (ok && co + 3 < a.Cout) v[q] = t;
+                } else if (ok) {
+                    const float* wr = a.wf + ((int64_t)c * K + k) * a.Cout + co;
+                    for (int e = 0; e < 4; ++e) v[q][e] = co + e < a.Cout ? wr[e] : 0.f;
                 }
             }
-            *(f32x4*)(Ws + r * BM + 4 * c4) = v;
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                if (it < nw) {
+                    const int r = it / BM4, c4 = it - r * BM4;
+                    *(f32x4*)(Ws + r * BM + 4 * c4) = v[q];
+                }
+            }
         }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
@@ -205,8 +239,7 @@ __global__ void conv_fwd_reduce(FwdArgs a) {
     const int64_t n = (int64_t)a.B * a.Cout * a.Tout;
     int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= n) return;
-    float v = 0.f;
-    for (int ks = 0; ks < a.KS; ++ks) v += a.part[(int64_t)ks * n + o];
+    const float v = sum_strided(a.part + o, a.KS, n);
     const int co = (int)((o / a.Tout) % a.Cout);
     fwd_store(a, o, co, v);
 }
@@ -285,38 +318,69 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
     const int BM4 = BM / 4, nw = J * CK * BM4;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
-        for (int it = tid; it < nitems; it += NT) {
-            const int cl = it / nv, vi = it - cl * nv, c = c0 + cl;
-            const int p = ab + 4 * vi;
-            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (c < cend) {
-                const float* ir = ib + (int64_t)c * a.Tin;
-                if (a.vec && p >= 0 && p + 3 < a.Tin) {
-                    v = *(const f32x4*)(ir + p);
-                } else {
-                    for (int e = 0; e < 4; ++e) v[e] = (p + e >= 0 && p + e < a.Tin) ? ir[p + e] : 0.f;
+        // batched staging as in conv_fwd_kernel: SPER float4 loads in flight per thread
+        for (int it0 = 0; it0 < nitems; it0 += NT * SPER) {
+            f32x4 v[SPER];
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                const int cl = it / nv, vi = it - cl * nv, c = c0 + cl, p = ab + 4 * vi;
+                const bool ok = it < nitems && c < cend;
+                v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                if (a.vec) {
+                    const int pc = p < 0 ? 0 : (p > a.Tin - 4 ? a.Tin - 4 : p);
+                    const f32x4 t = *(const f32x4*)(ib + (int64_t)(ok ? c : cbeg) * a.Tin + pc);
+                    if (ok && p >= 0 && p + 3 < a.Tin) v[q] = t;
                 }
             }
-            float* xs = Xs + cl * Ub;
-            const int q0 = 4 * vi - woff;
-            for (int e = 0; e < 4; ++e) {
-                const int q = q0 + e;
-                if (q >= 0 && q < wlen) xs[q] = act_apply(a.in_act, v[e]);
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                const int cl = it / nv, vi = it - cl * nv, c = c0 + cl, p = ab + 4 * vi;
+                if (it < nitems && c < cend && !(a.vec && p >= 0 && p + 3 < a.Tin)) {
+                    const float* ir = ib + (int64_t)c * a.Tin;
+                    for (int e = 0; e < 4; ++e) v[q][e] = (p + e >= 0 && p + e < a.Tin) ? ir[p + e] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                if (it >= nitems) continue;
+                const int cl = it / nv, vi = it - cl * nv;
+                float* xs = Xs + cl * Ub;
+                const int q0 = 4 * vi - woff;
+                for (int e = 0; e < 4; ++e) {
+                    const int qq = q0 + e;
+                    if (qq >= 0 && qq < wlen) xs[qq] = act_apply(a.in_act, v[q][e]);
+                }
             }
         }
-        for (int it = tid; it < nw; it += NT) {
-            const int r = it / BM4, c4 = it - r * BM4, q = r / CK, cl = r - q * CK;
-            const int c = c0 + cl, m = m0 + 4 * c4;
-            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (c < cend) {
-                const float* wr = a.wp + ((int64_t)c * J + q) * M + m;
-                if (a.vec && m + 3 < M) {
-                    v = *(const f32x4*)wr;
-                } else {
-                    for (int e = 0; e < 4; ++e) v[e] = m + e < M ? wr[e] : 0.f;
+        for (int it0 = 0; it0 < nw; it0 += NT * SPER) {
+            f32x4 v[SPER];
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                const int r = it / BM4, c4 = it - r * BM4, qj = r / CK, cl = r - qj * CK;
+                const int c = c0 + cl, m = m0 + 4 * c4;
+                const bool ok = it < nw && c < cend;
+                v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                if (a.vec) {
+                    const int mc = m + 3 < M ? m : M - 4;
+                    const f32x4 t = *(const f32x4*)(a.wp + ((int64_t)(ok ? c : cbeg) * J + (ok ? qj : 0)) * M + mc);
+                    if (ok && m + 3 < M) v[q] = t;
+                } else if (ok) {
+                    const float* wr = a.wp + ((int64_t)c * J + qj) * M + m;
+                    for (int e = 0; e < 4; ++e) v[q][e] = m + e < M ? wr[e] : 0.f;
                 }
             }
-            *(f32x4*)(As + r * BM + 4 * c4) = v;
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int it = it0 + q * NT + tid;
+                if (it < nw) {
+                    const int r = it / BM4, c4 = it - r * BM4;
+                    *(f32x4*)(As + r * BM + 4 * c4) = v[q];
+                }
+            }
         }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
@@ -395,8 +459,7 @@ __global__ void conv_poly_reduce(PolyArgs a) {
     const int64_t n = (int64_t)a.B * a.Co * a.Q;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    float v = 0.f;
-    for (int ks = 0; ks < a.KS; ++ks) v += a.part[(int64_t)ks * n + i];
+    const float v = sum_strided(a.part + i, a.KS, n);
     const int qpos = (int)(i % a.Q);
     const int64_t bo = i / a.Q;
     poly_store(a, (int)(bo / a.Co), (int)(bo % a.Co), qpos, v);
@@ -481,44 +544,80 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
         const float* Lb = a.L + (int64_t)b * a.A * a.Tl;
         const float* Rb = a.R + (int64_t)b * a.C * a.Tr;
         __syncthreads();
-        for (int i = tid; i < nl; i += NT) {
-            const int al = i / BT4, t = tc + 4 * (i - al * BT4), aa = a0 + al;
-            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (aa < a.A) {
-                const float* lr = Lb + (int64_t)aa * a.Tl;
-                if (a.vec && t + 3 < a.Tl) {
-                    v = *(const f32x4*)(lr + t);
-                } else {
-                    for (int e = 0; e < 4; ++e) v[e] = t + e < a.Tl ? lr[t + e] : 0.f;
+        // batched staging as in conv_fwd_kernel: SPER float4 loads in flight per thread
+        for (int i0 = 0; i0 < nl; i0 += NT * SPER) {
+            f32x4 v[SPER];
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int al = i / BT4, t = tc + 4 * (i - al * BT4), aa = a0 + al;
+                const bool ok = i < nl && aa < a.A;
+                v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                if (a.vec) {
+                    const int tcl = t + 3 < a.Tl ? t : a.Tl - 4;
+                    const f32x4 x = *(const f32x4*)(Lb + (int64_t)(ok ? aa : a0) * a.Tl + tcl);
+                    if (ok && t + 3 < a.Tl) v[q] = x;
                 }
             }
-            float* ls = Ls + al * BTp + (t - tc);
-            ls[0] = act_apply(a.actL, v[0]);
-            ls[1] = act_apply(a.actL, v[1]);
-            ls[2] = act_apply(a.actL, v[2]);
-            ls[3] = act_apply(a.actL, v[3]);
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int al = i / BT4, t = tc + 4 * (i - al * BT4), aa = a0 + al;
+                if (i < nl && aa < a.A && !(a.vec && t + 3 < a.Tl)) {
+                    const float* lr = Lb + (int64_t)aa * a.Tl;
+                    for (int e = 0; e < 4; ++e) v[q][e] = t + e < a.Tl ? lr[t + e] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i >= nl) continue;
+                const int al = i / BT4, t = tc + 4 * (i - al * BT4);
+                float* ls = Ls + al * BTp + (t - tc);
+                ls[0] = act_apply(a.actL, v[q][0]);
+                ls[1] = act_apply(a.actL, v[q][1]);
+                ls[2] = act_apply(a.actL, v[q][2]);
+                ls[3] = act_apply(a.actL, v[q][3]);
+            }
         }
         const int base = tc * a.s - a.pl - woff;  // input index of the first item's element 0
-        for (int i = tid; i < nr; i += NT) {
-            const int cr = i / nv, vi = i - cr * nv, c = c_first + cr;
-            const int p = base + 4 * vi;
-            f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (c < a.C) {
-                const float* rr = Rb + (int64_t)c * a.Tr;
-                if (a.vec && p >= 0 && p + 3 < a.Tr) {
-                    v = *(const f32x4*)(rr + p);
-                } else {
+        for (int i0 = 0; i0 < nr; i0 += NT * SPER) {
+            f32x4 v[SPER];
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int cr = i / nv, vi = i - cr * nv, c = c_first + cr, p = base + 4 * vi;
+                const bool ok = i < nr && c < a.C;
+                v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                if (a.vec) {
+                    const int pc = p < 0 ? 0 : (p > a.Tr - 4 ? a.Tr - 4 : p);
+                    const f32x4 x = *(const f32x4*)(Rb + (int64_t)(ok ? c : c_first) * a.Tr + pc);
+                    if (ok && p >= 0 && p + 3 < a.Tr) v[q] = x;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int cr = i / nv, vi = i - cr * nv, c = c_first + cr, p = base + 4 * vi;
+                if (i < nr && c < a.C && !(a.vec && p >= 0 && p + 3 < a.Tr)) {
+                    const float* rr = Rb + (int64_t)c * a.Tr;
                     for (int e = 0; e < 4; ++e) {
                         const int m = pad_src(p + e + a.pl, a.pl, a.Tr, a.e, a.mode);
-                        v[e] = m >= 0 ? rr[m] : 0.f;
+                        v[q][e] = m >= 0 ? rr[m] : 0.f;
                     }
                 }
             }
-            float* rs = Rs + cr * WLp;
-            const int q0 = 4 * vi - woff;
-            for (int e = 0; e < 4; ++e) {
-                const int q = q0 + e;
-                if (q >= 0 && q < WL) rs[q] = act_apply(a.actR, v[e]);
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i >= nr) continue;
+                const int cr = i / nv, vi = i - cr * nv;
+                float* rs = Rs + cr * WLp;
+                const int q0 = 4 * vi - woff;
+                for (int e = 0; e < 4; ++e) {
+                    const int qq = q0 + e;
+                    if (qq >= 0 && qq < WL) rs[qq] = act_apply(a.actR, v[q][e]);
+                }
             }
         }
         __syncthreads();
@@ -625,8 +724,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, float* dw, 
     const int sl = threadIdx.x % SL;
     const int64_t i = (int64_t)blockIdx.x * per_block + threadIdx.x / SL;
     float v = 0.f;
-    if (i < AN)
-        for (int s = sl; s < S; s += SL) v += ws[(int64_t)s * AN + i];
+    if (i < AN) v = sum_strided(ws + (int64_t)sl * AN + i, (S - sl + SL - 1) / SL, (int64_t)SL * AN);
     for (int o = SL >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (sl == 0 && i < AN) dw[i] = accumulate ? dw[i] + v : v;
 }
@@ -686,7 +784,8 @@ struct LdConvFlat {
         const int ci = k / p.K, tap = k - ci * p.K;
         const int bb = n / p.Tout, t = n - bb * p.Tout;
         const int m = pad_src(t * p.s + tap * p.d, p.pl, p.Tin, p.e, p.mode);
-        return m >= 0 ? act_apply(p.act, p.x[((int64_t)bb * p.Cin + ci) * p.Tin + m]) : 0.f;
+        const float v = p.x[((int64_t)bb * p.Cin + ci) * p.Tin + (m >= 0 ? m : 0)];  // no branch around the load
+        return m >= 0 ? act_apply(p.act, v) : 0.f;
     }
 };
 struct EpConvFlat {
@@ -726,7 +825,9 @@ struct LdPolyFlat {
     ENCX_DEV float b(int k, int n) const {
         const int i = k / p.J, q = k - i * p.J;
         const int bb = n / ncols, u = n - bb * ncols, t = u - q;
-        return (t >= 0 && t < p.Tin) ? act_apply(p.in_act, p.in[((int64_t)bb * p.Ci + i) * p.Tin + t]) : 0.f;
+        const bool in = t >= 0 && t < p.Tin;
+        const float v = p.in[((int64_t)bb * p.Ci + i) * p.Tin + (in ? t : 0)];  // no branch around the load
+        return in ? act_apply(p.in_act, v) : 0.f;
     }
 };
 struct EpPolyFlat {

@@ -23,6 +23,7 @@
 namespace {
 
 constexpr int NT = 256;
+constexpr int DPER = 8;  // staging loads in flight per thread
 
 struct C2Geo {
     int B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf;
@@ -73,23 +74,43 @@ __global__ __launch_bounds__(NT) void c2_fwd_kernel(C2Fwd a) {
     const float* xb = a.x + (int64_t)b * g.Ci * g.T2 * g.Fi;
     for (int c0 = 0; c0 < VC; c0 += CK) {
         __syncthreads();
-        for (int i = tid; i < CK * XR; i += NT) {
-            const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
-            const int vc = c0 + cl;
-            float v = 0.f;
-            if (vc < VC && rs < nr) {
-                const int ci = vc / g.KT, kt = vc - ci * g.KT;
+        // DPER loads in flight per thread from clamped addresses, values selected afterwards
+        for (int i0 = 0; i0 < CK * XR; i0 += NT * DPER) {
+            float v[DPER];
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
+                const int vc = c0 + cl, ci = vc / g.KT, kt = vc - ci * g.KT;
                 const int row = tf + rs + kt * g.dt - g.pt;
                 const int pos = (rs ? 0 : f0) * S - g.pf + w;
-                if (row >= 0 && row < g.T2 && pos >= 0 && pos < g.Fi)
-                    v = xb[((int64_t)ci * g.T2 + row) * g.Fi + pos];
+                const bool ok = i < CK * XR && vc < VC && rs < nr && row >= 0 && row < g.T2 && pos >= 0 &&
+                                pos < g.Fi;
+                const float t = xb[ok ? ((int64_t)ci * g.T2 + row) * g.Fi + pos : 0];
+                v[q] = ok ? t : 0.f;
             }
-            Xs[i] = v;
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i < CK * XR) Xs[i] = v[q];
+            }
         }
-        for (int i = tid; i < KF * CK * BM; i += NT) {
-            const int col = i % BM, r = i / BM, cl = r % CK, kf = r / CK;
-            const int vc = c0 + cl, co = co0 + col;
-            Ws[i] = (vc < VC && co < g.Co) ? a.wf[((int64_t)vc * KF + kf) * g.Co + co] : 0.f;
+        for (int i0 = 0; i0 < KF * CK * BM; i0 += NT * DPER) {
+            float v[DPER];
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int col = i % BM, r = i / BM, cl = r % CK, kf = r / CK;
+                const int vc = c0 + cl, co = co0 + col;
+                const bool ok = i < KF * CK * BM && vc < VC && co < g.Co;
+                const float t = a.wf[ok ? ((int64_t)vc * KF + kf) * g.Co + co : 0];
+                v[q] = ok ? t : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i < KF * CK * BM) Ws[i] = v[q];
+            }
         }
         __syncthreads();
         for (int kf = 0; kf < KF; ++kf) {
@@ -172,26 +193,47 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
     const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane : nullptr;
     for (int c0 = 0; c0 < VC; c0 += CK) {
         __syncthreads();
-        for (int i = tid; i < CK * XR; i += NT) {
-            const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
-            const int vc = c0 + cl;
-            float v = 0.f;
-            if (vc < VC && rs < nr) {
-                const int co = vc / g.KT, kt = vc - co * g.KT;
+        // DPER loads in flight per thread from clamped addresses (the LeakyReLU' mask source is
+        // dy itself when there is none: a uniform pointer choice, no per-element branch)
+        const float* ysrc = yab ? yab : dyb;
+        for (int i0 = 0; i0 < CK * XR; i0 += NT * DPER) {
+            float v[DPER], ym[DPER];
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
+                const int vc = c0 + cl, co = vc / g.KT, kt = vc - co * g.KT;
                 const int row = tf + rs + g.pt - kt * g.dt;        // output row feeding this x row
                 const int pos = (rs ? 0 : u0) - (J - 1) + w;     // output column f = u - q
-                if (row >= 0 && row < g.T2 && pos >= 0 && pos < g.Fo) {
-                    const int64_t o = (int64_t)co * plane + (int64_t)row * g.Fo + pos;
-                    v = dyb[o];
-                    if (yab) v *= lrelu_grad(yab[o]);
-                }
+                const bool ok = i < CK * XR && vc < VC && rs < nr && row >= 0 && row < g.T2 && pos >= 0 &&
+                                pos < g.Fo;
+                const int64_t o = ok ? (int64_t)co * plane + (int64_t)row * g.Fo + pos : 0;
+                const float t = dyb[o];
+                ym[q] = ysrc[o];
+                v[q] = ok ? t : 0.f;
             }
-            Xs[i] = v;
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i < CK * XR) Xs[i] = yab ? v[q] * lrelu_grad(ym[q]) : v[q];
+            }
         }
-        for (int i = tid; i < J * CK * BM; i += NT) {
-            const int col = i % BM, r = i / BM, cl = r % CK, q = r / CK;
-            const int vc = c0 + cl, row = m0 + col;
-            As[i] = (vc < VC && row < M) ? a.wp[((int64_t)vc * J + q) * M + row] : 0.f;
+        for (int i0 = 0; i0 < J * CK * BM; i0 += NT * DPER) {
+            float v[DPER];
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int col = i % BM, r = i / BM, cl = r % CK, qj = r / CK;
+                const int vc = c0 + cl, row = m0 + col;
+                const bool ok = i < J * CK * BM && vc < VC && row < M;
+                const float t = a.wp[ok ? ((int64_t)vc * J + qj) * M + row : 0];
+                v[q] = ok ? t : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i < J * CK * BM) As[i] = v[q];
+            }
         }
         __syncthreads();
         for (int q = 0; q < J; ++q) {
@@ -286,28 +328,47 @@ __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
         const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane_y : nullptr;
         const float* xb = a.x + (int64_t)b * g.Ci * plane_x;
         __syncthreads();
-        for (int i = tid; i < BT * BM; i += NT) {
-            const int tl = i % BT, col = i / BT, p = p0 + tl, co = co0 + col;
-            float v = 0.f;
-            if (p < pend && co < g.Co) {
-                const int64_t o = (int64_t)co * plane_y + p;
-                v = dyb[o];
-                if (yab) v *= lrelu_grad(yab[o]);
+        const float* ysrc = yab ? yab : dyb;
+        for (int i0 = 0; i0 < BT * BM; i0 += NT * DPER) {
+            float v[DPER], ym[DPER];
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int tl = i % BT, col = i / BT, p = p0 + tl, co = co0 + col;
+                const bool ok = i < BT * BM && p < pend && co < g.Co;
+                const int64_t o = ok ? (int64_t)co * plane_y + p : 0;
+                const float t = dyb[o];
+                ym[q] = ysrc[o];
+                v[q] = ok ? t : 0.f;
             }
-            Ls[tl * BM + col] = v;
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i < BT * BM) {
+                    const int tl = i % BT, col = i / BT;
+                    Ls[tl * BM + col] = yab ? v[q] * lrelu_grad(ym[q]) : v[q];
+                }
+            }
         }
-        for (int i = tid; i < a.NCmax * XR; i += NT) {
-            const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
-            const int vc = c_first + cl;
-            float v = 0.f;
-            if (vc < VC && rs < nr) {
-                const int ci = vc / g.KT, kt = vc - ci * g.KT;
+        for (int i0 = 0; i0 < a.NCmax * XR; i0 += NT * DPER) {
+            float v[DPER];
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
+                const int vc = c_first + cl, ci = vc / g.KT, kt = vc - ci * g.KT;
                 const int row = tf + rs + kt * g.dt - g.pt;
                 const int pos = (rs ? 0 : f0) * S - g.pf + w;
-                if (row >= 0 && row < g.T2 && pos >= 0 && pos < g.Fi)
-                    v = xb[(int64_t)ci * plane_x + (int64_t)row * g.Fi + pos];
+                const bool ok = i < a.NCmax * XR && vc < VC && rs < nr && row >= 0 && row < g.T2 && pos >= 0 &&
+                                pos < g.Fi;
+                const float t = xb[ok ? (int64_t)ci * plane_x + (int64_t)row * g.Fi + pos : 0];
+                v[q] = ok ? t : 0.f;
             }
-            Rs[i] = v;
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i < a.NCmax * XR) Rs[i] = v[q];
+            }
         }
         for (int tl = tid; tl < BT; tl += NT) {
             const int p = p0 + tl;
@@ -376,8 +437,7 @@ __global__ void c2_wg_reduce(const float* ws, int S, int Co, int N, float* dw, f
                              int acc_b) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)Co * N) return;
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += ws[(int64_t)s * Co * N + i];
+    const float v = sum_strided(ws + i, S, (int64_t)Co * N);
     const int co = (int)(i / N), n = (int)(i - (int64_t)co * N);
     const int Nw = N - 1;
     if (n < Nw) {

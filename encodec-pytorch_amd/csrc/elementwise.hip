@@ -7,27 +7,54 @@ namespace {
 constexpr int NT = 256;
 constexpr int CS_PARTS = 64;
 
-// pass 1 of db[c] = sum_{b,t} dy[b,c,t]: block (c, part) sums its slice of the B*T range
-__global__ __launch_bounds__(NT) void chan_sum_p1(const float* dy, float* ws, int B, int C, int T) {
+// db[c] = sum_{b,t} dy[b,c,t]. Block (c, part) sums a contiguous slice of the B*T positions,
+// CS_PER loads in flight per thread (clamped addresses, values selected after the load: a
+// branch around each load would serialise their latency); (b, t) advance incrementally, no
+// division in the loop. parts == 1: the block writes db[c]; else a second pass adds the parts
+// in a fixed order (bit-reproducible either way).
+constexpr int CS_PER = 8;
+__global__ __launch_bounds__(NT) void chan_sum_p1(const float* dy, float* ws, float* db, int B, int C, int T,
+                                                  int parts, int acc) {
     __shared__ float red[16];
     const int c = blockIdx.x, part = blockIdx.y;
     const int64_t tot = (int64_t)B * T;
-    const int64_t per = (tot + CS_PARTS - 1) / CS_PARTS;
+    const int64_t per = (tot + parts - 1) / parts;
     const int64_t beg = part * per, end = min(tot, beg + per);
-    float s = 0.f;
-    for (int64_t i = beg + threadIdx.x; i < end; i += NT) {
-        int64_t b = i / T, t = i - b * T;
-        s += dy[(b * C + c) * T + t];
+    const int dq = NT / T, dr = NT - dq * T;  // a step of NT positions as (rows, columns)
+    int64_t i = beg + threadIdx.x;
+    int b = (int)(i / T), t = (int)(i - (int64_t)b * T);
+    float sacc[CS_PER];
+#pragma unroll
+    for (int q = 0; q < CS_PER; ++q) sacc[q] = 0.f;
+    for (; i < end; i += CS_PER * NT) {
+        float v[CS_PER];
+#pragma unroll
+        for (int q = 0; q < CS_PER; ++q) {
+            const bool ok = i + (int64_t)q * NT < end;
+            const float x = dy[ok ? ((int64_t)b * C + c) * T + t : 0];
+            v[q] = ok ? x : 0.f;
+            b += dq;
+            t += dr;
+            if (t >= T) {
+                t -= T;
+                ++b;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < CS_PER; ++q) sacc[q] += v[q];
     }
+    float s = ((sacc[0] + sacc[1]) + (sacc[2] + sacc[3])) + ((sacc[4] + sacc[5]) + (sacc[6] + sacc[7]));
     s = block_sum(s, red);
-    if (threadIdx.x == 0) ws[c * CS_PARTS + part] = s;
+    if (threadIdx.x == 0) {
+        if (parts == 1) db[c] = acc ? db[c] + s : s;
+        else ws[c * parts + part] = s;
+    }
 }
 
-__global__ void chan_sum_p2(const float* ws, float* db, int C, int acc) {
+__global__ void chan_sum_p2(const float* ws, float* db, int C, int parts, int acc) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    float s = 0.f;
-    for (int p = 0; p < CS_PARTS; ++p) s += ws[c * CS_PARTS + p];
+    const float s = sum_strided(ws + c * parts, parts, 1);
     db[c] = acc ? db[c] + s : s;
 }
 
@@ -108,10 +135,17 @@ int encx_channel_sum(const float* dy, float* db, float* ws, int64_t B, int64_t C
                      int accumulate, encx_stream_t stream) {
     ENCX_REQUIRE(dy && db && ws && B > 0 && C > 0 && T > 0);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(chan_sum_p1, dim3(C, CS_PARTS), dim3(NT), 0, st, dy, ws, (int)B, (int)C, (int)T);
+    // ~4096 positions per block: one pass for the short rows of the low-rate stages
+    int64_t parts = B * T / 4096;
+    parts = parts < 1 ? 1 : (parts > CS_PARTS ? CS_PARTS : parts);
+    hipLaunchKernelGGL(chan_sum_p1, dim3(C, parts), dim3(NT), 0, st, dy, ws, db, (int)B, (int)C, (int)T,
+                       (int)parts, accumulate);
     ENCX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(chan_sum_p2, dim3(cdiv(C, 256)), dim3(256), 0, st, ws, db, (int)C, accumulate);
-    ENCX_CHECK_LAUNCH();
+    if (parts > 1) {
+        hipLaunchKernelGGL(chan_sum_p2, dim3(cdiv(C, 256)), dim3(256), 0, st, ws, db, (int)C, (int)parts,
+                           accumulate);
+        ENCX_CHECK_LAUNCH();
+    }
     return 0;
 }
 

@@ -41,6 +41,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
     constexpr int EA = BM * BK / 256, EB = BN * BK / 256;
     static_assert(EA * 256 == BM * BK && EB * 256 == BN * BK, "tile/thread mismatch");
     float ra[EA], rb[EB];
+    // Every element is loaded from a clamped in-range index and the value selected afterwards:
+    // a bounds test around each loader call compiles to an exec-masked branch per element, and
+    // a loader that transforms the loaded value (ELU, |X|^2, ...) then waits for each load
+    // before issuing the next (one memory round trip per element instead of one per fetch).
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int e = 0; e < EA; ++e) {
@@ -49,7 +53,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
             if (LD::A_K_FAST) { m = i / BK; k = i - m * BK; }
             else { k = i / BM; m = i - k * BM; }
             const int gm = m0 + m, gk = k0 + k;
-            ra[e] = (gm < M && gk < kend) ? ld.a(gm, gk) : 0.f;
+            const bool ok = gm < M && gk < kend;
+            const float v = ld.a(gm < M ? gm : M - 1, gk < kend ? gk : kend - 1);
+            ra[e] = ok ? v : 0.f;
         }
 #pragma unroll
         for (int e = 0; e < EB; ++e) {
@@ -58,7 +64,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
             if (LD::B_N_FAST) { k = i / BN; n = i - k * BN; }
             else { n = i / BK; k = i - n * BK; }
             const int gn = n0 + n, gk = k0 + k;
-            rb[e] = (gn < N && gk < kend) ? ld.b(gk, gn) : 0.f;
+            const bool ok = gn < N && gk < kend;
+            const float v = ld.b(gk < kend ? gk : kend - 1, gn < N ? gn : N - 1);
+            rb[e] = ok ? v : 0.f;
         }
     };
     if (kbeg < kend) fetch(kbeg);

@@ -45,6 +45,7 @@ ENCX_DEV uint64_t shfl_xor64(uint64_t v, int o) {
 // into Bs[d][code] (row stride 129: conflict-free transposed writes), so a workgroup does one
 // load phase, one barrier and 64 MFMA k-steps. 38 x 8 = 304 workgroups at N = 2400.
 constexpr int AR_ROWS = 64, AR_CODES = 128, AR_BS = AR_CODES + 1;
+constexpr int AR_PER = 8;  // staging loads in flight per thread
 
 __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed, uint64_t* keys,
                                                       int N, int D, int Kc) {
@@ -58,13 +59,46 @@ __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed
     const int n0 = blockIdx.x * AR_ROWS, k0 = blockIdx.y * AR_CODES;
     const int h = lane >> 5, l32 = lane & 31;
     const int wm0 = (wave >> 1) * 32, wn0 = (wave & 1) * 64;
-    for (int i = tid; i < D * AR_ROWS; i += NT) {
-        const int d = i / AR_ROWS, r = i - d * AR_ROWS, n = n0 + r;
-        As[i] = n < N ? x.at(n, d) : 0.f;
+    // staging: AR_PER loads in flight per thread from clamped addresses, values selected after
+    // the load (a branch around each load serialises the latency: one round trip per element)
+    {
+        const int r = tid & (AR_ROWS - 1), dq = tid / AR_ROWS, n = n0 + r;  // frame fixed per thread
+        const bool okn = n < N;
+        const int nc = okn ? n : N - 1;
+        const int bb = nc / x.Tf, tt = nc - bb * x.Tf;
+        const float* xp = x.p + bb * x.sB + tt * x.sT;
+        constexpr int DSTEP = NT / AR_ROWS;
+        for (int d0 = 0; d0 < D; d0 += DSTEP * AR_PER) {
+            float v[AR_PER];
+#pragma unroll
+            for (int q = 0; q < AR_PER; ++q) {
+                const int d = d0 + dq + DSTEP * q;
+                const float t = xp[(int64_t)(d < D ? d : D - 1) * x.sD];
+                v[q] = (okn && d < D) ? t : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < AR_PER; ++q) {
+                const int d = d0 + dq + DSTEP * q;
+                if (d < D) As[d * AR_ROWS + r] = v[q];
+            }
+        }
     }
-    for (int i = tid; i < AR_CODES * D; i += NT) {
-        const int c = i / D, d = i - c * D, k = k0 + c;
-        Bs[d * AR_BS + c] = k < Kc ? embed[(int64_t)k * D + d] : 0.f;
+    for (int i0 = 0; i0 < AR_CODES * D; i0 += NT * AR_PER) {
+        float v[AR_PER];
+#pragma unroll
+        for (int q = 0; q < AR_PER; ++q) {
+            const int i = i0 + q * NT + tid;
+            const int c = i / D, d = i - c * D, k = k0 + c;
+            const bool ok = i < AR_CODES * D && k < Kc;
+            const float t = embed[ok ? (int64_t)k * D + d : 0];
+            v[q] = ok ? t : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < AR_PER; ++q) {
+            const int i = i0 + q * NT + tid;
+            const int c = i / D, d = i - c * D;
+            if (i < AR_CODES * D) Bs[d * AR_BS + c] = v[q];
+        }
     }
     __syncthreads();
     // |x|^2 and |e|^2 in ascending d (fmaf chain)
@@ -225,11 +259,9 @@ template <int MODE>  // 0: EMA (core_vq.py:227-229), 1: kmeans (:92-100)
 __global__ void bucket_finish(const float* ws, int S, int Kc, int D, float* cs, float* ea,
                               float* means, int64_t* bins, float decay, float one_m) {
     const int c = blockIdx.x, W = D + 1;
-    float cnt = 0.f;
-    for (int z = 0; z < S; ++z) cnt += ws[((int64_t)z * Kc + c) * W + D];
+    const float cnt = sum_strided(ws + (int64_t)c * W + D, S, (int64_t)Kc * W);
     for (int d = threadIdx.x; d <= D; d += blockDim.x) {
-        float s = 0.f;
-        for (int z = 0; z < S; ++z) s += ws[((int64_t)z * Kc + c) * W + d];
+        const float s = sum_strided(ws + (int64_t)c * W + d, S, (int64_t)Kc * W);
         if (MODE == 0) {
             if (d < D) {
                 float* p = ea + (int64_t)c * D + d;
