@@ -274,6 +274,95 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
         }
 }
 
+// Narrow backward-data (M = Ci <= 4 rows, stride 1 along f: the first layer's grad into the
+// spectrogram). A 32-row MFMA tile would carry 2 useful rows, so this runs on the vector ALU:
+// a workgroup owns 16 t rows x 64 f columns of one batch item; the masked output grad for
+// NC_CO channels is staged in LDS with its (KT-1)*dt row and KF-1 column halo; a thread keeps
+// CI x 4 accumulators for 4 adjacent f and slides a 4+KF-1 window over its LDS row per tap;
+// the weights are wave-uniform (scalar loads).
+constexpr int DN_ROWS = 16, DN_COLS = 64, DN_FPT = 4, DN_CC = 8, DN_MAXHALO = 4;
+template <int CI, int KT, int KF>
+__global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
+    constexpr int RC = (DN_COLS + KF - 1 + 3) & ~3;  // LDS row length (float4 aligned)
+    constexpr int WIN4 = (DN_FPT + KF - 1 + 3) / 4;
+    __shared__ float Xs[DN_CC * (DN_ROWS + DN_MAXHALO) * RC];
+    const C2Geo g = a.g;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int f0 = blockIdx.x * DN_COLS, t0 = blockIdx.y * DN_ROWS, b = blockIdx.z;
+    const int halo = (KT - 1) * g.dt, NRW = DN_ROWS + halo;
+    const int tbase = t0 + g.pt - halo, fbase = f0 + g.pf - (KF - 1);
+    const int64_t plane = (int64_t)g.T2 * g.Fo;
+    const float* dyb = a.dy + (int64_t)b * g.Co * plane;
+    const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane : dyb;
+    const int items = DN_CC * NRW * RC;
+    float acc[CI][DN_FPT];
+#pragma unroll
+    for (int c = 0; c < CI; ++c)
+#pragma unroll
+        for (int e = 0; e < DN_FPT; ++e) acc[c][e] = 0.f;
+    for (int c0 = 0; c0 < g.Co; c0 += DN_CC) {
+        __syncthreads();
+        for (int i0 = 0; i0 < items; i0 += NT * DPER) {
+            float v[DPER], ym[DPER];
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int cl = i / (NRW * RC), rem = i - cl * (NRW * RC), r = rem / RC, c = rem - r * RC;
+                const int tr = tbase + r, fc = fbase + c;
+                const bool ok = i < items && tr >= 0 && tr < g.T2 && fc >= 0 && fc < g.Fo;
+                const int64_t o = ok ? (int64_t)(c0 + cl) * plane + (int64_t)tr * g.Fo + fc : 0;
+                const float t = dyb[o];
+                ym[q] = yab[o];
+                v[q] = ok ? t : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                if (i < items) Xs[i] = a.yact ? v[q] * lrelu_grad(ym[q]) : v[q];
+            }
+        }
+        __syncthreads();
+        for (int cl = 0; cl < DN_CC; ++cl) {
+            const int co = c0 + cl;
+#pragma unroll
+            for (int kt = 0; kt < KT; ++kt) {
+                const float* row = Xs + (cl * NRW + ty + (KT - 1 - kt) * g.dt) * RC + 4 * tx;
+                float win[WIN4 * 4];
+#pragma unroll
+                for (int j = 0; j < WIN4; ++j) {
+                    const f32x4 t = *(const f32x4*)(row + 4 * j);
+                    win[4 * j] = t[0];
+                    win[4 * j + 1] = t[1];
+                    win[4 * j + 2] = t[2];
+                    win[4 * j + 3] = t[3];
+                }
+                const float* wr = a.wp + (int64_t)(co * KT + kt) * KF * CI;
+#pragma unroll
+                for (int kf = 0; kf < KF; ++kf)
+#pragma unroll
+                    for (int c = 0; c < CI; ++c) {
+                        const float w = wr[kf * CI + c];
+#pragma unroll
+                        for (int e = 0; e < DN_FPT; ++e) acc[c][e] = fmaf(w, win[e + KF - 1 - kf], acc[c][e]);
+                    }
+            }
+        }
+    }
+    const int t = t0 + ty;
+    if (t >= g.T2) return;
+#pragma unroll
+    for (int c = 0; c < CI; ++c)
+#pragma unroll
+        for (int e = 0; e < DN_FPT; ++e) {
+            const int f = f0 + 4 * tx + e;
+            if (f >= g.Fi) continue;
+            const int64_t o = (((int64_t)b * CI + c) * g.T2 + t) * g.Fi + f;
+            float v = acc[c][e];
+            if (a.xact) v *= lrelu_grad(a.xact[o]);
+            a.dx[o] = a.accumulate ? a.dx[o] + v : v;
+        }
+}
+
 // ------------------------------------------------------------------------ weight grad
 struct C2Wg {
     C2Geo g;
@@ -698,6 +787,13 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
     a.NR = c2_rows(BN, a.U);
     a.RL = min(BN, a.U) - 1 + a.J;
     const int M = (int)(Ci * sf);
+    if (sf == 1 && KT == 3 && KF == 9 && (Ci == 2 || Ci == 4) && Co % DN_CC == 0 && (KT - 1) * dt <= DN_MAXHALO) {
+        dim3 grid((unsigned)cdiv(Fi, DN_COLS), (unsigned)cdiv(T2, DN_ROWS), (unsigned)B);
+        if (Ci == 2) hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((c2_dgrad_narrow<4, 3, 9>), grid, dim3(NT), 0, st, a);
+        ENCX_CHECK_LAUNCH();
+        return 0;
+    }
     if (M <= 32) {
         a.CK = c2_ck((int)(Co * KT), a.NR * a.RL + a.J * 32);
         return launch_dgrad<32, 128, 1, 4>(a, st);
