@@ -48,7 +48,7 @@ __global__ __launch_bounds__(NT) void c2_fwd_kernel(C2Fwd a) {
     const int CK = a.CK, NR = a.NR, RL = a.RL, KF = g.KF, S = g.sf;
     const int VC = g.Ci * g.KT, XR = NR * RL;
     float* Xs = smem;           // [CK][NR][RL]
-    float* Ws = smem + CK * XR; // [KF][CK][BM]
+    float* Ws = smem + CK * XR; // [CK][KF][BM]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
     const int h = lane >> 5, l32 = lane & 31;
@@ -72,54 +72,85 @@ __global__ __launch_bounds__(NT) void c2_fwd_kernel(C2Fwd a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
     const float* xb = a.x + (int64_t)b * g.Ci * g.T2 * g.Fi;
+    // Staging without per-element division: a table of the window rows (global row
+    // gr = vc*NR + rs -> source offset of column 0, first column position or "invalid"), built
+    // once; each thread walks its items (row r, column w) by a fixed step of NT; the weight
+    // items keep their column (NT is a multiple of BM) and step the (kf, cl) row.
+    int2* rtab = (int2*)(Ws + KF * CK * BM);  // {source offset of column 0, first position}
+    for (int gr = tid; gr < VC * NR; gr += NT) {
+        const int vc = gr / NR, rs = gr - vc * NR, ci = vc / g.KT, kt = vc - ci * g.KT;
+        const int row = tf + rs + kt * g.dt - g.pt, pos0 = (rs ? 0 : f0) * S - g.pf;
+        const bool ok = rs < nr && row >= 0 && row < g.T2;
+        rtab[gr] = make_int2(ok ? (ci * g.T2 + row) * g.Fi + pos0 : 0, ok ? pos0 : -(1 << 30));
+    }
+    const int dr = NT / RL, dw = NT - dr * RL, r_init = tid / RL, w_init = tid - r_init * RL;
+    const int wcol = tid & (BM - 1);
     for (int c0 = 0; c0 < VC; c0 += CK) {
         __syncthreads();
-        // DPER loads in flight per thread from clamped addresses, values selected afterwards
-        for (int i0 = 0; i0 < CK * XR; i0 += NT * DPER) {
-            float v[DPER];
+        {
+            const int nrows = min(CK, VC - c0) * NR, items = CK * XR;
+            int r = r_init, w = w_init;
+            for (int i0 = 0; i0 < items; i0 += NT * DPER) {
+                // (row, column) of the DPER items, then their table entries, then the loads
+                int rq[DPER], wq[DPER];
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
-                const int vc = c0 + cl, ci = vc / g.KT, kt = vc - ci * g.KT;
-                const int row = tf + rs + kt * g.dt - g.pt;
-                const int pos = (rs ? 0 : f0) * S - g.pf + w;
-                const bool ok = i < CK * XR && vc < VC && rs < nr && row >= 0 && row < g.T2 && pos >= 0 &&
-                                pos < g.Fi;
-                const float t = xb[ok ? ((int64_t)ci * g.T2 + row) * g.Fi + pos : 0];
-                v[q] = ok ? t : 0.f;
-            }
+                for (int q = 0; q < DPER; ++q) {
+                    rq[q] = r;
+                    wq[q] = w;
+                    w += dw;
+                    r += dr;
+                    if (w >= RL) {
+                        w -= RL;
+                        ++r;
+                    }
+                }
+                int2 e[DPER];
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                if (i < CK * XR) Xs[i] = v[q];
+                for (int q = 0; q < DPER; ++q) e[q] = rtab[c0 * NR + (rq[q] < nrows ? rq[q] : 0)];
+                float v[DPER];
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    const int pos = e[q].y + wq[q];
+                    const bool ok = rq[q] < nrows && pos >= 0 && pos < g.Fi;
+                    const float t = xb[ok ? e[q].x + wq[q] : 0];
+                    v[q] = ok ? t : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    const int i = i0 + q * NT + tid;
+                    if (i < items) Xs[i] = v[q];
+                }
             }
         }
-        for (int i0 = 0; i0 < KF * CK * BM; i0 += NT * DPER) {
-            float v[DPER];
+        {
+            // Ws[cl][kf][col] = wf[(c0 + cl, kf)][co0 + col]: rows (cl, kf) are consecutive rows
+            // of wf, so an item's source needs no division
+            const int items = KF * CK * BM, rows = (VC - c0) * KF, co = co0 + wcol;
+            const float* wsrc = a.wf + (int64_t)c0 * KF * g.Co + co;
+            for (int i0 = 0; i0 < items; i0 += NT * DPER) {
+                float v[DPER];
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int col = i % BM, r = i / BM, cl = r % CK, kf = r / CK;
-                const int vc = c0 + cl, co = co0 + col;
-                const bool ok = i < KF * CK * BM && vc < VC && co < g.Co;
-                const float t = a.wf[ok ? ((int64_t)vc * KF + kf) * g.Co + co : 0];
-                v[q] = ok ? t : 0.f;
-            }
+                for (int q = 0; q < DPER; ++q) {
+                    const int rr = (i0 + q * NT + tid) / BM;
+                    const bool ok = rr < rows && co < g.Co;
+                    const float t = wsrc[ok ? (int64_t)rr * g.Co : 0];
+                    v[q] = ok ? t : 0.f;
+                }
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                if (i < KF * CK * BM) Ws[i] = v[q];
+                for (int q = 0; q < DPER; ++q) {
+                    const int i = i0 + q * NT + tid;
+                    if (i < items) Ws[i] = v[q];
+                }
             }
         }
         __syncthreads();
         for (int kf = 0; kf < KF; ++kf) {
-            const float* wk = Ws + (kf * CK + h) * BM + wm0 + l32;
+            const float* wk = Ws + (h * KF + kf) * BM + wm0 + l32;
             const float* xk = Xs + h * XR + kf;
             for (int cp = 0; cp < CK; cp += 2) {
                 float av[TM], bv[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = wk[cp * BM + i * 32];
+                for (int i = 0; i < TM; ++i) av[i] = wk[cp * KF * BM + i * 32];
 #pragma unroll
                 for (int j = 0; j < TN; ++j) bv[j] = xk[cp * XR + boff[j]];
 #pragma unroll
@@ -137,8 +168,9 @@ __global__ __launch_bounds__(NT) void c2_fwd_kernel(C2Fwd a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int co = co0 + wm0 + i * 32 + mfma_row(r, lane);
+                const float bco = a.bias ? a.bias[co < g.Co ? co : g.Co - 1] : 0.f;  // unconditional load
                 if (co < g.Co && n < nend) {
-                    float v = acc[i][j][r] + (a.bias ? a.bias[co] : 0.f);
+                    float v = acc[i][j][r] + bco;
                     if (a.act) v = lrelu(v);
                     a.y[((int64_t)b * g.Co + co) * Nall + n] = v;
                 }
@@ -675,7 +707,8 @@ static int c2_rows(int BN, int len) { return (len + BN - 2) / len + 1; }
 
 template <int BM, int BN, int WM, int WN>
 int launch_fwd(C2Fwd a, hipStream_t st) {
-    const size_t lds = ((size_t)a.CK * a.NR * a.RL + (size_t)a.g.KF * a.CK * BM) * sizeof(float);
+    const size_t lds = ((size_t)a.CK * a.NR * a.RL + (size_t)a.g.KF * a.CK * BM +
+                        (size_t)2 * a.g.Ci * a.g.KT * a.NR + 2) * sizeof(float);
     dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.g.Fo, BN), (unsigned)cdiv(a.g.Co, BM), (unsigned)a.g.B);
     hipLaunchKernelGGL((c2_fwd_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
     ENCX_CHECK_LAUNCH();
