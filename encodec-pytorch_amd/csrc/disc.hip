@@ -24,6 +24,7 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int DPER = 8;  // staging loads in flight per thread
+constexpr int WG_BT = 64;  // wgrad: output positions per work item
 
 struct C2Geo {
     int B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf;
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
     const int CK = a.CK, NR = a.NR, RL = a.RL, J = a.J, U = a.U, S = g.sf;
     const int VC = g.Co * g.KT, XR = NR * RL, M = g.Ci * S;
     float* Xs = smem;            // [CK][NR][RL]
-    float* As = smem + CK * XR;  // [J][CK][BM]
+    float* As = smem + CK * XR;  // [CK][J][BM]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
     const int h = lane >> 5, l32 = lane & 31;
@@ -223,58 +224,83 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
     const int64_t plane = (int64_t)g.T2 * g.Fo;
     const float* dyb = a.dy + (int64_t)b * g.Co * plane;
     const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane : nullptr;
+    // staging as in c2_fwd_kernel: window-row table {offset, first position}, items walked by
+    // a fixed step, weights in source order As[cl][q][m]
+    int2* rtab = (int2*)(As + J * CK * BM);
+    for (int gr = tid; gr < VC * NR; gr += NT) {
+        const int vc = gr / NR, rs = gr - vc * NR, co = vc / g.KT, kt = vc - co * g.KT;
+        const int row = tf + rs + g.pt - kt * g.dt, pos0 = (rs ? 0 : u0) - (J - 1);
+        const bool ok = rs < nr && row >= 0 && row < g.T2;
+        rtab[gr] = make_int2(ok ? co * (int)plane + row * g.Fo + pos0 : 0, ok ? pos0 : -(1 << 30));
+    }
+    const int dr = NT / RL, dw = NT - dr * RL, r_init = tid / RL, w_init = tid - r_init * RL;
+    const int wcol = tid & (BM - 1);
+    const float* ysrc = yab ? yab : dyb;
     for (int c0 = 0; c0 < VC; c0 += CK) {
         __syncthreads();
-        // DPER loads in flight per thread from clamped addresses (the LeakyReLU' mask source is
-        // dy itself when there is none: a uniform pointer choice, no per-element branch)
-        const float* ysrc = yab ? yab : dyb;
-        for (int i0 = 0; i0 < CK * XR; i0 += NT * DPER) {
-            float v[DPER], ym[DPER];
+        {
+            const int nrows = min(CK, VC - c0) * NR, items = CK * XR;
+            int r = r_init, w = w_init;
+            for (int i0 = 0; i0 < items; i0 += NT * DPER) {
+                int rq[DPER], wq[DPER];
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
-                const int vc = c0 + cl, co = vc / g.KT, kt = vc - co * g.KT;
-                const int row = tf + rs + g.pt - kt * g.dt;        // output row feeding this x row
-                const int pos = (rs ? 0 : u0) - (J - 1) + w;     // output column f = u - q
-                const bool ok = i < CK * XR && vc < VC && rs < nr && row >= 0 && row < g.T2 && pos >= 0 &&
-                                pos < g.Fo;
-                const int64_t o = ok ? (int64_t)co * plane + (int64_t)row * g.Fo + pos : 0;
-                const float t = dyb[o];
-                ym[q] = ysrc[o];
-                v[q] = ok ? t : 0.f;
-            }
+                for (int q = 0; q < DPER; ++q) {
+                    rq[q] = r;
+                    wq[q] = w;
+                    w += dw;
+                    r += dr;
+                    if (w >= RL) {
+                        w -= RL;
+                        ++r;
+                    }
+                }
+                int2 e[DPER];
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                if (i < CK * XR) Xs[i] = yab ? v[q] * lrelu_grad(ym[q]) : v[q];
+                for (int q = 0; q < DPER; ++q) e[q] = rtab[c0 * NR + (rq[q] < nrows ? rq[q] : 0)];
+                float v[DPER], ym[DPER];
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    const int pos = e[q].y + wq[q];
+                    const bool ok = rq[q] < nrows && pos >= 0 && pos < g.Fo;
+                    const int o = ok ? e[q].x + wq[q] : 0;
+                    const float t = dyb[o];
+                    ym[q] = ysrc[o];
+                    v[q] = ok ? t : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    const int i = i0 + q * NT + tid;
+                    if (i < items) Xs[i] = yab ? v[q] * lrelu_grad(ym[q]) : v[q];
+                }
             }
         }
-        for (int i0 = 0; i0 < J * CK * BM; i0 += NT * DPER) {
-            float v[DPER];
+        {
+            const int items = J * CK * BM, rows = (VC - c0) * J, m = m0 + wcol;
+            const float* wsrc = a.wp + (int64_t)c0 * J * M + m;
+            for (int i0 = 0; i0 < items; i0 += NT * DPER) {
+                float v[DPER];
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int col = i % BM, r = i / BM, cl = r % CK, qj = r / CK;
-                const int vc = c0 + cl, row = m0 + col;
-                const bool ok = i < J * CK * BM && vc < VC && row < M;
-                const float t = a.wp[ok ? ((int64_t)vc * J + qj) * M + row : 0];
-                v[q] = ok ? t : 0.f;
-            }
+                for (int q = 0; q < DPER; ++q) {
+                    const int rr = (i0 + q * NT + tid) / BM;
+                    const bool ok = rr < rows && m < M;
+                    const float t = wsrc[ok ? (int64_t)rr * M : 0];
+                    v[q] = ok ? t : 0.f;
+                }
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                if (i < J * CK * BM) As[i] = v[q];
+                for (int q = 0; q < DPER; ++q) {
+                    const int i = i0 + q * NT + tid;
+                    if (i < items) As[i] = v[q];
+                }
             }
         }
         __syncthreads();
         for (int q = 0; q < J; ++q) {
-            const float* aq = As + (q * CK + h) * BM + wm0 + l32;
+            const float* aq = As + (h * J + q) * BM + wm0 + l32;
             const float* xq = Xs + h * XR - q;
             for (int cp = 0; cp < CK; cp += 2) {
                 float av[TM], bv[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = aq[cp * BM + i * 32];
+                for (int i = 0; i < TM; ++i) av[i] = aq[cp * J * BM + i * 32];
 #pragma unroll
                 for (int j = 0; j < TN; ++j) bv[j] = xq[cp * XR + boff[j]];
 #pragma unroll
@@ -411,9 +437,11 @@ __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
     static_assert(WM * WN * WK == 4, "4 waves");
     extern __shared__ float smem[];
     const C2Geo g = a.g;
-    const int BT = a.BT, NR = a.NR, RL = a.RL, KF = g.KF, S = g.sf;
+    constexpr int BT = WG_BT;
+    const int NR = a.NR, RL = a.RL, KF = g.KF, S = g.sf;
     const int VC = g.Ci * g.KT, Nw = VC * KF, N = Nw + 1, XR = NR * RL;
-    float* Ls = smem;                                 // [BT][BM]
+    int4* rtab = (int4*)smem;                         // [NCmax*NR]: window-row table
+    float* Ls = smem + 4 * a.NCmax * NR;              // [BT][BM]
     float* Rs = Ls + BT * BM;                         // [NCmax][NR][RL]
     int* poff = (int*)(Rs + a.NCmax * XR);            // [BT]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -438,6 +466,14 @@ __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    // rows r = cl*NR + rs of the x window: {offset relative to row tf, row relative to tf, rs,
+    // vc in range}; per item only tf / f0 / nr change, so the staging needs no division
+    for (int r = tid; r < a.NCmax * NR; r += NT) {
+        const int cl = r / NR, rs = r - cl * NR, vc = c_first + cl, ci = vc / g.KT, kt = vc - ci * g.KT;
+        const int rrel = rs + kt * g.dt - g.pt;
+        rtab[r] = make_int4(ci * (int)plane_x + rrel * g.Fi, rrel, rs, vc < VC);
+    }
+    const int dr = NT / RL, dw = NT - dr * RL, r_init = tid / RL, w_init = tid - r_init * RL;
     const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
     const int tw = BT / WK;
     for (int it = it_beg; it < it_end; ++it) {
@@ -471,24 +507,39 @@ __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
                 }
             }
         }
-        for (int i0 = 0; i0 < a.NCmax * XR; i0 += NT * DPER) {
-            float v[DPER];
+        {
+            const int items = a.NCmax * XR, nrows = a.NCmax * NR, tfo = tf * g.Fi;
+            int r = r_init, w = w_init;
+            for (int i0 = 0; i0 < items; i0 += NT * DPER) {
+                int rq[DPER], wq[DPER];
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int cl = i / XR, rem = i - cl * XR, rs = rem / RL, w = rem - rs * RL;
-                const int vc = c_first + cl, ci = vc / g.KT, kt = vc - ci * g.KT;
-                const int row = tf + rs + kt * g.dt - g.pt;
-                const int pos = (rs ? 0 : f0) * S - g.pf + w;
-                const bool ok = i < a.NCmax * XR && vc < VC && rs < nr && row >= 0 && row < g.T2 && pos >= 0 &&
-                                pos < g.Fi;
-                const float t = xb[ok ? (int64_t)ci * plane_x + (int64_t)row * g.Fi + pos : 0];
-                v[q] = ok ? t : 0.f;
-            }
+                for (int q = 0; q < DPER; ++q) {
+                    rq[q] = r;
+                    wq[q] = w;
+                    w += dw;
+                    r += dr;
+                    if (w >= RL) {
+                        w -= RL;
+                        ++r;
+                    }
+                }
+                int4 e[DPER];
 #pragma unroll
-            for (int q = 0; q < DPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                if (i < a.NCmax * XR) Rs[i] = v[q];
+                for (int q = 0; q < DPER; ++q) e[q] = rtab[rq[q] < nrows ? rq[q] : 0];
+                float v[DPER];
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    const int row = tf + e[q].y, pos = (e[q].z ? 0 : f0) * S - g.pf + wq[q];
+                    const bool ok = rq[q] < nrows && e[q].w && e[q].z < nr && row >= 0 && row < g.T2 && pos >= 0 &&
+                                    pos < g.Fi;
+                    const float t = xb[ok ? e[q].x + tfo + pos : 0];
+                    v[q] = ok ? t : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    const int i = i0 + q * NT + tid;
+                    if (i < items) Rs[i] = v[q];
+                }
             }
         }
         for (int tl = tid; tl < BT; tl += NT) {
@@ -716,7 +767,8 @@ int launch_fwd(C2Fwd a, hipStream_t st) {
 }
 template <int BM, int BN, int WM, int WN>
 int launch_dgrad(C2Dg a, hipStream_t st) {
-    const size_t lds = ((size_t)a.CK * a.NR * a.RL + (size_t)a.J * a.CK * BM) * sizeof(float);
+    const size_t lds = ((size_t)a.CK * a.NR * a.RL + (size_t)a.J * a.CK * BM +
+                        (size_t)2 * a.g.Co * a.g.KT * a.NR + 2) * sizeof(float);
     dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.U, BN), (unsigned)cdiv(a.g.Ci * a.g.sf, BM), (unsigned)a.g.B);
     hipLaunchKernelGGL((c2_dgrad_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
     ENCX_CHECK_LAUNCH();
@@ -742,7 +794,7 @@ struct WgPlan2 {
 };
 static WgPlan2 plan_wg2(const C2Geo& g) {
     WgPlan2 p;
-    p.BT = 64;
+    p.BT = WG_BT;
     const int Nall = g.T2 * g.Fo;
     p.NR = c2_rows(p.BT, g.Fo);
     p.RL = (min(p.BT, g.Fo) - 1) * g.sf + g.KF;
@@ -857,7 +909,8 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
     WgPlan2 p = plan_wg2(g);
     C2Wg a{g, dy, yact, x, ws, p.BT, p.NR, p.RL, p.NCmax, p.items, p.per_split, p.chunks};
     const int N = (int)(Ci * KT * KF + 1);
-    const size_t lds = ((size_t)p.BT * 32 + (size_t)p.NCmax * p.NR * p.RL) * sizeof(float) + p.BT * sizeof(int);
+    const size_t lds = ((size_t)4 * p.NCmax * p.NR + (size_t)p.BT * 32 + (size_t)p.NCmax * p.NR * p.RL) * sizeof(float) +
+                       p.BT * sizeof(int);
     if (p.narrow) {
         const size_t red = (size_t)4 * 16 * 64 * sizeof(float);  // all 4 waves' tiles
         hipLaunchKernelGGL((c2_wgrad_kernel<32, 64, 1, 2, 2>), dim3((unsigned)cdiv(N, 64), (unsigned)cdiv(Co, 32), p.splits),
