@@ -71,7 +71,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     extern __shared__ float smem[];
     const int CK = a.CK, S = a.s, Up = a.Up, K = a.K;
     float* Xs = smem;                       // [CK][S][Up]
-    float* Ws = smem + ((CK * S * Up + 3) & ~3);  // [K][CK][BM], 16-B aligned
+    float* Ws = smem + ((CK * S * Up + 3) & ~3);  // [CK][K][BM], 16-B aligned
     float* Bsm = Ws + K * CK * BM;          // [BM] bias of the block's rows
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
@@ -98,18 +98,32 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     const int nv = (woff + span + 3) >> 2;
     const int nitems = CK * nv;
     const int BM4 = BM / 4, nw = K * CK * BM4;
+    // item (cl, vi) of thread tid advances by NT items per step: no per-item division
+    const int dcl = NT / nv, dvi = NT - dcl * nv, cl_init = tid / nv, vi_init = tid - cl_init * nv;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
         // SPER items per thread in flight: interior items load as float4 from a clamped address
         // (value selected after the load), the rare items straddling a row end are patched
         // per element afterwards, then everything goes to LDS
+        int cl_n = cl_init, vi_n = vi_init;
         for (int it0 = 0; it0 < nitems; it0 += NT * SPER) {
             f32x4 v[SPER];
+            int clq[SPER], viq[SPER];
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
-                const int it = it0 + q * NT + tid;
-                const int cl = it / nv, vi = it - cl * nv, c = c0 + cl, p = ab + 4 * vi;
-                const bool ok = it < nitems && c < cend;
+                clq[q] = cl_n;
+                viq[q] = vi_n;
+                vi_n += dvi;
+                cl_n += dcl;
+                if (vi_n >= nv) {
+                    vi_n -= nv;
+                    ++cl_n;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int c = c0 + clq[q], p = ab + 4 * viq[q];
+                const bool ok = clq[q] < CK && c < cend;
                 v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
                 if (a.vec) {
                     const int pc = p < 0 ? 0 : (p > a.Tin - 4 ? a.Tin - 4 : p);
@@ -119,9 +133,8 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
             }
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
-                const int it = it0 + q * NT + tid;
-                const int cl = it / nv, vi = it - cl * nv, c = c0 + cl, p = ab + 4 * vi;
-                if (it < nitems && c < cend && !(a.vec && p >= 0 && p + 3 < a.Tin)) {
+                const int c = c0 + clq[q], p = ab + 4 * viq[q];
+                if (clq[q] < CK && c < cend && !(a.vec && p >= 0 && p + 3 < a.Tin)) {
                     const float* xr = xb + (int64_t)c * a.Tin;
                     for (int e = 0; e < 4; ++e) {
                         const int m = pad_src(p + e + a.pl, a.pl, a.Tin, a.e, a.mode);
@@ -131,11 +144,9 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
             }
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
-                const int it = it0 + q * NT + tid;
-                if (it >= nitems) continue;
-                const int cl = it / nv, vi = it - cl * nv;
-                float* xs = Xs + cl * span;
-                const int q0 = 4 * vi - woff;
+                if (clq[q] >= CK) continue;
+                float* xs = Xs + clq[q] * span;
+                const int q0 = 4 * viq[q] - woff;
                 if (S == 1 && q0 >= 0 && q0 + 3 < span) {
                     xs[q0] = act_apply(a.act, v[q][0]);
                     xs[q0 + 1] = act_apply(a.act, v[q][1]);
@@ -152,45 +163,43 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
                 }
             }
         }
-        // weights [k][ci][co] from wf[ci][k][co]: BM contiguous co per row, float4 items
+        // weights Ws[cl][k][co] = wf[c0 + cl][k][co0 + co]: rows (cl, k) are consecutive rows of
+        // wf, BM contiguous co per row, float4 items
+        const int wrows = (min(cend, c0 + CK) - c0) * K;
         for (int it0 = 0; it0 < nw; it0 += NT * SPER) {
             f32x4 v[SPER];
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
                 const int it = it0 + q * NT + tid;
-                const int r = it / BM4, c4 = it - r * BM4, k = r / CK, cl = r - k * CK;
-                const int c = c0 + cl, co = co0 + 4 * c4;
-                const bool ok = it < nw && c < cend;
+                const int r = it / BM4, c4 = it - r * BM4, co = co0 + 4 * c4;
+                const bool ok = r < wrows;
+                const float* wr = a.wf + ((int64_t)c0 * K + (ok ? r : 0)) * a.Cout;
                 v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
                 if (a.vec) {
                     const int coc = co + 3 < a.Cout ? co : a.Cout - 4;
-                    const f32x4 t = *(const f32x4*)(a.wf + ((int64_t)(ok ? c : cbeg) * K + (ok ? k : 0)) * a.Cout + coc);
+                    const f32x4 t = *(const f32x4*)(wr + coc);
                     if (ok && co + 3 < a.Cout) v[q] = t;
                 } else if (ok) {
-                    const float* wr = a.wf + ((int64_t)c * K + k) * a.Cout + co;
-                    for (int e = 0; e < 4; ++e) v[q][e] = co + e < a.Cout ? wr[e] : 0.f;
+                    for (int e = 0; e < 4; ++e) v[q][e] = co + e < a.Cout ? wr[co + e] : 0.f;
                 }
             }
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
                 const int it = it0 + q * NT + tid;
-                if (it < nw) {
-                    const int r = it / BM4, c4 = it - r * BM4;
-                    *(f32x4*)(Ws + r * BM + 4 * c4) = v[q];
-                }
+                if (it < nw) *(f32x4*)(Ws + 4 * it) = v[q];
             }
         }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
         for (int k = 0; k < K; ++k) {
             const int kd = k * a.d, ph = kd % S, off = kd / S;
-            const float* wk = Ws + (k * CK + h) * BM + wm0 + l32;
+            const float* wk = Ws + (h * K + k) * BM + wm0 + l32;
             const float* xk = Xs + (h * S + ph) * Up + wn0 + l32 + off;
 #pragma unroll 4
             for (int cp = 0; cp < CK; cp += 2) {
                 float av[TM], bv[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = wk[cp * BM + i * 32];
+                for (int i = 0; i < TM; ++i) av[i] = wk[cp * K * BM + i * 32];
 #pragma unroll
                 for (int j = 0; j < TN; ++j) bv[j] = xk[cp * S * Up + j * 32];
 #pragma unroll
@@ -294,7 +303,7 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
     const int CK = a.CK, J = a.J, Ub = a.Ub, S = a.s;
     const int M = a.Co * S;
     float* Xs = smem;                               // [CK][Ub]
-    float* As = smem + ((CK * Ub + 3) & ~3);        // [J][CK][BM], 16-B aligned
+    float* As = smem + ((CK * Ub + 3) & ~3);        // [CK][J][BM], 16-B aligned
     float* Bsm = As + J * CK * BM;                  // [BM] per-row bias (ConvTranspose1d mode)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
@@ -316,16 +325,30 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
     const int wb = u0 - (J - 1), ab = wb & ~3, woff = wb - ab;
     const int nv = (woff + wlen + 3) >> 2, nitems = CK * nv;
     const int BM4 = BM / 4, nw = J * CK * BM4;
+    const int dcl = NT / nv, dvi = NT - dcl * nv, cl_init = tid / nv, vi_init = tid - cl_init * nv;
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
-        // batched staging as in conv_fwd_kernel: SPER float4 loads in flight per thread
+        // batched staging as in conv_fwd_kernel: SPER float4 loads in flight per thread, items
+        // walked by a fixed step (no per-item division)
+        int cl_n = cl_init, vi_n = vi_init;
         for (int it0 = 0; it0 < nitems; it0 += NT * SPER) {
             f32x4 v[SPER];
+            int clq[SPER], viq[SPER];
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
-                const int it = it0 + q * NT + tid;
-                const int cl = it / nv, vi = it - cl * nv, c = c0 + cl, p = ab + 4 * vi;
-                const bool ok = it < nitems && c < cend;
+                clq[q] = cl_n;
+                viq[q] = vi_n;
+                vi_n += dvi;
+                cl_n += dcl;
+                if (vi_n >= nv) {
+                    vi_n -= nv;
+                    ++cl_n;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SPER; ++q) {
+                const int c = c0 + clq[q], p = ab + 4 * viq[q];
+                const bool ok = clq[q] < CK && c < cend;
                 v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
                 if (a.vec) {
                     const int pc = p < 0 ? 0 : (p > a.Tin - 4 ? a.Tin - 4 : p);
@@ -335,63 +358,58 @@ __global__ __launch_bounds__(NT) void conv_poly_kernel(PolyArgs a) {
             }
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
-                const int it = it0 + q * NT + tid;
-                const int cl = it / nv, vi = it - cl * nv, c = c0 + cl, p = ab + 4 * vi;
-                if (it < nitems && c < cend && !(a.vec && p >= 0 && p + 3 < a.Tin)) {
+                const int c = c0 + clq[q], p = ab + 4 * viq[q];
+                if (clq[q] < CK && c < cend && !(a.vec && p >= 0 && p + 3 < a.Tin)) {
                     const float* ir = ib + (int64_t)c * a.Tin;
                     for (int e = 0; e < 4; ++e) v[q][e] = (p + e >= 0 && p + e < a.Tin) ? ir[p + e] : 0.f;
                 }
             }
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
-                const int it = it0 + q * NT + tid;
-                if (it >= nitems) continue;
-                const int cl = it / nv, vi = it - cl * nv;
-                float* xs = Xs + cl * Ub;
-                const int q0 = 4 * vi - woff;
+                if (clq[q] >= CK) continue;
+                float* xs = Xs + clq[q] * Ub;
+                const int q0 = 4 * viq[q] - woff;
                 for (int e = 0; e < 4; ++e) {
                     const int qq = q0 + e;
                     if (qq >= 0 && qq < wlen) xs[qq] = act_apply(a.in_act, v[q][e]);
                 }
             }
         }
+        // As[cl][q][m] = wp[c0 + cl][q][m0 + m]: consecutive rows of wp, float4 items
+        const int wrows = (min(cend, c0 + CK) - c0) * J;
         for (int it0 = 0; it0 < nw; it0 += NT * SPER) {
             f32x4 v[SPER];
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
                 const int it = it0 + q * NT + tid;
-                const int r = it / BM4, c4 = it - r * BM4, qj = r / CK, cl = r - qj * CK;
-                const int c = c0 + cl, m = m0 + 4 * c4;
-                const bool ok = it < nw && c < cend;
+                const int r = it / BM4, c4 = it - r * BM4, m = m0 + 4 * c4;
+                const bool ok = r < wrows;
+                const float* wr = a.wp + ((int64_t)c0 * J + (ok ? r : 0)) * M;
                 v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
                 if (a.vec) {
                     const int mc = m + 3 < M ? m : M - 4;
-                    const f32x4 t = *(const f32x4*)(a.wp + ((int64_t)(ok ? c : cbeg) * J + (ok ? qj : 0)) * M + mc);
+                    const f32x4 t = *(const f32x4*)(wr + mc);
                     if (ok && m + 3 < M) v[q] = t;
                 } else if (ok) {
-                    const float* wr = a.wp + ((int64_t)c * J + qj) * M + m;
-                    for (int e = 0; e < 4; ++e) v[q][e] = m + e < M ? wr[e] : 0.f;
+                    for (int e = 0; e < 4; ++e) v[q][e] = m + e < M ? wr[m + e] : 0.f;
                 }
             }
 #pragma unroll
             for (int q = 0; q < SPER; ++q) {
                 const int it = it0 + q * NT + tid;
-                if (it < nw) {
-                    const int r = it / BM4, c4 = it - r * BM4;
-                    *(f32x4*)(As + r * BM + 4 * c4) = v[q];
-                }
+                if (it < nw) *(f32x4*)(As + 4 * it) = v[q];
             }
         }
         __syncthreads();
         const int h = lane >> 5, l32 = lane & 31;
         for (int q = 0; q < J; ++q) {
-            const float* aq = As + (q * CK + h) * BM + wm0 + l32;
+            const float* aq = As + (h * J + q) * BM + wm0 + l32;
             const float* xq = Xs + h * Ub + wn0 + l32 + (J - 1) - q;
 #pragma unroll 4
             for (int cp = 0; cp < CK; cp += 2) {
                 float av[TM], bv[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = aq[cp * BM + i * 32];
+                for (int i = 0; i < TM; ++i) av[i] = aq[cp * J * BM + i * 32];
 #pragma unroll
                 for (int j = 0; j < TN; ++j) bv[j] = xq[cp * Ub + j * 32];
 #pragma unroll
