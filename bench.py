@@ -158,8 +158,17 @@ def main():
                 ms, fl, by, launches = ms + m_.value, fl + f_.value, by + b_.value, launches + 1
         lib.encx_prof_enable(0)
         achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        # traffic: HBM bytes per conv-family ABI call from the committed rocprofv3 PMC passes
+        # (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic.py); null when no pass exists for the config
+        traffic = None
+        tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01',
+                             f'traffic_{args.config}.json')
+        if os.path.exists(tpath) and launches:
+            with open(tpath) as fh:
+                traffic = round(json.load(fh)['hbm_bytes_per_step'] / (launches / args.steps))
         roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MI355X_FP32_PEAK_TFLOPS,
-                'unit': 'TFLOP/s', 'frac': round(achieved / MI355X_FP32_PEAK_TFLOPS, 4), 'traffic': None,
+                'unit': 'TFLOP/s', 'frac': round(achieved / MI355X_FP32_PEAK_TFLOPS, 4), 'traffic': traffic,
+                'algorithmic_bytes_per_launch': round(by / launches) if launches else None,
                 'kernel': 'encx conv/convtr fwd + bwd-data + bwd-weight (implicit-GEMM f32 MFMA)',
                 'launches': launches, 'kernel_ms_per_step': round(ms / args.steps, 3),
                 'algorithmic_bytes_per_step': by / args.steps,

@@ -1,0 +1,70 @@
+"""HBM traffic of the conv family (the bench's roofline kernel family) from rocprofv3 PMC passes.
+
+    python tools/traffic.py --fetch gpurun_out/pmcF --write gpurun_out/pmcW --steps 3 \
+        --config gen --out profiles/r01/traffic_gen.json
+
+--fetch / --write: output dirs of `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs (one
+counter block per pass) of `bench.py --steps S --warmup W --no-roofline`; --steps = S + W (every
+train step the profiled process ran). Corrections as in MI355X_MICROARCH.md "HBM": counters are in
+KiB; FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B). The result is per train step
+and per conv-family ABI call (bench.py reads it into roofline.traffic)."""
+import argparse
+import collections
+import csv
+import json
+import re
+
+# kernels launched by the conv / convtr / conv2d ABI entry points (csrc/conv1d.hip, disc.hip)
+FAMILY = re.compile(r'conv_fwd_kernel|conv_poly_kernel|conv_wgrad_kernel|wgrad_reduce|conv_fwd_reduce|'
+                    r'conv_poly_reduce|conv_fold_edges|LdConvFlat|LdPolyFlat|c2_fwd_kernel|c2_dgrad|'
+                    r'c2_wgrad_kernel|c2_wg_reduce')
+
+
+def per_dispatch(d, counter):
+    out = collections.defaultdict(float)
+    names = {}
+    for r in csv.DictReader(open(f'{d}/run_counter_collection.csv')):
+        if r['Counter_Name'] != counter:
+            continue
+        key = int(r['Dispatch_Id'])
+        out[key] += float(r['Counter_Value'])
+        names[key] = r['Kernel_Name']
+    return out, names
+
+
+def family_kib(d, counter):
+    vals, names = per_dispatch(d, counter)
+    tot, n = 0.0, 0
+    for k, v in vals.items():
+        if FAMILY.search(names[k]):
+            tot += v
+            n += 1
+    return tot, n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--fetch', required=True)
+    ap.add_argument('--write', required=True)
+    ap.add_argument('--steps', type=int, required=True)
+    ap.add_argument('--config', default='gen')
+    ap.add_argument('--calls-per-step', type=int, default=None,
+                    help='conv-family ABI calls per step (bench roofline "launches" / steps)')
+    ap.add_argument('--out', required=True)
+    args = ap.parse_args()
+    f_kib, nf = family_kib(args.fetch, 'FETCH_SIZE')
+    w_kib, nw = family_kib(args.write, 'WRITE_SIZE')
+    fetch = 2.0 * f_kib * 1024 / args.steps
+    write = w_kib * 1024 / args.steps
+    res = {'config': args.config, 'fetch_bytes_per_step': fetch, 'write_bytes_per_step': write,
+           'hbm_bytes_per_step': fetch + write, 'kernel_dispatches_per_step': nf / args.steps,
+           'correction': 'FETCH_SIZE x2 (gfx950), KiB -> bytes', 'steps_profiled': args.steps}
+    if args.calls_per_step:
+        res['abi_calls_per_step'] = args.calls_per_step
+        res['hbm_bytes_per_call'] = (fetch + write) / args.calls_per_step
+    json.dump(res, open(args.out, 'w'), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == '__main__':
+    main()
