@@ -557,84 +557,109 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     // is the same for every chunk
     const int woff = (4 - (a.pl & 3)) & 3;
     const int nv = (woff + WL + 3) >> 2, nr = a.NCmax * nv;
+    const int dal = NT / BT4, dti = NT - dal * BT4, lal0 = tid / BT4, lti0 = tid - lal0 * BT4;
+    const int dcr = NT / nv, dvr = NT - dcr * nv, rcr0 = tid / nv, rvi0 = tid - rcr0 * nv;
     for (int it = it_beg; it < it_end; ++it) {
         const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
         const float* Lb = a.L + (int64_t)b * a.A * a.Tl;
         const float* Rb = a.R + (int64_t)b * a.C * a.Tr;
         __syncthreads();
-        // batched staging as in conv_fwd_kernel: SPER float4 loads in flight per thread
-        for (int i0 = 0; i0 < nl; i0 += NT * SPER) {
-            f32x4 v[SPER];
+        // batched staging as in conv_fwd_kernel: SPER float4 loads in flight per thread; items
+        // (row, column) walked by a fixed step of NT (no per-item division)
+        {
+            int al_n = lal0, ti_n = lti0;
+            for (int i0 = 0; i0 < nl; i0 += NT * SPER) {
+                f32x4 v[SPER];
+                int alq[SPER], tq[SPER];
 #pragma unroll
-            for (int q = 0; q < SPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int al = i / BT4, t = tc + 4 * (i - al * BT4), aa = a0 + al;
-                const bool ok = i < nl && aa < a.A;
-                v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
-                if (a.vec) {
-                    const int tcl = t + 3 < a.Tl ? t : a.Tl - 4;
-                    const f32x4 x = *(const f32x4*)(Lb + (int64_t)(ok ? aa : a0) * a.Tl + tcl);
-                    if (ok && t + 3 < a.Tl) v[q] = x;
+                for (int q = 0; q < SPER; ++q) {
+                    alq[q] = al_n;
+                    tq[q] = tc + 4 * ti_n;
+                    ti_n += dti;
+                    al_n += dal;
+                    if (ti_n >= BT4) {
+                        ti_n -= BT4;
+                        ++al_n;
+                    }
                 }
-            }
 #pragma unroll
-            for (int q = 0; q < SPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int al = i / BT4, t = tc + 4 * (i - al * BT4), aa = a0 + al;
-                if (i < nl && aa < a.A && !(a.vec && t + 3 < a.Tl)) {
-                    const float* lr = Lb + (int64_t)aa * a.Tl;
-                    for (int e = 0; e < 4; ++e) v[q][e] = t + e < a.Tl ? lr[t + e] : 0.f;
+                for (int q = 0; q < SPER; ++q) {
+                    const int t = tq[q], aa = a0 + alq[q];
+                    const bool ok = alq[q] < BM && aa < a.A;
+                    v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                    if (a.vec) {
+                        const int tcl = t + 3 < a.Tl ? t : a.Tl - 4;
+                        const f32x4 x = *(const f32x4*)(Lb + (int64_t)(ok ? aa : a0) * a.Tl + tcl);
+                        if (ok && t + 3 < a.Tl) v[q] = x;
+                    }
                 }
-            }
 #pragma unroll
-            for (int q = 0; q < SPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                if (i >= nl) continue;
-                const int al = i / BT4, t = tc + 4 * (i - al * BT4);
-                float* ls = Ls + al * BTp + (t - tc);
-                ls[0] = act_apply(a.actL, v[q][0]);
-                ls[1] = act_apply(a.actL, v[q][1]);
-                ls[2] = act_apply(a.actL, v[q][2]);
-                ls[3] = act_apply(a.actL, v[q][3]);
+                for (int q = 0; q < SPER; ++q) {
+                    const int t = tq[q], aa = a0 + alq[q];
+                    if (alq[q] < BM && aa < a.A && !(a.vec && t + 3 < a.Tl)) {
+                        const float* lr = Lb + (int64_t)aa * a.Tl;
+                        for (int e = 0; e < 4; ++e) v[q][e] = t + e < a.Tl ? lr[t + e] : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < SPER; ++q) {
+                    if (alq[q] >= BM) continue;
+                    float* ls = Ls + alq[q] * BTp + (tq[q] - tc);
+                    ls[0] = act_apply(a.actL, v[q][0]);
+                    ls[1] = act_apply(a.actL, v[q][1]);
+                    ls[2] = act_apply(a.actL, v[q][2]);
+                    ls[3] = act_apply(a.actL, v[q][3]);
+                }
             }
         }
         const int base = tc * a.s - a.pl - woff;  // input index of the first item's element 0
-        for (int i0 = 0; i0 < nr; i0 += NT * SPER) {
-            f32x4 v[SPER];
+        {
+            int cr_n = rcr0, vi_n = rvi0;
+            for (int i0 = 0; i0 < nr; i0 += NT * SPER) {
+                f32x4 v[SPER];
+                int crq[SPER], viq[SPER];
 #pragma unroll
-            for (int q = 0; q < SPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int cr = i / nv, vi = i - cr * nv, c = c_first + cr, p = base + 4 * vi;
-                const bool ok = i < nr && c < a.C;
-                v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
-                if (a.vec) {
-                    const int pc = p < 0 ? 0 : (p > a.Tr - 4 ? a.Tr - 4 : p);
-                    const f32x4 x = *(const f32x4*)(Rb + (int64_t)(ok ? c : c_first) * a.Tr + pc);
-                    if (ok && p >= 0 && p + 3 < a.Tr) v[q] = x;
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < SPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                const int cr = i / nv, vi = i - cr * nv, c = c_first + cr, p = base + 4 * vi;
-                if (i < nr && c < a.C && !(a.vec && p >= 0 && p + 3 < a.Tr)) {
-                    const float* rr = Rb + (int64_t)c * a.Tr;
-                    for (int e = 0; e < 4; ++e) {
-                        const int m = pad_src(p + e + a.pl, a.pl, a.Tr, a.e, a.mode);
-                        v[q][e] = m >= 0 ? rr[m] : 0.f;
+                for (int q = 0; q < SPER; ++q) {
+                    crq[q] = cr_n;
+                    viq[q] = vi_n;
+                    vi_n += dvr;
+                    cr_n += dcr;
+                    if (vi_n >= nv) {
+                        vi_n -= nv;
+                        ++cr_n;
                     }
                 }
-            }
 #pragma unroll
-            for (int q = 0; q < SPER; ++q) {
-                const int i = i0 + q * NT + tid;
-                if (i >= nr) continue;
-                const int cr = i / nv, vi = i - cr * nv;
-                float* rs = Rs + cr * WLp;
-                const int q0 = 4 * vi - woff;
-                for (int e = 0; e < 4; ++e) {
-                    const int qq = q0 + e;
-                    if (qq >= 0 && qq < WL) rs[qq] = act_apply(a.actR, v[q][e]);
+                for (int q = 0; q < SPER; ++q) {
+                    const int c = c_first + crq[q], p = base + 4 * viq[q];
+                    const bool ok = crq[q] < a.NCmax && c < a.C;
+                    v[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                    if (a.vec) {
+                        const int pc = p < 0 ? 0 : (p > a.Tr - 4 ? a.Tr - 4 : p);
+                        const f32x4 x = *(const f32x4*)(Rb + (int64_t)(ok ? c : c_first) * a.Tr + pc);
+                        if (ok && p >= 0 && p + 3 < a.Tr) v[q] = x;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < SPER; ++q) {
+                    const int c = c_first + crq[q], p = base + 4 * viq[q];
+                    if (crq[q] < a.NCmax && c < a.C && !(a.vec && p >= 0 && p + 3 < a.Tr)) {
+                        const float* rr = Rb + (int64_t)c * a.Tr;
+                        for (int e = 0; e < 4; ++e) {
+                            const int m = pad_src(p + e + a.pl, a.pl, a.Tr, a.e, a.mode);
+                            v[q][e] = m >= 0 ? rr[m] : 0.f;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < SPER; ++q) {
+                    if (crq[q] >= a.NCmax) continue;
+                    float* rs = Rs + crq[q] * WLp;
+                    const int q0 = 4 * viq[q] - woff;
+                    for (int e = 0; e < 4; ++e) {
+                        const int qq = q0 + e;
+                        if (qq >= 0 && qq < WL) rs[qq] = act_apply(a.actR, v[q][e]);
+                    }
                 }
             }
         }
