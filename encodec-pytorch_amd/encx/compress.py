@@ -1,0 +1,112 @@
+"""compress.py of the reference: waveform <-> `.ecdc` bytes through the encx HIP path.
+
+Encode (SEANet encoder + RVQ argmin) and decode (RVQ gather + SEANet decoder) run the encx
+kernels; each frame's codes are packed / unpacked on the GPU (csrc/bitstream.hip) and only the
+packed bytes cross PCIe. Byte format, metadata keys and error behaviour follow
+compress.py:30-191; `use_lm=True` (the remote-only pretrained LM entropy coder,
+quantization/ac.py) is out of scope and raises.
+"""
+import io
+import struct
+import typing as tp
+
+import torch
+
+from . import binary, ops
+from .model import EncodecModel, EncodedFrame
+
+MODELS = {  # compress.py:21-26
+    'encodec_24khz': EncodecModel.encodec_model_24khz,
+    'encodec_48khz': EncodecModel.encodec_model_48khz,
+    'my_encodec': EncodecModel.my_encodec_model,
+    'encodec_bw': EncodecModel.encodec_model_bw,
+}
+
+
+def _model_device(model):
+    return next(model.parameters()).device
+
+
+def _no_lm():
+    raise NotImplementedError('encx: use_lm=True needs the pretrained LM entropy coder '
+                              '(remote-only checkpoint, quantization/ac.py); use use_lm=False')
+
+
+def compress_to_file(model: EncodecModel, wav: torch.Tensor, fo: tp.IO[bytes], use_lm: bool = True):
+    """compress.py:30-101: header, then per frame the '!f' scale (normalising models) and the
+    frame's codes bit-packed t-major at model.bits_per_codebook bits, flushed per frame."""
+    assert wav.dim() == 2, "Only single waveform can be encoded."
+    if model.name not in MODELS:
+        raise ValueError(f"The provided model {model.name} is not supported.")
+    if use_lm:
+        _no_lm()
+    with torch.no_grad():
+        frames = model.encode(wav[None].to(_model_device(model), torch.float32))
+    metadata = {
+        'm': model.name,
+        'al': wav.shape[-1],
+        'nc': frames[0][0].shape[1],
+        'lm': use_lm,
+        'fr': frames[0][0].shape[2],
+    }
+    binary.write_ecdc_header(fo, metadata)
+    # pack every frame on the device, then one copy of all payloads (and scales) to the host
+    packed = [ops.pack_codes(frame, model.bits_per_codebook) for frame, _ in frames]
+    scales = [s.reshape(-1)[:1] for _, s in frames if s is not None]
+    host = [d.cpu() for d, _ in packed]
+    if any(int(err.item()) for _, err in packed):
+        raise ValueError(f'codes do not fit in {model.bits_per_codebook} bits')
+    scales = torch.cat(scales).cpu().tolist() if scales else []
+    si = 0
+    for (frame, scale), data in zip(frames, host):
+        if scale is not None:
+            fo.write(struct.pack('!f', scales[si]))
+            si += 1
+        fo.write(data.numpy().tobytes())
+    fo.flush()
+
+
+def decompress_from_file(model: EncodecModel, fo: tp.IO[bytes], device='cpu') -> tp.Tuple[torch.Tensor, int]:
+    """compress.py:104-162. Decoding runs on the model's GPU; the waveform comes back on the
+    host, as the reference returns it for both of its devices (compress.py:158-161). As in the
+    reference, every segment is read with the header's frame count `fr` (compress.py:126) and
+    the model check looks at `model.name` (compress.py:118)."""
+    metadata = binary.read_ecdc_header(fo)
+    model_name = metadata['m']
+    audio_length = metadata['al']
+    num_codebooks = metadata['nc']
+    use_lm = metadata['lm']
+    assert isinstance(audio_length, int)
+    assert isinstance(num_codebooks, int)
+    if model.name not in MODELS:
+        raise ValueError(f"The audio was compressed with an unsupported model {model_name}.")
+    if use_lm:
+        _no_lm()
+    dev = _model_device(model)
+    frames: tp.List[EncodedFrame] = []
+    segment_length = model.segment_length or audio_length
+    segment_stride = model.segment_stride or audio_length
+    for offset in range(0, audio_length, segment_stride):
+        frame_length = metadata['fr']
+        if model.normalize:
+            scale_f, = struct.unpack('!f', binary._read_exactly(fo, struct.calcsize('!f')))
+            scale = torch.tensor(scale_f, device=dev).view(1)
+        else:
+            scale = None
+        unpacker = binary.BitUnpacker(model.bits_per_codebook, fo, device=dev)
+        frames.append((unpacker.pull_frame(num_codebooks, frame_length)[None], scale))
+    with torch.no_grad():
+        wav = model.decode(frames)
+    return wav[0, :, :audio_length].cpu(), model.sample_rate
+
+
+def compress(model: EncodecModel, wav: torch.Tensor, use_lm: bool = False) -> bytes:
+    """compress.py:165-179."""
+    fo = io.BytesIO()
+    compress_to_file(model, wav, fo, use_lm=use_lm)
+    return fo.getvalue()
+
+
+def decompress(model: EncodecModel, compressed: bytes, device='cuda') -> tp.Tuple[torch.Tensor, int]:
+    """compress.py:182-191."""
+    return decompress_from_file(model, io.BytesIO(compressed), device=device)

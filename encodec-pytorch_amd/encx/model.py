@@ -159,6 +159,34 @@ class EncodecModel(nn.Module):
         return model
 
     @staticmethod
+    def _load_checkpoint(model, checkpoint):
+        """model.py:346-349: a trainer checkpoint's 'model_state_dict', with the old
+        'quantizer.model' prefix renamed. Loaded with weights_only=True (no unpickling)."""
+        import os
+        assert os.path.exists(checkpoint), "checkpoint not exists"
+        pre_dic = torch.load(checkpoint, map_location='cpu', weights_only=True)['model_state_dict']
+        model.load_state_dict({k.replace('quantizer.model', 'quantizer.vq'): v for k, v in pre_dic.items()})
+        model.eval()
+        return model
+
+    @staticmethod
+    def my_encodec_model(checkpoint: str, ratios=[8, 5, 4, 2]):
+        """model.py:332-349: 24 kHz mono, non-causal, time_group_norm, normalised, no segments."""
+        model = EncodecModel._get_model([1.5, 3., 6, 12., 24.], 24_000, 1, causal=False,
+                                        model_norm='time_group_norm', audio_normalize=True,
+                                        segment=None, name='my_encodec', ratios=ratios)
+        return EncodecModel._load_checkpoint(model, checkpoint)
+
+    @staticmethod
+    def encodec_model_bw(checkpoint: str, bandwidth: float):
+        """model.py:351-369: as my_encodec_model with 1 s segments and target_bandwidths =
+        `bandwidth` (the reference passes it through unwrapped; a list is expected)."""
+        model = EncodecModel._get_model(bandwidth, 24_000, 1, causal=False,
+                                        model_norm='time_group_norm', audio_normalize=True,
+                                        segment=1., name='my_encodec')
+        return EncodecModel._load_checkpoint(model, checkpoint)
+
+    @staticmethod
     def encodec_model_48khz(pretrained: bool = False, repository=None):
         """model.py:311-329 architecture: 48 kHz stereo, non-causal, time_group_norm, 1 s
         segments (pretrained weights are remote-only: out of scope)."""

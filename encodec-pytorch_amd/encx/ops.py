@@ -826,3 +826,41 @@ def linear_overlap_add(frames, stride):
     if len(frames) == 1:
         return frames[0]
     return OverlapAddFn.apply(stride, *frames)
+
+
+# ---------------------------------------------------------------------------- .ecdc payload
+def pack_codes(codes, bits):
+    """BitPacker over whole frames (binary.py:55-88, push order compress.py:88-98): codes
+    [F][K][T] int64 on the GPU (any strides) -> uint8 [F][ceil(K*T*bits/8)] on the GPU, each
+    frame its own byte-aligned stream. Raises ValueError if a code does not fit in `bits`."""
+    if not codes.is_cuda or codes.dtype != torch.int64 or codes.dim() != 3:
+        raise RuntimeError('encx: pack_codes takes int64 [F][K][T] codes on the GPU (no CPU fallback)')
+    ensure_device(codes.device)
+    Fn, K, T = codes.shape
+    nbytes = int(lib.encx_bitpack_bytes(K * T, int(bits)))
+    if nbytes < 0:
+        raise ValueError(f'encx: bits must be in 1..32 (got {bits})')
+    out = torch.empty(Fn, nbytes, device=codes.device, dtype=torch.uint8)
+    err = torch.zeros(1, device=codes.device, dtype=torch.int32)
+    s_f, s_k, s_t = codes.stride()
+    call('encx_bitpack', codes.data_ptr(), s_f, s_k, s_t, Fn, K, T, int(bits), out.data_ptr(), nbytes,
+         err.data_ptr(), stream())
+    return out, err
+
+
+def unpack_codes(data, K, T, bits):
+    """BitUnpacker.pull (binary.py:105-123) of F frames: data uint8 [F][>= ceil(K*T*bits/8)]
+    on the GPU -> int64 codes [F][K][T]."""
+    if not data.is_cuda or data.dtype != torch.uint8 or data.dim() != 2 or not data.is_contiguous():
+        raise RuntimeError('encx: unpack_codes takes contiguous uint8 [F][bytes] on the GPU (no CPU fallback)')
+    ensure_device(data.device)
+    Fn = data.shape[0]
+    need = int(lib.encx_bitpack_bytes(K * T, int(bits)))
+    if need < 0:
+        raise ValueError(f'encx: bits must be in 1..32 (got {bits})')
+    if data.shape[1] < need:
+        raise EOFError('The stream ended sooner than expected.')
+    codes = torch.empty(Fn, K, T, device=data.device, dtype=torch.int64)
+    call('encx_bitunpack', data.data_ptr(), data.shape[1], Fn, K, T, int(bits), codes.data_ptr(),
+         K * T, T, 1, stream())
+    return codes

@@ -339,6 +339,24 @@ int encx_overlap_add(const float* const* frames, const int64_t* lengths, int nf,
 int encx_overlap_add_bwd(const float* dout, int nf, int64_t stride, int64_t L0, int64_t BC, int64_t total, int k,
                          int64_t len, float* dframe, encx_stream_t stream);
 
+/* ------------------------------------------------------- .ecdc payload (binary.py, compress.py)
+ * The codes of one encoded frame [K][T] are pushed t-major, then codebook (compress.py:88-98),
+ * each as `bits` bits of a little-endian bit stream (BitPacker, binary.py:55-88); flush emits the
+ * last partial byte, so a frame of n = K*T codes is encx_bitpack_bytes(n, bits) = ceil(n*bits/8)
+ * bytes (-1 for bits outside 1..32). Codes are int64 addressed as codes[item*s_item + k*s_k +
+ * t*s_t] (any strides, e.g. the transposed view EncodecModel.encode returns); `items` frames of
+ * equal (K, T) go in one launch, frame i at out + i*out_stride. *err (device int, caller
+ * zeroed) gets 1 if a code is >= 2^bits, which the reference would silently mis-pack. */
+int64_t encx_bitpack_bytes(int64_t n_values, int bits);
+int encx_bitpack(const int64_t* codes, int64_t s_item, int64_t s_k, int64_t s_t, int64_t items,
+                 int64_t K, int64_t T, int bits, uint8_t* out, int64_t out_stride, int* err,
+                 encx_stream_t stream);
+/* BitUnpacker.pull (binary.py:105-123) for n = K*T codes of each of `items` frames, frame i's
+ * bytes at in + i*in_stride (in_stride >= ceil(n*bits/8)). */
+int encx_bitunpack(const uint8_t* in, int64_t in_stride, int64_t items, int64_t K, int64_t T,
+                   int bits, int64_t* codes, int64_t s_item, int64_t s_k, int64_t s_t,
+                   encx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

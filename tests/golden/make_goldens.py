@@ -14,6 +14,8 @@ Fixture map:
   g6_balancer.npz  Balancer known-answer test (balancer.py:121-139) + a 4-loss case
   g7_step.npz      one full train step (gen-only and GAN), B 2, T 4800, n_q 2
   g8_sched.npz     WarmupCosineLrScheduler learning-rate trace
+  g10_ecdc.npz     .ecdc: reference BitPacker vectors (bits 1..32), header, compress/decompress
+                   bytes + waves for the g1 model and the g9 48 kHz model (one / two segments)
   g9_step48k.npz   config-5 analogue: 48 kHz stereo, non-causal, time_group_norm, segment 0.1 s
                    (two frames: 4800 + 48 samples, linear overlap-add), gen-only and GAN steps
 """
@@ -452,8 +454,96 @@ def g8():
     save('g8_sched.npz', lr=np.array(lrs))
 
 
+# ------------------------------------------------------------------------------------ G10
+# (bits, count) cases for the reference BitPacker: the model's 10 bits, the reference test's
+# 1..15 range (binary.py:130-147), the ABI's 16..32, empty / single-value / ragged counts
+G10_CASES = [(10, 600), (10, 1), (10, 0), (1, 13), (2, 5), (3, 1000), (7, 17), (8, 64), (9, 71),
+             (11, 333), (13, 999), (15, 257), (16, 100), (20, 77), (31, 9), (32, 33)]
+
+
+def g10():
+    import io
+    import binary as ref_binary
+    import compress as ref_compress
+    out = {}
+    g = rng(1010)
+    tokens, packed, ghosts = [], [], []
+    for bits, n in G10_CASES:
+        tok = g.integers(0, 1 << bits, size=n, dtype=np.int64)
+        buf = io.BytesIO()
+        pk = ref_binary.BitPacker(bits, buf)
+        for v in tok.tolist():
+            pk.push(v)
+        pk.flush()
+        b = buf.getvalue()
+        buf.seek(0)
+        up = ref_binary.BitUnpacker(bits, buf)
+        pulled = []
+        while True:
+            v = up.pull()
+            if v is None:
+                break
+            pulled.append(v)
+        assert pulled[:n] == tok.tolist()
+        tokens.append(tok)
+        packed.append(np.frombuffer(b, np.uint8))
+        ghosts.append(len(pulled) - n)
+    out['bp_cases'] = np.array(G10_CASES, np.int64)
+    out['bp_tokens'] = np.concatenate(tokens)
+    out['bp_bytes'] = np.concatenate(packed)
+    out['bp_nbytes'] = np.array([len(p) for p in packed], np.int64)
+    out['bp_ghosts'] = np.array(ghosts, np.int64)
+    hb = io.BytesIO()
+    ref_binary.write_ecdc_header(hb, {'m': 'encodec_24khz', 'al': 24000, 'nc': 2, 'lm': False, 'fr': 75})
+    out['header'] = np.frombuffer(hb.getvalue(), np.uint8)
+
+    # 24 kHz: the g1 model and clip, bandwidth 1.5 (n_q 2), one frame, no scale
+    d1 = np.load(os.path.join(HERE, 'g1_eval24k.npz'))
+    m = R.model.EncodecModel._get_model([1.5, 3., 6., 12., 24.], 24000, 1, causal=True,
+                                        model_norm='weight_norm', audio_normalize=False,
+                                        segment=None, name='encodec_24khz')
+    load_synth(m, 1)
+    fill_codebooks(m, d1['stats'], 77, 2)
+    m.eval()
+    m.set_target_bandwidth(1.5)
+    x = t(d1['x'])[0]
+    b24 = ref_compress.compress(m, x, use_lm=False)
+    with torch.no_grad():
+        y24, sr = ref_compress.decompress_from_file(m, io.BytesIO(b24), device='cpu')
+    out['c24_bytes'] = np.frombuffer(b24, np.uint8)
+    out['c24_y'] = y24.numpy()
+
+    # 48 kHz stereo, normalised, 0.1 s segments (the g9 model): a 4752-sample clip is one
+    # segment (scale + codes); a 4800-sample clip is two (4800 + 48), and decompress reads the
+    # short one with the first frame's length -> EOFError (compress.py:126, 137-138)
+    d9 = np.load(os.path.join(HERE, 'g9_step48k.npz'))
+    m = R.model.EncodecModel._get_model([3.0], 48000, 2, causal=False, model_norm='time_group_norm',
+                                        audio_normalize=True, segment=G9_SEG, name='encodec_48khz')
+    load_synth(m, 91)
+    fill_codebooks(m, d9['gen/stats'], 93, 2)
+    m.eval()
+    m.set_target_bandwidth(3.0)
+    w = t(synth_wave((2, 4800), 1011))
+    b48 = ref_compress.compress(m, w[:, :4752], use_lm=False)
+    with torch.no_grad():
+        y48, _ = ref_compress.decompress_from_file(m, io.BytesIO(b48), device='cpu')
+        codes48 = m.encode(w[None, :, :4752])[0][0]
+    out['c48_x'] = w.numpy()
+    out['c48_bytes'] = np.frombuffer(b48, np.uint8)
+    out['c48_y'] = y48.numpy()
+    out['c48_codes'] = codes48.numpy().astype(np.int16)
+    b48s = ref_compress.compress(m, w, use_lm=False)
+    out['c48s_bytes'] = np.frombuffer(b48s, np.uint8)
+    try:
+        ref_compress.decompress_from_file(m, io.BytesIO(b48s), device='cpu')
+        out['c48s_eof'] = np.array(0)
+    except EOFError:
+        out['c48s_eof'] = np.array(1)
+    save('g10_ecdc.npz', **out)
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9', 'g10']
     for w in which:
         torch.manual_seed(0)
         globals()[w]()
