@@ -110,3 +110,33 @@ def compress(model: EncodecModel, wav: torch.Tensor, use_lm: bool = False) -> by
 def decompress(model: EncodecModel, compressed: bytes, device='cuda') -> tp.Tuple[torch.Tensor, int]:
     """compress.py:182-191."""
     return decompress_from_file(model, io.BytesIO(compressed), device=device)
+
+
+def compress_batch(model: EncodecModel, wavs: torch.Tensor) -> tp.List[bytes]:
+    """Serving form of `compress(model, wavs[i], use_lm=False)` for a batch [B][C][T] of
+    equal-length clips: one encode over the batch, one pack launch per segment for all B
+    streams, one device->host copy; each element is a complete `.ecdc` file."""
+    assert wavs.dim() == 3, "expects [B, C, T]"
+    if model.name not in MODELS:
+        raise ValueError(f"The provided model {model.name} is not supported.")
+    B = wavs.shape[0]
+    with torch.no_grad():
+        frames = model.encode(wavs.to(_model_device(model), torch.float32))
+    bits = model.bits_per_codebook
+    packed = [ops.pack_codes(frame, bits) for frame, _ in frames]
+    datas = [d.cpu().numpy() for d, _ in packed]
+    if any(int(err.item()) for _, err in packed):
+        raise ValueError(f'codes do not fit in {bits} bits')
+    scales = [s.reshape(B).cpu().tolist() if s is not None else None for _, s in frames]
+    out = []
+    for b in range(B):
+        fo = io.BytesIO()
+        binary.write_ecdc_header(fo, {'m': model.name, 'al': wavs.shape[-1],
+                                      'nc': frames[0][0].shape[1], 'lm': False,
+                                      'fr': frames[0][0].shape[2]})
+        for data, sc in zip(datas, scales):
+            if sc is not None:
+                fo.write(struct.pack('!f', sc[b]))
+            fo.write(data[b].tobytes())
+        out.append(fo.getvalue())
+    return out

@@ -244,3 +244,24 @@ def test_gpu_compress_decompress_48k_fixture():
     assert len(mine_s) == len(d['c48s_bytes'])
     with pytest.raises(EOFError):
         C.decompress(m, d['c48s_bytes'].tobytes())
+
+
+@pytest.mark.gpu
+def test_gpu_compress_batch_matches_per_clip_compress():
+    """compress_batch's B files == compress() of each clip (same header, payload layout and
+    scale handling); codes may differ only where fp reassociation across batch shapes can
+    move a near-tie argmin."""
+    from encx import compress as C
+    m = _model48()
+    d = load('g10_ecdc.npz')
+    w = T(d['c48_x'])[:, :4752]
+    batch = torch.stack([w, 0.5 * w.flip(-1), -w])
+    blobs = C.compress_batch(m, batch)
+    for b in range(3):
+        single = C.compress(m, batch[b])
+        assert len(blobs[b]) == len(single)
+        meta_b, fb = E.decompress_codes(blobs[b], 10, 1, True)
+        meta_s, fs = E.decompress_codes(single, 10, 1, True)
+        assert meta_b == meta_s
+        assert (fb[0][0] != fs[0][0]).mean() < 0.05
+        assert abs(fb[0][1] - fs[0][1]) <= 1e-6 * abs(fs[0][1])
