@@ -357,6 +357,16 @@ int encx_bitunpack(const uint8_t* in, int64_t in_stride, int64_t items, int64_t 
                    int bits, int64_t* codes, int64_t s_item, int64_t s_k, int64_t s_t,
                    encx_stream_t stream);
 
+/* ------------------------------------------------------ batch assembly (customAudioDataset.py)
+ * Clip i of the pool is [src_channels[i]][lengths[i]] fp32 at pool + offsets[i] (device arrays,
+ * int64). out [B][C][Tmax]: out[b][c][t] = clip_b[src_channels[b] == 1 ? 0 : c][starts[b] + t]
+ * for t < out_len[b], else 0 -- the random tensor_cut crop (customAudioDataset.py:64-69), the
+ * mono expand (:51-54) and the zero-pad collate (pad_sequence, :72-91) in one launch. The
+ * caller guarantees starts[b] + out_len[b] <= lengths[b] and src_channels[b] in {1, C}; B*C <= 65535. */
+int encx_crop_collate(const float* pool, const int64_t* offsets, const int64_t* lengths,
+                      const int64_t* src_channels, const int64_t* starts, const int64_t* out_len,
+                      float* out, int64_t B, int64_t C, int64_t Tmax, encx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

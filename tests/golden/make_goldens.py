@@ -16,6 +16,7 @@ Fixture map:
   g8_sched.npz     WarmupCosineLrScheduler learning-rate trace
   g10_ecdc.npz     .ecdc: reference BitPacker vectors (bits 1..32), header, compress/decompress
                    bytes + waves for the g1 model and the g9 48 kHz model (one / two segments)
+  g11_data.npz     customAudioDataset crop (seeded random) + mono expand + collate_fn
   g9_step48k.npz   config-5 analogue: 48 kHz stereo, non-causal, time_group_norm, segment 0.1 s
                    (two frames: 4800 + 48 samples, linear overlap-add), gen-only and GAN steps
 """
@@ -542,8 +543,48 @@ def g10():
     save('g10_ecdc.npz', **out)
 
 
+# ------------------------------------------------------------------------------------ G11
+def g11():
+    """customAudioDataset.__getitem__ (random tensor_cut crop, mono expand) + collate_fn, run
+    on preset decoded clips (the file decode, librosa.load, is replaced by `get`)."""
+    import random
+    import types as _types
+    sys.modules.setdefault('audioread', _types.ModuleType('audioread'))
+    import customAudioDataset as ref_ds
+    g = rng(1111)
+    out = {}
+    for name, channels, cut, lens in [('mono', 1, 2400, [5000, 2400, 2401, 7777, 1200, 3000]),
+                                      ('stereo', 2, 4800, [9000, 4800, 12000, 700])]:
+        clips = []
+        for i, L in enumerate(lens):
+            mono = channels == 1 or i % 2 == 1     # stereo set: odd clips are mono, expanded
+            clips.append(g.standard_normal(L if mono else (channels, L)).astype(np.float32))
+        ds = object.__new__(ref_ds.CustomAudioDataset)
+        ds.transform, ds.tensor_cut, ds.channels, ds.sample_rate = None, cut, channels, 24000
+        ds.fixed_length = 0
+
+        def get(idx=None, _clips=clips, _ds=ds):
+            w = torch.as_tensor(_clips[idx])
+            if len(w.shape) == 1:                       # customAudioDataset.py:51-54
+                w = w.unsqueeze(0).expand(_ds.channels, -1)
+            return w, 24000
+        ds.get = get
+        order = [int(v) for v in g.permutation(len(lens))]
+        random.seed(1212)
+        items = [ds[i] for i in order]
+        batch = ref_ds.collate_fn(items)
+        out[f'{name}/clips'] = np.concatenate([c.reshape(-1) for c in clips])
+        out[f'{name}/lens'] = np.array(lens, np.int64)
+        out[f'{name}/mono'] = np.array([c.ndim == 1 for c in clips])
+        out[f'{name}/order'] = np.array(order, np.int64)
+        out[f'{name}/cut'] = np.array(cut)
+        out[f'{name}/channels'] = np.array(channels)
+        out[f'{name}/batch'] = batch.numpy()
+    save('g11_data.npz', **out)
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9', 'g10']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9', 'g10', 'g11']
     for w in which:
         torch.manual_seed(0)
         globals()[w]()
