@@ -24,6 +24,27 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
         if (!(cond)) return ENCX_EINVAL;                                       \
     } while (0)
 
+// ---- division by a launch-invariant divisor ---------------------------------------------
+// q = n / d for 0 <= n, d < 2^31 as a multiply-high, add and shift (Granlund-Montgomery):
+// l = ceil(log2 d), mul = floor(2^32 (2^l - d) / d) + 1, q = (umulhi(n, mul) + n) >> l.
+// Loaders that split a flattened index per staged element use it instead of an integer
+// division (a ~40-instruction sequence on CDNA).
+struct FastDiv {
+    uint32_t d, mul, shr;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    FastDiv f;
+    f.d = d;
+    f.shr = l;
+    f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+    return f;
+}
+ENCX_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    return (__umulhi(n, f.mul) + n) >> f.shr;
+}
+
 // ---- activations ---------------------------------------------------------------------------
 // nn.ELU(alpha=1) (modules/seanet.py:49 etc.): x > 0 ? x : expm1(x)
 ENCX_DEV float elu(float x) { return x > 0.f ? x : expm1f(x); }

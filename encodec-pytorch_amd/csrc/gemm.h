@@ -184,6 +184,27 @@ int gemm_launch(const LD& ld, const EP& ep, int M, int N, int Kred, hipStream_t 
     return 0;
 }
 
+// 128x128 tiles regardless of the grid size, split over k to ~1024 workgroups: for the deep
+// weight-gradient GEMMs whose 128-tile grid alone is small (e.g. the LSTM's [4H] x [2H+1] over
+// B*T), 128x128 halves the staged bytes per MFMA against the 64x64 tile gemm_shape picks.
+static inline int gemm_splits_128(int M, int N, int Kred, int min_k = 256, int max_splits = 32) {
+    const int blocks = (int)(cdiv(N, 128) * cdiv(M, 128));
+    int sp = (int)cdiv(1024, blocks);
+    const int cap = Kred / min_k;
+    if (sp > cap) sp = cap;
+    if (sp > max_splits) sp = max_splits;
+    return sp < 1 ? 1 : sp;
+}
+template <class LD, class EP>
+int gemm_launch_128(const LD& ld, const EP& ep, int M, int N, int Kred, hipStream_t st, int splits) {
+    const int kchunk = splits > 1 ? (int)(cdiv(cdiv(Kred, splits), 32) * 32) : Kred;
+    const int z = (int)cdiv(Kred, kchunk);
+    hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, 32, LD, EP>), dim3(cdiv(N, 128), cdiv(M, 128), z),
+                       dim3(256), 0, st, ld, ep, M, N, Kred, kchunk);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
 // number of k-slabs gemm_launch actually uses for a requested split count
 static inline int gemm_slabs(int Kred, int splits) {
     if (splits <= 1) return 1;

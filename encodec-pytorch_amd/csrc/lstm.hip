@@ -298,6 +298,7 @@ struct LdWcat {
     const float* in;
     const float* Yl;
     int H, T;
+    FastDiv fT;
     ENCX_DEV float a(int j, int m) const { return DA[(int64_t)m * 4 * H + j]; }
     ENCX_DEV float b(int m, int n) const {
         // one load from a clamped address, the value chosen afterwards (no branch around it)
@@ -305,7 +306,7 @@ struct LdWcat {
         const int u = rec ? (n - H < H ? n - H : H - 1) : n;
         const int mm = rec ? (m > 0 ? m - 1 : 0) : m;
         const float v = (rec ? Yl : in)[(int64_t)mm * H + u];
-        const int t = m % T;
+        const int t = m - (int)fdiv((uint32_t)m, fT) * T;
         return n == 2 * H ? 1.f : (rec && t == 0 ? 0.f : v);
     }
 };
@@ -454,7 +455,7 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
 
 size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H) {
     const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
-    const int S = gemm_slabs(M, gemm_splits(N4, Nw, M));
+    const int S = gemm_slabs(M, gemm_splits_128(N4, Nw, M));
     return (size_t)S * N4 * Nw * sizeof(float);
 }
 
@@ -469,9 +470,9 @@ int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float
     const int64_t BTH = B * T * H;
     const float* in = layer == 0 ? xt : Y + (layer - 1) * BTH;
     const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
-    const int sp = gemm_splits(N4, Nw, M);
+    const int sp = gemm_splits_128(N4, Nw, M);
     const int S = gemm_slabs(M, sp);
-    int rc = gemm_launch(LdWcat{DA + layer * 4 * BTH, in, Y + layer * BTH, (int)H, (int)T}, EpSlabs{ws, N4, Nw},
+    int rc = gemm_launch_128(LdWcat{DA + layer * 4 * BTH, in, Y + layer * BTH, (int)H, (int)T, make_fastdiv((uint32_t)T)}, EpSlabs{ws, N4, Nw},
                          N4, Nw, M, st, sp);
     if (rc) return rc;
     hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 256)), dim3(256), 0, st, ws, S,

@@ -22,8 +22,9 @@ struct Rows {  // x_n[d] = p[b*sB + t*sT + d*sD], n = b*Tf + t
     const float* p;
     int64_t sB, sT, sD;
     int Tf;
+    FastDiv fTf;
     ENCX_DEV float at(int n, int d) const {
-        int b = n / Tf, t = n - b * Tf;
+        const int b = (int)fdiv((uint32_t)n, fTf), t = n - b * Tf;
         return p[b * sB + t * sT + d * sD];
     }
 };
@@ -335,12 +336,12 @@ __global__ __launch_bounds__(NT) void sample_rows_kernel(const float* samples, f
 
 Rows bdt_rows(const float* p, int64_t B, int64_t D, int64_t Tf) {
     Rows r;
-    r.p = p; r.sB = D * Tf; r.sT = 1; r.sD = Tf; r.Tf = (int)Tf;
+    r.p = p; r.sB = D * Tf; r.sT = 1; r.sD = Tf; r.Tf = (int)Tf; r.fTf = make_fastdiv((uint32_t)Tf);
     return r;
 }
 Rows nd_rows(const float* p, int64_t N, int64_t D) {
     Rows r;
-    r.p = p; r.sB = 0; r.sT = D; r.sD = 1; r.Tf = (int)N;
+    r.p = p; r.sB = 0; r.sT = D; r.sD = 1; r.Tf = (int)N; r.fTf = make_fastdiv((uint32_t)N);
     return r;
 }
 
