@@ -134,12 +134,12 @@ class SConv1d(nn.Module):
         self.causal = causal
         self.pad_mode = pad_mode
 
-    def forward(self, x, act=None, res=None):
+    def forward(self, x, act=None, res=None, link=None, link_role=None):
         c = self.conv
         v, g = c.conv.wv()
         if c.norm_type != 'time_group_norm':
             return ops.conv1d(x, v, g, c.conv.bias, c.kernel_size, c.stride, c.dilation, self.causal,
-                              self.pad_mode, act, res)
+                              self.pad_mode, act, res, link, link_role)
         # conv -> GroupNorm(1, C) (NormConv1d.forward, conv.py:119-122); a residual is added
         # after the norm, so it is not fused into the conv epilogue here
         y = ops.conv1d(x, v, g, c.conv.bias, c.kernel_size, c.stride, c.dilation, self.causal,

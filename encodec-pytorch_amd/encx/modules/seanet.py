@@ -5,9 +5,11 @@ parameter-free placeholders), so state-dict keys match. forward() walks the list
 every ELU into the conv that consumes it, and each resblock's residual sum into its second
 conv's epilogue: the SEANet stack never materialises an activation tensor on its own.
 """
+import types
 import typing as tp
 
 import numpy as np
+import torch
 import torch.nn as nn
 
 from .conv import SConv1d, SConvTranspose1d
@@ -50,9 +52,18 @@ class SEANetResnetBlock(nn.Module):
     def forward(self, x):
         sc = self.shortcut(x)
         convs = [m for m in self.block if isinstance(m, SConv1d)]
+        # identity shortcut, weight-norm convs, two or more convs: the skip gradient is summed
+        # into the head conv's bwd-data output (ops.Conv1dFn 'head' / 'tail' link) instead of
+        # by autograd's elementwise add
+        link = None
+        if (isinstance(self.shortcut, nn.Identity) and len(convs) > 1 and torch.is_grad_enabled()
+                and x.requires_grad and all(c.conv.norm_type != 'time_group_norm' for c in convs)):
+            link = types.SimpleNamespace(grad=None)
         h = x
         for i, c in enumerate(convs):
-            h = c(h, act=self.act, res=sc if i == len(convs) - 1 else None)
+            last = i == len(convs) - 1
+            role = None if link is None else ('tail' if last else 'head' if i == 0 else None)
+            h = c(h, act=self.act, res=sc if last else None, link=link, link_role=role)
         return h
 
 

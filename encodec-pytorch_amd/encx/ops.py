@@ -123,7 +123,7 @@ class Conv1dFn(torch.autograd.Function):
     """SConv1d.forward (modules/conv.py:195-210) incl. weight_norm and a fused pre-ELU."""
 
     @staticmethod
-    def forward(ctx, x, v, g, b, res, K, s, d, causal, pad_mode, act):
+    def forward(ctx, x, v, g, b, res, K, s, d, causal, pad_mode, act, link=None, link_role=None):
         _check(x)
         x = x.contiguous()
         B, Cin, T = x.shape
@@ -143,6 +143,7 @@ class Conv1dFn(torch.autograd.Function):
         ctx.save_for_backward(x, wp)
         ctx.params = (v, g, b)
         ctx.cfg = (K, s, d, pl, pr, e, tout, PAD[pad_mode], ACT[act], res is not None, b is not None)
+        ctx.link, ctx.link_role = link, link_role
         return y
 
     @staticmethod
@@ -151,26 +152,40 @@ class Conv1dFn(torch.autograd.Function):
         v, g, b = ctx.params
         K, s, d, pl, pr, e, tout, mode, act, has_res, has_b = ctx.cfg
         dy = dy.contiguous()
+        link, role = ctx.link, ctx.link_role
         B, Cin, T = x.shape
         Cout = v.shape[0]
         st = stream()
         dx = dv = dg = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
+            acc = 0
+            if role == 'head' and link.grad is not None:
+                # the block's skip gradient, handed over by its tail conv: accumulate into it
+                # in the bwd-data epilogue instead of a separate add (see residual_block)
+                dx, acc, link.grad = link.grad, 1, None
+            else:
+                dx = torch.empty_like(x)
             ws = _ws(lib.encx_conv1d_bwd_data_workspace(B, Cin, T, Cout, tout, K, s, pl, pr), x)
             call('encx_conv1d_bwd_data', ptr(dy), ptr(wp), ptr(x), ptr(dx), ptr(ws), B, Cin, T,
-                 Cout, tout, K, s, pl, pr, e, mode, act, 0, st)
+                 Cout, tout, K, s, pl, pr, e, mode, act, acc, st)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
             dw = torch.empty(Cout, Cin, K, device=x.device, dtype=torch.float32)
             ws = _f32(lib.encx_conv1d_bwd_weight_workspace(B, Cin, Cout, tout, K) // 4 + 1, x)
             call('encx_conv1d_bwd_weight', ptr(dy), ptr(x), ptr(dw), None, ptr(ws), B, Cin, T,
                  Cout, tout, K, s, d, pl, e, mode, act, 0, st)
             dv, dg, db = _param_grads(v, g, b, dw, dy, B, Cout, tout)
-        return dx, dv, dg, db, (dy if has_res else None), None, None, None, None, None, None
+        dres = dy if has_res else None
+        if role == 'tail' and has_res:
+            # skip gradient of an identity-shortcut residual block: the head conv of the same
+            # block adds its bwd-data result into this buffer (accumulate=1), so autograd sees
+            # no second path into the block input and launches no elementwise add
+            link.grad, dres = dy, None
+        return dx, dv, dg, db, dres, None, None, None, None, None, None, None, None
 
 
-def conv1d(x, v, g, b, K, stride=1, dilation=1, causal=True, pad_mode='reflect', act=None, res=None):
-    return Conv1dFn.apply(x, v, g, b, res, K, stride, dilation, causal, pad_mode, act)
+def conv1d(x, v, g, b, K, stride=1, dilation=1, causal=True, pad_mode='reflect', act=None, res=None,
+           link=None, link_role=None):
+    return Conv1dFn.apply(x, v, g, b, res, K, stride, dilation, causal, pad_mode, act, link, link_role)
 
 
 # ---------------------------------------------------------------------------- ConvTranspose1d
