@@ -1,0 +1,82 @@
+"""Long audio beyond the training crop: eval encode/decode of a 10 s
+24 kHz clip and of a 2.5 s 48 kHz stereo clip cut into 1 s segments (three, the last ragged)
+with the linear overlap-add (model.py:122-193, utils.py:22-61), against the CPU oracle; and the
+.ecdc round trip of the long clip against the model's own eval forward."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import encodec_oracle as O
+from fixtures import load, T, model_state, codebooks_from_stats, cfg48k
+from synth import synth_wave
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+def load_model(m, p, cbs):
+    sd = dict(p)
+    for i, cb in enumerate(cbs):
+        for k, v in cb.items():
+            sd[f'quantizer.vq.layers.{i}._codebook.{k}'] = v
+    m.load_state_dict(sd)
+    m.eval()
+    return m.to(DEV)
+
+
+def test_eval_10s_24k_vs_oracle_and_ecdc_roundtrip():
+    from encx.model import EncodecModel
+    from encx import compress as C
+    d = load('g1_eval24k.npz')
+    cfg = O.Config(target_bandwidths=(1.5, 3., 6., 12., 24.), audio_normalize=False)
+    p = model_state(cfg, 1)
+    cbs = codebooks_from_stats(d['stats'], 77, 2, cfg.n_q)
+    m = load_model(EncodecModel._get_model([1.5, 3., 6., 12., 24.], 24000, 1, causal=True,
+                                           model_norm='weight_norm', audio_normalize=False,
+                                           name='encodec_24khz'), p, cbs)
+    m.set_target_bandwidth(1.5)
+    x = T(synth_wave((1, 1, 240000), 4321))
+    with torch.no_grad():
+        emb = m.encoder(x.to(DEV))
+        codes = m.encode(x.to(DEV))[0][0]
+        y = m(x.to(DEV))
+        y_o, codes_o, emb_o = O.encodec_forward_eval(x, p, cbs, cfg, 1.5)
+    assert y.shape == (1, 1, 240000) and codes.shape == (1, 2, 750)
+    assert rel(emb, emb_o) < 1e-4, rel(emb, emb_o)
+    mism = float((codes.cpu() != codes_o).double().mean())
+    assert mism < 0.01, mism
+    if mism == 0:
+        assert rel(y, y_o) < 1e-3, rel(y, y_o)
+    # .ecdc round trip: decompress(compress(x)) is the eval forward's own decode
+    blob = C.compress(m, x[0])
+    assert len(blob) == len(C.compress(m, x[0]))
+    y2, sr = C.decompress(m, blob)
+    assert torch.equal(y2, y[0].cpu())
+
+
+def test_eval_48k_stereo_three_segments_vs_oracle():
+    from encx.model import EncodecModel
+    d9 = load('g9_step48k.npz')
+    cfg = cfg48k(segment=1.0)
+    p = model_state(cfg, 91)
+    cbs = codebooks_from_stats(d9['gen/stats'], 93, 2, cfg.n_q)
+    m = load_model(EncodecModel._get_model([3.0], 48000, 2, causal=False, model_norm='time_group_norm',
+                                           audio_normalize=True, segment=1.0), p, cbs)
+    m.set_target_bandwidth(3.0)
+    x = T(synth_wave((1, 2, 120000), 4322))
+    with torch.no_grad():
+        frames = m.encode(x.to(DEV))
+        y = m(x.to(DEV))
+        y_o, codes_o, _ = O.encodec_forward_eval(x, p, cbs, cfg, 3.0)
+    assert [f[0].shape[-1] for f in frames] == [150, 150, 78]   # 48000, 48000, 24960 samples
+    assert y.shape == (1, 2, 120000)
+    mism = float((frames[-1][0].cpu() != codes_o).double().mean())
+    assert mism < 0.02, mism
+    if mism == 0:
+        assert rel(y, y_o) < 1e-3, rel(y, y_o)
