@@ -32,6 +32,7 @@ class ResidualVectorQuantizer(nn.Module):
         self.kmeans_init = kmeans_init
         self.kmeans_iters = kmeans_iters
         self.threshold_ema_dead_code = threshold_ema_dead_code
+        self._bw_cache = {}
         self.vq = ResidualVectorQuantization(dim=self.dimension, codebook_size=self.bins,
                                              num_quantizers=self.n_q, decay=self.decay,
                                              kmeans_init=self.kmeans_init, kmeans_iters=self.kmeans_iters,
@@ -41,7 +42,12 @@ class ResidualVectorQuantizer(nn.Module):
         bw_per_q = self.get_bandwidth_per_quantizer(sample_rate)
         n_q = self.get_num_quantizers_for_bandwidth(sample_rate, bandwidth)
         quantized, codes, penalty = self.vq(x, n_q=n_q)
-        bw = torch.tensor(n_q * bw_per_q, device=x.device, dtype=x.dtype)
+        # the reported bandwidth is a constant per (n_q, device): built once, because a tensor
+        # from a host scalar is a pageable H2D copy that stalls the host until the stream drains
+        key = (n_q, str(x.device), x.dtype)
+        bw = self._bw_cache.get(key)
+        if bw is None:
+            bw = self._bw_cache[key] = torch.tensor(n_q * bw_per_q, device=x.device, dtype=x.dtype)
         return QuantizedResult(quantized, codes, bw, penalty=penalty)
 
     def get_num_quantizers_for_bandwidth(self, sample_rate: int, bandwidth: tp.Optional[float] = None) -> int:
