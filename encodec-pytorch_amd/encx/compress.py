@@ -84,7 +84,6 @@ def decompress_from_file(model: EncodecModel, fo: tp.IO[bytes], device='cpu') ->
         _no_lm()
     dev = _model_device(model)
     frames: tp.List[EncodedFrame] = []
-    segment_length = model.segment_length or audio_length
     segment_stride = model.segment_stride or audio_length
     for offset in range(0, audio_length, segment_stride):
         frame_length = metadata['fr']

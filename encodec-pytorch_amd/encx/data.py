@@ -73,8 +73,10 @@ class AudioPool:
         if np.any(starts < 0) or np.any(starts + out_len > self.lengths[idx]):
             raise ValueError('crop window outside the clip')
         B, Tmax = len(idx), int(out_len.max()) if len(idx) else 0
+        # pinned + non_blocking: a pageable H2D copy would block the host until the stream has
+        # drained (the previous train step), leaving the GPU idle while the next step is enqueued
         meta = torch.from_numpy(np.stack([self.offsets[idx], self.lengths[idx], src, starts, out_len])
-                                ).to(self.device)
+                                ).pin_memory().to(self.device, non_blocking=True)
         out = torch.empty(B, channels, Tmax, device=self.device, dtype=torch.float32)
         call('encx_crop_collate', self.data.data_ptr(), meta[0].data_ptr(), meta[1].data_ptr(),
              meta[2].data_ptr(), meta[3].data_ptr(), meta[4].data_ptr(), out.data_ptr(), B, channels,

@@ -17,6 +17,7 @@ python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
     encodec-pytorch_amd/encx/train_multi_gpu.py config/config.yaml
 """
 import logging
+import math
 import os
 import random
 import re
@@ -147,7 +148,8 @@ def train(local_rank, world_size, config):
     os.makedirs(config.checkpoint.save_folder, exist_ok=True)
     model, disc = build(config, device)
     dataset = CustomAudioDataset(config, mode='train', device=device)
-    steps = max(1, -(-(-(-len(dataset) // (world_size if dp else 1))) // config.datasets.batch_size))
+    per_rank = math.ceil(len(dataset) / (world_size if dp else 1))     # DistributedSampler pads
+    steps = max(1, math.ceil(per_rank / config.datasets.batch_size))  # no drop_last
     trainer = Trainer(model, disc if config.model.train_discriminator else None,
                       lr=float(config.optimization.lr), disc_lr=float(config.optimization.disc_lr),
                       weights=dict(vars(config.balancer.weights)), sample_rate=int(config.model.sample_rate),
