@@ -642,8 +642,9 @@ struct LdSpecD {  // A(m = (bc, fr), k) = x[bc][fr*hop + k]; B = DFT table [n][2
     const float* x;
     const float* bt;
     int T, Fr, hop, nb2;
+    FastDiv fFr;
     ENCX_DEV float a(int m, int k) const {
-        const int bc = m / Fr, fr = m - bc * Fr;
+        const int bc = (int)fdiv((uint32_t)m, fFr), fr = m - bc * Fr;
         return x[(int64_t)bc * T + (int64_t)fr * hop + k];
     }
     ENCX_DEV float b(int k, int n) const { return bt[(int64_t)k * nb2 + n]; }
@@ -938,7 +939,7 @@ int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B,
     const int M = (int)(B * C * Fr), N = 2 * nb, K = (int)n_fft;
     encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * (B * C * T + (int64_t)M * N), "spec_fwd");
     ps.tag(" n%ld", (long)n_fft);
-    return gemm_launch(LdSpecD{x, tables, (int)T, Fr, (int)hop, N}, EpSpecD{z, (int)C, Fr, nb, inv}, M, N, K, st);
+    return gemm_launch(LdSpecD{x, tables, (int)T, Fr, (int)hop, N, make_fastdiv((uint32_t)Fr)}, EpSpecD{z, (int)C, Fr, nb, inv}, M, N, K, st);
 }
 
 size_t encx_disc_spec_bwd_workspace(int64_t B, int64_t C, int64_t T, int64_t n_fft, int64_t hop) {

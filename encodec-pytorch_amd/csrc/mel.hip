@@ -32,8 +32,9 @@ struct LdSpec {  // A: framed reflect-padded audio, B: DFT table
     static constexpr bool A_K_FAST = true, B_N_FAST = true;
     const float* wav; const float* bt;
     int T, F, h, p, nb2;
+    FastDiv fF;  // m -> (clip, frame) without an integer division per staged element
     ENCX_DEV float a(int m, int k) const {
-        int b = m / F, f = m - b * F;
+        const int b = (int)fdiv((uint32_t)m, fF), f = m - b * F;
         int src = pad_src(f * h + k, p, T, 0, ENCX_PAD_REFLECT);
         return wav[(int64_t)b * T + src];
     }
@@ -231,7 +232,7 @@ int encx_mel_logmel(const float* x, const float* tables, float* ws, float* out, 
     const float* bt = tables;
     const float* mt = tables + (int64_t)g.n * 2 * g.nb;
     const int nb2 = 2 * g.nb;
-    int rc = gemm_launch(LdSpec{x, bt, (int)T, g.F, g.h, g.p, nb2}, EpStore{ws + g.spec, nb2}, g.rows,
+    int rc = gemm_launch(LdSpec{x, bt, (int)T, g.F, g.h, g.p, nb2, make_fastdiv((uint32_t)g.F)}, EpStore{ws + g.spec, nb2}, g.rows,
                          nb2, g.n, st);
     if (rc) return rc;
     return gemm_launch(LdMel{ws + g.spec, mt, g.nb, nm}, EpLogT{out, nm, g.F}, g.rows, nm, g.nb, st);
@@ -256,12 +257,12 @@ int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws
     const int nb2 = 2 * g.nb;
     int rc;
     // target: logmel(x)
-    rc = gemm_launch(LdSpec{x, bt, (int)T, g.F, g.h, g.p, nb2}, EpStore{spec, nb2}, g.rows, nb2, g.n, st);
+    rc = gemm_launch(LdSpec{x, bt, (int)T, g.F, g.h, g.p, nb2, make_fastdiv((uint32_t)g.F)}, EpStore{spec, nb2}, g.rows, nb2, g.n, st);
     if (rc) return rc;
     rc = gemm_launch(LdMel{spec, mt, g.nb, nm}, EpLog{lmx, nm}, g.rows, nm, g.nb, st);
     if (rc) return rc;
     // output: mel(y)
-    rc = gemm_launch(LdSpec{y, bt, (int)T, g.F, g.h, g.p, nb2}, EpStore{spec, nb2}, g.rows, nb2, g.n, st);
+    rc = gemm_launch(LdSpec{y, bt, (int)T, g.F, g.h, g.p, nb2, make_fastdiv((uint32_t)g.F)}, EpStore{spec, nb2}, g.rows, nb2, g.n, st);
     if (rc) return rc;
     rc = gemm_launch(LdMel{spec, mt, g.nb, nm}, EpStore{mely, nm}, g.rows, nm, g.nb, st);
     if (rc) return rc;
