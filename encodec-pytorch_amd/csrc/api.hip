@@ -69,9 +69,11 @@ int encx_init(int device) {
 int encx_prof_enable(int on) {
     std::lock_guard<std::mutex> g(g_prof.mu);
     if (on && !g_prof.created) {
+        // timing-only events: no system-scope fence on record, so bracketing a launch does not
+        // write back and invalidate L2 (which would slow the kernels being measured)
         for (int i = 0; i < kMaxSlots; ++i) {
-            if (hipEventCreate(&g_prof.ev0[i]) != hipSuccess) return ENCX_EINVAL;
-            if (hipEventCreate(&g_prof.ev1[i]) != hipSuccess) return ENCX_EINVAL;
+            if (hipEventCreateWithFlags(&g_prof.ev0[i], hipEventDisableSystemFence) != hipSuccess) return ENCX_EINVAL;
+            if (hipEventCreateWithFlags(&g_prof.ev1[i], hipEventDisableSystemFence) != hipSuccess) return ENCX_EINVAL;
         }
         g_prof.created = true;
     }

@@ -21,6 +21,8 @@
 // Plus VALU kernels for the 1-channel ends of the stack (Cout = 1 forward, tiny wgrads).
 #include <stdlib.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "gemm.h"
 #include "prof.h"
@@ -1159,7 +1161,9 @@ static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K)
         p.tiles = (int)(cdiv(N, p.BN) * cdiv(A, p.BM));
     }
     p.items = (int)(B * cdiv(Tl, p.BT));
-    int64_t want = cdiv(1024, p.tiles);                 // ~1024 workgroups in flight
+    // ~1024 workgroups in flight (ENCX_WG_TARGET overrides, for tuning runs)
+    static const int64_t target = getenv("ENCX_WG_TARGET") ? atoll(getenv("ENCX_WG_TARGET")) : 1024;
+    int64_t want = cdiv(target, p.tiles);
     int64_t cap = (64ll << 20) / (4 * A * N);           // <= 64 MB of partials
     int64_t minper = cdiv(p.items, (int64_t)p.items >= 8 ? 8 : 1);
     (void)minper;
