@@ -256,14 +256,17 @@ struct EpSlab {
     }
 };
 
-template <int MODE>  // 0: EMA (core_vq.py:227-229), 1: kmeans (:92-100)
+// MODE 0: EMA (core_vq.py:227-229), 1: kmeans (:92-100), 2: the raw sums into means [Kc][D+1]
+template <int MODE>
 __global__ void bucket_finish(const float* ws, int S, int Kc, int D, float* cs, float* ea,
                               float* means, int64_t* bins, float decay, float one_m) {
     const int c = blockIdx.x, W = D + 1;
-    const float cnt = sum_strided(ws + (int64_t)c * W + D, S, (int64_t)Kc * W);
+    const float cnt = MODE == 1 ? sum_strided(ws + (int64_t)c * W + D, S, (int64_t)Kc * W) : 0.f;
     for (int d = threadIdx.x; d <= D; d += blockDim.x) {
         const float s = sum_strided(ws + (int64_t)c * W + d, S, (int64_t)Kc * W);
-        if (MODE == 0) {
+        if (MODE == 2) {
+            means[(int64_t)c * W + d] = s;
+        } else if (MODE == 0) {
             if (d < D) {
                 float* p = ea + (int64_t)c * D + d;
                 *p = fmaf(s, one_m, *p * decay);
@@ -291,6 +294,21 @@ int bucket_run(Rows x, const int64_t* idx, int N, int D, int Kc, float* ws, floa
                        cs, ea, means, bins, decay, one_m);
     ENCX_CHECK_LAUNCH();
     return 0;
+}
+
+// the EMA of core_vq.py:227-229 from precomputed (e.g. all-reduced) sums [Kc][D+1]; the same
+// fmaf as bucket_finish<0>, so sums + this == encx_rvq_ema bit for bit
+__global__ void ema_from_sums(const float* sums, int D, float* cs, float* ea, float decay, float one_m) {
+    const int c = blockIdx.x, W = D + 1;
+    for (int d = threadIdx.x; d <= D; d += blockDim.x) {
+        const float s = sums[(int64_t)c * W + d];
+        if (d < D) {
+            float* p = ea + (int64_t)c * D + d;
+            *p = fmaf(s, one_m, *p * decay);
+        } else {
+            cs[c] = fmaf(s, one_m, cs[c] * decay);
+        }
+    }
 }
 
 // embed = embed_avg / (laplace(cluster_size) * sum(cluster_size)), core_vq.py:230-235
@@ -419,6 +437,28 @@ int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float*
     int rc = bucket_run<0>(bdt_rows(x, B, D, Tf), idx, (int)(B * Tf), (int)D, (int)Kc, ws,
                            cluster_size, embed_avg, nullptr, nullptr, decay, one_m, st);
     if (rc) return rc;
+    hipLaunchKernelGGL(ema_normalize, dim3(Kc), dim3(D < 64 ? 64 : (D > 256 ? 256 : D)), 0, st,
+                       cluster_size, embed_avg, embed, (int)D, (int)Kc, eps,
+                       (float)((double)Kc * (double)eps));
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_rvq_code_sums(const float* x, const int64_t* idx, float* sums, float* ws, int64_t B,
+                       int64_t D, int64_t Tf, int64_t Kc, encx_stream_t stream) {
+    ENCX_REQUIRE(x && idx && sums && ws && B > 0 && D > 0 && D <= 256 && Tf > 0 && Kc > 0);
+    return bucket_run<2>(bdt_rows(x, B, D, Tf), idx, (int)(B * Tf), (int)D, (int)Kc, ws, nullptr,
+                         nullptr, sums, nullptr, 0.f, 0.f, (hipStream_t)stream);
+}
+
+int encx_rvq_ema_from_sums(const float* sums, float* cluster_size, float* embed_avg, float* embed,
+                           int64_t D, int64_t Kc, float decay, float eps, encx_stream_t stream) {
+    ENCX_REQUIRE(sums && cluster_size && embed_avg && embed && D > 0 && D <= 256 && Kc > 0);
+    hipStream_t st = (hipStream_t)stream;
+    const float one_m = (float)(1.0 - (double)decay);
+    hipLaunchKernelGGL(ema_from_sums, dim3(Kc), dim3(D + 1 < 64 ? 64 : 256), 0, st, sums, (int)D,
+                       cluster_size, embed_avg, decay, one_m);
+    ENCX_CHECK_LAUNCH();
     hipLaunchKernelGGL(ema_normalize, dim3(Kc), dim3(D < 64 ? 64 : (D > 256 ? 256 : D)), 0, st,
                        cluster_size, embed_avg, embed, (int)D, (int)Kc, eps,
                        (float)((double)Kc * (double)eps));

@@ -138,13 +138,15 @@ class EncodecModel(nn.Module):
     def _get_model(target_bandwidths: tp.List[float], sample_rate: int = 24_000, channels: int = 1,
                    causal: bool = True, model_norm: str = 'weight_norm', audio_normalize: bool = False,
                    segment: tp.Optional[float] = None, name: str = 'unset', ratios=[8, 5, 4, 2],
-                   n_q: tp.Optional[int] = None):
-        """model.py:242-276."""
+                   n_q: tp.Optional[int] = None, sync_codebooks: bool = False):
+        """model.py:242-276. sync_codebooks (not in the reference): all-reduce the RVQ EMA sums and
+        broadcast rank 0's kmeans init across data-parallel ranks."""
         encoder = m.SEANetEncoder(channels=channels, norm=model_norm, causal=causal, ratios=ratios)
         decoder = m.SEANetDecoder(channels=channels, norm=model_norm, causal=causal, ratios=ratios)
         if n_q is None:
             n_q = int(1000 * target_bandwidths[-1] // (math.ceil(sample_rate / encoder.hop_length) * 10))
-        quantizer = qt.ResidualVectorQuantizer(dimension=encoder.dimension, n_q=n_q, bins=1024)
+        quantizer = qt.ResidualVectorQuantizer(dimension=encoder.dimension, n_q=n_q, bins=1024,
+                                               sync_codebooks=sync_codebooks)
         return EncodecModel(encoder, decoder, quantizer, target_bandwidths, sample_rate, channels,
                             normalize=audio_normalize, segment=segment, name=name)
 

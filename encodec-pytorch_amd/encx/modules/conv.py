@@ -110,14 +110,15 @@ class NormConv2d(nn.Module):
         self.norm = nn.Identity()
         self.norm_type = norm
 
-    def forward(self, x, act=False, param_grads=True):
+    def forward(self, x, act=False, param_grads=True, mode=None, first=False):
         v, g = self.conv.wv()
         b = self.conv.bias
         if not param_grads:
             v = v.detach()
             g = g.detach() if g is not None else None
             b = b.detach() if b is not None else None
-        return ops.conv2d(x, v, g, b, self.kernel_size, self.stride, self.dilation, self.padding, act)
+        return ops.conv2d(x, v, g, b, self.kernel_size, self.stride, self.dilation, self.padding, act,
+                          mode if mode is not None else ops.DiscGradMode(), first)
 
 
 class SConv1d(nn.Module):

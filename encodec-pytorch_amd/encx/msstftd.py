@@ -1,9 +1,11 @@
 """MS-STFT discriminator (msstftd.py of the reference) and its losses on the encx kernels.
 
 Same classes, constructor arguments and state-dict keys (`discriminators.{k}.convs.{i}.conv.*`,
-`discriminators.{k}.conv_post.conv.*`). forward(x, param_grads=True) takes one flag the
-reference does not have: param_grads=False evaluates the discriminator as a function of its
-input only (Trainer.step's generator phase), so no weight-gradient kernels run there.
+`discriminators.{k}.conv_post.conv.*`). forward(x, param_grads=True, mode=None) takes two
+arguments the reference does not have: param_grads=False evaluates the discriminator as a
+function of its input only; mode (ops.DiscGradMode) lets one forward graph serve both phases
+of a GAN step (Trainer.step), so no weight-gradient kernel runs in the generator phase and the
+discriminator phase reuses the generator phase's activations.
 """
 import typing as tp
 
@@ -72,14 +74,14 @@ class DiscriminatorSTFT(nn.Module):
         self.convs.append(NormConv2d(in_chs, out_chs, kernel_size=k2, padding=get_2d_padding(k2), norm=norm))
         self.conv_post = NormConv2d(out_chs, out_channels, kernel_size=k2, padding=get_2d_padding(k2), norm=norm)
 
-    def forward(self, x: torch.Tensor, param_grads: bool = True):
+    def forward(self, x: torch.Tensor, param_grads: bool = True, mode=None):
         """msstftd.py:86-105: x [B, C, T] -> (logits [B, out, frames, bins'], 5 feature maps)."""
         fmap = []
         z = ops.DiscSpecFn.apply(x, self.n_fft, self.hop_length, self.sample_rate)
-        for layer in self.convs:
-            z = layer(z, act=True, param_grads=param_grads)
+        for i, layer in enumerate(self.convs):
+            z = layer(z, act=True, param_grads=param_grads, mode=mode, first=i == 0)
             fmap.append(z)
-        z = self.conv_post(z, act=False, param_grads=param_grads)
+        z = self.conv_post(z, act=False, param_grads=param_grads, mode=mode)
         return z, fmap
 
 
@@ -98,10 +100,12 @@ class MultiScaleSTFTDiscriminator(nn.Module):
         ])
         self.num_discriminators = len(self.discriminators)
 
-    def forward(self, x: torch.Tensor, param_grads: bool = True) -> DiscriminatorOutput:
+    def forward(self, x: torch.Tensor, param_grads: bool = True, mode=None) -> DiscriminatorOutput:
+        """mode: an ops.DiscGradMode shared by every layer of this forward's graph (Trainer
+        flips it between the generator and the discriminator phase of one step)."""
         logits, fmaps = [], []
         for disc in self.discriminators:
-            logit, fmap = disc(x, param_grads=param_grads)
+            logit, fmap = disc(x, param_grads=param_grads, mode=mode)
             logits.append(logit)
             fmaps.append(fmap)
         return logits, fmaps

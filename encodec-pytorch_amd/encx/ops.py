@@ -405,7 +405,10 @@ class RVQTrainFn(torch.autograd.Function):
     (per-layer straight-through, Appendix A quirk 1)."""
 
     @staticmethod
-    def forward(ctx, emb, codebooks, decay, eps):
+    def forward(ctx, emb, codebooks, decay, eps, sync=False):
+        """sync: all-reduce (SUM) each layer's per-code sums over the data-parallel ranks
+        before its EMA, so every rank applies the same update (the reference never
+        syncs, core_vq.py:157,175 / train_multi_gpu.py:318 -- off by default)."""
         _check(emb, 'emb')
         emb = emb.contiguous()
         B, D, T = emb.shape
@@ -422,6 +425,10 @@ class RVQTrainFn(torch.autograd.Function):
         keys = torch.empty(B * T, device=emb.device, dtype=torch.int64)
         Kc = codebooks[0].embed.shape[0]
         bws = _ws(lib.encx_rvq_bucket_workspace(B * T, D, Kc), emb)
+        sums = None
+        if sync and codebooks[0].training and torch.distributed.is_initialized() \
+                and torch.distributed.get_world_size() > 1:
+            sums = torch.empty(Kc, D + 1, device=emb.device, dtype=torch.float32)
         for i, cb in enumerate(codebooks):
             x = res[i % 2]
             cb.init_embed_(x)
@@ -430,7 +437,12 @@ class RVQTrainFn(torch.autograd.Function):
             # dequantize with the pre-update codebook (core_vq.py:221), then update it (:223-235)
             call('encx_rvq_apply', ptr(x), ptr(res[(i + 1) % 2]), ptr(cb.embed), ptr(codes[i]),
                  ptr(out), ptr(cdir), ptr(parts[i]), B, D, T, int(i == 0), 1, st)
-            if cb.training:
+            if cb.training and sums is not None:
+                call('encx_rvq_code_sums', ptr(x), ptr(codes[i]), ptr(sums), ptr(bws), B, D, T, Kc, st)
+                torch.distributed.all_reduce(sums)  # 1024 x 129 fp32 = 528 KB per layer
+                call('encx_rvq_ema_from_sums', ptr(sums), ptr(cb.cluster_size), ptr(cb.embed_avg),
+                     ptr(cb.embed), D, Kc, float(decay), float(eps), st)
+            elif cb.training:
                 call('encx_rvq_ema', ptr(x), ptr(codes[i]), ptr(cb.cluster_size), ptr(cb.embed_avg),
                      ptr(cb.embed), ptr(bws), B, D, T, cb.embed.shape[0], float(decay), float(eps), st)
             call('encx_reduce_sum', ptr(parts[i]), P, 1.0 / numel, ptr(commits[i:i + 1]), 0, st)
@@ -455,7 +467,7 @@ class RVQTrainFn(torch.autograd.Function):
         else:
             call('encx_lincomb', ptr(dq), ptr(cdir), ptr(demb), demb.numel(), float(n_q),
                  ptr(dpen.contiguous().view(1)), 2.0 / (n_q * numel), stream())
-        return demb, None, None, None
+        return demb, None, None, None, None
 
 
 def rvq_encode(emb, embeds):
@@ -516,7 +528,9 @@ class LSTMFn(torch.autograd.Function):
         out = torch.empty_like(x)
         call('encx_lstm_fwd', ptr(x), ptr(wcat), ptr(bsum), ptr(xt), ptr(Y), ptr(Cs), ptr(Gs), ptr(out),
              int(bool(skip)), B, T, H, L, st)
-        ctx.state = (xt, Y, Cs, Gs, wcatT)
+        # saved (not ctx attributes) so autograd frees them after the backward unless the
+        # graph is retained (a second backward through the same LSTM, e.g. the commit loss)
+        ctx.save_for_backward(xt, Y, Cs, Gs, wcatT)
         ctx.weights = weights
         ctx.skip = skip
         return out
@@ -526,7 +540,7 @@ class LSTMFn(torch.autograd.Function):
         dout = dout.contiguous()
         B, H, T = dout.shape
         weights = ctx.weights
-        xt, Y, Cs, Gs, wcatT = ctx.state
+        xt, Y, Cs, Gs, wcatT = ctx.saved_tensors
         L = len(weights) // 4
         st = stream()
         if ctx.needs_input_grad[0]:  # the skip passes dout through; the kernels add the rest
@@ -552,7 +566,6 @@ class LSTMFn(torch.autograd.Function):
                 wsw = _ws(lib.encx_lstm_bwd_weight_workspace(B, T, H), dout)
             call('encx_lstm_bwd_weight', ptr(DA), ptr(xt), ptr(Y), ptr(dws[0]), ptr(dws[1]), ptr(dws[2]),
                  ptr(dws[3]), acc_w, ptr(wsw), B, T, H, L, l, st)
-        ctx.state = None
         return (dx, None, *grads)
 
 
@@ -570,14 +583,32 @@ def conv2d_geometry(Fi, kernel, stride, dilation, padding):
     return KT, KF, sf, dt, pt, pf, Fo
 
 
+class DiscGradMode:
+    """Which gradients a discriminator graph's backward produces. One forward graph of the
+    discriminator serves both phases of a GAN step (encx.train.Trainer): the generator phase
+    differentiates it w.r.t. the audio only (params=False: no weight-gradient kernels), the
+    discriminator phase w.r.t. its weights only (input=False: no gradient into the
+    spectrogram, as the reference's disc(output.detach()), train_multi_gpu.py:114-116)."""
+
+    def __init__(self, params=True, input=True):
+        self.params, self.input = params, input
+
+    def set(self, params, input):
+        self.params, self.input = params, input
+
+
+_ALL_GRADS = DiscGradMode()
+
+
 class Conv2dFn(torch.autograd.Function):
     """NormConv2d.forward (modules/conv.py:136-139) + the LeakyReLU(0.2) that follows it in
     DiscriminatorSTFT.forward (msstftd.py:100-103) when act. Returns the post-activation map
     (the fmap entry); its sign is the pre-activation's, so it also serves as the LeakyReLU'
-    mask in the backward."""
+    mask in the backward. mode (DiscGradMode) gates the weight grads, and the input grad of
+    the layer that reads the spectrogram (first=True)."""
 
     @staticmethod
-    def forward(ctx, x, v, g, b, geo, act):
+    def forward(ctx, x, v, g, b, geo, act, mode=_ALL_GRADS, first=False):
         _check(x)
         x = x.contiguous()
         B, Ci, T2, Fi = x.shape
@@ -592,10 +623,14 @@ class Conv2dFn(torch.autograd.Function):
         ctx.save_for_backward(x, y, wf)
         ctx.params = (v, g, b)
         ctx.geo, ctx.act = geo, act
+        ctx.mode, ctx.first = mode, first
+        ctx.set_materialize_grads(False)
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        if dy is None:
+            return None, None, None, None, None, None, None, None
         x, y, wf = ctx.saved_tensors
         v, g, b = ctx.params
         KT, KF, sf, dt, pt, pf, Fo = ctx.geo
@@ -606,13 +641,14 @@ class Conv2dFn(torch.autograd.Function):
         yact = y if ctx.act else None
         dims = (B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf)
         dx = dv = dg = db = None
-        if ctx.needs_input_grad[0]:
+        mode = ctx.mode
+        if ctx.needs_input_grad[0] and (mode.input or not ctx.first):
             J = -(-KF // sf)
             wp = _f32(Co * KT * J * Ci * sf, x)
             call('encx_conv2d_wpoly', ptr(wf), ptr(wp), Co, Ci, KT, KF, sf, st)
             dx = torch.empty_like(x)
             call('encx_conv2d_bwd_data', ptr(dy), ptr(yact), ptr(wp), None, ptr(dx), 0, *dims, st)
-        if any(ctx.needs_input_grad[1:4]):
+        if any(ctx.needs_input_grad[1:4]) and mode.params:
             ws = _ws(lib.encx_conv2d_bwd_weight_workspace(*dims), x)
             direct = _direct(v) and _direct(g) and _direct(b)
             if direct and g is None:   # plain weight: straight into the flat grad views
@@ -630,12 +666,13 @@ class Conv2dFn(torch.autograd.Function):
                 call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(dw), ptr(db), 0, 0,
                      ptr(ws), *dims, st)
                 dv, dg = _weight_bwd(v, g, dw)
-        return dx, dv, dg, db, None, None
+        return dx, dv, dg, db, None, None, None, None
 
 
-def conv2d(x, v, g, b, kernel, stride=(1, 1), dilation=(1, 1), padding=(0, 0), act=False):
+def conv2d(x, v, g, b, kernel, stride=(1, 1), dilation=(1, 1), padding=(0, 0), act=False, mode=_ALL_GRADS,
+           first=False):
     geo = conv2d_geometry(x.shape[-1], kernel, stride, dilation, padding)
-    return Conv2dFn.apply(x, v, g, b, geo, act)
+    return Conv2dFn.apply(x, v, g, b, geo, act, mode, first)
 
 
 class DiscSpecFn(torch.autograd.Function):
@@ -653,10 +690,13 @@ class DiscSpecFn(torch.autograd.Function):
         call('encx_disc_spec_fwd', ptr(x), ptr(tab), ptr(z), B, C, T, n_fft, hop, stream())
         ctx.cfg = (B, C, T, n_fft, hop)
         ctx.tab = tab
+        ctx.set_materialize_grads(False)
         return z
 
     @staticmethod
     def backward(ctx, dz):
+        if dz is None:  # the first conv produced no input grad (DiscGradMode.input False)
+            return None, None, None, None
         B, C, T, n_fft, hop = ctx.cfg
         dz = dz.contiguous()
         dx = torch.empty(B, C, T, device=dz.device, dtype=torch.float32)

@@ -38,6 +38,10 @@ class EuclideanCodebook(nn.Module):
         self.register_buffer('embed', embed)
         self.register_buffer('embed_avg', embed.clone())
         self._inited_host = None  # host mirror of `inited` (read once, then trusted)
+        # opt-in data-parallel codebook sync: rank 0's kmeans init is broadcast and
+        # the EMA sums are all-reduced before every update. Off = the reference (core_vq.py:157,
+        # 175 keep their broadcasts commented out; train_multi_gpu.py:318 broadcast_buffers=False)
+        self.sync_codebooks = False
 
     def _load_from_state_dict(self, *args, **kwargs):
         self._inited_host = None
@@ -58,6 +62,11 @@ class EuclideanCodebook(nn.Module):
         self.cluster_size.data.copy_(bins)
         self.inited.data.fill_(1.0)
         self._inited_host = True
+        if self.sync_codebooks and torch.distributed.is_initialized() \
+                and torch.distributed.get_world_size() > 1:
+            # the broadcast core_vq.py:157 intends: every rank starts from rank 0's codebook
+            for b in (self.embed, self.embed_avg, self.cluster_size, self.inited):
+                torch.distributed.broadcast(b.data, src=0)
 
     def quantize(self, x):
         """core_vq.py:181-189 on [N, D] rows."""
@@ -116,11 +125,15 @@ class ResidualVectorQuantization(nn.Module):
         super().__init__()
         self.layers = nn.ModuleList([VectorQuantization(**kwargs) for _ in range(num_quantizers)])
 
+    def set_sync_codebooks(self, on: bool = True):
+        for layer in self.layers:
+            layer._codebook.sync_codebooks = bool(on)
+
     @staticmethod
     def run(layers, x):
         cbs = [layer._codebook for layer in layers]
         if layers[0].training:
-            return ops.RVQTrainFn.apply(x, cbs, cbs[0].decay, cbs[0].epsilon)
+            return ops.RVQTrainFn.apply(x, cbs, cbs[0].decay, cbs[0].epsilon, cbs[0].sync_codebooks)
         # eval forward (no STE, no commit loss, no EMA)
         codes = ops.rvq_encode(x, [c.embed for c in cbs])
         q = ops.rvq_decode(codes, [c.embed for c in cbs])

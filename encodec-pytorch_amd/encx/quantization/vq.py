@@ -23,7 +23,8 @@ class ResidualVectorQuantizer(nn.Module):
     """vq.py:28-128."""
 
     def __init__(self, dimension: int = 256, n_q: int = 8, bins: int = 1024, decay: float = 0.99,
-                 kmeans_init: bool = True, kmeans_iters: int = 50, threshold_ema_dead_code: int = 2):
+                 kmeans_init: bool = True, kmeans_iters: int = 50, threshold_ema_dead_code: int = 2,
+                 sync_codebooks: bool = False):
         super().__init__()
         self.n_q = n_q
         self.dimension = dimension
@@ -37,6 +38,12 @@ class ResidualVectorQuantizer(nn.Module):
                                              num_quantizers=self.n_q, decay=self.decay,
                                              kmeans_init=self.kmeans_init, kmeans_iters=self.kmeans_iters,
                                              threshold_ema_dead_code=self.threshold_ema_dead_code)
+        self.set_sync_codebooks(sync_codebooks)
+
+    def set_sync_codebooks(self, on: bool = True):
+        """Opt-in cross-rank codebook sync (not in the reference; see core_vq.EuclideanCodebook)."""
+        self.sync_codebooks = bool(on)
+        self.vq.set_sync_codebooks(on)
 
     def forward(self, x: torch.Tensor, sample_rate: int, bandwidth: tp.Optional[float] = None) -> QuantizedResult:
         bw_per_q = self.get_bandwidth_per_quantizer(sample_rate)

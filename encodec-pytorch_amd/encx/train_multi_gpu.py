@@ -122,7 +122,8 @@ def build(config, device):
 def train_one_step(epoch, trainer, dataset, config, rank=0, world=1):
     """train_multi_gpu.py:32-143: one epoch; the discriminator trains from warmup_epoch on, with
     probability eval(train_discriminator) per step (:105-107)."""
-    prob = float(eval(str(config.model.train_discriminator)))
+    td = config.model.train_discriminator
+    prob = float(td) if isinstance(td, (bool, int, float)) else float(eval(str(td)))
     trainer.disc_prob = prob if epoch >= config.lr_scheduler.warmup_epoch else 0.0
     batches = shard_order(len(dataset), rank, world, config.datasets.batch_size, world > 1)
     last = {}
@@ -137,6 +138,10 @@ def train_one_step(epoch, trainer, dataset, config, rank=0, world=1):
 
 def train(local_rank, world_size, config):
     """train_multi_gpu.py:172-352."""
+    if world_size > 1 and not config.distributed.data_parallel:
+        # the reference would run W independent copies that all log and write the same
+        # checkpoint paths; refuse instead of racing on the files
+        raise ValueError(f'WORLD_SIZE={world_size} but distributed.data_parallel is off')
     dp = bool(config.distributed.data_parallel) and world_size > 1
     device = torch.device('cuda', local_rank)
     torch.cuda.set_device(device)
@@ -150,28 +155,34 @@ def train(local_rank, world_size, config):
     dataset = CustomAudioDataset(config, mode='train', device=device)
     per_rank = math.ceil(len(dataset) / (world_size if dp else 1))     # DistributedSampler pads
     steps = max(1, math.ceil(per_rank / config.datasets.batch_size))  # no drop_last
-    trainer = Trainer(model, disc if config.model.train_discriminator else None,
-                      lr=float(config.optimization.lr), disc_lr=float(config.optimization.disc_lr),
+    if getattr(config.distributed, 'sync_codebooks', False):  # opt-in, not a reference key
+        model.quantizer.set_sync_codebooks(True)
+    # the discriminator always takes part in the generator loss (train_multi_gpu.py:61-71); the
+    # train_discriminator flag only gates its update (train_one_step sets disc_prob)
+    trainer = Trainer(model, disc, lr=float(config.optimization.lr), disc_lr=float(config.optimization.disc_lr),
                       weights=dict(vars(config.balancer.weights)), sample_rate=int(config.model.sample_rate),
                       max_iter=config.common.max_epoch * steps,
                       warmup_iter=config.lr_scheduler.warmup_epoch * steps)
     start_epoch = 1
     if config.checkpoint.resume:
+        # train_multi_gpu.py:226-238 + :303-308; weights_only loads (no unpickling)
         ck = torch.load(config.checkpoint.checkpoint_path, map_location='cpu', weights_only=True)
         dk = torch.load(config.checkpoint.disc_checkpoint_path, map_location='cpu', weights_only=True)
         model.load_state_dict(ck['model_state_dict'])
         disc.load_state_dict(dk['model_state_dict'])
-        start_epoch = ck['epoch'] + 1
+        start_epoch = max(1, ck['epoch'] + 1)
         if start_epoch > config.common.max_epoch:
             raise ValueError(f'resume epoch {ck["epoch"]} is larger than total epochs {config.common.max_epoch}')
+        if 'scheduler_state_dict' in ck and 'scheduler_state_dict' in dk:
+            trainer.load_state_dicts(ck['optimizer_state_dict'], ck['scheduler_state_dict'],
+                                     dk['optimizer_state_dict'], dk['scheduler_state_dict'])
     for epoch in range(start_epoch, config.common.max_epoch + 1):
         train_one_step(epoch, trainer, dataset, config, rank, world_size if dp else 1)
         if epoch % config.common.save_interval == 0 and rank == 0:
             base = f'{config.checkpoint.save_location}epoch{epoch}_lr{config.optimization.lr}'
             save_master_checkpoint(epoch, model, trainer.opt, trainer.sched, base + '.pt')
-            if trainer.opt_d is not None:
-                save_master_checkpoint(epoch, disc, trainer.opt_d, trainer.sched_d,
-                                       f'{config.checkpoint.save_location}epoch{epoch}_disc_lr{config.optimization.lr}.pt')
+            save_master_checkpoint(epoch, disc, trainer.opt_d, trainer.sched_d,
+                                   f'{config.checkpoint.save_location}epoch{epoch}_disc_lr{config.optimization.lr}.pt')
     if dp:
         torch.distributed.destroy_process_group()
     return trainer

@@ -174,6 +174,16 @@ size_t encx_rvq_bucket_workspace(int64_t N, int64_t D, int64_t Kc);
 int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float* embed_avg,
                  float* embed, float* ws, int64_t B, int64_t D, int64_t Tf, int64_t Kc,
                  float decay, float eps, encx_stream_t stream);
+/* encx_rvq_ema in two halves, for the opt-in cross-rank codebook sync: the
+ * per-code sums of core_vq.py:227-228 (embed_onehot.sum(0), x.t() @ embed_onehot) land in
+ * sums [Kc][D+1] (column D = the count), so a caller can all-reduce them across data-parallel
+ * ranks before the EMA; encx_rvq_ema_from_sums then applies :227-235 from them. sums may alias
+ * nothing else; ws as for encx_rvq_ema. Same fixed summation order as encx_rvq_ema, so the two
+ * halves back to back give bit-identical buffers. */
+int encx_rvq_code_sums(const float* x, const int64_t* idx, float* sums, float* ws, int64_t B,
+                       int64_t D, int64_t Tf, int64_t Kc, encx_stream_t stream);
+int encx_rvq_ema_from_sums(const float* sums, float* cluster_size, float* embed_avg, float* embed,
+                           int64_t D, int64_t Kc, float decay, float eps, encx_stream_t stream);
 /* One kmeans iteration (core_vq.py:85-100): means <- bucket means where bins > 0.
  * samples [N][D] row-major; means [Kc][D] in/out; bins int64 [Kc] out; ws as above. */
 int encx_kmeans_step(const float* samples, float* means, int64_t* bins, int64_t* idx,

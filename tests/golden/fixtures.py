@@ -72,5 +72,33 @@ def certified(gaps, x_norm2, e_norm2, factor=256):
     return gaps > factor * eps * (x_norm2 + e_norm2)
 
 
+def rvq_certified(emb, embeds, factor=256):
+    """Eval-mode RVQ (core_vq.py:357-367) of emb [B, D, T] in fp64 -> (codes [n_q, B, T] int64,
+    cert [n_q, B, T] bool). A frame's code at layer l is certified when its fp64 top-2 distance
+    gap clears fp32 rounding (certified()) AND every earlier layer's code of that frame is
+    certified (otherwise its residual may differ). Where cert holds, an fp32 implementation
+    fed the same emb must produce exactly these codes. factor 256 = 2 x the worst-case
+    rounding bound of a 128-term fp32 dot product (n eps (|x| + |e|)^2 per distance) -- a proof;
+    smaller factors (e.g. 32, about 3 sigma of random-walk rounding) certify far more frames
+    of the synthetic codebooks and are used as a second, statistical check."""
+    x = torch.as_tensor(emb).detach().cpu().double().permute(0, 2, 1)  # [B, T, D]
+    B, Tn, D = x.shape
+    r = x.reshape(-1, D).clone()
+    ok = torch.ones(B * Tn, dtype=torch.bool)
+    codes, certs = [], []
+    for E in embeds:
+        E = torch.as_tensor(E).detach().cpu().double()
+        dist = (r ** 2).sum(1, keepdim=True) - 2 * r @ E.t() + (E ** 2).sum(1)[None]
+        s, idx = torch.sort(dist, 1)
+        gap = (s[:, 1] - s[:, 0]).numpy()
+        c = certified(gap, (r ** 2).sum(1).numpy(), float((E ** 2).sum(1).max()), factor)
+        ok = ok & torch.from_numpy(c)
+        k = idx[:, 0]
+        codes.append(k.view(B, Tn))
+        certs.append(ok.view(B, Tn).clone())
+        r = r - E[k]
+    return torch.stack(codes), torch.stack(certs)
+
+
 __all__ = ['load', 'T', 'model_state', 'disc_state', 'cfg48k', 'codebooks_from_stats', 'g3_codebooks',
-           'certified', 'synth_wave', 'rng']
+           'certified', 'rvq_certified', 'synth_wave', 'rng']

@@ -99,3 +99,31 @@ def test_bandwidth_rule():
     from encx.quantization import ResidualVectorQuantizer
     q = ResidualVectorQuantizer(dimension=128, n_q=32, bins=1024)
     assert [q.get_num_quantizers_for_bandwidth(75, b) for b in (1.5, 3., 6., 12., 24.)] == [2, 4, 8, 16, 32]
+
+
+def test_flat_adam_state_dict_is_torch_adam_layout():
+    """FlatAdam.state_dict / load_state_dict interchange with torch.optim.Adam (the reference's
+    optimizer_state_dict, train_multi_gpu.py:303-308). Host logic only: no step is taken."""
+    import torch
+    from encx.optim import FlatAdam
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(3, 4)), torch.nn.Parameter(torch.randn(5))]
+    opt = FlatAdam(ps, lr=3e-4, betas=(0.5, 0.9))
+    assert opt.state_dict()['state'] == {}
+    opt.exp_avg.copy_(torch.randn(17))
+    opt.exp_avg_sq.copy_(torch.rand(17))
+    opt.n_step = 7
+    sd = opt.state_dict()
+    ref = torch.optim.Adam([torch.nn.Parameter(p.detach().clone()) for p in ps], lr=1.0, betas=(0.5, 0.9))
+    ref.load_state_dict(sd)
+    rsd = ref.state_dict()
+    assert set(rsd['param_groups'][0]) >= {'lr', 'betas', 'eps', 'weight_decay', 'amsgrad', 'params'}
+    assert rsd['param_groups'][0]['lr'] == 3e-4
+    assert torch.equal(rsd['state'][1]['exp_avg'], opt.exp_avg[12:].view(5))
+    assert torch.equal(rsd['state'][0]['exp_avg_sq'], opt.exp_avg_sq[:12].view(3, 4))
+    assert float(rsd['state'][0]['step']) == 7.0
+    # and back: a torch Adam state dict restores FlatAdam's flat moments and step
+    opt2 = FlatAdam([torch.nn.Parameter(p.detach().clone()) for p in ps], lr=1.0, betas=(0.5, 0.9))
+    opt2.load_state_dict(rsd)
+    assert opt2.n_step == 7 and opt2.param_groups[0]['lr'] == 3e-4
+    assert torch.equal(opt2.exp_avg, opt.exp_avg) and torch.equal(opt2.exp_avg_sq, opt.exp_avg_sq)

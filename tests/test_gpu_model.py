@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from oracle import encodec_oracle as O
-from fixtures import load, T, model_state, codebooks_from_stats, certified
+from fixtures import load, T, model_state, codebooks_from_stats, certified, rvq_certified
 from synth import synth_wave
 
 pytestmark = pytest.mark.gpu
@@ -52,9 +52,17 @@ def test_eval_model_fixture():
     e2 = max(float((cb['embed'] ** 2).sum(1).max()) for cb in cbs[:2])
     cert = certified(d['gaps'], float((emb.cpu() ** 2).sum(1).max()), e2)
     mine = codes.cpu().numpy()
+    # layer 0 against the reference's own codes, on the frames the fixture's fp64 gap certifies
     assert (mine[0][cert] == ref[0][cert]).all()
-    if (mine == ref).all():
-        assert rel(y, d['y']) < 1e-3, rel(y, d['y'])
+    # every layer against the fp64 RVQ of our latent, on every certified frame
+    for factor in (256, 32):
+        want, cert_all = rvq_certified(emb, [cb['embed'] for cb in cbs[:2]], factor)
+        assert cert_all.any()
+        assert torch.equal(torch.from_numpy(mine).transpose(0, 1)[cert_all], want[cert_all]), factor
+    # decode unconditionally from the reference's codes (model.py:170-193)
+    with torch.no_grad():
+        y_ref_codes = m.decode([(G(ref).view(1, 2, -1), None)])
+    assert rel(y_ref_codes, d['y']) < 1e-3, rel(y_ref_codes, d['y'])
 
 
 def test_train_step_gen_fixture():
@@ -67,8 +75,12 @@ def test_train_step_gen_fixture():
         out = tr.step(x)
         for k in ('l_t', 'l_f'):
             np.testing.assert_allclose(float(out[k]), float(d[f'gen/it{it}_{k}'].reshape(-1)[0]), rtol=1e-4)
+        # the commit loss is a mean of (q - x)^2 over residuals ~10x smaller than x, so the
+        # latent's ~1e-6 fp32 rounding is amplified; step 0 against the fp32 reference to 1e-4,
+        # and test_train_grads_vs_oracle_fp64 pins it against an fp64 run. After one Adam step
+        # near-zero grads may flip sign (see below), which moves the second step's latent.
         np.testing.assert_allclose(float(out['loss_w']), float(d[f'gen/it{it}_loss_w'].reshape(-1)[0]),
-                                   rtol=5e-3, atol=1e-6)
+                                   rtol=1e-4 if it == 0 else 2e-3)
     sd = m.state_dict()
     worst = 0.0
     for k, v in sd.items():
@@ -181,6 +193,9 @@ def test_train_grads_vs_oracle_fp64():
 
     assert torch.equal(codes.cpu().long(), torch.as_tensor(codes64).long().reshape(codes.shape))
     assert rel(y, y64) < 1e-4
+    lw_err = rel(loss_w, lw64)
+    print(f'loss_w rel err vs fp64 {lw_err:.3e}')
+    assert lw_err < 2e-5, lw_err
     worst, where = 0.0, ''
     params = dict(m.named_parameters())
     for k, v in p64.items():

@@ -1,0 +1,111 @@
+"""Run-twice determinism of a full GAN step and checkpoint / resume parity
+(train_multi_gpu.py:224-238, 303-308; utils.py:132-148) on the HIP path.
+
+Determinism: the kernels use no floating-point atomics and fixed-order reductions, so two
+identical trainers fed the same clips must produce bit-identical parameters, Adam moments,
+codebooks and losses after several GAN steps.
+
+Resume: the reference checkpoints {epoch, model_state_dict, optimizer_state_dict,
+scheduler_state_dict} per model. A trainer rebuilt from those four state dicts and stepped once
+must match the uninterrupted run bit for bit. The reference's Balancer keeps its EMA
+statistics outside every state dict (balancer.py:31-118), so a resumed reference run restarts
+them; the uninterrupted run here resets its balancer at the same step to compare like with
+like.
+"""
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from fixtures import model_state, codebooks_from_stats, disc_state
+from synth import synth_wave
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def make_trainer(B=4):
+    from oracle import encodec_oracle as O
+    from encx.model import EncodecModel
+    from encx.msstftd import MultiScaleSTFTDiscriminator
+    from encx.train import Trainer
+    cfg = O.Config(target_bandwidths=(6.0,), audio_normalize=True)
+    m = EncodecModel._get_model([6.0], 24000, 1, causal=True, model_norm='weight_norm', audio_normalize=True)
+    sd = dict(model_state(cfg, 3))
+    stats = np.zeros((cfg.n_q, 2, 128), np.float32)
+    stats[:, 1] = 0.05
+    for i, cb in enumerate(codebooks_from_stats(stats, 4, cfg.n_q, cfg.n_q)):
+        for k, v in cb.items():
+            sd[f'quantizer.vq.layers.{i}._codebook.{k}'] = v
+    m.load_state_dict(sd)
+    disc = MultiScaleSTFTDiscriminator(filters=32)
+    disc.load_state_dict(disc_state(5), strict=False)
+    tr = Trainer(m.to(DEV), disc.to(DEV), lr=3e-4, disc_lr=3e-4, max_iter=100, warmup_iter=3)
+    return tr
+
+
+def batches(n, B=4):
+    return [torch.from_numpy(synth_wave((B, 1, 24000), 200 + i)).to(DEV) for i in range(n)]
+
+
+def snapshot(tr):
+    out = {'gen': tr.opt.flat.clone(), 'gen_m': tr.opt.exp_avg.clone(), 'gen_v': tr.opt.exp_avg_sq.clone(),
+           'disc': tr.opt_d.flat.clone(), 'disc_m': tr.opt_d.exp_avg.clone()}
+    for k, v in tr.model.state_dict().items():
+        if '_codebook' in k:
+            out[k] = v.clone()
+    return out
+
+
+def assert_same(a, b):
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+def test_gan_step_run_twice_bit_identical():
+    xs = batches(3)
+    outs, snaps = [], []
+    for _ in range(2):
+        tr = make_trainer()
+        losses = [tr.step(x) for x in xs]
+        torch.cuda.synchronize()
+        outs.append([{k: float(v) for k, v in o.items()} for o in losses])
+        snaps.append(snapshot(tr))
+    assert outs[0] == outs[1]
+    assert_same(snaps[0], snaps[1])
+
+
+def _roundtrip(obj):
+    """torch.save -> torch.load(weights_only=True): what a checkpoint file goes through."""
+    buf = io.BytesIO()
+    torch.save(obj, buf)
+    buf.seek(0)
+    return torch.load(buf, map_location='cpu', weights_only=True)
+
+
+def test_resume_matches_uninterrupted_run():
+    from encx.balancer import Balancer
+    xs = batches(4)
+    # uninterrupted: 3 steps, (balancer restart as a resume has it), 1 more step
+    tr = make_trainer()
+    for x in xs[:3]:
+        tr.step(x)
+    ck = _roundtrip({'model_state_dict': tr.model.state_dict(), **tr.state_dicts(),
+                     'disc_state_dict': tr.disc.state_dict()})
+    assert set(ck['optimizer']['state'][0]) == {'step', 'exp_avg', 'exp_avg_sq'}
+    assert float(ck['optimizer']['state'][0]['step']) == 3.0
+    assert ck['scheduler']['last_epoch'] == 3
+    tr.balancer = Balancer(tr.balancer.weights)
+    tr.step(xs[3])
+    torch.cuda.synchronize()
+    want = snapshot(tr)
+    # resumed: a fresh trainer from the checkpoint's state dicts, then the same step
+    tr2 = make_trainer()
+    tr2.model.load_state_dict(ck['model_state_dict'])
+    tr2.disc.load_state_dict(ck['disc_state_dict'])
+    tr2.load_state_dicts(ck['optimizer'], ck['scheduler'], ck['disc_optimizer'], ck['disc_scheduler'])
+    assert tr2.opt.n_step == 3 and tr2.sched.last_epoch == 3
+    tr2.step(xs[3])
+    torch.cuda.synchronize()
+    assert_same(want, snapshot(tr2))
