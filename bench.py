@@ -4,9 +4,11 @@ python bench.py [--gpus N] [--steps K] [--warmup W] [--config gen|gan]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 A step = one train_multi_gpu.py:train_one_step iteration on one batch of 32 synthetic 1 s clips
-per GPU (config 2, the metric's configuration: generator + RVQ (n_q 8) + l_t/l_f through the
-Balancer + Adam; `--config gan` adds the MS-STFT discriminator, config 3). Inputs are resident
-in HBM before the timed region. Rank 0 prints one JSON line.
+per GPU. Default `--config gan` = BASELINE config 3, the configuration the metric's 1/2/4/8-GPU
+series scales (config 4 = config 3 per rank): generator + RVQ (n_q 8) + MS-STFT discriminator,
+l_t / l_f / l_g / l_feat through the Balancer, commit loss, Adam, then the discriminator update
+(every step). `--config gen` = config 2 (no discriminator), `--config 48k` = config 5. Inputs are
+resident in HBM before the timed region. Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -36,7 +38,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', choices=['gen', 'gan', '48k'], default='gen')
+    ap.add_argument('--config', choices=['gen', 'gan', '48k'], default='gan')
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
@@ -142,18 +144,24 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t)
-    roof = None
+    roof = whole = None
     if prof:
         import ctypes
         n = ctypes.c_int64()
         lib.encx_prof_read(None, None, None, ctypes.byref(n))
-        # the dominant family: conv / convtr (+ the disc's Conv2d in GAN configs); the library's
-        # other scopes (LSTM, ...) are left out of this roofline
+        # the dominant family: the implicit-GEMM conv kernels, SEANet Conv1d / ConvTranspose1d and
+        # the discriminator's Conv2d (fwd + bwd-data + bwd-weight); every other booked scope
+        # (LSTM, RVQ, mel, STFT, Adam, elementwise) enters the whole-step totals only
         ms = fl = by = 0.0
         launches = 0
+        all_fl = all_by = all_ms = 0.0
         for i in range(n.value):
             m_, f_, b_, tag = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_char_p()
             lib.encx_prof_slot(i, ctypes.byref(m_), ctypes.byref(f_), ctypes.byref(b_), ctypes.byref(tag))
+            all_fl += f_.value
+            all_by += b_.value
+            if m_.value > 0:
+                all_ms += m_.value
             if tag.value.decode().startswith(('conv', 'c2_')):
                 ms, fl, by, launches = ms + m_.value, fl + f_.value, by + b_.value, launches + 1
         lib.encx_prof_enable(0)
@@ -161,7 +169,7 @@ def main():
         # traffic: HBM bytes per conv-family ABI call from the committed rocprofv3 PMC passes
         # (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic.py); null when no pass exists for the config
         traffic = None
-        tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01',
+        tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r02',
                              f'traffic_{args.config}.json')
         if os.path.exists(tpath) and launches:
             with open(tpath) as fh:
@@ -169,10 +177,23 @@ def main():
         roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MI355X_FP32_PEAK_TFLOPS,
                 'unit': 'TFLOP/s', 'frac': round(achieved / MI355X_FP32_PEAK_TFLOPS, 4), 'traffic': traffic,
                 'algorithmic_bytes_per_launch': round(by / launches) if launches else None,
-                'kernel': 'encx conv/convtr fwd + bwd-data + bwd-weight (implicit-GEMM f32 MFMA)',
+                'kernel': 'encx conv/convtr/conv2d fwd + bwd-data + bwd-weight (implicit-GEMM f32 MFMA)',
                 'launches': launches, 'kernel_ms_per_step': round(ms / args.steps, 3),
                 'algorithmic_bytes_per_step': by / args.steps,
                 'algorithmic_flops_per_step': fl / args.steps}
+        # whole step: every booked kernel's algorithmic FLOPs / bytes over the wall
+        # time of a step; hbm_frac = bytes / (t * 8 TB/s), max_roofline_frac = max(bytes / 8 TB/s,
+        # flops / 157.3 TF/s) / t
+        t_step = dt / args.steps
+        f_step, b_step = all_fl / args.steps, all_by / args.steps
+        whole = {'flops_per_step': f_step, 'bytes_per_step': b_step,
+                 'timed_kernel_ms_per_step': round(all_ms / args.steps, 3),
+                 'achieved_tflops': round(f_step / t_step / 1e12, 2),
+                 'achieved_gbs': round(b_step / t_step / 1e9, 1),
+                 'hbm_frac': round(b_step / (t_step * MI355X_HBM_PEAK_GBS * 1e9), 4),
+                 'mfma_frac': round(f_step / (t_step * MI355X_FP32_PEAK_TFLOPS * 1e12), 4),
+                 'max_roofline_frac': round(max(b_step / (MI355X_HBM_PEAK_GBS * 1e9),
+                                                f_step / (MI355X_FP32_PEAK_TFLOPS * 1e12)) / t_step, 4)}
 
     value = B * world * args.steps * 1.0 / dt
     if rank == 0:
@@ -187,6 +208,7 @@ def main():
                        'sample_rate': 48000 if args.config == '48k' else 24000,
                        'parallelism': f'dp{world}'},
             'roofline': roof,
+            'whole_step': whole,
         }
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(args.config, min(16, os.cpu_count() or 1))

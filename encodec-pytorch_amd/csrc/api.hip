@@ -19,6 +19,7 @@ struct ProfState {
     hipEvent_t ev1[kMaxSlots];
     double flops[kMaxSlots];
     double bytes[kMaxSlots];
+    bool timed[kMaxSlots];
     char tags[kMaxSlots][64];
     bool created = false;
 };
@@ -26,15 +27,17 @@ ProfState g_prof;
 std::atomic<bool> g_prof_on{false};
 }  // namespace
 
-encx_prof_scope::encx_prof_scope(hipStream_t s, double f, double b, const char* kind) : st(s), slot(-1) {
+encx_prof_scope::encx_prof_scope(hipStream_t s, double f, double b, const char* kind, bool timed)
+    : st(s), slot(-1) {
     if (!g_prof_on.load(std::memory_order_relaxed)) return;
     std::lock_guard<std::mutex> g(g_prof.mu);
     if (!g_prof.on || g_prof.next >= kMaxSlots) return;
     slot = g_prof.next++;
     g_prof.flops[slot] = f;
     g_prof.bytes[slot] = b;
+    g_prof.timed[slot] = timed;
     snprintf(g_prof.tags[slot], sizeof(g_prof.tags[slot]), "%s", kind ? kind : "");
-    (void)hipEventRecord(g_prof.ev0[slot], st);
+    if (timed) (void)hipEventRecord(g_prof.ev0[slot], st);
 }
 
 void encx_prof_scope::tag(const char* fmt, ...) {
@@ -48,7 +51,7 @@ void encx_prof_scope::tag(const char* fmt, ...) {
 }
 
 encx_prof_scope::~encx_prof_scope() {
-    if (slot >= 0) (void)hipEventRecord(g_prof.ev1[slot], st);
+    if (slot >= 0 && g_prof.timed[slot]) (void)hipEventRecord(g_prof.ev1[slot], st);
 }
 
 extern "C" {
@@ -87,14 +90,15 @@ int encx_prof_read(double* total_ms, double* total_flops, double* total_bytes, i
     std::lock_guard<std::mutex> g(g_prof.mu);
     double ms = 0, fl = 0, by = 0;
     for (int i = 0; i < g_prof.next; ++i) {
+        fl += g_prof.flops[i];
+        by += g_prof.bytes[i];
+        if (!g_prof.timed[i]) continue;
         hipError_t e = hipEventSynchronize(g_prof.ev1[i]);
         if (e != hipSuccess) return (int)e;
         float t = 0.f;
         e = hipEventElapsedTime(&t, g_prof.ev0[i], g_prof.ev1[i]);
         if (e != hipSuccess) return (int)e;
         ms += t;
-        fl += g_prof.flops[i];
-        by += g_prof.bytes[i];
     }
     if (total_ms) *total_ms = ms;
     if (total_flops) *total_flops = fl;
@@ -106,11 +110,13 @@ int encx_prof_read(double* total_ms, double* total_flops, double* total_bytes, i
 int encx_prof_slot(int64_t i, double* ms, double* flops, double* bytes, const char** tag) {
     std::lock_guard<std::mutex> g(g_prof.mu);
     if (i < 0 || i >= g_prof.next) return ENCX_EINVAL;
-    hipError_t e = hipEventSynchronize(g_prof.ev1[i]);
-    if (e != hipSuccess) return (int)e;
-    float t = 0.f;
-    e = hipEventElapsedTime(&t, g_prof.ev0[i], g_prof.ev1[i]);
-    if (e != hipSuccess) return (int)e;
+    float t = -1.f;  // untimed (booked-only) slot
+    if (g_prof.timed[i]) {
+        hipError_t e = hipEventSynchronize(g_prof.ev1[i]);
+        if (e != hipSuccess) return (int)e;
+        e = hipEventElapsedTime(&t, g_prof.ev0[i], g_prof.ev1[i]);
+        if (e != hipSuccess) return (int)e;
+    }
     if (ms) *ms = t;
     if (flops) *flops = g_prof.flops[i];
     if (bytes) *bytes = g_prof.bytes[i];

@@ -41,7 +41,7 @@ struct C2Fwd {
     int CK, NR, RL;
 };
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int KFC = 0>
 __global__ __launch_bounds__(NT) void c2_fwd_kernel(C2Fwd a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     extern __shared__ float smem[];
@@ -145,19 +145,40 @@ __global__ __launch_bounds__(NT) void c2_fwd_kernel(C2Fwd a) {
             }
         }
         __syncthreads();
-        for (int kf = 0; kf < KF; ++kf) {
-            const float* wk = Ws + (h * KF + kf) * BM + wm0 + l32;
-            const float* xk = Xs + h * XR + kf;
+        if constexpr (KFC > 0) {
+            // k-pairs = combo pairs (cp, cp+1); the KF taps of a pair unrolled, so every
+            // accumulator sees KFC independent MFMAs per loop trip and the loads run ahead
             for (int cp = 0; cp < CK; cp += 2) {
-                float av[TM], bv[TN];
+                const float* wk = Ws + (cp + h) * KFC * BM + wm0 + l32;
+                const float* xk = Xs + (cp + h) * XR;
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = wk[cp * KF * BM + i * 32];
+                for (int kf = 0; kf < KFC; ++kf) {
+                    float av[TM], bv[TN];
 #pragma unroll
-                for (int j = 0; j < TN; ++j) bv[j] = xk[cp * XR + boff[j]];
+                    for (int i = 0; i < TM; ++i) av[i] = wk[kf * BM + i * 32];
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
+                    for (int j = 0; j < TN; ++j) bv[j] = xk[boff[j] + kf];
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+                }
+            }
+        } else {
+            for (int kf = 0; kf < KF; ++kf) {
+                const float* wk = Ws + (h * KF + kf) * BM + wm0 + l32;
+                const float* xk = Xs + h * XR + kf;
+                for (int cp = 0; cp < CK; cp += 2) {
+                    float av[TM], bv[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) av[i] = wk[cp * KF * BM + i * 32];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) bv[j] = xk[cp * XR + boff[j]];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+                }
             }
         }
     }
@@ -179,6 +200,120 @@ __global__ __launch_bounds__(NT) void c2_fwd_kernel(C2Fwd a) {
         }
 }
 
+// Forward, register-pipelined. Same implicit GEMM and LDS image as c2_fwd_kernel (BM = 32 rows,
+// BN columns, CK combos of (ci, kt) per chunk, KF taps unrolled), but the next chunk's window
+// and weights are fetched into registers (MX + MW values per thread, every load issued from a
+// clamped address and selected afterwards) before the current chunk's MFMAs run: the staging
+// latency hides behind the matrix work instead of stalling every workgroup of a CU in step.
+template <int BN, int KFC, int CK, int MX>
+__global__ __launch_bounds__(NT) void c2_fwdp_kernel(C2Fwd a) {
+    constexpr int BM = 32, TN = BN / 128, WI = KFC * CK * BM, MW = (WI + NT - 1) / NT;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int NR = a.NR, RL = a.RL, S = g.sf;
+    const int VC = g.Ci * g.KT, XR = NR * RL, XI = CK * XR;
+    float* Xs = smem;                  // [CK][NR][RL]
+    float* Ws = smem + XI;             // [CK][KFC][BM]
+    int2* rtab = (int2*)(Ws + WI);     // [VC*NR]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.z, n0 = blockIdx.x * BN, co0 = blockIdx.y * BM;
+    const int wn0 = wave * TN * 32;
+    const int Nall = g.T2 * g.Fo, nend = min(Nall, n0 + BN);
+    const int tf = n0 / g.Fo, f0 = n0 - tf * g.Fo;
+    const int nr = (nend - 1) / g.Fo - tf + 1;
+    int boff[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+        boff[j] = 0;
+        if (n < nend) {
+            const int tr = n / g.Fo, f = n - tr * g.Fo, rs = tr - tf;
+            boff[j] = rs * RL + (f - (rs ? 0 : f0)) * S;
+        }
+    }
+    f32x16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = (f32x16){0};
+    const float* xb = a.x + (int64_t)b * g.Ci * g.T2 * g.Fi;
+    for (int gr = tid; gr < VC * NR; gr += NT) {
+        const int vc = gr / NR, rs = gr - vc * NR, ci = vc / g.KT, kt = vc - ci * g.KT;
+        const int row = tf + rs + kt * g.dt - g.pt, pos0 = (rs ? 0 : f0) * S - g.pf;
+        const bool ok = rs < nr && row >= 0 && row < g.T2;
+        rtab[gr] = make_int2(ok ? (ci * g.T2 + row) * g.Fi + pos0 : 0, ok ? pos0 : -(1 << 30));
+    }
+    __syncthreads();
+    const int dr = NT / RL, dw = NT - dr * RL, r_init = tid / RL, w_init = tid - r_init * RL;
+    float rx[MX], rw[MW];
+    auto fetch = [&](int c0) {
+        const int nrows = min(CK, VC - c0) * NR;
+        int r = r_init, w = w_init;
+#pragma unroll
+        for (int q = 0; q < MX; ++q) {
+            const int2 e = rtab[c0 * NR + (r < nrows ? r : 0)];
+            const int pos = e.y + w;
+            const bool ok = r < nrows && pos >= 0 && pos < g.Fi;
+            const float t = xb[ok ? e.x + w : 0];
+            rx[q] = ok ? t : 0.f;
+            w += dw;
+            r += dr;
+            if (w >= RL) {
+                w -= RL;
+                ++r;
+            }
+        }
+        const float* wsrc = a.wf + (int64_t)c0 * KFC * g.Co + co0;
+        const int wrows = (VC - c0) * KFC;
+#pragma unroll
+        for (int q = 0; q < MW; ++q) {
+            const int j = q * NT + tid, rr = j / BM, col = j & (BM - 1);
+            const bool ok = j < WI && rr < wrows && co0 + col < g.Co;
+            const float t = wsrc[ok ? (int64_t)rr * g.Co + col : 0];
+            rw[q] = ok ? t : 0.f;
+        }
+    };
+    fetch(0);
+    for (int c0 = 0; c0 < VC; c0 += CK) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < MX; ++q)
+            if (q * NT + tid < XI) Xs[q * NT + tid] = rx[q];
+#pragma unroll
+        for (int q = 0; q < MW; ++q)
+            if (q * NT + tid < WI) Ws[q * NT + tid] = rw[q];
+        __syncthreads();
+        if (c0 + CK < VC) fetch(c0 + CK);
+#pragma unroll 2
+        for (int cp = 0; cp < CK; cp += 2) {
+            const float* wk = Ws + (cp + h) * KFC * BM + l32;
+            const float* xk = Xs + (cp + h) * XR;
+#pragma unroll
+            for (int kf = 0; kf < KFC; ++kf) {
+                const float av = wk[kf * BM];
+                float bv[TN];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xk[boff[j] + kf];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[j] = mfma32(av, bv[j], acc[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = co0 + mfma_row(r, lane);
+            const float bco = a.bias ? a.bias[co < g.Co ? co : g.Co - 1] : 0.f;
+            if (co < g.Co && n < nend) {
+                float v = acc[j][r] + bco;
+                if (a.act) v = lrelu(v);
+                a.y[((int64_t)b * g.Co + co) * Nall + n] = v;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------ backward data
 struct C2Dg {
     C2Geo g;
@@ -190,7 +325,7 @@ struct C2Dg {
     int J, U, CK, NR, RL, accumulate;
 };
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int JC = 0>
 __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     extern __shared__ float smem[];
@@ -294,19 +429,38 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
             }
         }
         __syncthreads();
-        for (int q = 0; q < J; ++q) {
-            const float* aq = As + (h * J + q) * BM + wm0 + l32;
-            const float* xq = Xs + h * XR - q;
+        if constexpr (JC > 0) {
             for (int cp = 0; cp < CK; cp += 2) {
-                float av[TM], bv[TN];
+                const float* aq = As + (cp + h) * JC * BM + wm0 + l32;
+                const float* xq = Xs + (cp + h) * XR;
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = aq[cp * J * BM + i * 32];
+                for (int q = 0; q < JC; ++q) {
+                    float av[TM], bv[TN];
 #pragma unroll
-                for (int j = 0; j < TN; ++j) bv[j] = xq[cp * XR + boff[j]];
+                    for (int i = 0; i < TM; ++i) av[i] = aq[q * BM + i * 32];
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
+                    for (int j = 0; j < TN; ++j) bv[j] = xq[boff[j] - q];
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+                }
+            }
+        } else {
+            for (int q = 0; q < J; ++q) {
+                const float* aq = As + (h * J + q) * BM + wm0 + l32;
+                const float* xq = Xs + h * XR - q;
+                for (int cp = 0; cp < CK; cp += 2) {
+                    float av[TM], bv[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) av[i] = aq[cp * J * BM + i * 32];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) bv[j] = xq[cp * XR + boff[j]];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+                }
             }
         }
     }
@@ -604,6 +758,166 @@ __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
         }
 }
 
+// Weight grad, column-group form. dW[co][n] (n = vc*KF + kf, vc = ci*KT + kt) as a GEMM over
+// the positions (b, t, f). A workgroup owns GC combos = GC*KF columns = NW*NTW tiles of 32 and
+// all Co <= 32 rows; wave w keeps NTW column tiles, so the masked dy value a lane reads once per
+// k-pair (the A operand) feeds NTW independent MFMA chains. Positions are staged W2_P at a time
+// (one batch item per chunk): dy' = dy * LeakyReLU'(y) transposed into Ls[p][33] (the pad keeps
+// the transposing store conflict-free) and the x window of the GC combos, Rs[GC][NR][RL]. A
+// workgroup walks a contiguous range of chunks and writes one partial slab [Co][N + 1] (column
+// Nw = the bias, summed by wave 0 of group 0 on the vector ALU); c2_wg_reduce adds the slabs in
+// a fixed order.
+constexpr int W2_P = 64;
+struct C2Wg2 {
+    C2Geo g;
+    const float* dy;
+    const float* yact;
+    const float* x;
+    float* ws;  // [splits][Co][N], N = VC*KF + 1
+    int NR, RL, GC, items, per_split, chunks;
+};
+
+template <int KF, int NTW, int NW>
+__global__ __launch_bounds__(NW * 64) void c2_wgrad2_kernel(C2Wg2 a) {
+    constexpr int NTH = NW * 64, P = W2_P, LDA = 33;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int NR = a.NR, RL = a.RL, GC = a.GC, S = g.sf, XR = NR * RL;
+    const int VC = g.Ci * g.KT, Nw = VC * KF, N = Nw + 1;
+    int4* rtab = (int4*)smem;                  // [GC*NR]: {offset at row tf, row - tf, rs, valid}
+    float* Ls = smem + 4 * GC * NR;            // [P][LDA]
+    int* poff = (int*)(Ls + P * LDA);          // [P]
+    float* Rs = (float*)(poff + P);            // [GC][NR][RL]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int vc0 = blockIdx.x * GC, split = blockIdx.y;
+    const int n0 = vc0 * KF + wave * NTW * 32;
+    const int Nall = g.T2 * g.Fo;
+    const int64_t plane_y = (int64_t)Nall, plane_x = (int64_t)g.T2 * g.Fi;
+    const bool do_bias = blockIdx.x == 0 && wave == 0;
+    int cbase[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = n0 + j * 32 + l32;
+        const int vc = n / KF, kf = n - vc * KF;
+        cbase[j] = (n < Nw) ? (vc - vc0) * XR + kf : 0;
+    }
+    f32x16 acc[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[j] = (f32x16){0};
+    float bsum = 0.f;
+    for (int r = tid; r < GC * NR; r += NTH) {
+        const int cl = r / NR, rs = r - cl * NR, vc = vc0 + cl, ci = vc / g.KT, kt = vc - ci * g.KT;
+        const int rrel = rs + kt * g.dt - g.pt;
+        rtab[r] = make_int4(ci * (int)plane_x + rrel * g.Fi, rrel, rs, vc < VC);
+    }
+    const int dr = NTH / RL, dw = NTH - dr * RL, r_init = tid / RL, w_init = tid - r_init * RL;
+    const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
+    for (int it = it_beg; it < it_end; ++it) {
+        const int b = it / a.chunks, p0 = (it - b * a.chunks) * P;
+        const int pend = min(Nall, p0 + P);
+        const int tf = p0 / g.Fo, f0 = p0 - tf * g.Fo;
+        const int nr = (pend - 1) / g.Fo - tf + 1;
+        const float* dyb = a.dy + (int64_t)b * g.Co * plane_y;
+        const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane_y : dyb;
+        const float* xb = a.x + (int64_t)b * g.Ci * plane_x;
+        __syncthreads();
+        // dy' chunk, read along positions (coalesced), stored transposed
+        for (int i0 = 0; i0 < P * 32; i0 += NTH * DPER) {
+            float v[DPER], ym[DPER];
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NTH + tid;
+                const int co = i / P, tl = i - co * P, p = p0 + tl;
+                const bool ok = i < P * 32 && p < pend && co < g.Co;
+                const int64_t o = ok ? (int64_t)co * plane_y + p : 0;
+                const float t = dyb[o];
+                ym[q] = yab[o];
+                v[q] = ok ? t : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < DPER; ++q) {
+                const int i = i0 + q * NTH + tid;
+                if (i < P * 32) {
+                    const int co = i / P, tl = i - co * P;
+                    Ls[tl * LDA + co] = a.yact ? v[q] * lrelu_grad(ym[q]) : v[q];
+                }
+            }
+        }
+        {  // x window of the group's combos
+            const int items = GC * XR, nrows = GC * NR, tfo = tf * g.Fi;
+            int r = r_init, w = w_init;
+            for (int i0 = 0; i0 < items; i0 += NTH * DPER) {
+                int rq[DPER], wq[DPER];
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    rq[q] = r;
+                    wq[q] = w;
+                    w += dw;
+                    r += dr;
+                    if (w >= RL) {
+                        w -= RL;
+                        ++r;
+                    }
+                }
+                int4 e[DPER];
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) e[q] = rtab[rq[q] < nrows ? rq[q] : 0];
+                float v[DPER];
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    const int row = tf + e[q].y, pos = (e[q].z ? 0 : f0) * S - g.pf + wq[q];
+                    const bool ok = rq[q] < nrows && e[q].w && e[q].z < nr && row >= 0 && row < g.T2 && pos >= 0 &&
+                                    pos < g.Fi;
+                    const float t = xb[ok ? e[q].x + tfo + pos : 0];
+                    v[q] = ok ? t : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < DPER; ++q) {
+                    const int i = i0 + q * NTH + tid;
+                    if (i < items) Rs[i] = v[q];
+                }
+            }
+        }
+        for (int tl = tid; tl < P; tl += NTH) {
+            const int p = p0 + tl;
+            int off = 0;
+            if (p < pend) {
+                const int tr = p / g.Fo, f = p - tr * g.Fo, rs = tr - tf;
+                off = rs * RL + (f - (rs ? 0 : f0)) * S;
+            }
+            poff[tl] = off;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int kp = 0; kp < P / 2; ++kp) {
+            const int tl = 2 * kp + h;
+            const int po = poff[tl];
+            const float av = Ls[tl * LDA + l32];
+            if (do_bias) bsum += av;
+            float bv[NTW];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) bv[j] = Rs[cbase[j] + po];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) acc[j] = mfma32(av, bv[j], acc[j]);
+        }
+    }
+    float* wsb = a.ws + (int64_t)split * g.Co * N;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = n0 + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = mfma_row(r, lane);
+            if (co < g.Co && n < Nw) wsb[(int64_t)co * N + n] = acc[j][r];
+        }
+    }
+    if (do_bias) {
+        bsum += __shfl_xor(bsum, 32, 64);
+        if (h == 0 && l32 < g.Co) wsb[(int64_t)l32 * N + Nw] = bsum;
+    }
+}
+
 // dw[co][n] (+)= sum_s ws[s][co][n] for n < Nw; db[co] (+)= sum_s ws[s][co][Nw]. Fixed order.
 __global__ void c2_wg_reduce(const float* ws, int S, int Co, int N, float* dw, float* db, int acc_w,
                              int acc_b) {
@@ -757,27 +1071,100 @@ __global__ void feat_grad_kernel(const float* fr, const float* ff, int64_t n, fl
 // ---------------------------------------------------------------------------- planning
 static int c2_rows(int BN, int len) { return (len + BN - 2) / len + 1; }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int KFC = 0>
 int launch_fwd(C2Fwd a, hipStream_t st) {
     const size_t lds = ((size_t)a.CK * a.NR * a.RL + (size_t)a.g.KF * a.CK * BM +
                         (size_t)2 * a.g.Ci * a.g.KT * a.NR + 2) * sizeof(float);
     dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.g.Fo, BN), (unsigned)cdiv(a.g.Co, BM), (unsigned)a.g.B);
-    hipLaunchKernelGGL((c2_fwd_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((c2_fwd_kernel<BM, BN, WM, WN, KFC>), grid, dim3(NT), lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int JC = 0>
 int launch_dgrad(C2Dg a, hipStream_t st) {
     const size_t lds = ((size_t)a.CK * a.NR * a.RL + (size_t)a.J * a.CK * BM +
                         (size_t)2 * a.g.Co * a.g.KT * a.NR + 2) * sizeof(float);
     dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.U, BN), (unsigned)cdiv(a.g.Ci * a.g.sf, BM), (unsigned)a.g.B);
-    hipLaunchKernelGGL((c2_dgrad_kernel<BM, BN, WM, WN>), grid, dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((c2_dgrad_kernel<BM, BN, WM, WN, JC>), grid, dim3(NT), lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
 
 // channels per LDS chunk: even, <= VC rounded up to even, LDS <= budget floats
-static int c2_ck(int VC, int per_ch, int budget = 12288) {
+static int c2_ck(int VC, int per_ch, int budget = 12288);
+
+// planned launches: window geometry and LDS chunking for the column tile BN
+template <int BM, int BN, int WM, int WN, int KFC = 0>
+int run_fwd(C2Fwd a, hipStream_t st, int budget = 12288) {
+    a.NR = c2_rows(BN, a.g.Fo);
+    a.RL = (min(BN, a.g.Fo) - 1) * a.g.sf + a.g.KF;
+    a.CK = c2_ck(a.g.Ci * a.g.KT, a.NR * a.RL + a.g.KF * BM, budget);
+    return launch_fwd<BM, BN, WM, WN, KFC>(a, st);
+}
+template <int BM, int BN, int WM, int WN, int JC = 0>
+int run_dgrad(C2Dg a, hipStream_t st, int budget = 12288) {
+    a.J = (int)cdiv(a.g.KF, a.g.sf);
+    a.U = (a.g.Fi - 1 + a.g.pf) / a.g.sf + 1;
+    a.NR = c2_rows(BN, a.U);
+    a.RL = min(BN, a.U) - 1 + a.J;
+    a.CK = c2_ck(a.g.Co * a.g.KT, a.NR * a.RL + a.J * BM, budget);
+    return launch_dgrad<BM, BN, WM, WN, JC>(a, st);
+}
+
+template <int BN, int KFC, int CK, int MX>
+int run_fwdp(C2Fwd a, hipStream_t st) {
+    a.NR = c2_rows(BN, a.g.Fo);
+    a.RL = (min(BN, a.g.Fo) - 1) * a.g.sf + a.g.KF;
+    a.CK = CK;
+    if (a.g.KF != KFC || (int64_t)CK * a.NR * a.RL > (int64_t)MX * NT) return ENCX_EINVAL;
+    const size_t lds = ((size_t)CK * a.NR * a.RL + (size_t)KFC * CK * 32 + (size_t)2 * a.g.Ci * a.g.KT * a.NR) *
+                       sizeof(float);
+    dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.g.Fo, BN), (unsigned)cdiv(a.g.Co, 32), (unsigned)a.g.B);
+    hipLaunchKernelGGL((c2_fwdp_kernel<BN, KFC, CK, MX>), grid, dim3(NT), lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+// weight grad, column-group form (c2_wgrad2_kernel)
+struct WgPlan3 {
+    int NR, RL, GC, chunks, items, splits, per_split;
+    size_t lds;
+};
+static WgPlan3 plan_wg3(const C2Geo& g, int GC, int target = 1024) {
+    WgPlan3 p;
+    const int P = W2_P, Nall = g.T2 * g.Fo;
+    p.GC = GC;
+    p.NR = c2_rows(P, g.Fo);
+    p.RL = (min(P, g.Fo) - 1) * g.sf + g.KF;
+    p.chunks = (int)cdiv(Nall, P);
+    p.items = g.B * p.chunks;
+    const int groups = (int)cdiv(g.Ci * g.KT, GC);
+    int sp = (int)cdiv(target, groups);
+    if (sp > p.items) sp = p.items;
+    p.per_split = (int)cdiv(p.items, sp);
+    p.splits = (int)cdiv(p.items, p.per_split);
+    p.lds = ((size_t)4 * GC * p.NR + (size_t)P * 33 + P + (size_t)GC * p.NR * p.RL) * sizeof(float);
+    return p;
+}
+// combos per workgroup for the column-group wgrad, 0 when the layer does not fit its tiling
+static int wg3_gc(const C2Geo& g) {
+    const int VC = g.Ci * g.KT;
+    if (g.Co > 32) return 0;
+    if (g.KF == 9 && VC % 32 == 0) return 32;   // 288 columns = 3 waves x 3 tiles
+    if (g.KF == 3 && VC % 96 == 0) return 96;   // 288 columns
+    return 0;
+}
+template <int KF, int NTW, int NW>
+int run_wgrad2(const C2Geo& g, const float* dy, const float* yact, const float* x, float* ws, const WgPlan3& p,
+               hipStream_t st) {
+    C2Wg2 a{g, dy, yact, x, ws, p.NR, p.RL, p.GC, p.items, p.per_split, p.chunks};
+    dim3 grid((unsigned)cdiv(g.Ci * g.KT, p.GC), (unsigned)p.splits);
+    hipLaunchKernelGGL((c2_wgrad2_kernel<KF, NTW, NW>), grid, dim3(NW * 64), p.lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+static int c2_ck(int VC, int per_ch, int budget) {
     int ck = budget / per_ch;
     if (ck > 32) ck = 32;
     int vce = (VC + 1) & ~1;
@@ -974,6 +1361,7 @@ size_t encx_disc_loss_workspace(void) { return (size_t)2 * LP * sizeof(float); }
 int encx_hinge_loss(const float* x, int64_t n, double s, double scale, float* out, int accumulate, float* ws,
                     encx_stream_t stream) {
     ENCX_REQUIRE(x && out && ws && n > 0);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * n, 4.0 * n, "hinge", false);
     hipStream_t st = (hipStream_t)stream;
     const int nb = (int)min((int64_t)LP, cdiv(n, 256));
     hipLaunchKernelGGL(hinge_kernel, dim3(nb), dim3(256), 0, st, x, n, (float)s, ws);
@@ -988,6 +1376,7 @@ int encx_hinge_loss(const float* x, int64_t n, double s, double scale, float* ou
 int encx_feat_loss(const float* fr, const float* ff, int64_t n, double scale, float* out, float* denom,
                    int accumulate, float* ws, encx_stream_t stream) {
     ENCX_REQUIRE(fr && ff && out && ws && n > 0);
+    encx_prof_scope ps((hipStream_t)stream, 4.0 * n, 8.0 * n, "feat", false);
     hipStream_t st = (hipStream_t)stream;
     const int nb = (int)min((int64_t)LP, cdiv(n, 256));
     hipLaunchKernelGGL(feat_kernel, dim3(nb), dim3(256), 0, st, fr, ff, n, ws);
@@ -1001,6 +1390,7 @@ int encx_feat_loss(const float* fr, const float* ff, int64_t n, double scale, fl
 int encx_hinge_loss_bwd(const float* x, int64_t n, double s, double scale, const float* g0, float* dx,
                         encx_stream_t stream) {
     ENCX_REQUIRE(x && dx && n > 0);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * n, 8.0 * n, "hinge_bwd", false);
     hipLaunchKernelGGL(hinge_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, x, n,
                        (float)s, (float)scale, g0, dx);
     ENCX_CHECK_LAUNCH();
@@ -1011,6 +1401,7 @@ int encx_hinge_loss_bwd(const float* x, int64_t n, double s, double scale, const
 int encx_feat_loss_bwd(const float* fr, const float* ff, int64_t n, double scale, const float* denom,
                        const float* g0, float* dff, encx_stream_t stream) {
     ENCX_REQUIRE(fr && ff && denom && dff && n > 0);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * n, 12.0 * n, "feat_bwd", false);
     hipLaunchKernelGGL(feat_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, fr, ff, n,
                        (float)scale, denom, g0, dff);
     ENCX_CHECK_LAUNCH();

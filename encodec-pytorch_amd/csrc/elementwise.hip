@@ -2,6 +2,7 @@
 // EncodecModel._encode_frame, output rescale, the L1 time-domain loss, fixed-order reductions.
 // All reductions are two-pass with a fixed partition (no float atomics): bit-reproducible.
 #include "common.h"
+#include "prof.h"
 
 namespace {
 constexpr int NT = 256;
@@ -134,6 +135,7 @@ size_t encx_channel_sum_workspace(int64_t C) { return (size_t)C * CS_PARTS * siz
 int encx_channel_sum(const float* dy, float* db, float* ws, int64_t B, int64_t C, int64_t T,
                      int accumulate, encx_stream_t stream) {
     ENCX_REQUIRE(dy && db && ws && B > 0 && C > 0 && T > 0);
+    encx_prof_scope ps((hipStream_t)stream, 1.0 * B * C * T, 4.0 * B * C * T, "chan_sum", false);
     hipStream_t st = (hipStream_t)stream;
     // ~4096 positions per block: one pass for the short rows of the low-rate stages
     int64_t parts = B * T / 4096;
@@ -152,6 +154,7 @@ int encx_channel_sum(const float* dy, float* db, float* ws, int64_t B, int64_t C
 int encx_normalize_fwd(const float* x, float* xn, float* scale, int64_t B, int64_t C, int64_t T,
                        encx_stream_t stream) {
     ENCX_REQUIRE(x && xn && scale && B > 0 && C > 0 && T > 0);
+    encx_prof_scope ps((hipStream_t)stream, 4.0 * B * C * T, 8.0 * B * C * T, "normalize", false);
     hipLaunchKernelGGL(normalize_kernel, dim3(B), dim3(1024), 0, (hipStream_t)stream, x, xn, scale,
                        (int)C, (int)T);
     ENCX_CHECK_LAUNCH();
@@ -161,6 +164,7 @@ int encx_normalize_fwd(const float* x, float* xn, float* scale, int64_t B, int64
 int encx_scale_rows(const float* x, const float* scale, float* y, int64_t B, int64_t CT,
                     encx_stream_t stream) {
     ENCX_REQUIRE(x && scale && y && B > 0 && CT > 0);
+    encx_prof_scope ps((hipStream_t)stream, 1.0 * B * CT, 8.0 * B * CT, "scale_rows", false);
     int64_t n = B * CT;
     hipLaunchKernelGGL(scale_rows_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, x,
                        scale, y, CT, n);
@@ -171,6 +175,7 @@ int encx_scale_rows(const float* x, const float* scale, float* y, int64_t B, int
 int encx_axpby(const float* x, float* y, int64_t n, float alpha, const float* alpha_dev,
                float beta, encx_stream_t stream) {
     ENCX_REQUIRE(x && y && n >= 0);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * n, (beta != 0.f ? 12.0 : 8.0) * n, "axpby", false);
     if (n == 0) return 0;
     hipLaunchKernelGGL(axpby_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, x, y, n,
                        alpha, alpha_dev, beta);
@@ -181,6 +186,7 @@ int encx_axpby(const float* x, float* y, int64_t n, float alpha, const float* al
 int encx_l1_loss(const float* x, const float* y, float* loss, float* grad, float* ws, int64_t n,
                  encx_stream_t stream) {
     ENCX_REQUIRE(x && y && loss && ws && n > 0);
+    encx_prof_scope ps((hipStream_t)stream, 3.0 * n, (grad ? 12.0 : 8.0) * n, "l1_loss", false);
     hipStream_t st = (hipStream_t)stream;
     int blocks = (int)std::min<int64_t>(1024, cdiv(n, NT * 8));
     hipLaunchKernelGGL(l1_p1, dim3(blocks), dim3(NT), 0, st, x, y, grad, ws, n, 1.f / (float)n);

@@ -9,6 +9,7 @@
 // and for d/dy: dmel = (sign(d) + 2d)/Nel / (mel ln10) [mel >= 1e-5]; dP = dmel @ mel_basis;
 // G = [2 re dP | 2 im dP]; dframe = G @ [w*cos | -w*sin]^T; overlap-add + reflect fold -> dy.
 #include "common.h"
+#include "prof.h"
 #include "gemm.h"
 
 namespace {
@@ -242,6 +243,9 @@ int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws
                   float* grad, int64_t B, int64_t T, int64_t n_fft, int64_t n_mels,
                   encx_stream_t stream) {
     ENCX_REQUIRE(x && y && tables && ws && loss && B > 0 && n_fft >= 4 && (n_fft % 4) == 0);
+    const double rows_ = (double)geo(B, T, n_fft, n_mels).rows, nb_ = (double)(n_fft / 2 + 1);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * rows_ * (2 * nb_ * n_fft * 2 + nb_ * n_mels * 2) + (grad ? 2.0 * rows_ * (nb_ * n_mels + 2 * nb_ * n_fft) : 0.0),
+                       4.0 * B * T * (grad ? 3 : 2), "mel_loss");
     hipStream_t st = (hipStream_t)stream;
     const int nm = (int)n_mels;
     Geo g = geo(B, T, n_fft, n_mels);

@@ -6,6 +6,7 @@
 // finalise kernel per sample / channel, and one elementwise pass. All reductions run in a fixed
 // order (deterministic).
 #include "common.h"
+#include "prof.h"
 
 namespace {
 
@@ -186,6 +187,7 @@ int encx_groupnorm_fwd(const float* x, const float* gamma, const float* beta, fl
                        int64_t B, int64_t C, int64_t T, int64_t trim_left, int64_t Ty, double eps,
                        encx_stream_t stream) {
     ENCX_REQUIRE(x && y && stats && ws && B > 0 && C > 0 && T > 0);
+    encx_prof_scope ps((hipStream_t)stream, 6.0 * B * C * T, 8.0 * B * C * T, "groupnorm", false);
     ENCX_REQUIRE(trim_left >= 0 && Ty > 0 && trim_left + Ty <= T);
     hipStream_t st = (hipStream_t)stream;
     double* rows = (double*)ws;
@@ -203,6 +205,7 @@ int encx_groupnorm_bwd(const float* dy, const float* x, const float* gamma, cons
                        float* dgamma, float* dbeta, int acc_x, int acc_params, void* ws, float* coef, int64_t B,
                        int64_t C, int64_t T, int64_t trim_left, int64_t Ty, encx_stream_t stream) {
     ENCX_REQUIRE(dy && x && stats && ws && coef && B > 0 && C > 0 && T > 0);
+    encx_prof_scope ps((hipStream_t)stream, 8.0 * B * C * T, 12.0 * B * C * T, "groupnorm_bwd", false);
     ENCX_REQUIRE(trim_left >= 0 && Ty > 0 && trim_left + Ty <= T);
     hipStream_t st = (hipStream_t)stream;
     double* rows = (double*)ws;

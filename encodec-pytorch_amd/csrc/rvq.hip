@@ -12,6 +12,7 @@
 //                   visited in ascending order (deterministic), used by the EMA update (:227-235)
 //                   and by kmeans (:92-100).
 #include "common.h"
+#include "prof.h"
 #include "gemm.h"
 
 namespace {
@@ -391,6 +392,7 @@ int encx_rvq_argmin(const float* res, const float* embed, int64_t* idx, uint64_t
                     int64_t B, int64_t D, int64_t Tf, int64_t Kc, int direct,
                     encx_stream_t stream) {
     ENCX_REQUIRE(res && embed && idx && keys && B > 0 && D > 0 && D <= 256 && Tf > 0 && Kc > 0);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * B * Tf * Kc * D, 4.0 * (B * D * Tf + Kc * D) + 8.0 * B * Tf, "rvq_argmin");
     return argmin_run(bdt_rows(res, B, D, Tf), embed, idx, keys, (int)(B * Tf), (int)D, (int)Kc,
                       direct, (hipStream_t)stream);
 }
@@ -405,6 +407,7 @@ int encx_rvq_apply(const float* x, float* res_out, const float* embed, const int
                    float* out, float* commit_dir, float* commit_part, int64_t B, int64_t D,
                    int64_t Tf, int first, int ste, encx_stream_t stream) {
     ENCX_REQUIRE(x && res_out && embed && idx && B > 0 && D > 0 && Tf > 0);
+    encx_prof_scope ps((hipStream_t)stream, 4.0 * B * D * Tf, 4.0 * B * D * Tf * (2 + (out != nullptr) * 2 + (commit_dir != nullptr) * 2) + 8.0 * B * Tf, "rvq_apply", false);
     int64_t total = B * D * Tf;
     hipLaunchKernelGGL(rvq_apply_kernel, dim3(encx_rvq_apply_parts(B, D, Tf)), dim3(NT), 0,
                        (hipStream_t)stream, x, res_out, embed, idx, out, commit_dir, commit_part,
@@ -416,6 +419,7 @@ int encx_rvq_apply(const float* x, float* res_out, const float* embed, const int
 int encx_rvq_gather(const float* embed, const int64_t* idx, float* out, int64_t B, int64_t D,
                     int64_t Tf, int accumulate, encx_stream_t stream) {
     ENCX_REQUIRE(embed && idx && out && B > 0 && D > 0 && Tf > 0);
+    encx_prof_scope ps((hipStream_t)stream, 0.0, 4.0 * B * D * Tf * (accumulate ? 3 : 2), "rvq_gather", false);
     int64_t total = B * D * Tf;
     hipLaunchKernelGGL(rvq_gather_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream,
                        embed, idx, out, (int)D, (int)Tf, total, accumulate);
@@ -432,6 +436,7 @@ int encx_rvq_ema(const float* x, const int64_t* idx, float* cluster_size, float*
                  float* embed, float* ws, int64_t B, int64_t D, int64_t Tf, int64_t Kc,
                  float decay, float eps, encx_stream_t stream) {
     ENCX_REQUIRE(x && idx && cluster_size && embed_avg && embed && ws && D <= 256 && Kc > 0);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * B * Tf * Kc * (D + 1), 4.0 * (B * D * Tf + 4 * Kc * D) + 8.0 * B * Tf, "rvq_ema");
     hipStream_t st = (hipStream_t)stream;
     const float one_m = (float)(1.0 - (double)decay);
     int rc = bucket_run<0>(bdt_rows(x, B, D, Tf), idx, (int)(B * Tf), (int)D, (int)Kc, ws,

@@ -2,6 +2,7 @@
 // (balancer.py:83-118) and Adam (torch.optim.Adam as configured at train_multi_gpu.py:295-296).
 // Nothing here syncs with the host, so a whole train step can be captured in a hipGraph.
 #include "common.h"
+#include "prof.h"
 
 namespace {
 constexpr int NT = 256;
@@ -103,6 +104,7 @@ extern "C" {
 int encx_lincomb(const float* x, const float* z, float* out, int64_t n, float a, const float* bdev,
                  float bscale, encx_stream_t stream) {
     ENCX_REQUIRE(x && z && out && n >= 0);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * n, 12.0 * n, "lincomb", false);
     if (!n) return 0;
     hipLaunchKernelGGL(lincomb_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, x, z,
                        out, n, a, bdev, bscale);
@@ -115,6 +117,7 @@ size_t encx_item_norm_workspace(int64_t B) { return (size_t)B * NP * sizeof(floa
 int encx_item_norm_mean(const float* g, float* out, float* ws, int64_t B, int64_t L,
                         encx_stream_t stream) {
     ENCX_REQUIRE(g && out && ws && B > 0 && L > 0);
+    encx_prof_scope ps((hipStream_t)stream, 2.0 * B * L, 4.0 * B * L, "item_norm", false);
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(item_sq_kernel, dim3(B, NP), dim3(NT), 0, st, g, ws, L);
     ENCX_CHECK_LAUNCH();
@@ -145,6 +148,7 @@ int encx_balancer_scales(const double* avg, const float* red, const double* rati
 int encx_balancer_combine(const float* g0, const float* g1, const float* g2, const float* g3,
                           const float* scales, float* out, int64_t n, encx_stream_t stream) {
     ENCX_REQUIRE(g0 && scales && out && n > 0);
+    encx_prof_scope ps((hipStream_t)stream, 8.0 * n, 4.0 * n * (1 + (g0 != nullptr) + (g1 != nullptr) + (g2 != nullptr) + (g3 != nullptr)), "balancer_combine", false);
     hipLaunchKernelGGL(balancer_combine_kernel, dim3(cdiv(n, 256)), dim3(256), 0,
                        (hipStream_t)stream, g0, g1, g2, g3, scales, out, n);
     ENCX_CHECK_LAUNCH();
@@ -154,6 +158,7 @@ int encx_balancer_combine(const float* g0, const float* g1, const float* g2, con
 int encx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
                    double beta2, double eps, int64_t step, encx_stream_t stream) {
     ENCX_REQUIRE(p && g && m && v && n >= 0 && step >= 1);
+    encx_prof_scope ps((hipStream_t)stream, 10.0 * n, 28.0 * n, "adam");
     if (!n) return 0;
     const double bc1 = 1.0 - pow(beta1, (double)step);
     const double bc2 = 1.0 - pow(beta2, (double)step);

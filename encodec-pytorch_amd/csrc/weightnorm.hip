@@ -3,6 +3,7 @@
 // The forward writes the weight directly in the operand layouts of the conv kernels, so the
 // normalisation and the per-step re-layout are a single pass over the (small) weight.
 #include "common.h"
+#include "prof.h"
 
 namespace {
 
@@ -68,6 +69,7 @@ extern "C" {
 int encx_weightnorm_fwd(const float* v, const float* g, float* wf, float* wp, int64_t A0,
                         int64_t A1, int64_t K, int64_t stride, encx_stream_t stream) {
     ENCX_REQUIRE(v && A0 > 0 && A1 > 0 && K > 0 && stride > 0);
+    encx_prof_scope ps((hipStream_t)stream, 3.0 * A0 * A1 * K, 4.0 * A0 * A1 * K * (1 + (wf != nullptr) + (wp != nullptr)), "weightnorm", false);
     const int J = (int)cdiv(K, stride);
     hipLaunchKernelGGL(wn_fwd_kernel, dim3(A0), dim3(NT), 0, (hipStream_t)stream, v, g, wf, wp,
                        (int)A0, (int)A1, (int)K, (int)stride, J);
@@ -78,6 +80,7 @@ int encx_weightnorm_fwd(const float* v, const float* g, float* wf, float* wp, in
 int encx_weightnorm_bwd(const float* v, const float* g, const float* dw, float* dv, float* dg,
                         int64_t rows, int64_t cols, int accumulate, encx_stream_t stream) {
     ENCX_REQUIRE(v && g && dw && dv && dg && rows > 0 && cols > 0);
+    encx_prof_scope ps((hipStream_t)stream, 4.0 * rows * cols, 4.0 * rows * cols * (accumulate ? 4 : 3), "weightnorm_bwd", false);
     hipLaunchKernelGGL(wn_bwd_kernel, dim3(rows), dim3(NT), 0, (hipStream_t)stream, v, g, dw, dv,
                        dg, (int)cols, accumulate);
     ENCX_CHECK_LAUNCH();
