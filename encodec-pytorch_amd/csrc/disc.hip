@@ -314,6 +314,466 @@ __global__ __launch_bounds__(NT) void c2_fwdp_kernel(C2Fwd a) {
     }
 }
 
+// 4 floats from a dword-aligned global address (one global_load_dwordx4: the HSA target runs in
+// unaligned-access mode)
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+ENCX_DEV f32x4 ld4u(const float* p) { return *(const f32x4u*)p; }
+
+// One window row of the LDS image, as float4 quads: src = global offset of window column 0,
+// pos0 = its input column (-2^30 when the row lies outside the input), lim = input width.
+// Interior quads are one 16-byte load; quads that straddle the zero padding load per element
+// from clamped addresses.
+ENCX_DEV f32x4 window_quad(const float* base, int src, int pos0, int w, int lim) {
+    const int pos = pos0 + w;
+    if (pos >= 0 && pos + 3 < lim) return ld4u(base + src + w);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const bool ok = pos + e >= 0 && pos + e < lim;
+        const float t = base[ok ? src + w + e : 0];
+        v[e] = ok ? t : 0.f;
+    }
+    return v;
+}
+
+// Forward with vectorised staging: the implicit GEMM of c2_fwd_kernel (rows co, BN flattened
+// (t, f) columns, CK combos (ci, kt) x KFC taps per chunk, 4 waves x TN column tiles), but every
+// window row is moved as float4 quads (row stride RLp = RL rounded up to 4, so each quad is one
+// ds_write_b128) and the weights as float4 rows: ~10 vector instructions per 4 staged values
+// instead of ~12 per value, which left the matrix pipe idle behind the address arithmetic.
+template <int BN, int KFC, int CK>
+__global__ __launch_bounds__(NT) void c2_fwdv_kernel(C2Fwd a) {
+    constexpr int BM = 32, TN = BN / 128, WQ = KFC * CK * BM / 4, QU = 4;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int NR = a.NR, RL = a.RL, S = g.sf;
+    const int RLp = (RL + 3) & ~3, NQ = RLp >> 2;
+    const int VC = g.Ci * g.KT, XR = NR * RLp;
+    float* Xs = smem;                      // [CK][NR][RLp]
+    float* Ws = smem + CK * XR;            // [CK][KFC][BM]
+    int2* rtab = (int2*)(Ws + KFC * CK * BM);  // [VC*NR]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.z, n0 = blockIdx.x * BN, co0 = blockIdx.y * BM;
+    const int wn0 = wave * TN * 32;
+    const int Nall = g.T2 * g.Fo, nend = min(Nall, n0 + BN);
+    const int tf = n0 / g.Fo, f0 = n0 - tf * g.Fo;
+    const int nr = (nend - 1) / g.Fo - tf + 1;
+    int boff[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+        boff[j] = 0;
+        if (n < nend) {
+            const int tr = n / g.Fo, f = n - tr * g.Fo, rs = tr - tf;
+            boff[j] = rs * RLp + (f - (rs ? 0 : f0)) * S;
+        }
+    }
+    f32x16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = (f32x16){0};
+    const float* xb = a.x + (int64_t)b * g.Ci * g.T2 * g.Fi;
+    for (int gr = tid; gr < VC * NR; gr += NT) {
+        const int vc = gr / NR, rs = gr - vc * NR, ci = vc / g.KT, kt = vc - ci * g.KT;
+        const int row = tf + rs + kt * g.dt - g.pt, pos0 = (rs ? 0 : f0) * S - g.pf;
+        const bool ok = rs < nr && row >= 0 && row < g.T2;
+        rtab[gr] = make_int2(ok ? (ci * g.T2 + row) * g.Fi + pos0 : 0, ok ? pos0 : -(1 << 30));
+    }
+    // quad items (row, q) walked by a fixed step of NT: no division per item
+    const int dr = NT / NQ, dq = NT - dr * NQ, r_init = tid / NQ, q_init = tid - r_init * NQ;
+    for (int c0 = 0; c0 < VC; c0 += CK) {
+        __syncthreads();
+        {
+            // QU quads per thread in flight: interior quads are one 16-byte load from their own
+            // address; the rest load nothing here and are patched per element below (the row's
+            // ends, next to the zero padding)
+            const int nrows = min(CK, VC - c0) * NR, rows = CK * NR;
+            int r = r_init, q = q_init;
+            while (r < rows) {
+                int rq[QU], wq[QU];
+                bool in[QU];
+                int2 e[QU];
+                f32x4 v[QU];
+#pragma unroll
+                for (int u = 0; u < QU; ++u) {
+                    rq[u] = r;
+                    wq[u] = 4 * q;
+                    q += dq;
+                    r += dr;
+                    if (q >= NQ) {
+                        q -= NQ;
+                        ++r;
+                    }
+                    e[u] = rtab[c0 * NR + (rq[u] < nrows ? rq[u] : 0)];
+                    const int pos = e[u].y + wq[u];
+                    in[u] = rq[u] < nrows && pos >= 0 && pos + 3 < g.Fi;
+                    v[u] = ld4u(xb + (in[u] ? e[u].x + wq[u] : 0));
+                }
+#pragma unroll
+                for (int u = 0; u < QU; ++u) {
+                    if (!in[u]) {
+                        const int pos = e[u].y + wq[u];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const bool ok = rq[u] < nrows && pos + k >= 0 && pos + k < g.Fi;
+                            v[u][k] = ok ? xb[e[u].x + wq[u] + k] : 0.f;
+                        }
+                    }
+                    if (rq[u] < rows) *(f32x4*)(Xs + rq[u] * RLp + wq[u]) = v[u];
+                }
+            }
+        }
+        {
+            // Ws[cl][kf][col] = wf[(c0 + cl) * KFC + kf][co0 + col]: rows of BM floats, 8 quads each
+            const float* wsrc = a.wf + (int64_t)c0 * KFC * g.Co + co0;
+            const int wrows = (VC - c0) * KFC;
+            constexpr int WU = (WQ + NT - 1) / NT;
+            f32x4 v[WU];
+#pragma unroll
+            for (int u = 0; u < WU; ++u) {
+                const int j = u * NT + tid, rr = j >> 3, col = (j & 7) * 4;
+                const bool ok = j < WQ && rr < wrows && co0 + col + 3 < g.Co;
+                v[u] = ld4u(wsrc + (ok ? (int64_t)rr * g.Co + col : 0));
+                if (!ok) v[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < WU; ++u) {
+                const int j = u * NT + tid, rr = j >> 3, col = (j & 7) * 4;
+                if (j < WQ && rr < wrows && co0 + col + 3 >= g.Co)  // a partial last row tile (Co % 4 != 0)
+                    for (int k = 0; k < 4; ++k)
+                        v[u][k] = co0 + col + k < g.Co ? wsrc[(int64_t)rr * g.Co + col + k] : 0.f;
+                if (j < WQ) *(f32x4*)(Ws + rr * BM + col) = v[u];
+            }
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int cp = 0; cp < CK; cp += 2) {
+            const float* wk = Ws + (cp + h) * KFC * BM + l32;
+            const float* xk = Xs + (cp + h) * XR;
+#pragma unroll
+            for (int kf = 0; kf < KFC; ++kf) {
+                const float av = wk[kf * BM];
+                float bv[TN];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xk[boff[j] + kf];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[j] = mfma32(av, bv[j], acc[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = co0 + mfma_row(r, lane);
+            const float bco = a.bias ? a.bias[co < g.Co ? co : g.Co - 1] : 0.f;
+            if (co < g.Co && n < nend) {
+                float v = acc[j][r] + bco;
+                if (a.act) v = lrelu(v);
+                a.y[((int64_t)b * g.Co + co) * Nall + n] = v;
+            }
+        }
+    }
+}
+
+// Window quad through a CLAMPED 16-byte load: the load always reads 4 in-row floats starting at
+// c = clamp(pos, 0, lim - 4) (so it never leaves the row, whatever the padding), and the quad
+// for columns pos..pos+3 is recovered in registers: shift by s = pos - c, zeros outside
+// [0, lim). Every quad issues the same one load; only straddling quads run the (register-only)
+// fix-up, so a batch of quads keeps all its loads in flight.
+struct QuadSrc {
+    int addr;  // element offset of the clamped load (0 for a row outside the input)
+    int pos;   // first column of the quad; INT_MIN/2 -> the quad is all padding
+};
+ENCX_DEV QuadSrc quad_src(int2 e, int w, int lim, bool live) {
+    QuadSrc q;
+    const bool rowok = live && e.y > -(1 << 29);
+    const int pos = e.y + w;
+    const int c = min(max(pos, 0), lim - 4);
+    q.addr = rowok ? e.x - e.y + c : 0;
+    q.pos = rowok ? pos : -(1 << 30);
+    return q;
+}
+ENCX_DEV f32x4 quad_fix(f32x4 v, int pos, int lim) {
+    const int c = min(max(pos, 0), lim - 4), s = pos - c;
+    if (s == 0) return v;  // interior quad (also: every row outside the input has pos = -2^30)
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int k = e + s;
+        const float t = k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
+        o[e] = (k >= 0 && k < 4 && pos + e >= 0 && pos + e < lim) ? t : 0.f;
+    }
+    return o;
+}
+
+// Forward, vectorised AND register-pipelined: c2_fwdv_kernel's LDS image and compute loop, with
+// the next chunk's quads (window: MQ per thread, clamped loads; weights: MW) fetched into
+// registers before the current chunk's MFMAs, so each chunk costs one overlapped memory round
+// trip. CK (runtime, even) is sized so a chunk's window fits MQ quads per thread.
+template <int BN, int KFC, int MQ, int CKM, int DBG = 0>  // DBG: microbenchmark ablations only
+__global__ __launch_bounds__(NT) void c2_fwdq_kernel(C2Fwd a) {
+    constexpr int BM = 32, TN = BN / 128, MW = (KFC * CKM * BM / 4 + NT - 1) / NT;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int CK = a.CK, NR = a.NR, RL = a.RL, S = g.sf;
+    const int RLp = (RL + 3) & ~3, NQ = RLp >> 2;
+    const int VC = g.Ci * g.KT, XR = NR * RLp, WQ = KFC * CK * BM / 4;
+    float* Xs = smem;                      // [CK][NR][RLp]
+    float* Ws = smem + CK * XR;            // [CK][KFC][BM]
+    int2* rtab = (int2*)(Ws + KFC * CK * BM);  // [VC*NR]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.z, n0 = blockIdx.x * BN, co0 = blockIdx.y * BM;
+    const int wn0 = wave * TN * 32;
+    const int Nall = g.T2 * g.Fo, nend = min(Nall, n0 + BN);
+    const int tf = n0 / g.Fo, f0 = n0 - tf * g.Fo;
+    const int nr = (nend - 1) / g.Fo - tf + 1;
+    int boff[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+        boff[j] = 0;
+        if (n < nend) {
+            const int tr = n / g.Fo, f = n - tr * g.Fo, rs = tr - tf;
+            boff[j] = rs * RLp + (f - (rs ? 0 : f0)) * S;
+        }
+    }
+    f32x16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = (f32x16){0};
+    const float* xb = a.x + (int64_t)b * g.Ci * g.T2 * g.Fi;
+    for (int gr = tid; gr < VC * NR; gr += NT) {
+        const int vc = gr / NR, rs = gr - vc * NR, ci = vc / g.KT, kt = vc - ci * g.KT;
+        const int row = tf + rs + kt * g.dt - g.pt, pos0 = (rs ? 0 : f0) * S - g.pf;
+        const bool ok = rs < nr && row >= 0 && row < g.T2;
+        rtab[gr] = make_int2(ok ? (ci * g.T2 + row) * g.Fi + pos0 : 0, ok ? pos0 : -(1 << 30));
+    }
+    __syncthreads();
+    const int rows = CK * NR;
+    const int dr = NT / NQ, dq = NT - dr * NQ, r_init = tid / NQ, q_init = tid - r_init * NQ;
+    f32x4 xv[MQ], wv[MW];
+    int xpos[MQ], xdst[MQ];
+    auto fetch = [&](int c0) {
+        const int nrows = min(CK, VC - c0) * NR;
+        int r = r_init, q = q_init;
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            const bool live = r < nrows;
+            const QuadSrc s = quad_src(rtab[c0 * NR + (live ? r : 0)], 4 * q, g.Fi, live);
+            if (DBG & 1) xv[u] = (f32x4){1.f, 1.f, 1.f, (float)s.addr};
+            else xv[u] = ld4u(xb + s.addr);
+            xpos[u] = s.pos;
+            xdst[u] = r < rows ? r * RLp + 4 * q : -1;
+            q += dq;
+            r += dr;
+            if (q >= NQ) {
+                q -= NQ;
+                ++r;
+            }
+        }
+        const float* wsrc = a.wf + (int64_t)c0 * KFC * g.Co + co0;
+        const int wrows = (VC - c0) * KFC;
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const int j = u * NT + tid, rr = j >> 3, col = (j & 7) * 4;
+            const bool ok = j < WQ && rr < wrows && co0 + col + 3 < g.Co;
+            wv[u] = ld4u(wsrc + (ok ? (int64_t)rr * g.Co + col : 0));
+            if (!ok) wv[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    fetch(0);
+    for (int c0 = 0; c0 < VC; c0 += CK) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < MQ; ++u)
+            if (!(DBG & 2) && xdst[u] >= 0) *(f32x4*)(Xs + xdst[u]) = quad_fix(xv[u], xpos[u], g.Fi);
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const int j = u * NT + tid, rr = j >> 3, col = (j & 7) * 4;
+            if (j < WQ && rr < (VC - c0) * KFC && co0 + col + 3 >= g.Co)  // partial co tile (Co % 4)
+                for (int k = 0; k < 4; ++k)
+                    wv[u][k] = co0 + col + k < g.Co ? a.wf[((int64_t)c0 * KFC + rr) * g.Co + co0 + col + k] : 0.f;
+            if (j < WQ) *(f32x4*)(Ws + rr * BM + col) = wv[u];
+        }
+        __syncthreads();
+        if (c0 + CK < VC) fetch(c0 + CK);
+#pragma unroll 2
+        for (int cp = 0; cp < CK; cp += 2) {
+            const float* wk = Ws + (cp + h) * KFC * BM + l32;
+            const float* xk = Xs + (cp + h) * XR;
+#pragma unroll
+            for (int kf = 0; kf < KFC; ++kf) {
+                const float av = wk[kf * BM];
+                float bv[TN];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xk[boff[j] + kf];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[j] = mfma32(av, bv[j], acc[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = co0 + mfma_row(r, lane);
+            const float bco = a.bias ? a.bias[co < g.Co ? co : g.Co - 1] : 0.f;
+            if (co < g.Co && n < nend && (!(DBG & 4) || acc[j][r] == 1234.5f)) {
+                float v = acc[j][r] + bco;
+                if (a.act) v = lrelu(v);
+                a.y[((int64_t)b * g.Co + co) * Nall + n] = v;
+            }
+        }
+    }
+}
+
+// Forward with column-aligned window quads. A window row holds input columns [base, base + RLp)
+// of one input row, base = the row's first needed column rounded DOWN to a multiple of 4 (the
+// compute reads at an offset of col - base), so every quad is aligned to input columns: a quad
+// is entirely padding (left of column 0, or a row outside the input: a select, no load),
+// entirely interior, or the one quad holding column Fi - 1 whose tail lanes are masked. The
+// loads are issued for the next chunk before the current chunk's MFMAs (MQ quads per thread),
+// and the commit is a masked select + ds_write_b128: no per-element paths, no shifts.
+template <int BN, int KFC, int MQ, int CKM>
+__global__ __launch_bounds__(NT) void c2_fwdr_kernel(C2Fwd a) {
+    constexpr int BM = 32, TN = BN / 128, MW = (KFC * CKM * BM / 4 + NT - 1) / NT;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int CK = a.CK, NR = a.NR, RL = a.RL, S = g.sf;
+    const int RLp = (RL + 3) & ~3, NQ = RLp >> 2;
+    const int VC = g.Ci * g.KT, XR = NR * RLp, WQ = KFC * CK * BM / 4;
+    float* Xs = smem;                      // [CK][NR][RLp]
+    float* Ws = smem + CK * XR;            // [CK][KFC][BM]
+    int2* rtab = (int2*)(Ws + KFC * CK * BM);  // [VC*NR]: {offset of column `base`, base} / invalid
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.z, n0 = blockIdx.x * BN, co0 = blockIdx.y * BM;
+    const int wn0 = wave * TN * 32;
+    const int Nall = g.T2 * g.Fo, nend = min(Nall, n0 + BN);
+    const int tf = n0 / g.Fo, f0 = n0 - tf * g.Fo;
+    const int nr = (nend - 1) / g.Fo - tf + 1;
+    const int base0 = ((f0 * S - g.pf) & ~3), baseN = ((-g.pf) & ~3);  // floor to a multiple of 4
+    int boff[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+        boff[j] = 0;
+        if (n < nend) {
+            const int tr = n / g.Fo, f = n - tr * g.Fo, rs = tr - tf;
+            boff[j] = rs * RLp + f * S - g.pf - (rs ? baseN : base0);
+        }
+    }
+    f32x16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = (f32x16){0};
+    const int64_t xtot = (int64_t)g.B * g.Ci * g.T2 * g.Fi;
+    const float* xb = a.x + (int64_t)b * g.Ci * g.T2 * g.Fi;
+    const int64_t xleft = xtot - (int64_t)b * g.Ci * g.T2 * g.Fi;  // floats from xb to the tensor end
+    for (int gr = tid; gr < VC * NR; gr += NT) {
+        const int vc = gr / NR, rs = gr - vc * NR, ci = vc / g.KT, kt = vc - ci * g.KT;
+        const int row = tf + rs + kt * g.dt - g.pt, base = rs ? baseN : base0;
+        const bool ok = rs < nr && row >= 0 && row < g.T2;
+        rtab[gr] = make_int2(ok ? (ci * g.T2 + row) * g.Fi + base : 0, ok ? base : -(1 << 30));
+    }
+    __syncthreads();
+    const int rows = CK * NR;
+    const int dr = NT / NQ, dq = NT - dr * NQ, r_init = tid / NQ, q_init = tid - r_init * NQ;
+    f32x4 xv[MQ], wv[MW];
+    int xmask[MQ], xdst[MQ];
+    auto fetch = [&](int c0) {
+        const int nrows = min(CK, VC - c0) * NR;
+        int r = r_init, q = q_init;
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            const bool live = r < nrows;
+            const int2 e = rtab[c0 * NR + (live ? r : 0)];
+            const int col = e.y + 4 * q;  // first input column of the quad
+            const bool any = live && col >= 0 && col < g.Fi;  // e.y = -2^30 for rows outside
+            int off = any ? e.x + 4 * q : 0;
+            // the last quad of the tensor may run past its end: read it one quad earlier
+            // (only columns < Fi are kept, and those are then at lanes shifted... see mask)
+            if (off > xleft - 4) off = (int)xleft - 4;
+            xv[u] = ld4u(xb + off);
+            const int sh = (any ? e.x + 4 * q : 0) - off;  // 0 except at the tensor's very end
+            xmask[u] = any ? (min(g.Fi - col, 4) | (sh << 4)) : 0;  // valid lanes, shift
+            xdst[u] = r < rows ? r * RLp + 4 * q : -1;
+            q += dq;
+            r += dr;
+            if (q >= NQ) {
+                q -= NQ;
+                ++r;
+            }
+        }
+        const float* wsrc = a.wf + (int64_t)c0 * KFC * g.Co + co0;
+        const int wrows = (VC - c0) * KFC;
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const int j = u * NT + tid, rr = j >> 3, col = (j & 7) * 4;
+            const bool ok = j < WQ && rr < wrows && co0 + col + 3 < g.Co;
+            wv[u] = ld4u(wsrc + (ok ? (int64_t)rr * g.Co + col : 0));
+            if (!ok) wv[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    fetch(0);
+    for (int c0 = 0; c0 < VC; c0 += CK) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            const int m = xmask[u], nv = m & 15, sh = m >> 4;
+            f32x4 v = xv[u];
+            if (sh) {  // the tensor's last quad, read shifted back by sh lanes (one quad in all)
+                const f32x4 t = v;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = k + sh < 4 ? (k + sh == 1 ? t[1] : k + sh == 2 ? t[2] : t[3]) : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = k < nv ? v[k] : 0.f;
+            if (xdst[u] >= 0) *(f32x4*)(Xs + xdst[u]) = v;
+        }
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const int j = u * NT + tid, rr = j >> 3, col = (j & 7) * 4;
+            if (j < WQ && rr < (VC - c0) * KFC && co0 + col + 3 >= g.Co)  // partial co tile (Co % 4)
+                for (int k = 0; k < 4; ++k)
+                    wv[u][k] = co0 + col + k < g.Co ? a.wf[((int64_t)c0 * KFC + rr) * g.Co + co0 + col + k] : 0.f;
+            if (j < WQ) *(f32x4*)(Ws + rr * BM + col) = wv[u];
+        }
+        __syncthreads();
+        if (c0 + CK < VC) fetch(c0 + CK);
+#pragma unroll 2
+        for (int cp = 0; cp < CK; cp += 2) {
+            const float* wk = Ws + (cp + h) * KFC * BM + l32;
+            const float* xk = Xs + (cp + h) * XR;
+#pragma unroll
+            for (int kf = 0; kf < KFC; ++kf) {
+                const float av = wk[kf * BM];
+                float bv[TN];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xk[boff[j] + kf];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[j] = mfma32(av, bv[j], acc[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = co0 + mfma_row(r, lane);
+            const float bco = a.bias ? a.bias[co < g.Co ? co : g.Co - 1] : 0.f;
+            if (co < g.Co && n < nend) {
+                float v = acc[j][r] + bco;
+                if (a.act) v = lrelu(v);
+                a.y[((int64_t)b * g.Co + co) * Nall + n] = v;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------ backward data
 struct C2Dg {
     C2Geo g;
@@ -474,6 +934,162 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (m >= M) continue;
+                const int ci = m / S, rr = m - ci * S;
+                const int f = u * S + rr - g.pf;
+                if (f < 0 || f >= g.Fi) continue;
+                const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
+                float v = acc[i][j][r];
+                if (a.xact) v *= lrelu_grad(a.xact[o]);
+                a.dx[o] = a.accumulate ? a.dx[o] + v : v;
+            }
+        }
+}
+
+// Backward-data with column-aligned quads and register pipelining (c2_fwdr_kernel's staging
+// applied to c2_dgrad_kernel's polyphase GEMM): rows m = (ci, r) (BM = 32 * TM), columns
+// (t, u), reduction (co, kt) pairs x JC taps; the staged B image is dy * LeakyReLU'(y), both
+// read as aligned quads (dy columns [base, base + RLp), base = the window start rounded down to
+// a multiple of 4) and masked in the commit.
+template <int TM, int BN, int JC, int MQ, int CKM>
+__global__ __launch_bounds__(NT) void c2_dgradr_kernel(C2Dg a) {
+    constexpr int BM = 32 * TM, TN = BN / 128, MW = (JC * CKM * BM / 4 + NT - 1) / NT;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int CK = a.CK, NR = a.NR, RL = a.RL, U = a.U, S = g.sf;
+    const int RLp = (RL + 3) & ~3, NQ = RLp >> 2;
+    const int VC = g.Co * g.KT, XR = NR * RLp, M = g.Ci * S, WQ = JC * CK * BM / 4;
+    float* Xs = smem;                     // [CK][NR][RLp]
+    float* As = smem + CK * XR;           // [CK][JC][BM]
+    int2* rtab = (int2*)(As + JC * CK * BM);  // [VC*NR]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.z, n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const int wn0 = wave * TN * 32;
+    const int Nall = g.T2 * U, nend = min(Nall, n0 + BN);
+    const int tf = n0 / U, u0 = n0 - tf * U;
+    const int nr = (nend - 1) / U - tf + 1;
+    const int base0 = (u0 - (JC - 1)) & ~3, baseN = (-(JC - 1)) & ~3;
+    int boff[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l32;
+        boff[j] = JC - 1;  // in-range reads for masked columns
+        if (n < nend) {
+            const int tr = n / U, u = n - tr * U, rs = tr - tf;
+            boff[j] = rs * RLp + u - (rs ? baseN : base0);
+        }
+    }
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    const int64_t plane = (int64_t)g.T2 * g.Fo;
+    const float* dyb = a.dy + (int64_t)b * g.Co * plane;
+    const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane : dyb;
+    const int64_t left = (int64_t)(g.B - b) * g.Co * plane;  // floats from dyb to the tensor end
+    for (int gr = tid; gr < VC * NR; gr += NT) {
+        const int vc = gr / NR, rs = gr - vc * NR, co = vc / g.KT, kt = vc - co * g.KT;
+        const int row = tf + rs + g.pt - kt * g.dt, base = rs ? baseN : base0;
+        const bool ok = rs < nr && row >= 0 && row < g.T2;
+        rtab[gr] = make_int2(ok ? co * (int)plane + row * g.Fo + base : 0, ok ? base : -(1 << 30));
+    }
+    __syncthreads();
+    const int rows = CK * NR;
+    const int dr = NT / NQ, dq = NT - dr * NQ, r_init = tid / NQ, q_init = tid - r_init * NQ;
+    f32x4 xv[MQ], yv[MQ], wv[MW];
+    int xmask[MQ], xdst[MQ];
+    auto fetch = [&](int c0) {
+        const int nrows = min(CK, VC - c0) * NR;
+        int r = r_init, q = q_init;
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            const bool live = r < nrows;
+            const int2 e = rtab[c0 * NR + (live ? r : 0)];
+            const int col = e.y + 4 * q;
+            const bool any = live && col >= 0 && col < g.Fo;
+            int off = any ? e.x + 4 * q : 0;
+            if (off > left - 4) off = (int)left - 4;
+            xv[u] = ld4u(dyb + off);
+            yv[u] = ld4u(yab + off);
+            const int sh = (any ? e.x + 4 * q : 0) - off;
+            xmask[u] = any ? (min(g.Fo - col, 4) | (sh << 4)) : 0;
+            xdst[u] = r < rows ? r * RLp + 4 * q : -1;
+            q += dq;
+            r += dr;
+            if (q >= NQ) {
+                q -= NQ;
+                ++r;
+            }
+        }
+        const float* wsrc = a.wp + (int64_t)c0 * JC * M + m0;
+        const int wrows = (VC - c0) * JC;
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const int j = u * NT + tid, rr = j / (BM / 4), col = (j % (BM / 4)) * 4;
+            const bool ok = j < WQ && rr < wrows && m0 + col + 3 < M;
+            wv[u] = ld4u(wsrc + (ok ? (int64_t)rr * M + col : 0));
+            if (!ok) wv[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    fetch(0);
+    for (int c0 = 0; c0 < VC; c0 += CK) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            const int m = xmask[u], nv = m & 15, sh = m >> 4;
+            f32x4 v = xv[u], y = yv[u];
+            if (sh) {
+                const f32x4 t = v, ty = y;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    v[k] = k + sh < 4 ? (k + sh == 1 ? t[1] : k + sh == 2 ? t[2] : t[3]) : 0.f;
+                    y[k] = k + sh < 4 ? (k + sh == 1 ? ty[1] : k + sh == 2 ? ty[2] : ty[3]) : 0.f;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = k < nv ? (a.yact ? v[k] * lrelu_grad(y[k]) : v[k]) : 0.f;
+            if (xdst[u] >= 0) *(f32x4*)(Xs + xdst[u]) = v;
+        }
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const int j = u * NT + tid, rr = j / (BM / 4), col = (j % (BM / 4)) * 4;
+            if (j < WQ && rr < (VC - c0) * JC && m0 + col + 3 >= M)
+                for (int k = 0; k < 4; ++k)
+                    wv[u][k] = m0 + col + k < M ? a.wp[((int64_t)c0 * JC + rr) * M + m0 + col + k] : 0.f;
+            if (j < WQ) *(f32x4*)(As + rr * BM + col) = wv[u];
+        }
+        __syncthreads();
+        if (c0 + CK < VC) fetch(c0 + CK);
+#pragma unroll 2
+        for (int cp = 0; cp < CK; cp += 2) {
+            const float* aq = As + (cp + h) * JC * BM + l32;
+            const float* xq = Xs + (cp + h) * XR;
+#pragma unroll
+            for (int q = 0; q < JC; ++q) {
+                float av[TM], bv[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = aq[q * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xq[boff[j] - q];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 32 + l32;
+            if (n >= nend) continue;
+            const int tr = n / U, u = n - tr * U;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + i * 32 + mfma_row(r, lane);
                 if (m >= M) continue;
                 const int ci = m / S, rr = m - ci * S;
                 const int f = u * S + rr - g.pf;
@@ -918,6 +1534,182 @@ __global__ __launch_bounds__(NW * 64) void c2_wgrad2_kernel(C2Wg2 a) {
     }
 }
 
+// Weight grad, column-group form with vectorised staging: c2_wgrad2_kernel's GEMM (a
+// workgroup owns GC combos = NW * NTW column tiles and all Co <= 32 rows, positions staged
+// W3_P per chunk), but every staged value moves in aligned quads: dy and y along the positions
+// (then transposed into Ls[p][33] by four ds_write_b32), the x window as column-aligned quads
+// (c2_fwdr_kernel). All of a chunk's loads are issued before any of its LDS stores.
+constexpr int W3_P = 64;
+struct C2Wg3 {
+    C2Geo g;
+    const float* dy;
+    const float* yact;
+    const float* x;
+    float* ws;  // [splits][Co][N], N = VC*KF + 1
+    int NR, RL, GC, items, per_split, chunks;
+};
+template <int KF, int NTW, int NW, int MQ, int ML>
+__global__ __launch_bounds__(NW * 64) void c2_wgrad3_kernel(C2Wg3 a) {
+    constexpr int NTH = NW * 64, P = W3_P, LDA = 33, PQ = P / 4;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    const int NR = a.NR, RL = a.RL, GC = a.GC, S = g.sf;
+    const int RLp = (RL + 3) & ~3, NQ = RLp >> 2, XR = NR * RLp;
+    const int VC = g.Ci * g.KT, Nw = VC * KF, N = Nw + 1;
+    int4* rtab = (int4*)smem;                  // [GC*NR]: {offset at row tf, row - tf, rs, valid}
+    float* Ls = smem + 4 * GC * NR;            // [P][LDA]
+    int* poff = (int*)(Ls + P * LDA);          // [P]
+    float* Rs = (float*)(poff + P);            // [GC][NR][RLp] (16-byte aligned: see plan_wg3r)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int vc0 = blockIdx.x * GC, split = blockIdx.y;
+    const int n0 = vc0 * KF + wave * NTW * 32;
+    const int Nall = g.T2 * g.Fo;
+    const int64_t plane_y = (int64_t)Nall, plane_x = (int64_t)g.T2 * g.Fi;
+    const int64_t ytot = (int64_t)g.B * g.Co * plane_y, xtot = (int64_t)g.B * g.Ci * plane_x;
+    const bool do_bias = blockIdx.x == 0 && wave == 0;
+    const int baseN = (-g.pf) & ~3;
+    int cbase[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = n0 + j * 32 + l32;
+        const int vc = n / KF, kf = n - vc * KF;
+        cbase[j] = (n < Nw) ? (vc - vc0) * XR + kf : 0;
+    }
+    f32x16 acc[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[j] = (f32x16){0};
+    float bsum = 0.f;
+    for (int r = tid; r < GC * NR; r += NTH) {
+        const int cl = r / NR, rs = r - cl * NR, vc = vc0 + cl, ci = vc / g.KT, kt = vc - ci * g.KT;
+        const int rrel = rs + kt * g.dt - g.pt;
+        rtab[r] = make_int4(ci * (int)plane_x + rrel * g.Fi, rrel, rs, vc < VC);
+    }
+    const int dr = NTH / NQ, dq = NTH - dr * NQ, r_init = tid / NQ, q_init = tid - r_init * NQ;
+    const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
+    __syncthreads();
+    for (int it = it_beg; it < it_end; ++it) {
+        const int b = it / a.chunks, p0 = (it - b * a.chunks) * P;
+        const int pend = min(Nall, p0 + P);
+        const int tf = p0 / g.Fo, f0 = p0 - tf * g.Fo;
+        const int nr = (pend - 1) / g.Fo - tf + 1;
+        const int base0 = (f0 * S - g.pf) & ~3;
+        const int64_t yb = (int64_t)b * g.Co * plane_y, xbo = (int64_t)b * g.Ci * plane_x;
+        // ---- loads: dy / y quads along positions, x window quads
+        f32x4 dv[ML], yv[ML], xv[MQ];
+        int dmask[ML], xmask[MQ];
+#pragma unroll
+        for (int u = 0; u < ML; ++u) {
+            const int i = u * NTH + tid, co = i / PQ, k = i - co * PQ, p = p0 + 4 * k;
+            const bool any = i < 32 * PQ && co < g.Co && p < pend;
+            int64_t off = any ? yb + (int64_t)co * plane_y + p : 0;
+            const int64_t offc = off > ytot - 4 ? ytot - 4 : off;
+            dv[u] = ld4u(a.dy + offc);
+            yv[u] = ld4u((a.yact ? a.yact : a.dy) + offc);
+            dmask[u] = any ? (min(pend - p, 4) | ((int)(off - offc) << 4)) : 0;
+        }
+        {
+            int r = r_init, q = q_init;
+#pragma unroll
+            for (int u = 0; u < MQ; ++u) {
+                const int rr = r < GC * NR ? r : 0;
+                const int4 e = rtab[rr];
+                const int base = e.z ? baseN : base0, col = base + 4 * q;
+                const int row = tf + e.y;
+                const bool any = r < GC * NR && e.w && e.z < nr && row >= 0 && row < g.T2 && col >= 0 && col < g.Fi;
+                int64_t off = any ? xbo + e.x + (int64_t)tf * g.Fi + col : 0;
+                const int64_t offc = off > xtot - 4 ? xtot - 4 : off;
+                xv[u] = ld4u(a.x + offc);
+                xmask[u] = any ? (min(g.Fi - col, 4) | ((int)(off - offc) << 4)) : 0;
+                q += dq;
+                r += dr;
+                if (q >= NQ) {
+                    q -= NQ;
+                    ++r;
+                }
+            }
+        }
+        __syncthreads();  // the previous chunk's MFMAs are done with Ls / Rs
+#pragma unroll
+        for (int u = 0; u < ML; ++u) {
+            const int i = u * NTH + tid, co = i / PQ, k = i - co * PQ;
+            if (i < 32 * PQ) {
+                const int m = dmask[u], nv = m & 15, sh = m >> 4;
+                f32x4 v = dv[u], y = yv[u];
+                if (sh) {
+                    const f32x4 t = v, ty = y;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        v[c] = c + sh < 4 ? (c + sh == 1 ? t[1] : c + sh == 2 ? t[2] : t[3]) : 0.f;
+                        y[c] = c + sh < 4 ? (c + sh == 1 ? ty[1] : c + sh == 2 ? ty[2] : ty[3]) : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    Ls[(4 * k + c) * LDA + co] = c < nv ? (a.yact ? v[c] * lrelu_grad(y[c]) : v[c]) : 0.f;
+            }
+        }
+        {
+            int r = r_init, q = q_init;
+#pragma unroll
+            for (int u = 0; u < MQ; ++u) {
+                const int m = xmask[u], nv = m & 15, sh = m >> 4;
+                f32x4 v = xv[u];
+                if (sh) {
+                    const f32x4 t = v;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) v[c] = c + sh < 4 ? (c + sh == 1 ? t[1] : c + sh == 2 ? t[2] : t[3]) : 0.f;
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) v[c] = c < nv ? v[c] : 0.f;
+                if (r < GC * NR) *(f32x4*)(Rs + r * RLp + 4 * q) = v;
+                q += dq;
+                r += dr;
+                if (q >= NQ) {
+                    q -= NQ;
+                    ++r;
+                }
+            }
+        }
+        for (int tl = tid; tl < P; tl += NTH) {
+            const int p = p0 + tl;
+            int off = 0;
+            if (p < pend) {
+                const int tr = p / g.Fo, f = p - tr * g.Fo, rs = tr - tf;
+                off = rs * RLp + f * S - g.pf - (rs ? baseN : base0);
+            }
+            poff[tl] = off;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int kp = 0; kp < P / 2; ++kp) {
+            const int tl = 2 * kp + h;
+            const int po = poff[tl];
+            const float av = Ls[tl * LDA + l32];
+            if (do_bias) bsum += av;
+            float bv[NTW];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) bv[j] = Rs[cbase[j] + po];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) acc[j] = mfma32(av, bv[j], acc[j]);
+        }
+    }
+    float* wsb = a.ws + (int64_t)split * g.Co * N;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = n0 + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = mfma_row(r, lane);
+            if (co < g.Co && n < Nw) wsb[(int64_t)co * N + n] = acc[j][r];
+        }
+    }
+    if (do_bias) {
+        bsum += __shfl_xor(bsum, 32, 64);
+        if (h == 0 && l32 < g.Co) wsb[(int64_t)l32 * N + Nw] = bsum;
+    }
+}
+
 // dw[co][n] (+)= sum_s ws[s][co][n] for n < Nw; db[co] (+)= sum_s ws[s][co][Nw]. Fixed order.
 __global__ void c2_wg_reduce(const float* ws, int S, int Co, int N, float* dw, float* db, int acc_w,
                              int acc_b) {
@@ -1125,6 +1917,78 @@ int run_fwdp(C2Fwd a, hipStream_t st) {
     return 0;
 }
 
+template <int BN, int KFC, int CK>
+int run_fwdv(C2Fwd a, hipStream_t st) {
+    a.NR = c2_rows(BN, a.g.Fo);
+    a.RL = (min(BN, a.g.Fo) - 1) * a.g.sf + a.g.KF;
+    a.CK = CK;
+    if (a.g.KF != KFC) return ENCX_EINVAL;
+    const int RLp = (a.RL + 3) & ~3;
+    const size_t lds = ((size_t)CK * a.NR * RLp + (size_t)KFC * CK * 32 + (size_t)2 * a.g.Ci * a.g.KT * a.NR) *
+                       sizeof(float);
+    dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.g.Fo, BN), (unsigned)cdiv(a.g.Co, 32), (unsigned)a.g.B);
+    hipLaunchKernelGGL((c2_fwdv_kernel<BN, KFC, CK>), grid, dim3(NT), lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+// CK for c2_fwdq_kernel: the largest even combo count (<= CKM, <= VC rounded up to even) whose
+// window fits MQ quads per thread; 0 when not even 2 combos fit
+static int fwdq_ck(int VC, int NR, int RL, int MQ, int CKM) {
+    const int quads = NR * (((RL + 3) & ~3) >> 2);
+    int ck = MQ * NT / quads;
+    ck = min(ck, CKM);
+    ck = min(ck, (VC + 1) & ~1);
+    ck &= ~1;
+    return ck;
+}
+template <int BN, int KFC, int MQ, int CKM, int DBG = 0>
+int run_fwdq(C2Fwd a, hipStream_t st) {
+    a.NR = c2_rows(BN, a.g.Fo);
+    a.RL = (min(BN, a.g.Fo) - 1) * a.g.sf + a.g.KF;
+    a.CK = fwdq_ck(a.g.Ci * a.g.KT, a.NR, a.RL, MQ, CKM);
+    if (a.g.KF != KFC || a.CK < 2 || a.g.Fi < 4) return ENCX_EINVAL;
+    const int RLp = (a.RL + 3) & ~3;
+    const size_t lds = ((size_t)a.CK * a.NR * RLp + (size_t)KFC * a.CK * 32 + (size_t)2 * a.g.Ci * a.g.KT * a.NR) *
+                       sizeof(float);
+    dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.g.Fo, BN), (unsigned)cdiv(a.g.Co, 32), (unsigned)a.g.B);
+    hipLaunchKernelGGL((c2_fwdq_kernel<BN, KFC, MQ, CKM, DBG>), grid, dim3(NT), lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+template <int BN, int KFC, int MQ, int CKM>
+int run_fwdr(C2Fwd a, hipStream_t st) {
+    a.NR = c2_rows(BN, a.g.Fo);
+    a.RL = (min(BN, a.g.Fo) - 1) * a.g.sf + a.g.KF + 3;  // + alignment slack of the column base
+    a.CK = fwdq_ck(a.g.Ci * a.g.KT, a.NR, a.RL, MQ, CKM);
+    if (a.g.KF != KFC || a.CK < 2 || a.g.Fi < 4 || a.g.pf > 4) return ENCX_EINVAL;
+    const int RLp = (a.RL + 3) & ~3;
+    const size_t lds = ((size_t)a.CK * a.NR * RLp + (size_t)KFC * a.CK * 32 + (size_t)2 * a.g.Ci * a.g.KT * a.NR) *
+                       sizeof(float);
+    dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.g.Fo, BN), (unsigned)cdiv(a.g.Co, 32), (unsigned)a.g.B);
+    hipLaunchKernelGGL((c2_fwdr_kernel<BN, KFC, MQ, CKM>), grid, dim3(NT), lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+template <int TM, int BN, int JC, int MQ, int CKM>
+int run_dgradr(C2Dg a, hipStream_t st) {
+    a.J = (int)cdiv(a.g.KF, a.g.sf);
+    a.U = (a.g.Fi - 1 + a.g.pf) / a.g.sf + 1;
+    a.NR = c2_rows(BN, a.U);
+    a.RL = min(BN, a.U) - 1 + a.J + 3;
+    a.CK = fwdq_ck(a.g.Co * a.g.KT, a.NR, a.RL, MQ, CKM);
+    if (a.J != JC || a.CK < 2 || a.g.Fo < 4 || JC > 5 || a.g.Ci * a.g.sf > 32 * TM) return ENCX_EINVAL;
+    const int RLp = (a.RL + 3) & ~3;
+    const size_t lds = ((size_t)a.CK * a.NR * RLp + (size_t)JC * a.CK * 32 * TM + (size_t)2 * a.g.Co * a.g.KT * a.NR) *
+                       sizeof(float);
+    dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.U, BN), 1, (unsigned)a.g.B);
+    hipLaunchKernelGGL((c2_dgradr_kernel<TM, BN, JC, MQ, CKM>), grid, dim3(NT), lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
 // weight grad, column-group form (c2_wgrad2_kernel)
 struct WgPlan3 {
     int NR, RL, GC, chunks, items, splits, per_split;
@@ -1163,6 +2027,42 @@ int run_wgrad2(const C2Geo& g, const float* dy, const float* yact, const float* 
     ENCX_CHECK_LAUNCH();
     return 0;
 }
+
+static WgPlan3 plan_wg3r(const C2Geo& g, int GC, int target = 1024) {
+    WgPlan3 p;
+    const int P = W3_P, Nall = g.T2 * g.Fo;
+    p.GC = GC;
+    p.NR = c2_rows(P, g.Fo);
+    p.RL = (min(P, g.Fo) - 1) * g.sf + g.KF + 3;
+    p.chunks = (int)cdiv(Nall, P);
+    p.items = g.B * p.chunks;
+    const int groups = (int)cdiv(g.Ci * g.KT, GC);
+    int sp = (int)cdiv(target, groups);
+    if (sp > p.items) sp = p.items;
+    p.per_split = (int)cdiv(p.items, sp);
+    p.splits = (int)cdiv(p.items, p.per_split);
+    // rtab int4 [GC*NR] + Ls [P][33] + poff [P]: P*33 + P = 34*64 floats keeps Rs 16-byte aligned
+    p.lds = ((size_t)4 * GC * p.NR + (size_t)P * 33 + P + (size_t)GC * p.NR * (((p.RL + 3) & ~3))) * sizeof(float);
+    return p;
+}
+// the layers c2_wgrad3_kernel<9, 1, 9, 6, 1> serves: 3x9 taps, 32-combo groups, <= 32 rows
+static bool wg3r_ok(const C2Geo& g) {
+    if (g.KF != 9 || (g.Ci * g.KT) % 32 != 0 || g.Co > 32 || g.Fi < 4 || g.pf > 4) return false;
+    const WgPlan3 q = plan_wg3r(g, 32, 512);
+    return q.GC * q.NR * (((q.RL + 3) & ~3) >> 2) <= 6 * 9 * 64;
+}
+template <int KF, int NTW, int NW, int MQ, int ML>
+int run_wgrad3(const C2Geo& g, const float* dy, const float* yact, const float* x, float* ws, const WgPlan3& p,
+               hipStream_t st) {
+    const int quads = p.GC * p.NR * (((p.RL + 3) & ~3) >> 2);
+    if (quads > MQ * NW * 64 || 32 * (W3_P / 4) > ML * NW * 64 || g.Co > 32 || g.Fi < 4 || g.pf > 4) return ENCX_EINVAL;
+    C2Wg3 a{g, dy, yact, x, ws, p.NR, p.RL, p.GC, p.items, p.per_split, p.chunks};
+    dim3 grid((unsigned)cdiv(g.Ci * g.KT, p.GC), (unsigned)p.splits);
+    hipLaunchKernelGGL((c2_wgrad3_kernel<KF, NTW, NW, MQ, ML>), grid, dim3(NW * 64), p.lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
 
 static int c2_ck(int VC, int per_ch, int budget) {
     int ck = budget / per_ch;
@@ -1234,6 +2134,12 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + B * Co * T2 * Fo), "c2_fwd");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
+    // column-aligned, register-pipelined staging (c2_fwdr_kernel) for the 32-channel layers; the
+    // 2-channel first layer (K = 54) keeps the round-1 kernel, which is faster there
+    if (Co <= 32 && Ci * KT >= 16) {
+        if (KF == 9 && run_fwdr<256, 9, 6, 16>(a, st) == 0) return 0;
+        if (KF == 3 && run_fwdr<256, 3, 6, 32>(a, st) == 0) return 0;
+    }
     constexpr int BN = 128;
     a.NR = c2_rows(BN, (int)Fo);
     a.RL = (min(BN, (int)Fo) - 1) * (int)sf + (int)KF;
@@ -1260,6 +2166,8 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
     a.NR = c2_rows(BN, a.U);
     a.RL = min(BN, a.U) - 1 + a.J;
     const int M = (int)(Ci * sf);
+    if (M == 64 && KF == 9 && sf == 2 && run_dgradr<2, 256, 5, 6, 16>(a, st) == 0) return 0;
+    if (M <= 32 && KF == 3 && sf == 1 && run_dgradr<1, 256, 3, 6, 32>(a, st) == 0) return 0;
     if (sf == 1 && KT == 3 && KF == 9 && (Ci == 2 || Ci == 4) && Co % DN_CC == 0 && (KT - 1) * dt <= DN_MAXHALO) {
         dim3 grid((unsigned)cdiv(Fi, DN_COLS), (unsigned)cdiv(T2, DN_ROWS), (unsigned)B);
         if (Ci == 2) hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9>), grid, dim3(NT), 0, st, a);
@@ -1279,7 +2187,9 @@ size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64
                                         int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf) {
     C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
     WgPlan2 p = plan_wg2(g);
-    return (size_t)p.splits * Co * (Ci * KT * KF + 1) * sizeof(float);
+    int splits = p.splits;
+    if (wg3r_ok(g)) splits = max(splits, plan_wg3r(g, 32, 512).splits);
+    return (size_t)splits * Co * (Ci * KT * KF + 1) * sizeof(float);
 }
 
 /* dw [Co][Ci][KT][KF] and db [Co] (either may be NULL) of the layer whose output grad is dy,
@@ -1294,9 +2204,18 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
     hipStream_t st = (hipStream_t)stream;
     encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo), "c2_wgrad");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
+    const int N = (int)(Ci * KT * KF + 1);
+    if (wg3r_ok(g)) {  // 9 waves x one 32-column tile each, vectorised staging (c2_wgrad3_kernel)
+        const WgPlan3 q = plan_wg3r(g, 32, 512);
+        if (run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st) == 0) {
+            hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 256)), dim3(256), 0, st, ws, q.splits, (int)Co,
+                               N, dw, db, acc_w, acc_b);
+            ENCX_CHECK_LAUNCH();
+            return 0;
+        }
+    }
     WgPlan2 p = plan_wg2(g);
     C2Wg a{g, dy, yact, x, ws, p.BT, p.NR, p.RL, p.NCmax, p.items, p.per_split, p.chunks};
-    const int N = (int)(Ci * KT * KF + 1);
     const size_t lds = ((size_t)4 * p.NCmax * p.NR + (size_t)p.BT * 32 + (size_t)p.NCmax * p.NR * p.RL) * sizeof(float) +
                        p.BT * sizeof(int);
     if (p.narrow) {

@@ -10,7 +10,7 @@
 #include <functional>
 
 // the library's profiler scope is compiled out here
-encx_prof_scope::encx_prof_scope(hipStream_t s, double, double, const char*) : st(s), slot(-1) {}
+encx_prof_scope::encx_prof_scope(hipStream_t s, double, double, const char*, bool) : st(s), slot(-1) {}
 encx_prof_scope::~encx_prof_scope() {}
 void encx_prof_scope::tag(const char*, ...) {}
 
@@ -131,22 +131,31 @@ int main(int argc, char** argv) {
             };
             if (l.Co <= 32) {
                 if (l.KF == 9) {
-                    var("p<256,9,8,40>", [&] { if (run_fwdp<256, 9, 8, 40>(b, st)) printf("    (n/a)\n"); });
-                    var("p<128,9,8,24>", [&] { if (run_fwdp<128, 9, 8, 24>(b, st)) printf("    (n/a)\n"); });
+                    var("r<256,9,8,16>", [&] { if (run_fwdr<256, 9, 8, 16>(b, st)) printf("    (n/a)\n"); });
+                    var("r<256,9,12,16>", [&] { if (run_fwdr<256, 9, 12, 16>(b, st)) printf("    (n/a)\n"); });
+                    var("r<256,9,6,16>", [&] { if (run_fwdr<256, 9, 6, 16>(b, st)) printf("    (n/a)\n"); });
+                    var("r<512,9,12,16>", [&] { if (run_fwdr<512, 9, 12, 16>(b, st)) printf("    (n/a)\n"); });
+                    var("q<256,9,8,16>", [&] { if (run_fwdq<256, 9, 8, 16>(b, st)) printf("    (n/a)\n"); });
+                    var("q<256,9,16,16>", [&] { if (run_fwdq<256, 9, 16, 16>(b, st)) printf("    (n/a)\n"); });
+                    var("q<128,9,8,16>", [&] { if (run_fwdq<128, 9, 8, 16>(b, st)) printf("    (n/a)\n"); });
+                    var("q<512,9,16,16>", [&] { if (run_fwdq<512, 9, 16, 16>(b, st)) printf("    (n/a)\n"); });
+                    var("v<256,9,8>", [&] { run_fwdv<256, 9, 8>(b, st); });
+                    var("v<256,9,4>", [&] { run_fwdv<256, 9, 4>(b, st); });
+                    var("v<512,9,4>", [&] { run_fwdv<512, 9, 4>(b, st); });
+                    var("v<512,9,8>", [&] { run_fwdv<512, 9, 8>(b, st); });
+                    var("v<128,9,8>", [&] { run_fwdv<128, 9, 8>(b, st); });
+                    var("v<256,9,2>", [&] { run_fwdv<256, 9, 2>(b, st); });
                     var("p<256,9,4,24>", [&] { if (run_fwdp<256, 9, 4, 24>(b, st)) printf("    (n/a)\n"); });
-                    var("p<512,9,4,40>", [&] { if (run_fwdp<512, 9, 4, 40>(b, st)) printf("    (n/a)\n"); });
-                    var("<32,128,1,4,9>", [&] { run_fwd<32, 128, 1, 4, 9>(b, st); });
-                    var("<32,256,1,4,9>", [&] { run_fwd<32, 256, 1, 4, 9>(b, st); });
-                    var("<32,512,1,4,9>", [&] { run_fwd<32, 512, 1, 4, 9>(b, st); });
-                    var("<32,512,1,4,9> b8k", [&] { run_fwd<32, 512, 1, 4, 9>(b, st, 8192); });
-                    var("<32,256,1,4,9> b8k", [&] { run_fwd<32, 256, 1, 4, 9>(b, st, 8192); });
                 } else {
-                    var("p<256,3,16,32>", [&] { if (run_fwdp<256, 3, 16, 32>(b, st)) printf("    (n/a)\n"); });
+                    var("r<256,3,8,32>", [&] { if (run_fwdr<256, 3, 8, 32>(b, st)) printf("    (n/a)\n"); });
+                    var("r<256,3,6,32>", [&] { if (run_fwdr<256, 3, 6, 32>(b, st)) printf("    (n/a)\n"); });
+                    var("q<256,3,8,32>", [&] { if (run_fwdq<256, 3, 8, 32>(b, st)) printf("    (n/a)\n"); });
+                    var("q<256,3,12,32>", [&] { if (run_fwdq<256, 3, 12, 32>(b, st)) printf("    (n/a)\n"); });
+                    var("v<256,3,16>", [&] { run_fwdv<256, 3, 16>(b, st); });
+                    var("v<256,3,8>", [&] { run_fwdv<256, 3, 8>(b, st); });
+                    var("v<512,3,8>", [&] { run_fwdv<512, 3, 8>(b, st); });
                     var("p<256,3,8,16>", [&] { if (run_fwdp<256, 3, 8, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("<32,256,1,4,3>", [&] { run_fwd<32, 256, 1, 4, 3>(b, st); });
-                    var("<32,512,1,4,3>", [&] { run_fwd<32, 512, 1, 4, 3>(b, st); });
                 }
-                var("<32,256,1,4>", [&] { run_fwd<32, 256, 1, 4>(b, st); });
             }
             tot_new[0] += best;
         }
@@ -171,14 +180,15 @@ int main(int argc, char** argv) {
                 if (e <= 1e-5 && t < best) best = t;
             };
             if (M == 64 && J == 5) {
+                var("r<2,256,5,6,16>", [&] { if (run_dgradr<2, 256, 5, 6, 16>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,8,16>", [&] { if (run_dgradr<2, 256, 5, 8, 16>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,128,5,6,16>", [&] { if (run_dgradr<2, 128, 5, 6, 16>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,512,5,8,16>", [&] { if (run_dgradr<2, 512, 5, 8, 16>(b, st)) printf("    (n/a)\n"); });
                 var("<64,128,2,2,5>", [&] { run_dgrad<64, 128, 2, 2, 5>(b, st); });
-                var("<64,256,1,4,5>", [&] { run_dgrad<64, 256, 1, 4, 5>(b, st); });
-                var("<64,256,2,2,5>", [&] { run_dgrad<64, 256, 2, 2, 5>(b, st); });
-                var("<64,512,1,4,5>", [&] { run_dgrad<64, 512, 1, 4, 5>(b, st); });
-                var("<64,256,1,4,5> b8k", [&] { run_dgrad<64, 256, 1, 4, 5>(b, st, 8192); });
             } else if (M == 32 && J == 3) {
+                var("r<1,256,3,6,32>", [&] { if (run_dgradr<1, 256, 3, 6, 32>(b, st)) printf("    (n/a)\n"); });
+                var("r<1,256,3,8,32>", [&] { if (run_dgradr<1, 256, 3, 8, 32>(b, st)) printf("    (n/a)\n"); });
                 var("<32,256,1,4,3>", [&] { run_dgrad<32, 256, 1, 4, 3>(b, st); });
-                var("<32,512,1,4,3>", [&] { run_dgrad<32, 512, 1, 4, 3>(b, st); });
             }
             tot_new[1] += best;
         }
@@ -224,11 +234,33 @@ int main(int argc, char** argv) {
                        flops / t * 1e-9, e, e > 1e-5 ? "  MISMATCH" : "", q.splits, q.lds);
                 if (e <= 1e-5 && t < best) best = t;
             };
+            auto var3 = [&](const char* nm, int gc3, int target, std::function<int(const WgPlan3&)> f) {
+                WgPlan3 q = plan_wg3r(g, gc3, target);
+                CK(hipMemset(dw1, 0, (size_t)l.Co * N * 4));
+                bool bad = false;
+                double t = time_ms([&] {
+                    if (f(q)) bad = true;
+                    hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 256)), dim3(256), 0, st, ws, q.splits,
+                                       l.Co, N, dw1, db1, 0, 0);
+                });
+                if (bad) { printf("  wgrad %-23s n/a\n", nm); return; }
+                double e = fmax(rel_err(dw1, dw0, (size_t)l.Co * (N - 1)), rel_err(db1, db0, l.Co));
+                printf("  wgrad %-23s %8.1f us  %6.1f TF/s  err %.1e%s  (splits %d, lds %zu)\n", nm, t * 1e3,
+                       flops / t * 1e-9, e, e > 1e-5 ? "  MISMATCH" : "", q.splits, q.lds);
+                if (e <= 1e-5 && t < best) best = t;
+            };
             if (gc && l.KF == 9) {
+                var3("3<9,1,9,6,1> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,9,6,1> 32/1024", 32, 1024, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,3,3,16,3> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 16, 3>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,3,3,16,3> 32/1024", 32, 1024, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 16, 3>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,2,9,12,1> 64/512", 64, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 9, 12, 1>(g, dy, yact, x, ws, q, st); });
                 var("2<9,3,3> 512", 512, [&](const WgPlan3& q) { run_wgrad2<9, 3, 3>(g, dy, yact, x, ws, q, st); });
                 var("2<9,3,3> 1024", 1024, [&](const WgPlan3& q) { run_wgrad2<9, 3, 3>(g, dy, yact, x, ws, q, st); });
                 var("2<9,3,3> 2048", 2048, [&](const WgPlan3& q) { run_wgrad2<9, 3, 3>(g, dy, yact, x, ws, q, st); });
             } else if (gc && l.KF == 3) {
+                var3("3<3,1,9,16,1> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<3,3,3,24,3> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 3, 3, 24, 3>(g, dy, yact, x, ws, q, st); });
                 var("2<3,3,3> 512", 512, [&](const WgPlan3& q) { run_wgrad2<3, 3, 3>(g, dy, yact, x, ws, q, st); });
                 var("2<3,3,3> 1024", 1024, [&](const WgPlan3& q) { run_wgrad2<3, 3, 3>(g, dy, yact, x, ws, q, st); });
             }
