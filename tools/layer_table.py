@@ -52,7 +52,7 @@ def main():
         k = tag.value.decode()
         a = agg.setdefault(k, [0, 0.0, 0.0, 0.0])
         a[0] += 1
-        a[1] += ms.value
+        a[1] += max(ms.value, 0.0)  # booked-only (untimed) scopes report -1
         a[2] += fl.value
         a[3] += by.value
     lib.encx_prof_enable(0)
@@ -60,6 +60,8 @@ def main():
     tot = sum(a[1] for a in agg.values()) / S
     print(f'| op shape | calls/step | us/step | TFLOP/s | GB/s | % |\n|---|---|---|---|---|---|')
     for k, (c, ms, fl, by) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        if ms <= 0:
+            continue
         print(f'| {k} | {c // S} | {1e3 * ms / S:.1f} | {fl / ms / 1e9:.1f} | {by / ms / 1e6:.0f} | '
               f'{100 * ms / S / tot:.1f} |')
     print(f'\ntotal {tot:.3f} ms/step over {n.value // S} scopes; '
