@@ -9,6 +9,11 @@ series scales (config 4 = config 3 per rank): generator + RVQ (n_q 8) + MS-STFT 
 l_t / l_f / l_g / l_feat through the Balancer, commit loss, Adam, then the discriminator update
 (every step). `--config gen` = config 2 (no discriminator), `--config 48k` = config 5. Inputs are
 resident in HBM before the timed region. Rank 0 prints one JSON line.
+
+Steps replay HIP graphs (encx.train.Trainer(graphs=True): each step's device work captured once
+after one eager step, the collectives eager between segments at N > 1); --no-graphs steps eagerly.
+The warmup covers the eager step and the capture. The roofline / whole-step books come from a
+second, untimed, profiled pass of K eager steps (identical kernels).
 """
 import argparse
 import json
@@ -42,6 +47,7 @@ def parse():
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--no-graphs', action='store_true', help='eager steps instead of HIP-graph replay')
     return ap.parse_args()
 
 
@@ -109,7 +115,8 @@ def main():
         from encx.msstftd import MultiScaleSTFTDiscriminator
         disc = MultiScaleSTFTDiscriminator(filters=32, in_channels=2, out_channels=2).to(dev)
         trainer = Trainer(model, disc, lr=1e-4, disc_lr=1e-4, max_iter=100000, warmup_iter=500,
-                          weights={'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4}, sample_rate=48000)
+                          weights={'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4}, sample_rate=48000,
+                          graphs=not args.no_graphs)
         shape = (B, 2, 48000)
     else:
         model = EncodecModel._get_model([6.0], 24000, 1, causal=True, model_norm='weight_norm',
@@ -118,7 +125,8 @@ def main():
         if args.config == 'gan':
             from encx.msstftd import MultiScaleSTFTDiscriminator
             disc = MultiScaleSTFTDiscriminator(filters=32).to(dev)
-        trainer = Trainer(model, disc, lr=3e-4, disc_lr=3e-4, max_iter=100000, warmup_iter=500)
+        trainer = Trainer(model, disc, lr=3e-4, disc_lr=3e-4, max_iter=100000, warmup_iter=500,
+                          graphs=not args.no_graphs)
         shape = (B, 1, 24000)
     batches = [torch.from_numpy((0.1 * g.standard_normal(shape)).astype(np.float32)).to(dev)
                for _ in range(4)]
@@ -127,9 +135,6 @@ def main():
         trainer.step(batches[i % 4])
     torch.cuda.synchronize()
 
-    prof = not args.no_roofline
-    if prof:
-        lib.encx_prof_enable(1)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -144,6 +149,16 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t)
+    prof = not args.no_roofline
+    if prof:
+        # a second, untimed pass of the same K steps with the encx profiler on (eager: profiler
+        # events are not graph-captured) books every kernel's algorithmic FLOPs / bytes and times
+        # the conv family with HIP events on the launch stream; whole-step rates use the timed
+        # region's wall time above
+        lib.encx_prof_enable(1)
+        for i in range(args.steps):
+            trainer.step(batches[i % 4])
+        torch.cuda.synchronize()
     roof = whole = None
     if prof:
         import ctypes

@@ -86,6 +86,8 @@ int encx_prof_enable(int on) {
     return 0;
 }
 
+int encx_prof_enabled(void) { return g_prof_on.load() ? 1 : 0; }
+
 int encx_prof_read(double* total_ms, double* total_flops, double* total_bytes, int64_t* launches) {
     std::lock_guard<std::mutex> g(g_prof.mu);
     double ms = 0, fl = 0, by = 0;

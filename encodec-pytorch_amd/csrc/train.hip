@@ -97,6 +97,37 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, int64_
     m[i] = mi;
     v[i] = vi;
 }
+// Same update as adam_kernel with the per-step scalars read from device memory (written by
+// adam_hyper_kernel), so a HIP graph that captured this launch picks up each step's lr and bias
+// corrections on replay.
+__global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, int64_t n,
+                                const float* __restrict__ hp) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float w1 = hp[0], beta2 = hp[1], one_m_b2 = hp[2], step_size = hp[3], bc2_sqrt = hp[4],
+                eps = hp[5];
+    const float gi = g[i];
+    float mi = m[i];
+    mi = w1 < 0.5f ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.f - w1);
+    float vi = v[i] * beta2;
+    vi = vi + one_m_b2 * (gi * gi);
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] + (-step_size) * (mi / denom);
+    m[i] = mi;
+    v[i] = vi;
+}
+
+__global__ void adam_hyper_kernel(float* hp, float w1, float beta2, float one_m_b2, float step_size,
+                                  float bc2_sqrt, float eps) {
+    if (threadIdx.x == 0) {
+        hp[0] = w1;
+        hp[1] = beta2;
+        hp[2] = one_m_b2;
+        hp[3] = step_size;
+        hp[4] = bc2_sqrt;
+        hp[5] = eps;
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -165,6 +196,29 @@ int encx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, doub
     hipLaunchKernelGGL(adam_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                        n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
                        (float)(lr / bc1), (float)sqrt(bc2), (float)eps);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_adam_hyper(float* hp, double lr, double beta1, double beta2, double eps, int64_t step,
+                    encx_stream_t stream) {
+    ENCX_REQUIRE(hp && step >= 1);
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
+    hipLaunchKernelGGL(adam_hyper_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hp,
+                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)(lr / bc1),
+                       (float)sqrt(bc2), (float)eps);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hp,
+                       encx_stream_t stream) {
+    ENCX_REQUIRE(p && g && m && v && hp && n >= 0);
+    encx_prof_scope ps((hipStream_t)stream, 10.0 * n, 28.0 * n, "adam");
+    if (!n) return 0;
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g,
+                       m, v, n, hp);
     ENCX_CHECK_LAUNCH();
     return 0;
 }

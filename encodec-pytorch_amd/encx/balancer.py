@@ -54,41 +54,59 @@ class Balancer:
 
     def combine(self, grads):
         """grads: ordered dict name -> d loss / d input. Returns the out_grad of :110-118."""
+        self.combine_start(grads)
+        self.reduce_stats()
+        return self.combine_finish()
+
+    # combine() in three parts, so a HIP-graph-captured step can run the cross-rank statistics
+    # all-reduce eagerly between two captured segments (Trainer, graphs=True).
+    def combine_start(self, grads):
+        """Per-item norms and the EMA update (balancer.py:88-101) up to the all-reduce."""
         names = tuple(grads)
         g0 = next(iter(grads.values()))
         st = self._buffers(names, g0.device)
         s = stream()
-        gl = [g.contiguous() for g in grads.values()]
+        self._gl = [g.contiguous() for g in grads.values()]
         if self.rescale_grads:
             B = g0.shape[0] if self.per_batch_item else 1
             L = g0.numel() // B
             ws = torch.empty(lib.encx_item_norm_workspace(B) // 4, device=g0.device, dtype=torch.float32)
-            for i, g in enumerate(gl):
+            for i, g in enumerate(self._gl):
                 call('encx_item_norm_mean', ptr(g), ptr(st['norms'][i:i + 1]), ptr(ws), B, L, s)
             call('encx_balancer_update', ptr(st['norms']), ptr(st['total']), ptr(st['fix']),
                  ptr(st['avg']), ptr(st['red']), len(names), float(self.beta), float(B), s)
-            dist = distrib.is_distributed()
-            if dist:  # average_metrics (distrib.py:112-124)
-                torch.distributed.all_reduce(st['red'])
+
+    def reduce_stats(self):
+        """average_metrics (distrib.py:112-124): one all-reduce of nl+1 floats."""
+        if self.rescale_grads and distrib.is_distributed():
+            torch.distributed.all_reduce(self._state['red'])
+
+    def combine_finish(self):
+        """Scales and the rescaled gradient sum (balancer.py:102-118)."""
+        st, gl, s = self._state, self._gl, stream()
+        names = st['names']
+        if self.rescale_grads:
             call('encx_balancer_scales', ptr(st['avg']), ptr(st['red']), ptr(st['ratio']),
-                 ptr(st['scales']), len(names), float(self.total_norm), float(self.epsilon), int(dist), s)
+                 ptr(st['scales']), len(names), float(self.total_norm), float(self.epsilon),
+                 int(distrib.is_distributed()), s)
             scales = st['scales']
         else:
             scales = st['plain']
         out = torch.empty_like(gl[0])
         gp = [ptr(g) for g in gl] + [None] * (4 - len(gl))
         call('encx_balancer_combine', gp[0], gp[1], gp[2], gp[3], ptr(scales), ptr(out), out.numel(), s)
+        self._gl = None
         if self.monitor:
             avg = st['avg'].tolist()
             tot = sum(avg)
             self._metrics = {f'ratio_{k}': v / tot for k, v in zip(names, avg)}
         return out
 
+    def grads(self, losses, input):
+        return {name: autograd.grad(loss, [input], retain_graph=True)[0] for name, loss in losses.items()}
+
     def compute(self, losses, input):
-        grads = {}
-        for name, loss in losses.items():
-            grads[name], = autograd.grad(loss, [input], retain_graph=True)
-        return self.combine(grads)
+        return self.combine(self.grads(losses, input))
 
     def backward(self, losses, input, retain_graph=False):
         input.backward(self.compute(losses, input), retain_graph=retain_graph)

@@ -112,11 +112,13 @@ class EncodecModel(nn.Module):
             index = int(t.item())
         return self.target_bandwidths[index]
 
-    def forward(self, x: torch.Tensor):
-        """model.py:195-213. Train mode -> (output, loss_w, frames); eval -> output."""
+    def forward(self, x: torch.Tensor, bandwidth: tp.Optional[float] = None):
+        """model.py:195-213. Train mode -> (output, loss_w, frames); eval -> output.
+        `bandwidth` (train mode, not in the reference) fixes the step's target bandwidth instead
+        of drawing it here: the HIP-graph trainer draws it on the host before replaying."""
         frames = self.encode(x)
         if self.training:
-            bw = self._pick_bandwidth(x.device)
+            bw = self._pick_bandwidth(x.device) if bandwidth is None else bandwidth
             codes = []
             loss_w = None
             for emb, scale in frames:
@@ -125,6 +127,9 @@ class EncodecModel(nn.Module):
                 loss_w = pen if loss_w is None else loss_w + pen
                 codes.append((qv.quantized, scale))
             self.last_codes = [qv.codes]
+            # the decoder's input: its gradient is ready once every decoder weight grad is (the
+            # trainer's overlapped all-reduce of the decoder bucket hooks it)
+            self.last_decoder_input = codes[0][0] if len(codes) == 1 else None
             return self.decode(codes)[:, :, :x.shape[-1]], loss_w, frames
         return self.decode(frames)[:, :, :x.shape[-1]]
 

@@ -30,7 +30,9 @@ class FlatAdam(torch.optim.Optimizer):
         self.flat_grad = torch.zeros(n, device=dev, dtype=torch.float32)
         self.exp_avg = torch.zeros(n, device=dev, dtype=torch.float32)
         self.exp_avg_sq = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.hp = torch.zeros(8, device=dev, dtype=torch.float32)  # per-step scalars (encx_adam_hyper)
         self.n_step = 0
+        self._pending = []  # async all-reduce handles of buckets launched during backward
         o = 0
         self._views = []
         self.offsets = []
@@ -60,20 +62,61 @@ class FlatAdam(torch.optim.Optimizer):
                 g.copy_(p.grad)
                 p.grad = g
 
-    def all_reduce_grads(self):
+    def span(self, params):
+        """(start, end) of the flat-grad slice holding `params` (must be contiguous)."""
+        ids = {id(p) for p in params}
+        offs = [(o, k) for (p, _), (o, k) in zip(self._views, self.offsets) if id(p) in ids]
+        a, b = min(o for o, _ in offs), max(o + k for o, k in offs)
+        if sum(k for _, k in offs) != b - a:
+            raise ValueError('encx FlatAdam.span: params are not contiguous in the flat buffer')
+        return a, b
+
+    def all_reduce_bucket(self, a, b):
+        """Start the RCCL sum of flat_grad[a:b] now (async on the communicator's stream, ordered
+        after the work already queued on the current stream), so it overlaps the rest of the
+        backward. all_reduce_grads() reduces the remainder and waits."""
         if distrib.is_distributed():
-            torch.distributed.all_reduce(self.flat_grad)
+            work = torch.distributed.all_reduce(self.flat_grad[a:b], async_op=True)
+            self._pending.append((a, b, work))
+
+    def all_reduce_grads(self, scale=True):
+        """Sum flat_grad over ranks (buckets already started by all_reduce_bucket included), then
+        divide by the world size unless scale=False (the caller folds it in later)."""
+        if not distrib.is_distributed():
+            return
+        done = sorted((a, b) for a, b, _ in self._pending)
+        o = 0
+        for a, b in done + [(self.flat_grad.numel(), None)]:
+            if a > o:
+                torch.distributed.all_reduce(self.flat_grad[o:a])
+            o = b if b is not None else o
+        for _, _, work in self._pending:
+            work.wait()
+        self._pending = []
+        if scale:
             self.flat_grad.div_(distrib.world_size())
+
+    def prepare(self):
+        """Host half of a step: advance the step count and write this step's scalars into
+        self.hp with one small launch (its arguments are fixed at launch time, so the host may
+        run steps ahead of the device)."""
+        self.n_step += 1
+        self._opt_called = True  # what torch's LR-scheduler step-order check looks for
+        grp = self.param_groups[0]
+        b1, b2 = grp['betas']
+        call('encx_adam_hyper', ptr(self.hp), float(grp['lr']), float(b1), float(b2),
+             float(grp['eps']), self.n_step, stream())
+
+    def launch(self):
+        """Device half: the update itself, reading self.hp (HIP-graph capturable)."""
+        self.gather_grads()
+        call('encx_adam_step_dev', ptr(self.flat), ptr(self.flat_grad), ptr(self.exp_avg),
+             ptr(self.exp_avg_sq), self.flat.numel(), ptr(self.hp), stream())
 
     @torch.no_grad()
     def step(self, closure=None):
-        self.gather_grads()
-        self.n_step += 1
-        grp = self.param_groups[0]
-        b1, b2 = grp['betas']
-        call('encx_adam_step', ptr(self.flat), ptr(self.flat_grad), ptr(self.exp_avg),
-             ptr(self.exp_avg_sq), self.flat.numel(), float(grp['lr']), float(b1), float(b2),
-             float(grp['eps']), self.n_step, stream())
+        self.prepare()
+        self.launch()
 
     # ------------------------------------------------------------------ checkpoints
     def state_dict(self):

@@ -36,7 +36,7 @@ DEFAULT_WEIGHTS = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}  # config/config
 class Trainer:
     def __init__(self, model: EncodecModel, disc=None, lr=3e-4, disc_lr=3e-4, betas=(0.5, 0.9),
                  weights=None, max_iter=100000, warmup_iter=0, disc_prob=1.0, sample_rate=24000,
-                 scheduler=True, balancer_kwargs=None):
+                 scheduler=True, balancer_kwargs=None, graphs=False):
         self.model = model
         self.disc = disc
         self.sample_rate = sample_rate
@@ -59,51 +59,170 @@ class Trainer:
                                                        warmup_iter=warmup_iter, warmup_ratio=1e-4)
         self.disc_prob = disc_prob
         self.disc_mode = DiscGradMode()
+        self.graphs = graphs
+        self._graphs = {}
+        dec = [p for p in model.decoder.parameters() if p.requires_grad]
+        self._dec_span = self.opt.span(dec) if dec else None
 
+    # ------------------------------------------------------------------ step
+    # step() = host part (draw the bandwidth and the discriminator coin, advance the optimiser step
+    # counts and write their scalars) + device part. The device part is a list of segments with
+    # the cross-rank collectives between them:
+    #   A  forward, discriminator, losses, per-loss grads, balancer statistics
+    #   -- all-reduce balancer statistics (world > 1)
+    #   B  balancer scales + combine, the one backward (decoder-grad bucket all-reduce overlaps
+    #      the encoder backward when eager)
+    #   -- all-reduce generator grads
+    #   C  generator Adam; discriminator loss + weight-grad backward
+    #   -- all-reduce discriminator grads
+    #   D  discriminator Adam
+    # With graphs=True each (bandwidth, coin, shape) key runs eagerly once, is then captured into
+    # HIP graphs (one per segment; world 1: the whole step is one graph), and is replayed after.
     def step(self, x):
         model, disc = self.model, self.disc
         model.train()
-        self.opt.zero_grad()
-        y, loss_w, _ = model(x)
         if disc is not None:
             disc.train()
-            # generator phase: the balancer's autograd.grad calls differentiate the shared
-            # discriminator graph w.r.t. the fake audio only
-            self.disc_mode.set(params=False, input=True)
-            yd = y.detach().requires_grad_()
-            logits_real, fmap_real = disc(x, mode=self.disc_mode)
-            logits_fake, fmap_fake = disc(yd, mode=self.disc_mode)
-            losses = total_loss(fmap_real, logits_fake, fmap_fake, x, yd, self.sample_rate)
-            out_grad = self.balancer.compute(losses, yd)
+        bw = model._pick_bandwidth(x.device)
+        train_d = disc is not None and self._pick_train_d(x.device)
+        self.opt.prepare()
+        if train_d:
+            self.opt_d.prepare()
+        key = (bw, train_d, tuple(x.shape))
+        if self.graphs and self._graph_ok():
+            out = self._graph_step(key, x)
         else:
-            losses = total_loss(None, None, None, x, y, self.sample_rate)
-            out_grad = self.balancer.compute(losses, y)
-        torch.autograd.backward([y, loss_w], [out_grad, torch.ones_like(loss_w)])
-        self.opt.all_reduce_grads()
-        self.opt.step()
-        out = dict(losses)
-        out['loss_w'] = loss_w
-        if disc is not None:
-            train_d = random.random() < self.disc_prob
-            if distrib.is_distributed() and self.disc_prob < 1.0:
-                t = torch.tensor([train_d], device=x.device)
-                torch.distributed.broadcast(t, 0)
-                train_d = bool(t.item())
-            if train_d:
-                # discriminator phase on the same graph: weight grads only (train_multi_gpu.py:112-124)
-                self.disc_mode.set(params=True, input=False)
-                self.opt_d.zero_grad()
-                ld = disc_loss(logits_real, logits_fake)
-                ld.backward()
-                self.opt_d.all_reduce_grads()
-                self.opt_d.step()
-                out['l_d'] = ld
-            del logits_real, fmap_real, logits_fake, fmap_fake
+            out = self._run(x, bw, train_d, overlap=True)
         if self.sched is not None:
             self.sched.step()
         if self.sched_d is not None:
             self.sched_d.step()
         return out
+
+    def _pick_train_d(self, device):
+        train_d = random.random() < self.disc_prob
+        if distrib.is_distributed() and self.disc_prob < 1.0:
+            t = torch.tensor([train_d], device=device)
+            torch.distributed.broadcast(t, 0)
+            train_d = bool(t.item())
+        return train_d
+
+    def _segments(self, x, bw, train_d, overlap):
+        """The device part as (segment, collective) pairs; state flows through `c`."""
+        c = {}
+        dist = distrib.is_distributed()
+
+        def seg_a():
+            self.opt.zero_grad()
+            y, loss_w, _ = self.model(x, bandwidth=bw)
+            c['y'], c['loss_w'] = y, loss_w
+            if overlap and dist:
+                q = self.model.last_decoder_input
+                if q is not None and q.requires_grad:
+                    a, b = self._dec_span
+                    q.register_hook(lambda g: self.opt.all_reduce_bucket(a, b))
+            if self.disc is not None:
+                # generator phase: the balancer's autograd.grad calls differentiate the shared
+                # discriminator graph w.r.t. the fake audio only
+                self.disc_mode.set(params=False, input=True)
+                yd = y.detach().requires_grad_()
+                c['logits_real'], fmap_real = self.disc(x, mode=self.disc_mode)
+                c['logits_fake'], fmap_fake = self.disc(yd, mode=self.disc_mode)
+                losses = total_loss(fmap_real, c['logits_fake'], fmap_fake, x, yd, self.sample_rate)
+                wrt = yd
+            else:
+                losses = total_loss(None, None, None, x, y, self.sample_rate)
+                wrt = y
+            c['losses'] = losses
+            self.balancer.combine_start(self.balancer.grads(losses, wrt))
+
+        def seg_b():
+            out_grad = self.balancer.combine_finish()
+            y, loss_w = c.pop('y'), c['loss_w']
+            torch.autograd.backward([y, loss_w], [out_grad, torch.ones_like(loss_w)])
+
+        def seg_c():
+            if dist:
+                self.opt.flat_grad.div_(distrib.world_size())
+            self.opt.launch()
+            out = dict(c['losses'])
+            out['loss_w'] = c['loss_w']
+            if train_d:
+                # discriminator phase on the same graph: weight grads only (train_multi_gpu.py:112-124)
+                self.disc_mode.set(params=True, input=False)
+                self.opt_d.zero_grad()
+                out['l_d'] = disc_loss(c['logits_real'], c['logits_fake'])
+                out['l_d'].backward()
+            c.clear()
+            c['out'] = out
+
+        def seg_d():
+            if train_d:
+                if dist:
+                    self.opt_d.flat_grad.div_(distrib.world_size())
+                self.opt_d.launch()
+
+        return [(seg_a, self.balancer.reduce_stats),
+                (seg_b, lambda: self.opt.all_reduce_grads(scale=False)),
+                (seg_c, (lambda: self.opt_d.all_reduce_grads(scale=False)) if train_d else None),
+                (seg_d, None)], c
+
+    def _run(self, x, bw, train_d, overlap=False):
+        segs, c = self._segments(x, bw, train_d, overlap)
+        for seg, coll in segs:
+            seg()
+            if coll is not None:
+                coll()
+        return c['out']
+
+    def _graph_ok(self):
+        from ._lib import lib
+        if lib.encx_prof_enabled() or self.balancer.monitor:
+            return False  # profiler events / the monitor's host read are not capturable
+        q = getattr(self.model, 'quantizer', None)
+        return not (distrib.is_distributed() and q is not None and getattr(q, 'sync_codebooks', False))
+
+    def _graph_step(self, key, x):
+        ent = self._graphs.get(key)
+        if ent is None:
+            # first occurrence: eager (kmeans init, lazily built tables and the balancer state
+            # happen here, outside any capture)
+            self._graphs[key] = 'warm'
+            return self._run(x, key[0], key[1])
+        if ent == 'warm':  # second occurrence: capture, which also runs this step
+            ent = self._graphs[key] = self._capture(key, x)
+            return ent[3]
+        graphs, colls, xs, out = ent
+        xs.copy_(x)
+        for g, coll in zip(graphs, colls):
+            g.replay()
+            if coll is not None:
+                coll()
+        return out
+
+    def _capture(self, key, x):
+        xs = x.detach().clone()
+        segs, c = self._segments(xs, key[0], key[1], overlap=False)
+        if not distrib.is_distributed():  # no collectives: the whole step is one graph
+            parts = [s for s, _ in segs]
+            segs = [(lambda: [s() for s in parts], None)]
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        graphs, colls = [], []
+        for seg, coll in segs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                seg()
+            graphs.append(g)
+            colls.append(coll)
+            if coll is not None:  # capture only records: run the segment for real before the
+                g.replay()        # collective, which the next capture does not depend on
+                coll()
+        # the segments before the last collective already ran; replay the rest
+        start = max([i + 1 for i, cl in enumerate(colls) if cl is not None], default=0)
+        for g in graphs[start:]:
+            g.replay()
+        return graphs, colls, xs, c['out']
 
     # ------------------------------------------------------------------ checkpoints
     def state_dicts(self):

@@ -162,7 +162,9 @@ def train(local_rank, world_size, config):
     trainer = Trainer(model, disc, lr=float(config.optimization.lr), disc_lr=float(config.optimization.disc_lr),
                       weights=dict(vars(config.balancer.weights)), sample_rate=int(config.model.sample_rate),
                       max_iter=config.common.max_epoch * steps,
-                      warmup_iter=config.lr_scheduler.warmup_epoch * steps)
+                      warmup_iter=config.lr_scheduler.warmup_epoch * steps,
+                      # opt-in, not a reference key: replay each step from HIP graphs
+                      graphs=bool(getattr(config.common, 'hip_graphs', False)))
     start_epoch = 1
     if config.checkpoint.resume:
         # train_multi_gpu.py:226-238 + :303-308; weights_only loads (no unpickling)

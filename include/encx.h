@@ -43,6 +43,8 @@ int encx_init(int device);
  * family is bracketed by hipEvents on its own stream together with its algorithmic FLOPs and
  * bytes. family: 0 = all conv/GEMM MFMA kernels. */
 int encx_prof_enable(int on);
+/* 1 while profiling is on (the HIP-graph trainer steps eagerly then: events are not captured) */
+int encx_prof_enabled(void);
 int encx_prof_read(double* total_ms, double* total_flops, double* total_bytes, int64_t* launches);
 /* One recorded launch group: event time, algorithmic FLOPs / bytes and its label
  * ("<op> <shape>"), for per-layer tables (tools/layer_table.py). */
@@ -251,6 +253,14 @@ int encx_balancer_combine(const float* g0, const float* g1, const float* g2, con
  * step count after increment (train_multi_gpu.py:295-296 betas (0.5, 0.9)). */
 int encx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
                    double beta2, double eps, int64_t step, encx_stream_t stream);
+/* The same step split for HIP-graph replay: encx_adam_hyper writes the step's scalars
+ * {1-beta1, beta2, 1-beta2, lr/bc1, sqrt(bc2), eps} (6 floats) into device memory `hp` as a
+ * launch argument (eager, before the replay); encx_adam_step_dev (the captured launch) reads them.
+ * Bit-identical to encx_adam_step for the same arguments. */
+int encx_adam_hyper(float* hp, double lr, double beta1, double beta2, double eps, int64_t step,
+                    encx_stream_t stream);
+int encx_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hp,
+                       encx_stream_t stream);
 
 /* ---- SLSTM (modules/lstm.py:12-28 -> torch.nn.LSTM(dim, dim, num_layers) + skip) ----
  * All L layers run as one diagonal wavefront (launch k advances layer l to frame k - l):

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda:0'
 
 
-def make_trainer(B=4):
+def make_trainer(B=4, graphs=False, disc_on=True, disc_prob=1.0):
     from oracle import encodec_oracle as O
     from encx.model import EncodecModel
     from encx.msstftd import MultiScaleSTFTDiscriminator
@@ -39,9 +39,13 @@ def make_trainer(B=4):
         for k, v in cb.items():
             sd[f'quantizer.vq.layers.{i}._codebook.{k}'] = v
     m.load_state_dict(sd)
-    disc = MultiScaleSTFTDiscriminator(filters=32)
-    disc.load_state_dict(disc_state(5), strict=False)
-    tr = Trainer(m.to(DEV), disc.to(DEV), lr=3e-4, disc_lr=3e-4, max_iter=100, warmup_iter=3)
+    disc = None
+    if disc_on:
+        disc = MultiScaleSTFTDiscriminator(filters=32)
+        disc.load_state_dict(disc_state(5), strict=False)
+        disc = disc.to(DEV)
+    tr = Trainer(m.to(DEV), disc, lr=3e-4, disc_lr=3e-4, max_iter=100, warmup_iter=3,
+                 graphs=graphs, disc_prob=disc_prob)
     return tr
 
 
@@ -50,8 +54,9 @@ def batches(n, B=4):
 
 
 def snapshot(tr):
-    out = {'gen': tr.opt.flat.clone(), 'gen_m': tr.opt.exp_avg.clone(), 'gen_v': tr.opt.exp_avg_sq.clone(),
-           'disc': tr.opt_d.flat.clone(), 'disc_m': tr.opt_d.exp_avg.clone()}
+    out = {'gen': tr.opt.flat.clone(), 'gen_m': tr.opt.exp_avg.clone(), 'gen_v': tr.opt.exp_avg_sq.clone()}
+    if tr.opt_d is not None:
+        out.update({'disc': tr.opt_d.flat.clone(), 'disc_m': tr.opt_d.exp_avg.clone()})
     for k, v in tr.model.state_dict().items():
         if '_codebook' in k:
             out[k] = v.clone()
@@ -109,3 +114,28 @@ def test_resume_matches_uninterrupted_run():
     tr2.step(xs[3])
     torch.cuda.synchronize()
     assert_same(want, snapshot(tr2))
+
+
+@pytest.mark.parametrize('case', ['gan', 'gen', 'gan_coin'])
+def test_hip_graph_steps_match_eager(case):
+    """Trainer(graphs=True): step 1 eager, step 2 captured + replayed, steps 3.. replayed, with
+    the LR changing every step (warmup) and a new batch each step. Every step's losses and the
+    final parameters, Adam moments and codebooks must equal the eager trainer's bit for bit.
+    gan_coin trains the discriminator with probability 0.5: two graph keys."""
+    import random
+    xs = batches(6)
+    kw = dict(disc_on=case != 'gen', disc_prob=0.5 if case == 'gan_coin' else 1.0)
+    runs = []
+    for graphs in (False, True):
+        random.seed(11)
+        tr = make_trainer(graphs=graphs, **kw)
+        losses = []
+        for x in xs:
+            o = tr.step(x)
+            losses.append({k: float(v) for k, v in o.items()})
+        torch.cuda.synchronize()
+        runs.append((losses, snapshot(tr), tr))
+    assert runs[0][0] == runs[1][0]
+    assert_same(runs[0][1], runs[1][1])
+    g = runs[1][2]._graphs
+    assert any(isinstance(v, tuple) for v in g.values())
