@@ -1860,6 +1860,150 @@ __global__ void feat_grad_kernel(const float* fr, const float* ff, int64_t n, fl
     dff[i] = d > 0.f ? g : (d < 0.f ? -g : 0.f);
 }
 
+// ------------------------------------------------------------- single output channel (Co = 1)
+// The post conv of each DiscriminatorSTFT (msstftd.py:80-81, 32 -> 1, 3x3) has one output
+// channel, so an MFMA tile would idle 31 of its 32 rows. These are VALU kernels with the taps
+// unrolled (KT, KF, stride compile-time) and clamped loads, so every lane keeps its KT*KF loads in
+// flight; lanes run along the frequency axis (coalesced). Each input element is read KT*KF
+// times through L1/L2; the HBM traffic is the algorithmic |x| + |y| (+ |dx|).
+constexpr int C1_ROWS = 4;  // fwd: ci groups per block (waves); dgrad: rows per block
+
+// y[b][0][t][fo]: block = 64 output columns x 4 ci groups of one (b, t); the 4 partial sums meet
+// in LDS in a fixed order.
+template <int KT, int KF, int S>
+__global__ __launch_bounds__(256) void c2_co1_fwd(C2Fwd a) {
+    const C2Geo g = a.g;
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, cg = threadIdx.x >> 6;
+    const int plane = g.T2 * g.Fo, p = blockIdx.x * 64 + lane, b = blockIdx.y;
+    const int pc = p < plane ? p : plane - 1;
+    const int t = pc / g.Fo, fo = pc - t * g.Fo;
+    const int64_t xplane = (int64_t)g.T2 * g.Fi;
+    const int cper = (g.Ci + 3) >> 2, c0 = cg * cper, c1 = min(g.Ci, c0 + cper);
+    const int fb = fo * S - g.pf;
+    float acc = 0.f;
+    for (int ci = c0; ci < c1; ++ci) {
+        const float* xc = a.x + ((int64_t)b * g.Ci + ci) * xplane;
+        const float* w = a.wf + ci * KT * KF;
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+            const int tr = t + kt * g.dt - g.pt;
+            const bool rok = tr >= 0 && tr < g.T2;
+            const float* row = xc + (int64_t)(rok ? tr : 0) * g.Fi;
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf) {
+                const int f = fb + kf;
+                const bool ok = rok && f >= 0 && f < g.Fi;
+                const float v = row[ok ? f : 0];
+                acc = fmaf(w[kt * KF + kf], ok ? v : 0.f, acc);
+            }
+        }
+    }
+    part[cg][lane] = acc;
+    __syncthreads();
+    if (cg == 0 && p < plane) {
+        float v = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+        if (a.bias) v += a.bias[0];
+        a.y[(int64_t)b * plane + p] = a.act ? lrelu(v) : v;
+    }
+}
+
+// dx[b][ci][ti][fi] = sum_{kt,kf} W[ci][kt][kf] * dy'[b][ti - kt*dt + pt][(fi - kf + pf)/S]
+// (terms whose output column is fractional or out of range drop), dy' = dy * LeakyReLU'(yact).
+// Block = 64 columns x 4 rows of one (b, ci) plane.
+template <int KT, int KF, int S>
+__global__ __launch_bounds__(256) void c2_co1_dgrad(C2Dg a) {
+    const C2Geo g = a.g;
+    const int xplane = g.T2 * g.Fi, p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= xplane) return;
+    const int ti = p / g.Fi, fi = p - ti * g.Fi;
+    const int bc = blockIdx.y, b = bc / g.Ci, ci = bc - b * g.Ci;
+    const int64_t plane = (int64_t)g.T2 * g.Fo;
+    const float* dyb = a.dy + (int64_t)b * plane;
+    const float* yab = a.yact ? a.yact + (int64_t)b * plane : dyb;
+    const int M = g.Ci * S;
+    float acc = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+        const int to = ti - kt * g.dt + g.pt;
+        const bool rok = to >= 0 && to < g.T2;
+#pragma unroll
+        for (int kf = 0; kf < KF; ++kf) {
+            const int fs = fi - kf + g.pf;
+            const int fo = fs / S;  // S is 1 or 2: a shift
+            const bool ok = rok && fs >= 0 && (S == 1 || fs % S == 0) && fo < g.Fo;
+            const int64_t o = ok ? (int64_t)to * g.Fo + fo : 0;
+            float d = dyb[o];
+            if (a.yact) d *= lrelu_grad(yab[o]);
+            const float w = a.wp[(kt * a.J + kf / S) * M + ci * S + kf % S];
+            acc = fmaf(w, ok ? d : 0.f, acc);
+        }
+    }
+    const int64_t i = (int64_t)bc * xplane + p;
+    if (a.xact) acc *= lrelu_grad(a.xact[i]);
+    a.dx[i] = a.accumulate ? a.dx[i] + acc : acc;
+}
+
+// ws[s][0][n], s = (b, row chunk): n = (ci*KT + kt)*KF + kf -> sum over the chunk's output
+// positions of dy'[b][to][fo] * x[b][ci][to + kt*dt - pt][fo*S + kf - pf]; n = Ci*KT*KF -> the
+// chunk's sum of dy' (bias). Block = 4 waves (one ci each, blockIdx.z picks the ci group) x 64
+// lanes along fo; per-lane partials are summed over the wave in a fixed order through LDS.
+template <int KT, int KF, int S>
+__global__ __launch_bounds__(256) void c2_co1_wgrad(C2Wg a) {
+    constexpr int K = KT * KF;
+    const C2Geo g = a.g;
+    __shared__ float red[4][K + 1][65];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int rc = blockIdx.x, b = blockIdx.y, ci = blockIdx.z * 4 + wave;
+    const int N = g.Ci * K + 1, rows = a.BT;
+    const int to0 = rc * rows, to1 = min(g.T2, to0 + rows);
+    const int64_t plane = (int64_t)g.T2 * g.Fo, xplane = (int64_t)g.T2 * g.Fi;
+    const float* dyb = a.dy + (int64_t)b * plane;
+    const float* yab = a.yact ? a.yact + (int64_t)b * plane : dyb;
+    const float* xc = a.x + ((int64_t)b * g.Ci + (ci < g.Ci ? ci : 0)) * xplane;
+    float acc[K], bacc = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.f;
+    const int p1 = to1 * g.Fo;
+    for (int base = to0 * g.Fo; base < p1; base += 64) {
+        {
+            const int p = base + lane;
+            const bool cok = p < p1;
+            const int pc = cok ? p : p1 - 1;
+            const int to = pc / g.Fo, fo = pc - to * g.Fo;
+            const int64_t o = pc;
+            float d = dyb[o];
+            if (a.yact) d *= lrelu_grad(yab[o]);
+            d = cok ? d : 0.f;
+            bacc += d;
+#pragma unroll
+            for (int kt = 0; kt < KT; ++kt) {
+                const int tr = to + kt * g.dt - g.pt;
+                const bool rok = tr >= 0 && tr < g.T2;
+                const float* row = xc + (int64_t)(rok ? tr : 0) * g.Fi;
+#pragma unroll
+                for (int kf = 0; kf < KF; ++kf) {
+                    const int f = fo * S + kf - g.pf;
+                    const bool ok = rok && f >= 0 && f < g.Fi;
+                    const float v = row[ok ? f : 0];
+                    acc[kt * KF + kf] = fmaf(d, ok ? v : 0.f, acc[kt * KF + kf]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[wave][k][lane] = acc[k];
+    red[wave][K][lane] = bacc;
+    __syncthreads();
+    if (lane <= K) {
+        float v = 0.f;
+        for (int l = 0; l < 64; ++l) v += red[wave][lane][l];
+        float* out = a.ws + ((int64_t)b * gridDim.x + rc) * N;
+        if (lane < K && ci < g.Ci) out[ci * K + lane] = v;
+        if (lane == K && blockIdx.z == 0 && wave == 0) out[N - 1] = v;
+    }
+}
+
 // ---------------------------------------------------------------------------- planning
 static int c2_rows(int BN, int len) { return (len + BN - 2) / len + 1; }
 
@@ -2100,6 +2244,20 @@ static WgPlan2 plan_wg2(const C2Geo& g) {
     return p;
 }
 
+// Co = 1 wgrad: splits = (b, row chunk), about 512 of them
+struct WgPlanC1 {
+    int rows, chunks, splits;
+};
+static bool co1_ok(const C2Geo& g) { return g.Co == 1 && g.KT == 3 && g.KF == 3 && (g.sf == 1 || g.sf == 2); }
+static WgPlanC1 plan_co1(const C2Geo& g) {
+    WgPlanC1 p;
+    const int per_b = max(1, 512 / g.B);
+    p.rows = (int)cdiv(g.T2, per_b);
+    p.chunks = (int)cdiv(g.T2, p.rows);
+    p.splits = g.B * p.chunks;
+    return p;
+}
+
 static bool geo_ok(const C2Geo& g) {
     return g.B > 0 && g.Ci > 0 && g.T2 > 0 && g.Fi > 0 && g.Co > 0 && g.Fo > 0 && g.KT > 0 && g.KF > 0 &&
            g.sf > 0 && g.dt > 0 && g.pt >= 0 && g.pf >= 0 &&
@@ -2134,6 +2292,13 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + B * Co * T2 * Fo), "c2_fwd");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
+    if (Co == 1 && KT == 3 && KF == 3 && (sf == 1 || sf == 2)) {
+        dim3 grid((unsigned)cdiv(T2 * Fo, 64), (unsigned)B);
+        if (sf == 1) hipLaunchKernelGGL((c2_co1_fwd<3, 3, 1>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((c2_co1_fwd<3, 3, 2>), grid, dim3(256), 0, st, a);
+        ENCX_CHECK_LAUNCH();
+        return 0;
+    }
     // column-aligned, register-pipelined staging (c2_fwdr_kernel) for the 32-channel layers; the
     // 2-channel first layer (K = 54) keeps the round-1 kernel, which is faster there
     if (Co <= 32 && Ci * KT >= 16) {
@@ -2166,6 +2331,13 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
     a.NR = c2_rows(BN, a.U);
     a.RL = min(BN, a.U) - 1 + a.J;
     const int M = (int)(Ci * sf);
+    if (Co == 1 && KT == 3 && KF == 3 && (sf == 1 || sf == 2)) {
+        dim3 grid((unsigned)cdiv(T2 * Fi, 256), (unsigned)(B * Ci));
+        if (sf == 1) hipLaunchKernelGGL((c2_co1_dgrad<3, 3, 1>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((c2_co1_dgrad<3, 3, 2>), grid, dim3(256), 0, st, a);
+        ENCX_CHECK_LAUNCH();
+        return 0;
+    }
     if (M == 64 && KF == 9 && sf == 2 && run_dgradr<2, 256, 5, 6, 16>(a, st) == 0) return 0;
     if (M <= 32 && KF == 3 && sf == 1 && run_dgradr<1, 256, 3, 6, 32>(a, st) == 0) return 0;
     if (sf == 1 && KT == 3 && KF == 9 && (Ci == 2 || Ci == 4) && Co % DN_CC == 0 && (KT - 1) * dt <= DN_MAXHALO) {
@@ -2189,6 +2361,7 @@ size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64
     WgPlan2 p = plan_wg2(g);
     int splits = p.splits;
     if (wg3r_ok(g)) splits = max(splits, plan_wg3r(g, 32, 512).splits);
+    if (co1_ok(g)) splits = max(splits, plan_co1(g).splits);
     return (size_t)splits * Co * (Ci * KT * KF + 1) * sizeof(float);
 }
 
@@ -2205,6 +2378,18 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
     encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo), "c2_wgrad");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     const int N = (int)(Ci * KT * KF + 1);
+    if (co1_ok(g)) {
+        const WgPlanC1 q = plan_co1(g);
+        C2Wg a{g, dy, yact, x, ws, q.rows, 0, 0, 0, 0, 0, 0};
+        dim3 grid((unsigned)q.chunks, (unsigned)B, (unsigned)cdiv(Ci, 4));
+        if (sf == 1) hipLaunchKernelGGL((c2_co1_wgrad<3, 3, 1>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((c2_co1_wgrad<3, 3, 2>), grid, dim3(256), 0, st, a);
+        ENCX_CHECK_LAUNCH();
+        hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, st, ws, q.splits, 1, N, dw, db,
+                           acc_w, acc_b);
+        ENCX_CHECK_LAUNCH();
+        return 0;
+    }
     if (wg3r_ok(g)) {  // 9 waves x one 32-column tile each, vectorised staging (c2_wgrad3_kernel)
         const WgPlan3 q = plan_wg3r(g, 32, 512);
         if (run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st) == 0) {

@@ -197,7 +197,8 @@ LAYERS = [(2, 32, (3, 9), (1, 1), (1, 1), (1, 4)),
           (32, 32, (3, 9), (1, 2), (4, 1), (4, 4)),
           (32, 32, (3, 3), (1, 1), (1, 1), (1, 1)),
           (32, 1, (3, 3), (1, 1), (1, 1), (1, 1)),
-          (4, 32, (3, 9), (1, 1), (1, 1), (1, 4))]  # first layer of the 48 kHz stereo disc
+          (4, 32, (3, 9), (1, 1), (1, 1), (1, 4)),  # first layer of the 48 kHz stereo disc
+          (32, 1, (3, 3), (1, 2), (2, 1), (2, 1))]  # one output channel, strided + dilated (+ act)
 
 
 @pytest.mark.parametrize('li', range(len(LAYERS)))
@@ -226,4 +227,9 @@ def test_conv2d_vs_torch_fp64(li, T2, Fi):
     assert rel(y, y64) < 1e-5
     assert rel(x.grad, x64.grad) < 1e-5, rel(x.grad, x64.grad)
     assert rel(v.grad, v64.grad) < 1e-5, rel(v.grad, v64.grad)
-    assert rel(b.grad, b64.grad) < 1e-5, rel(b.grad, b64.grad)
+    # the bias grad is a plain sum of dy' (thousands of O(1) terms that largely cancel): bound
+    # its error by the fp32 summation scale as well as relatively
+    dyl = dy64 * (torch.where(y64 > 0, 1.0, 0.2) if act else 1.0)
+    bscale = float(dyl.abs().sum(dim=(0, 2, 3)).max())
+    berr = float((b.grad.double().cpu() - b64.grad).abs().max())
+    assert rel(b.grad, b64.grad) < 1e-5 or berr <= 1e-7 * bscale, (rel(b.grad, b64.grad), berr, bscale)
