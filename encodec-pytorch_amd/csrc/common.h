@@ -122,4 +122,17 @@ ENCX_DEV float sum_strided(const float* p, int n, int64_t stride) {
     return acc;
 }
 
+// Slab reduction by a 256-thread block: lane l of wave w sums splits s = w, w + 4, ... of output
+// i (= the block's 64 consecutive outputs, one per lane: every wave load is one coalesced 256-byte
+// row segment), then wave 0 adds the 4 partials in order w = 0..3. Deterministic; the result is
+// valid in wave 0 only. red: __shared__ float[4][64].
+ENCX_DEV float slab_sum_256(const float* p, int S, int64_t stride, bool valid, float* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float v = 0.f;
+    if (valid && w < S) v = sum_strided(p + (int64_t)w * stride, (S - w + 3) >> 2, 4 * stride);
+    red[w * 64 + lane] = v;
+    __syncthreads();
+    return ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+}
+
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -761,17 +761,14 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
     if (tid < AN) a.ws[(int64_t)split * AN + tid] = acc;
 }
 
-// dw[i] = [acc ? dw : 0] + sum_s ws[s][i]: SL lanes per output, each summing a strided slice
-// of the splits, then a fixed xor-tree across the SL lanes (deterministic).
-__global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, float* dw, int64_t AN, int S,
-                                                    int SL, int accumulate) {
-    const int per_block = 256 / SL;
-    const int sl = threadIdx.x % SL;
-    const int64_t i = (int64_t)blockIdx.x * per_block + threadIdx.x / SL;
-    float v = 0.f;
-    if (i < AN) v = sum_strided(ws + (int64_t)sl * AN + i, (S - sl + SL - 1) / SL, (int64_t)SL * AN);
-    for (int o = SL >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (sl == 0 && i < AN) dw[i] = accumulate ? dw[i] + v : v;
+// dw[i] = [acc ? dw : 0] + sum_s ws[s][i] (slab_sum_256: 64 outputs per block, 4 split slices,
+// fixed order).
+__global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, float* dw, int64_t AN, int S, int accumulate) {
+    __shared__ float red[256];
+    const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool valid = i < AN;
+    const float v = slab_sum_256(ws + (valid ? i : 0), S, AN, valid, red);
+    if (threadIdx.x < 64 && valid) dw[i] = accumulate ? dw[i] + v : v;
 }
 
 // VALU forward for Cout <= 4 (decoder's final 32 -> 1 conv): thread per output sample.
@@ -1221,10 +1218,7 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
         else launch_wg<128, 128, 2, 2, 1>(a, p.splits, st);
     }
     ENCX_CHECK_LAUNCH();
-    int SL = 1;
-    while (SL < 64 && SL * 16 < p.splits) SL <<= 1;
-    hipLaunchKernelGGL(wgrad_reduce, dim3(cdiv(AN, 256 / SL)), dim3(256), 0, st, ws, dw, AN, p.splits,
-                       SL, accumulate);
+    hipLaunchKernelGGL(wgrad_reduce, dim3(cdiv(AN, 64)), dim3(256), 0, st, ws, dw, AN, p.splits, accumulate);
     ENCX_CHECK_LAUNCH();
     return 0;
 }

@@ -783,7 +783,23 @@ struct C2Dg {
     const float* xact;  // input (LeakyReLU' of the previous layer) or null
     float* dx;          // [B][Ci][T2][Fi]
     int J, U, CK, NR, RL, accumulate;
+    // optional feature-matching term added to dx (FeatFn's grad of this input map, fused here
+    // instead of a separate grad tensor + add): c * sign(ffx - ffr), c = fg[0] * fscale / fden[0]
+    const float* ffr;   // real map [B][Ci][T2][Fi] or null
+    const float* ffx;   // fake map (this layer's input)
+    const float* fden;  // mean |fr| of the pair
+    const float* fg;    // upstream grad of the loss (null: 1)
+    float fscale;
 };
+
+ENCX_DEV float feat_coef(const C2Dg& a) {
+    return a.ffr ? (a.fg ? a.fg[0] : 1.f) * a.fscale / a.fden[0] : 0.f;
+}
+// same value as feat_grad_kernel's dff for element o
+ENCX_DEV float feat_term(const C2Dg& a, float c, int64_t o) {
+    const float d = a.ffx[o] - a.ffr[o];
+    return d > 0.f ? c : (d < 0.f ? -c : 0.f);
+}
 
 template <int BM, int BN, int WM, int WN, int JC = 0>
 __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
@@ -941,6 +957,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
                 const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
                 float v = acc[i][j][r];
                 if (a.xact) v *= lrelu_grad(a.xact[o]);
+                if (a.ffr) v += feat_term(a, feat_coef(a), o);
                 a.dx[o] = a.accumulate ? a.dx[o] + v : v;
             }
         }
@@ -989,6 +1006,7 @@ __global__ __launch_bounds__(NT) void c2_dgradr_kernel(C2Dg a) {
     const float* dyb = a.dy + (int64_t)b * g.Co * plane;
     const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane : dyb;
     const int64_t left = (int64_t)(g.B - b) * g.Co * plane;  // floats from dyb to the tensor end
+    const float fc = feat_coef(a);
     for (int gr = tid; gr < VC * NR; gr += NT) {
         const int vc = gr / NR, rs = gr - vc * NR, co = vc / g.KT, kt = vc - co * g.KT;
         const int row = tf + rs + g.pt - kt * g.dt, base = rs ? baseN : base0;
@@ -1097,6 +1115,7 @@ __global__ __launch_bounds__(NT) void c2_dgradr_kernel(C2Dg a) {
                 const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
                 float v = acc[i][j][r];
                 if (a.xact) v *= lrelu_grad(a.xact[o]);
+                if (a.ffr) v += feat_term(a, fc, o);
                 a.dx[o] = a.accumulate ? a.dx[o] + v : v;
             }
         }
@@ -1187,6 +1206,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
             const int64_t o = (((int64_t)b * CI + c) * g.T2 + t) * g.Fi + f;
             float v = acc[c][e];
             if (a.xact) v *= lrelu_grad(a.xact[o]);
+            if (a.ffr) v += feat_term(a, feat_coef(a), o);
             a.dx[o] = a.accumulate ? a.dx[o] + v : v;
         }
 }
@@ -1710,12 +1730,15 @@ __global__ __launch_bounds__(NW * 64) void c2_wgrad3_kernel(C2Wg3 a) {
     }
 }
 
-// dw[co][n] (+)= sum_s ws[s][co][n] for n < Nw; db[co] (+)= sum_s ws[s][co][Nw]. Fixed order.
-__global__ void c2_wg_reduce(const float* ws, int S, int Co, int N, float* dw, float* db, int acc_w,
-                             int acc_b) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)Co * N) return;
-    const float v = sum_strided(ws + i, S, (int64_t)Co * N);
+// dw[co][n] (+)= sum_s ws[s][co][n] for n < Nw; db[co] (+)= sum_s ws[s][co][Nw]. Fixed order
+// (slab_sum_256: 64 outputs per block, 4 split slices).
+__global__ __launch_bounds__(256) void c2_wg_reduce(const float* ws, int S, int Co, int N, float* dw, float* db,
+                                                    int acc_w, int acc_b) {
+    __shared__ float red[256];
+    const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool valid = i < (int64_t)Co * N;
+    const float v = slab_sum_256(ws + (valid ? i : 0), S, (int64_t)Co * N, valid, red);
+    if (threadIdx.x >= 64 || !valid) return;
     const int co = (int)(i / N), n = (int)(i - (int64_t)co * N);
     const int Nw = N - 1;
     if (n < Nw) {
@@ -1941,6 +1964,7 @@ __global__ __launch_bounds__(256) void c2_co1_dgrad(C2Dg a) {
     }
     const int64_t i = (int64_t)bc * xplane + p;
     if (a.xact) acc *= lrelu_grad(a.xact[i]);
+    if (a.ffr) acc += feat_term(a, feat_coef(a), i);
     a.dx[i] = a.accumulate ? a.dx[i] + acc : acc;
 }
 
@@ -2318,13 +2342,25 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
                          int accumulate, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
                          int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
                          encx_stream_t stream) {
+    return encx_conv2d_bwd_data_feat(dy, yact, wp, xact, dx, accumulate, nullptr, nullptr, nullptr, nullptr, 0.0, B,
+                                     Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf, stream);
+}
+
+int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
+                              int accumulate, const float* feat_real, const float* feat_fake, const float* feat_denom,
+                              const float* feat_g, double feat_scale, int64_t B, int64_t Ci, int64_t T2, int64_t Fi,
+                              int64_t Co, int64_t Fo, int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt,
+                              int64_t pf, encx_stream_t stream) {
     ENCX_REQUIRE(dy && wp && dx);
+    ENCX_REQUIRE(!feat_real || (feat_fake && feat_denom));
     C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
     ENCX_REQUIRE(geo_ok(g));
     hipStream_t st = (hipStream_t)stream;
-    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + 2 * B * Co * T2 * Fo), "c2_dgrad");
+    encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF,
+                       4.0 * (B * Ci * T2 * Fi * (feat_real ? 3 : 1) + 2 * B * Co * T2 * Fo), "c2_dgrad");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
-    C2Dg a{g, dy, yact, wp, xact, dx, 0, 0, 0, 0, 0, accumulate};
+    C2Dg a{g, dy, yact, wp, xact, dx, 0, 0, 0, 0, 0, accumulate, feat_real, feat_fake, feat_denom, feat_g,
+           (float)feat_scale};
     constexpr int BN = 128;
     a.J = (int)cdiv(KF, sf);
     a.U = (int)((Fi - 1 + pf) / sf + 1);
@@ -2385,7 +2421,7 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
         if (sf == 1) hipLaunchKernelGGL((c2_co1_wgrad<3, 3, 1>), grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((c2_co1_wgrad<3, 3, 2>), grid, dim3(256), 0, st, a);
         ENCX_CHECK_LAUNCH();
-        hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, st, ws, q.splits, 1, N, dw, db,
+        hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(N, 64)), dim3(256), 0, st, ws, q.splits, 1, N, dw, db,
                            acc_w, acc_b);
         ENCX_CHECK_LAUNCH();
         return 0;
@@ -2393,7 +2429,7 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
     if (wg3r_ok(g)) {  // 9 waves x one 32-column tile each, vectorised staging (c2_wgrad3_kernel)
         const WgPlan3 q = plan_wg3r(g, 32, 512);
         if (run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st) == 0) {
-            hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 256)), dim3(256), 0, st, ws, q.splits, (int)Co,
+            hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, q.splits, (int)Co,
                                N, dw, db, acc_w, acc_b);
             ENCX_CHECK_LAUNCH();
             return 0;
@@ -2412,7 +2448,7 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
                            dim3(NT), lds, st, a);
     }
     ENCX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 256)), dim3(256), 0, st, ws, p.splits, (int)Co, N,
+    hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, p.splits, (int)Co, N,
                        dw, db, acc_w, acc_b);
     ENCX_CHECK_LAUNCH();
     return 0;

@@ -319,12 +319,14 @@ struct EpSlabs {  // split-K partial slabs [z][M][N]
 };
 // sum split slabs [S][4H][2H+1] in ascending slab order into dw_ih (n < H), dw_hh (n < 2H) and
 // the bias grad (n == 2H, written to both b_ih and b_hh grads); += when acc
-__global__ void lstm_slab_reduce(const float* ws, int S, int H, float* dwi, float* dwh, float* db1, float* db2,
-                                 int acc) {
+__global__ __launch_bounds__(256) void lstm_slab_reduce(const float* ws, int S, int H, float* dwi, float* dwh,
+                                                        float* db1, float* db2, int acc) {
+    __shared__ float red[256];
     const int M = 4 * H, N = 2 * H + 1;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)M * N) return;
-    const float s = sum_strided(ws + i, S, (int64_t)M * N);
+    const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool valid = i < (int64_t)M * N;
+    const float s = slab_sum_256(ws + (valid ? i : 0), S, (int64_t)M * N, valid, red);
+    if (threadIdx.x >= 64 || !valid) return;
     const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
     float* p = n < H ? dwi + (int64_t)m * H + n : n < 2 * H ? dwh + (int64_t)m * H + (n - H) : nullptr;
     if (p) {
@@ -475,7 +477,7 @@ int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float
     int rc = gemm_launch_128(LdWcat{DA + layer * 4 * BTH, in, Y + layer * BTH, (int)H, (int)T, make_fastdiv((uint32_t)T)}, EpSlabs{ws, N4, Nw},
                          N4, Nw, M, st, sp);
     if (rc) return rc;
-    hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 256)), dim3(256), 0, st, ws, S,
+    hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 64)), dim3(256), 0, st, ws, S,
                        (int)H, dw_ih, dw_hh, db_ih, db_hh, acc);
     ENCX_CHECK_LAUNCH();
     return 0;

@@ -596,6 +596,17 @@ class DiscGradMode:
     def set(self, params, input):
         self.params, self.input = params, input
 
+    def reuse_weights(self, on=True):
+        """Within one train step the discriminator runs forward twice (real, fake) with the same
+        weights: while on, each Conv2d derives its weight-normed and polyphase weights once and
+        shares them between the two graphs. Turning it off (or on again) drops the cache; the
+        owner must do so before the weights change."""
+        self.reuse = bool(on)
+        self.cache = {}
+
+    reuse = False
+    cache = None
+
 
 _ALL_GRADS = DiscGradMode()
 
@@ -608,19 +619,29 @@ class Conv2dFn(torch.autograd.Function):
     the layer that reads the spectrogram (first=True)."""
 
     @staticmethod
-    def forward(ctx, x, v, g, b, geo, act, mode=_ALL_GRADS, first=False):
+    def forward(ctx, x, v, g, b, geo, act, mode=_ALL_GRADS, first=False, feat_slot=None):
         _check(x)
         x = x.contiguous()
         B, Ci, T2, Fi = x.shape
         Co = v.shape[0]
         KT, KF, sf, dt, pt, pf, Fo = geo
         st = stream()
-        wf = _f32(Co * Ci * KT * KF, x)
-        call('encx_weightnorm_fwd', ptr(v), ptr(g), ptr(wf), None, Co, Ci * KT, KF, 1, st)
+        ent = mode.cache.get(id(v)) if mode.reuse else None
+        if ent is None:
+            wf = _f32(Co * Ci * KT * KF, x)
+            call('encx_weightnorm_fwd', ptr(v), ptr(g), ptr(wf), None, Co, Ci * KT, KF, 1, st)
+            wp = None
+            if mode.reuse:
+                wp = _wpoly(wf, Co, Ci, KT, KF, sf, x)
+                mode.cache[id(v)] = (wf, wp)
+        else:
+            wf, wp = ent
         y = torch.empty(B, Co, T2, Fo, device=x.device, dtype=torch.float32)
         call('encx_conv2d_fwd', ptr(x), ptr(wf), ptr(b), ptr(y), B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt,
              pf, int(act), st)
         ctx.save_for_backward(x, y, wf)
+        ctx.wp = wp
+        ctx.feat_slot = feat_slot
         ctx.params = (v, g, b)
         ctx.geo, ctx.act = geo, act
         ctx.mode, ctx.first = mode, first
@@ -630,8 +651,12 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         if dy is None:
-            return None, None, None, None, None, None, None, None
+            return (None,) * 9
         x, y, wf = ctx.saved_tensors
+        slot = ctx.feat_slot
+        feat = slot.pending if slot is not None else None
+        if feat is not None:
+            slot.pending = None
         v, g, b = ctx.params
         KT, KF, sf, dt, pt, pf, Fo = ctx.geo
         dy = dy.contiguous()
@@ -643,11 +668,17 @@ class Conv2dFn(torch.autograd.Function):
         dx = dv = dg = db = None
         mode = ctx.mode
         if ctx.needs_input_grad[0] and (mode.input or not ctx.first):
-            J = -(-KF // sf)
-            wp = _f32(Co * KT * J * Ci * sf, x)
-            call('encx_conv2d_wpoly', ptr(wf), ptr(wp), Co, Ci, KT, KF, sf, st)
+            wp = ctx.wp if ctx.wp is not None else _wpoly(wf, Co, Ci, KT, KF, sf, x)
             dx = torch.empty_like(x)
-            call('encx_conv2d_bwd_data', ptr(dy), ptr(yact), ptr(wp), None, ptr(dx), 0, *dims, st)
+            if feat is None:
+                call('encx_conv2d_bwd_data', ptr(dy), ptr(yact), ptr(wp), None, ptr(dx), 0, *dims, st)
+            else:  # + FeatFn's grad of this input map, in the epilogue
+                fr, den, fg, fscale = feat
+                call('encx_conv2d_bwd_data_feat', ptr(dy), ptr(yact), ptr(wp), None, ptr(dx), 0, ptr(fr),
+                     ptr(x), ptr(den), ptr(fg), float(fscale), *dims, st)
+        elif feat is not None:
+            raise RuntimeError('encx: a feature-matching grad was handed to a Conv2d whose input grad '
+                               'is not computed')
         if any(ctx.needs_input_grad[1:4]) and mode.params:
             ws = _ws(lib.encx_conv2d_bwd_weight_workspace(*dims), x)
             direct = _direct(v) and _direct(g) and _direct(b)
@@ -666,13 +697,39 @@ class Conv2dFn(torch.autograd.Function):
                 call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(dw), ptr(db), 0, 0,
                      ptr(ws), *dims, st)
                 dv, dg = _weight_bwd(v, g, dw)
-        return dx, dv, dg, db, None, None, None, None
+        return dx, dv, dg, db, None, None, None, None, None
+
+
+class FeatSlot:
+    """Attached to every Conv2d output map: FeatFn.backward parks its grad of the map here
+    (the real map, the pair's mean |fr|, the upstream grad, the scale) and the Conv2d that reads
+    the map adds it in its bwd-data epilogue (encx_conv2d_bwd_data_feat), so the map's grad is
+    never materialised twice and autograd does no add. FeatFn runs before every Conv2d of its
+    graph in a traversal (it is the loss node), and the consumer clears the slot."""
+    __slots__ = ('pending', 'consumer_out')
+
+    def __init__(self):
+        self.pending = None
+        self.consumer_out = None  # the slot of the map the reading Conv2d produces
+
+
+def _wpoly(wf, Co, Ci, KT, KF, sf, like):
+    """Polyphase (along f) weight layout of the bwd-data kernel."""
+    J = -(-KF // sf)
+    wp = _f32(Co * KT * J * Ci * sf, like)
+    call('encx_conv2d_wpoly', ptr(wf), ptr(wp), Co, Ci, KT, KF, sf, stream())
+    return wp
 
 
 def conv2d(x, v, g, b, kernel, stride=(1, 1), dilation=(1, 1), padding=(0, 0), act=False, mode=_ALL_GRADS,
            first=False):
     geo = conv2d_geometry(x.shape[-1], kernel, stride, dilation, padding)
-    return Conv2dFn.apply(x, v, g, b, geo, act, mode, first)
+    in_slot = getattr(x, '_encx_feat_slot', None)
+    y = Conv2dFn.apply(x, v, g, b, geo, act, mode, first, in_slot)
+    y._encx_feat_slot = FeatSlot()
+    if in_slot is not None:
+        in_slot.consumer_out = y._encx_feat_slot
+    return y
 
 
 class DiscSpecFn(torch.autograd.Function):
@@ -754,6 +811,11 @@ class FeatFn(torch.autograd.Function):
                  1, ptr(ws), stream())
         ctx.save_for_backward(denom, *frs, *ffs)
         ctx.scale, ctx.n = scale, n_pairs
+        # park a map's grad only when the Conv2d reading it produces another map of this loss:
+        # that Conv2d is then on every traversal from this loss and is sure to collect it
+        slots = [getattr(f, '_encx_feat_slot', None) for f in maps[n_pairs:]]
+        live = {id(sl) for sl in slots if sl is not None}
+        ctx.slots = [sl if sl is not None and id(sl.consumer_out) in live else None for sl in slots]
         return out
 
     @staticmethod
@@ -764,7 +826,9 @@ class FeatFn(torch.autograd.Function):
         frs, ffs = maps[:n], maps[n:]
         grads = [None] * (2 * n)
         for i, (fr, ff) in enumerate(zip(frs, ffs)):
-            if ctx.needs_input_grad[2 + n + i]:
+            if ctx.needs_input_grad[2 + n + i] and ctx.slots[i] is not None:
+                ctx.slots[i].pending = (fr, denom[i:i + 1], g, ctx.scale)  # the reading Conv2d adds it
+            elif ctx.needs_input_grad[2 + n + i]:
                 d = torch.empty_like(ff)
                 call('encx_feat_loss_bwd', ptr(fr), ptr(ff), ff.numel(), float(ctx.scale), ptr(denom[i:i + 1]),
                      ptr(g), ptr(d), stream())

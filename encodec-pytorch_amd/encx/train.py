@@ -125,9 +125,11 @@ class Trainer:
                 # generator phase: the balancer's autograd.grad calls differentiate the shared
                 # discriminator graph w.r.t. the fake audio only
                 self.disc_mode.set(params=False, input=True)
+                self.disc_mode.reuse_weights(True)  # same weights for both forwards
                 yd = y.detach().requires_grad_()
                 c['logits_real'], fmap_real = self.disc(x, mode=self.disc_mode)
                 c['logits_fake'], fmap_fake = self.disc(yd, mode=self.disc_mode)
+                self.disc_mode.reuse_weights(False)
                 losses = total_loss(fmap_real, c['logits_fake'], fmap_fake, x, yd, self.sample_rate)
                 wrt = yd
             else:

@@ -307,6 +307,15 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
                          int accumulate, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
                          int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
                          encx_stream_t stream);
+/* encx_conv2d_bwd_data + the feature-matching loss's grad of this layer's input map added in the
+ * epilogue (FeatFn's d l_feat / d ff, losses.py:53, fused instead of a grad tensor and an add):
+ * dx += c * sign(feat_fake - feat_real), c = feat_g[0] * feat_scale / feat_denom[0] (feat_g NULL:
+ * 1); feat_fake is this layer's input map, feat_real its real-audio counterpart. */
+int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
+                              int accumulate, const float* feat_real, const float* feat_fake,
+                              const float* feat_denom, const float* feat_g, double feat_scale, int64_t B,
+                              int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo, int64_t KT, int64_t KF,
+                              int64_t sf, int64_t dt, int64_t pt, int64_t pf, encx_stream_t stream);
 size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
                                         int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf);
 /* dw [Co][Ci][KT][KF] and db [Co] (either may be NULL), written or added (acc_w / acc_b). */
