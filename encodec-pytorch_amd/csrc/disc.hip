@@ -801,6 +801,14 @@ ENCX_DEV float feat_term(const C2Dg& a, float c, int64_t o) {
     return d > 0.f ? c : (d < 0.f ? -c : 0.f);
 }
 
+// dx element o (+ masks / feature term) for the epilogues below
+ENCX_DEV float dg_out(const C2Dg& a, float fc, int64_t o, float v) {
+    if (a.xact) v *= lrelu_grad(a.xact[o]);
+    if (a.ffr) v += feat_term(a, fc, o);
+    return a.accumulate ? a.dx[o] + v : v;
+}
+typedef float f32x2u __attribute__((ext_vector_type(2), aligned(4)));
+
 template <int BM, int BN, int WM, int WN, int JC = 0>
 __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -1105,6 +1113,41 @@ __global__ __launch_bounds__(NT) void c2_dgradr_kernel(C2Dg a) {
             const int n = n0 + wn0 + j * 32 + l32;
             if (n >= nend) continue;
             const int tr = n / U, u = n - tr * U;
+            if (S == 2) {
+                // rows m, m + 1 (registers r, r + 1) are phases 0 / 1 of the same ci: the two
+                // adjacent f of this column, stored (and masked) as one 8-byte access
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                    const int m = m0 + i * 32 + mfma_row(r, lane);
+                    if (m >= M) continue;
+                    const int f = 2 * u - g.pf;
+                    const int64_t o = (((int64_t)b * g.Ci + (m >> 1)) * g.T2 + tr) * g.Fi + f;
+                    float v0 = acc[i][j][r], v1 = acc[i][j][r + 1];
+                    if (f >= 0 && f + 1 < g.Fi) {
+                        if (a.xact) {
+                            const f32x2u t = *(const f32x2u*)(a.xact + o);
+                            v0 *= lrelu_grad(t[0]);
+                            v1 *= lrelu_grad(t[1]);
+                        }
+                        if (a.ffr) {
+                            const f32x2u x2 = *(const f32x2u*)(a.ffx + o), r2 = *(const f32x2u*)(a.ffr + o);
+                            const float d0 = x2[0] - r2[0], d1 = x2[1] - r2[1];
+                            v0 += d0 > 0.f ? fc : (d0 < 0.f ? -fc : 0.f);
+                            v1 += d1 > 0.f ? fc : (d1 < 0.f ? -fc : 0.f);
+                        }
+                        if (a.accumulate) {
+                            const f32x2u t = *(const f32x2u*)(a.dx + o);
+                            v0 += t[0];
+                            v1 += t[1];
+                        }
+                        *(f32x2u*)(a.dx + o) = (f32x2u){v0, v1};
+                    } else {
+                        if (f >= 0 && f < g.Fi) a.dx[o] = dg_out(a, fc, o, v0);
+                        if (f + 1 >= 0 && f + 1 < g.Fi) a.dx[o + 1] = dg_out(a, fc, o + 1, v1);
+                    }
+                }
+                continue;
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + i * 32 + mfma_row(r, lane);
@@ -1113,13 +1156,11 @@ __global__ __launch_bounds__(NT) void c2_dgradr_kernel(C2Dg a) {
                 const int f = u * S + rr - g.pf;
                 if (f < 0 || f >= g.Fi) continue;
                 const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
-                float v = acc[i][j][r];
-                if (a.xact) v *= lrelu_grad(a.xact[o]);
-                if (a.ffr) v += feat_term(a, fc, o);
-                a.dx[o] = a.accumulate ? a.dx[o] + v : v;
+                a.dx[o] = dg_out(a, fc, o, acc[i][j][r]);
             }
         }
 }
+
 
 // Narrow backward-data (M = Ci <= 4 rows, stride 1 along f: the first layer's grad into the
 // spectrogram). A 32-row MFMA tile would carry 2 useful rows, so this runs on the vector ALU:

@@ -20,7 +20,7 @@ args = ap.parse_args()
 
 rows = list(csv.DictReader(open(f'{args.dir}/run_kernel_trace.csv')))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-idx = [i for i, r in enumerate(rows) if 'adam_kernel' in r['Kernel_Name']]
+idx = [i for i, r in enumerate(rows) if 'adam_kernel' in r['Kernel_Name'] or 'adam_dev_kernel' in r['Kernel_Name']]
 n_adam = args.adams_per_step
 if n_adam is None:
     sizes = {r.get('Grid_Size', r.get('Grid_Size_X', '')) for r in (rows[i] for i in idx)}
