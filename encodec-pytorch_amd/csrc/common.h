@@ -135,4 +135,31 @@ ENCX_DEV float slab_sum_256(const float* p, int S, int64_t stride, bool valid, f
     return ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
 }
 
+// XCD-aware tile order. The dispatcher deals workgroups to the 8 XCDs round-robin by linear id,
+// so neighbouring tiles (which share input halo rows or a staged operand) land on different
+// XCDs and each re-fetches the shared data into its own L2. Remapped, XCD k works through one
+// contiguous run of tiles in order. Returns the remapped linear id of this workgroup.
+ENCX_DEV int xcd_linear_id() {
+    const int n = (int)(gridDim.x * gridDim.y * gridDim.z);
+    const int i = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    const int k = i & 7;
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+        if (j < k) base += (n - j + 7) >> 3;  // workgroups dealt to XCD j
+    return base + (i >> 3);
+}
+// the remapped id as (x, y, z) over gridDim
+struct TileId {
+    int x, y, z;
+};
+ENCX_DEV TileId xcd_tile() {
+    const int id = xcd_linear_id(), gx = (int)gridDim.x, gy = (int)gridDim.y;
+    TileId t;
+    t.x = id % gx;
+    t.y = (id / gx) % gy;
+    t.z = id / (gx * gy);
+    return t;
+}
+
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

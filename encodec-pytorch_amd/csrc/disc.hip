@@ -650,7 +650,8 @@ __global__ __launch_bounds__(NT) void c2_fwdr_kernel(C2Fwd a) {
     int2* rtab = (int2*)(Ws + KFC * CK * BM);  // [VC*NR]: {offset of column `base`, base} / invalid
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, l32 = lane & 31;
-    const int b = blockIdx.z, n0 = blockIdx.x * BN, co0 = blockIdx.y * BM;
+    const TileId tile = xcd_tile();
+    const int b = tile.z, n0 = tile.x * BN, co0 = tile.y * BM;
     const int wn0 = wave * TN * 32;
     const int Nall = g.T2 * g.Fo, nend = min(Nall, n0 + BN);
     const int tf = n0 / g.Fo, f0 = n0 - tf * g.Fo;
@@ -989,7 +990,8 @@ __global__ __launch_bounds__(NT) void c2_dgradr_kernel(C2Dg a) {
     int2* rtab = (int2*)(As + JC * CK * BM);  // [VC*NR]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, l32 = lane & 31;
-    const int b = blockIdx.z, n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    const TileId tile = xcd_tile();
+    const int b = tile.z, n0 = tile.x * BN, m0 = tile.y * BM;
     const int wn0 = wave * TN * 32;
     const int Nall = g.T2 * U, nend = min(Nall, n0 + BN);
     const int tf = n0 / U, u0 = n0 - tf * U;
@@ -1623,12 +1625,13 @@ __global__ __launch_bounds__(NW * 64) void c2_wgrad3_kernel(C2Wg3 a) {
     float* Rs = (float*)(poff + P);            // [GC][NR][RLp] (16-byte aligned: see plan_wg3r)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, l32 = lane & 31;
-    const int vc0 = blockIdx.x * GC, split = blockIdx.y;
+    const TileId tile = xcd_tile();  // the combo groups of one split share its dy chunks
+    const int vc0 = tile.x * GC, split = tile.y;
     const int n0 = vc0 * KF + wave * NTW * 32;
     const int Nall = g.T2 * g.Fo;
     const int64_t plane_y = (int64_t)Nall, plane_x = (int64_t)g.T2 * g.Fi;
     const int64_t ytot = (int64_t)g.B * g.Co * plane_y, xtot = (int64_t)g.B * g.Ci * plane_x;
-    const bool do_bias = blockIdx.x == 0 && wave == 0;
+    const bool do_bias = tile.x == 0 && wave == 0;
     const int baseN = (-g.pf) & ~3;
     int cbase[NTW];
 #pragma unroll
@@ -1871,14 +1874,33 @@ __global__ __launch_bounds__(256) void hinge_kernel(const float* x, int64_t n, f
     acc = block_sum(acc, red);
     if (threadIdx.x == 0) parts[blockIdx.x] = acc;
 }
-// parts[b] = (sum |fr - ff|, sum |fr|) over a grid-stride slice
+// parts[b] = (sum |fr - ff|, sum |fr|) over a grid-stride slice: float4 loads, 4 in flight per
+// operand and thread (n % 4 == 0, 16-byte aligned maps: torch allocations of 32-channel maps)
 __global__ __launch_bounds__(256) void feat_kernel(const float* fr, const float* ff, int64_t n, float* parts) {
     __shared__ float red[16];
+    const f32x4* r4 = (const f32x4*)fr;
+    const f32x4* f4 = (const f32x4*)ff;
+    const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * 256;
     float s1 = 0.f, s2 = 0.f;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const float r = fr[i];
-        s1 += fabsf(r - ff[i]);
-        s2 += fabsf(r);
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += 4 * stride) {
+        f32x4 rv[4], fv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + u * stride;
+            const int64_t ic = i < n4 ? i : 0;
+            rv[u] = r4[ic];
+            fv[u] = f4[ic];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i0 + u * stride < n4) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    s1 += fabsf(rv[u][c] - fv[u][c]);
+                    s2 += fabsf(rv[u][c]);
+                }
+            }
+        }
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
@@ -2556,10 +2578,10 @@ int encx_hinge_loss(const float* x, int64_t n, double s, double scale, float* ou
  * backward. */
 int encx_feat_loss(const float* fr, const float* ff, int64_t n, double scale, float* out, float* denom,
                    int accumulate, float* ws, encx_stream_t stream) {
-    ENCX_REQUIRE(fr && ff && out && ws && n > 0);
+    ENCX_REQUIRE(fr && ff && out && ws && n > 0 && n % 4 == 0 && ((uintptr_t)fr & 15) == 0 && ((uintptr_t)ff & 15) == 0);
     encx_prof_scope ps((hipStream_t)stream, 4.0 * n, 8.0 * n, "feat", false);
     hipStream_t st = (hipStream_t)stream;
-    const int nb = (int)min((int64_t)LP, cdiv(n, 256));
+    const int nb = (int)min((int64_t)LP, cdiv(n, 1024));
     hipLaunchKernelGGL(feat_kernel, dim3(nb), dim3(256), 0, st, fr, ff, n, ws);
     hipLaunchKernelGGL(loss_finish, dim3(1), dim3(256), 0, st, ws, nb, 2, (double)n, (float)scale, out, denom,
                        accumulate);

@@ -10,7 +10,7 @@ C=${CONFIG:-gen}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$C -o run --output-format csv -- \
     python3 bench.py --config $C --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_$C.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcF_$C -o run --output-format csv -- \
-    python3 bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline --no-roofline > gpurun_out/pmcF_$C.log 2>&1 || exit $?
+    python3 bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline --no-roofline --no-graphs > gpurun_out/pmcF_$C.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcW_$C -o run --output-format csv -- \
-    python3 bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline --no-roofline > gpurun_out/pmcW_$C.log 2>&1 || exit $?
+    python3 bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline --no-roofline --no-graphs > gpurun_out/pmcW_$C.log 2>&1 || exit $?
 grep '^{' gpurun_out/prof_$C.log

@@ -213,7 +213,7 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((c2_wgrad_kernel<32, 128, 1, 4, 1>), dim3((unsigned)cdiv(N, 128), 1, p.splits),
                                        dim3(NT), lds, st, a);
                 }
-                hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 256)), dim3(256), 0, st, ws, p.splits,
+                hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 64)), dim3(256), 0, st, ws, p.splits,
                                    l.Co, N, dw0, db0, 0, 0);
             };
             double t0 = time_ms(old);
@@ -226,7 +226,7 @@ int main(int argc, char** argv) {
                 CK(hipMemset(dw1, 0, (size_t)l.Co * N * 4));
                 double t = time_ms([&] {
                     f(q);
-                    hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 256)), dim3(256), 0, st, ws, q.splits,
+                    hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 64)), dim3(256), 0, st, ws, q.splits,
                                        l.Co, N, dw1, db1, 0, 0);
                 });
                 double e = fmax(rel_err(dw1, dw0, (size_t)l.Co * (N - 1)), rel_err(db1, db0, l.Co));
@@ -240,7 +240,7 @@ int main(int argc, char** argv) {
                 bool bad = false;
                 double t = time_ms([&] {
                     if (f(q)) bad = true;
-                    hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 256)), dim3(256), 0, st, ws, q.splits,
+                    hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 64)), dim3(256), 0, st, ws, q.splits,
                                        l.Co, N, dw1, db1, 0, 0);
                 });
                 if (bad) { printf("  wgrad %-23s n/a\n", nm); return; }
