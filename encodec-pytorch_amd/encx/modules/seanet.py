@@ -50,18 +50,30 @@ class SEANetResnetBlock(nn.Module):
                                     causal=causal, pad_mode=pad_mode)
 
     def forward(self, x):
-        sc = self.shortcut(x)
         convs = [m for m in self.block if isinstance(m, SConv1d)]
-        # identity shortcut, weight-norm convs, two or more convs: the skip gradient is summed
-        # into the head conv's bwd-data output (ops.Conv1dFn 'head' / 'tail' link) instead of
-        # by autograd's elementwise add
+        linkable = (len(convs) > 1 and torch.is_grad_enabled() and x.requires_grad
+                    and all(c.conv.norm_type != 'time_group_norm' for c in convs))
+        # conv shortcut (true_skip False, the EnCodec default): the shortcut conv and the head
+        # conv both read x; whichever backward runs second adds its bwd-data result into the
+        # other's (ops.Conv1dFn 'join'), so autograd sees one grad for x and launches no add
+        join = None
+        if linkable and isinstance(self.shortcut, SConv1d) and self.shortcut.conv.norm_type != 'time_group_norm':
+            join = types.SimpleNamespace(grad=None)
+            sc = self.shortcut(x, link=join, link_role='join')
+        else:
+            sc = self.shortcut(x)
+        # identity shortcut: the skip gradient is summed into the head conv's bwd-data output
+        # (ops.Conv1dFn 'head' / 'tail' link) instead of by autograd's elementwise add
         link = None
-        if (isinstance(self.shortcut, nn.Identity) and len(convs) > 1 and torch.is_grad_enabled()
-                and x.requires_grad and all(c.conv.norm_type != 'time_group_norm' for c in convs)):
+        if linkable and isinstance(self.shortcut, nn.Identity):
             link = types.SimpleNamespace(grad=None)
         h = x
         for i, c in enumerate(convs):
             last = i == len(convs) - 1
+            if join is not None:
+                h = c(h, act=self.act, res=sc if last else None, link=join if i == 0 else None,
+                      link_role='join' if i == 0 else None)
+                continue
             role = None if link is None else ('tail' if last else 'head' if i == 0 else None)
             h = c(h, act=self.act, res=sc if last else None, link=link, link_role=role)
         return h

@@ -157,17 +157,25 @@ class Conv1dFn(torch.autograd.Function):
         Cout = v.shape[0]
         st = stream()
         dx = dv = dg = db = None
+        park = False
         if ctx.needs_input_grad[0]:
             acc = 0
             if role == 'head' and link.grad is not None:
                 # the block's skip gradient, handed over by its tail conv: accumulate into it
                 # in the bwd-data epilogue instead of a separate add (see residual_block)
                 dx, acc, link.grad = link.grad, 1, None
+            elif role == 'join' and link.grad is not None:
+                # the second of a conv-shortcut block's two convs that read the block input:
+                # add into the first one's parked input grad; autograd gets the sum
+                dx, acc, link.grad = link.grad, 1, None
             else:
                 dx = torch.empty_like(x)
+                park = role == 'join'  # the first of the two: park it, hand autograd nothing
             ws = _ws(lib.encx_conv1d_bwd_data_workspace(B, Cin, T, Cout, tout, K, s, pl, pr), x)
             call('encx_conv1d_bwd_data', ptr(dy), ptr(wp), ptr(x), ptr(dx), ptr(ws), B, Cin, T,
                  Cout, tout, K, s, pl, pr, e, mode, act, acc, st)
+            if park:
+                link.grad, dx = dx, None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
             dw = torch.empty(Cout, Cin, K, device=x.device, dtype=torch.float32)
             ws = _f32(lib.encx_conv1d_bwd_weight_workspace(B, Cin, Cout, tout, K) // 4 + 1, x)
