@@ -515,6 +515,8 @@ struct WgArgs {
     int WLp;         // LDS row length of the R window
     int NCmax;       // R window rows
     int vec;         // L / R rows 16-B aligned: float4 staging loads
+    float* wsb;      // non-null: also sum L over t (the bias grad of a conv, L = dy) into
+                     // wsb[split][A] (the ones column of the GEMM, on the vector ALU)
 };
 
 // WK > 1: the WK waves share one (32*TM) x (32*TN) tile and split each chunk's t range.
@@ -549,6 +551,12 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    // bias grad: the first column tile's waves that hold column 0 sum the A operand they load
+    const bool bias_blk = a.wsb && blockIdx.x == 0;
+    const bool do_bias = bias_blk && wn0 == 0;
+    float bsum[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
 
     const int it_beg = split * a.per_split;
     const int it_end = min(a.items, it_beg + a.per_split);
@@ -672,12 +680,32 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
             float av[TM], bv[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i) av[i] = Ls[(wm0 + i * 32 + l32) * BTp + tl];
+            if (do_bias)
+#pragma unroll
+                for (int i = 0; i < TM; ++i) bsum[i] += av[i];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bv[j] = Rs[boff[j] + tl * a.s];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+        }
+    }
+    if (bias_blk) {  // the bias column: halves (even / odd t), then the WK waves in order
+        __shared__ float bred[4][128];
+        __syncthreads();
+        if (do_bias)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const float v = bsum[i] + __shfl_xor(bsum[i], 32, 64);
+                if (h == 0) bred[wave][wm0 + i * 32 + l32] = v;
+            }
+        __syncthreads();
+        if (tid < BM && a0 + tid < a.A) {
+            const int wrow = tid / (TM * 32);  // the wave row (of WM) holding this tile row
+            float v = 0.f;
+            for (int w = 0; w < WK; ++w) v += bred[(wrow * WN) * WK + w][tid];
+            a.wsb[(int64_t)split * a.A + a0 + tid] = v;
         }
     }
     if (WK > 1) {  // combine the waves' partial tiles in wave order (deterministic)
@@ -727,7 +755,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
     const int split = blockIdx.x, tid = threadIdx.x;
     const int nchunks_t = (a.Tl + BT - 1) / BT;
     const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
-    float acc = 0.f;  // AN <= NT
+    float acc = 0.f, bacc = 0.f;  // AN (+ A with the bias) <= NT
     const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
     for (int it = it_beg; it < it_end; ++it) {
         const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
@@ -744,6 +772,15 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
             Rs[c * a.WLp + w] = m >= 0 ? act_apply(a.actR, Rb[(int64_t)c * a.Tr + m]) : 0.f;
         }
         __syncthreads();
+        if (a.wsb && tid >= AN && tid < AN + a.A) {  // bias: sum of the L row over the chunk
+            const float* lp = Ls + (tid - AN) * BT;
+            float s0 = 0.f, s1 = 0.f;
+            for (int tl = 0; tl < BT; tl += 2) {
+                s0 += lp[tl];
+                s1 += lp[tl + 1];
+            }
+            bacc += s0 + s1;
+        }
         if (tid < AN) {
             int aa = tid / N, n = tid - aa * N, c = n / K, k = n - c * K;
             const float* lp = Ls + aa * BT;
@@ -759,12 +796,22 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
         }
     }
     if (tid < AN) a.ws[(int64_t)split * AN + tid] = acc;
+    if (a.wsb && tid >= AN && tid < AN + a.A) a.wsb[(int64_t)split * a.A + (tid - AN)] = bacc;
 }
 
 // dw[i] = [acc ? dw : 0] + sum_s ws[s][i] (slab_sum_256: 64 outputs per block, 4 split slices,
-// fixed order).
-__global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, float* dw, int64_t AN, int S, int accumulate) {
+// fixed order); blocks past cdiv(AN, 64) reduce the bias slabs wsb[s][A] into db the same way.
+__global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, float* dw, int64_t AN, int S, int accumulate,
+                                                    const float* wsb, float* db, int A, int acc_b) {
     __shared__ float red[256];
+    const int64_t nbw = (AN + 63) / 64;
+    if (blockIdx.x >= nbw) {
+        const int i = (int)((blockIdx.x - nbw) * 64) + (threadIdx.x & 63);
+        const bool valid = i < A;
+        const float v = slab_sum_256(wsb + (valid ? i : 0), S, A, valid, red);
+        if (threadIdx.x < 64 && valid) db[i] = acc_b ? db[i] + v : v;
+        return;
+    }
     const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const bool valid = i < AN;
     const float v = slab_sum_256(ws + (valid ? i : 0), S, AN, valid, red);
@@ -1189,12 +1236,22 @@ void launch_wg(WgArgs a, int splits, hipStream_t st) {
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, WK>), grid, dim3(NT), lds, st, a);
 }
 
+// whether wgrad_run can also produce the bias grad (sum over t of L) for this shape
+static bool wgrad_bias_ok(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
+    const WgPlan p = plan_wgrad(B, A, Tl, C, K);
+    return p.kind != 0 || A * C * K + A <= NT;
+}
+
 int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, int64_t A,
               int64_t Tl, int64_t C, int64_t Tr, int64_t K, int64_t s, int64_t d, int64_t pl,
-              int64_t e, int mode, int actL, int actR, int accumulate, hipStream_t st) {
+              int64_t e, int mode, int actL, int actR, int accumulate, hipStream_t st,
+              float* db = nullptr, int acc_b = 0) {
     WgPlan p = plan_wgrad(B, A, Tl, C, K);
     WgArgs a;
     a.L = L; a.R = R; a.ws = ws;
+    // the bias slabs follow the weight slabs (db = sum over t of L: L must be the conv's dy, act none)
+    if (db && (actL != ENCX_ACT_NONE || (p.kind == 0 && A * C * K + A > NT))) return ENCX_EINVAL;
+    a.wsb = db ? ws + (int64_t)p.splits * A * C * K : nullptr;
     a.B = (int)B; a.A = (int)A; a.Tl = (int)Tl; a.C = (int)C; a.Tr = (int)Tr; a.K = (int)K;
     a.s = (int)s; a.d = (int)d; a.pl = (int)pl; a.e = (int)e; a.mode = mode; a.actL = actL;
     a.actR = actR; a.BT = p.BT; a.items = p.items; a.per_split = p.per_split;
@@ -1218,14 +1275,15 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
         else launch_wg<128, 128, 2, 2, 1>(a, p.splits, st);
     }
     ENCX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(wgrad_reduce, dim3(cdiv(AN, 64)), dim3(256), 0, st, ws, dw, AN, p.splits, accumulate);
+    hipLaunchKernelGGL(wgrad_reduce, dim3(cdiv(AN, 64) + (db ? cdiv(A, 64) : 0)), dim3(256), 0, st, ws, dw, AN,
+                       p.splits, accumulate, a.wsb, db, (int)A, acc_b);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
 
 size_t wgrad_ws_bytes(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
     WgPlan p = plan_wgrad(B, A, Tl, C, K);
-    return (size_t)p.splits * A * C * K * sizeof(float);
+    return (size_t)p.splits * A * (C * K + 1) * sizeof(float);  // + the bias slabs
 }
 
 static size_t maxz(size_t a, size_t b) { return a > b ? a : b; }
@@ -1308,15 +1366,23 @@ int encx_conv1d_bwd_weight(const float* dy, const float* x, float* dw, float* db
                            int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
                            int64_t short_ext, int pad_mode, int pre_act, int accumulate,
                            encx_stream_t stream) {
+    return encx_conv1d_bwd_weight_bias(dy, x, dw, db, ws, B, Cin, Tin, Cout, Tout, K, stride, dilation, pad_left,
+                                       short_ext, pad_mode, pre_act, accumulate, accumulate, stream);
+}
+
+int encx_conv1d_bwd_weight_bias(const float* dy, const float* x, float* dw, float* db, float* ws, int64_t B,
+                                int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout, int64_t K, int64_t stride,
+                                int64_t dilation, int64_t pad_left, int64_t short_ext, int pad_mode, int pre_act,
+                                int acc_w, int acc_b, encx_stream_t stream) {
     ENCX_REQUIRE(dy && x && dw && ws && B > 0);
     hipStream_t st = (hipStream_t)stream;
     encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K, 4.0 * (B * Cout * Tout + B * Cin * Tin + Cin * K * Cout), "conv_wgrad");
     ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
-    int rc = wgrad_run(dy, x, dw, ws, B, Cout, Tout, Cin, Tin, K, stride, dilation, pad_left,
-                       short_ext, pad_mode, ENCX_ACT_NONE, pre_act, accumulate, st);
-    if (rc) return rc;
-    if (db) return encx_channel_sum(dy, db, ws, B, Cout, Tout, accumulate, stream);
-    return 0;
+    const bool fused = db && wgrad_bias_ok(B, Cout, Tout, Cin, K);
+    int rc = wgrad_run(dy, x, dw, ws, B, Cout, Tout, Cin, Tin, K, stride, dilation, pad_left, short_ext, pad_mode,
+                       ENCX_ACT_NONE, pre_act, acc_w, st, fused ? db : nullptr, acc_b);
+    if (rc || !db || fused) return rc;
+    return encx_channel_sum(dy, db, ws, B, Cout, Tout, acc_b, stream);
 }
 
 size_t encx_conv1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout,

@@ -179,9 +179,18 @@ class Conv1dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
             dw = torch.empty(Cout, Cin, K, device=x.device, dtype=torch.float32)
             ws = _f32(lib.encx_conv1d_bwd_weight_workspace(B, Cin, Cout, tout, K) // 4 + 1, x)
-            call('encx_conv1d_bwd_weight', ptr(dy), ptr(x), ptr(dw), None, ptr(ws), B, Cin, T,
-                 Cout, tout, K, s, d, pl, e, mode, act, 0, st)
-            dv, dg, db = _param_grads(v, g, b, dw, dy, B, Cout, tout)
+            # the bias grad comes out of the same launch (the GEMM's ones column): straight into
+            # the flat grad view (accumulate) or into a fresh tensor
+            direct_b = b is not None and _direct(v) and _direct(g) and _direct(b)
+            db = None
+            if b is not None and not direct_b:
+                db = torch.empty(Cout, device=x.device, dtype=torch.float32)
+            dbp = ptr(b.grad) if direct_b else ptr(db)
+            call('encx_conv1d_bwd_weight_bias', ptr(dy), ptr(x), ptr(dw), dbp, ptr(ws), B, Cin, T,
+                 Cout, tout, K, s, d, pl, e, mode, act, 0, int(direct_b), st)
+            dv, dg, _ = _param_grads(v, g, None, dw, dy, B, Cout, tout)
+            if direct_b and dv is not None:
+                raise RuntimeError('encx: bias grad went to the flat view but the weight grads did not')
         dres = dy if has_res else None
         if role == 'tail' and has_res:
             # skip gradient of an identity-shortcut residual block: the head conv of the same

@@ -95,6 +95,13 @@ int encx_conv1d_bwd_weight(const float* dy, const float* x, float* dw, float* db
                            int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
                            int64_t short_ext, int pad_mode, int pre_act, int accumulate,
                            encx_stream_t stream);
+/* encx_conv1d_bwd_weight with separate accumulate flags for dw and db; the bias grad (sum of dy
+ * over b, t) is the GEMM's ones column, summed from the staged dy tile in the same kernel (no
+ * separate channel-sum pass; falls back to one for the tiny VALU shapes). */
+int encx_conv1d_bwd_weight_bias(const float* dy, const float* x, float* dw, float* db, float* ws, int64_t B,
+                                int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout, int64_t K, int64_t stride,
+                                int64_t dilation, int64_t pad_left, int64_t short_ext, int pad_mode, int pre_act,
+                                int acc_w, int acc_b, encx_stream_t stream);
 size_t encx_conv1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout,
                                         int64_t K);
 
