@@ -637,8 +637,8 @@ __global__ __launch_bounds__(NT) void c2_fwdq_kernel(C2Fwd a) {
 // entirely interior, or the one quad holding column Fi - 1 whose tail lanes are masked. The
 // loads are issued for the next chunk before the current chunk's MFMAs (MQ quads per thread),
 // and the commit is a masked select + ds_write_b128: no per-element paths, no shifts.
-template <int BN, int KFC, int MQ, int CKM>
-__global__ __launch_bounds__(NT) void c2_fwdr_kernel(C2Fwd a) {
+template <int BN, int KFC, int MQ, int CKM, int OCC = 1>  // OCC: min waves per SIMD (register cap)
+__global__ __launch_bounds__(NT, OCC) void c2_fwdr_kernel(C2Fwd a) {
     constexpr int BM = 32, TN = BN / 128, MW = (KFC * CKM * BM / 4 + NT - 1) / NT;
     extern __shared__ float smem[];
     const C2Geo g = a.g;
@@ -977,8 +977,8 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
 // (t, u), reduction (co, kt) pairs x JC taps; the staged B image is dy * LeakyReLU'(y), both
 // read as aligned quads (dy columns [base, base + RLp), base = the window start rounded down to
 // a multiple of 4) and masked in the commit.
-template <int TM, int BN, int JC, int MQ, int CKM>
-__global__ __launch_bounds__(NT) void c2_dgradr_kernel(C2Dg a) {
+template <int TM, int BN, int JC, int MQ, int CKM, int OCC = 1>
+__global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
     constexpr int BM = 32 * TM, TN = BN / 128, MW = (JC * CKM * BM / 4 + NT - 1) / NT;
     extern __shared__ float smem[];
     const C2Geo g = a.g;
@@ -1611,8 +1611,8 @@ struct C2Wg3 {
     float* ws;  // [splits][Co][N], N = VC*KF + 1
     int NR, RL, GC, items, per_split, chunks;
 };
-template <int KF, int NTW, int NW, int MQ, int ML>
-__global__ __launch_bounds__(NW * 64) void c2_wgrad3_kernel(C2Wg3 a) {
+template <int KF, int NTW, int NW, int MQ, int ML, int OCC = 1>
+__global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
     constexpr int NTH = NW * 64, P = W3_P, LDA = 33, PQ = P / 4;
     extern __shared__ float smem[];
     const C2Geo g = a.g;
@@ -2188,7 +2188,7 @@ int run_fwdq(C2Fwd a, hipStream_t st) {
     return 0;
 }
 
-template <int BN, int KFC, int MQ, int CKM>
+template <int BN, int KFC, int MQ, int CKM, int OCC = 1>
 int run_fwdr(C2Fwd a, hipStream_t st) {
     a.NR = c2_rows(BN, a.g.Fo);
     a.RL = (min(BN, a.g.Fo) - 1) * a.g.sf + a.g.KF + 3;  // + alignment slack of the column base
@@ -2198,12 +2198,12 @@ int run_fwdr(C2Fwd a, hipStream_t st) {
     const size_t lds = ((size_t)a.CK * a.NR * RLp + (size_t)KFC * a.CK * 32 + (size_t)2 * a.g.Ci * a.g.KT * a.NR) *
                        sizeof(float);
     dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.g.Fo, BN), (unsigned)cdiv(a.g.Co, 32), (unsigned)a.g.B);
-    hipLaunchKernelGGL((c2_fwdr_kernel<BN, KFC, MQ, CKM>), grid, dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((c2_fwdr_kernel<BN, KFC, MQ, CKM, OCC>), grid, dim3(NT), lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
 
-template <int TM, int BN, int JC, int MQ, int CKM>
+template <int TM, int BN, int JC, int MQ, int CKM, int OCC = 1>
 int run_dgradr(C2Dg a, hipStream_t st) {
     a.J = (int)cdiv(a.g.KF, a.g.sf);
     a.U = (a.g.Fi - 1 + a.g.pf) / a.g.sf + 1;
@@ -2215,7 +2215,7 @@ int run_dgradr(C2Dg a, hipStream_t st) {
     const size_t lds = ((size_t)a.CK * a.NR * RLp + (size_t)JC * a.CK * 32 * TM + (size_t)2 * a.g.Co * a.g.KT * a.NR) *
                        sizeof(float);
     dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.U, BN), 1, (unsigned)a.g.B);
-    hipLaunchKernelGGL((c2_dgradr_kernel<TM, BN, JC, MQ, CKM>), grid, dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((c2_dgradr_kernel<TM, BN, JC, MQ, CKM, OCC>), grid, dim3(NT), lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
@@ -2282,14 +2282,14 @@ static bool wg3r_ok(const C2Geo& g) {
     const WgPlan3 q = plan_wg3r(g, 32, 512);
     return q.GC * q.NR * (((q.RL + 3) & ~3) >> 2) <= 6 * 9 * 64;
 }
-template <int KF, int NTW, int NW, int MQ, int ML>
+template <int KF, int NTW, int NW, int MQ, int ML, int OCC = 1>
 int run_wgrad3(const C2Geo& g, const float* dy, const float* yact, const float* x, float* ws, const WgPlan3& p,
                hipStream_t st) {
     const int quads = p.GC * p.NR * (((p.RL + 3) & ~3) >> 2);
     if (quads > MQ * NW * 64 || 32 * (W3_P / 4) > ML * NW * 64 || g.Co > 32 || g.Fi < 4 || g.pf > 4) return ENCX_EINVAL;
     C2Wg3 a{g, dy, yact, x, ws, p.NR, p.RL, p.GC, p.items, p.per_split, p.chunks};
     dim3 grid((unsigned)cdiv(g.Ci * g.KT, p.GC), (unsigned)p.splits);
-    hipLaunchKernelGGL((c2_wgrad3_kernel<KF, NTW, NW, MQ, ML>), grid, dim3(NW * 64), p.lds, st, a);
+    hipLaunchKernelGGL((c2_wgrad3_kernel<KF, NTW, NW, MQ, ML, OCC>), grid, dim3(NW * 64), p.lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
@@ -2437,7 +2437,12 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
         ENCX_CHECK_LAUNCH();
         return 0;
     }
-    if (M == 64 && KF == 9 && sf == 2 && run_dgradr<2, 256, 5, 6, 16>(a, st) == 0) return 0;
+    // tile choice from tools/mb/c2_mb sweeps: 128-column tiles for the narrow late layers, 8-combo
+    // chunks + a 3-waves/SIMD register cap for the wide ones
+    if (M == 64 && KF == 9 && sf == 2) {
+        if (Fo <= 65 ? run_dgradr<2, 128, 5, 4, 16, 3>(a, st) == 0 : run_dgradr<2, 256, 5, 4, 8, 3>(a, st) == 0)
+            return 0;
+    }
     if (M <= 32 && KF == 3 && sf == 1 && run_dgradr<1, 256, 3, 6, 32>(a, st) == 0) return 0;
     if (sf == 1 && KT == 3 && KF == 9 && (Ci == 2 || Ci == 4) && Co % DN_CC == 0 && (KT - 1) * dt <= DN_MAXHALO) {
         dim3 grid((unsigned)cdiv(Fi, DN_COLS), (unsigned)cdiv(T2, DN_ROWS), (unsigned)B);

@@ -131,21 +131,11 @@ int main(int argc, char** argv) {
             };
             if (l.Co <= 32) {
                 if (l.KF == 9) {
-                    var("r<256,9,8,16>", [&] { if (run_fwdr<256, 9, 8, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("r<256,9,12,16>", [&] { if (run_fwdr<256, 9, 12, 16>(b, st)) printf("    (n/a)\n"); });
                     var("r<256,9,6,16>", [&] { if (run_fwdr<256, 9, 6, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("r<512,9,12,16>", [&] { if (run_fwdr<512, 9, 12, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("q<256,9,8,16>", [&] { if (run_fwdq<256, 9, 8, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("q<256,9,16,16>", [&] { if (run_fwdq<256, 9, 16, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("q<128,9,8,16>", [&] { if (run_fwdq<128, 9, 8, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("q<512,9,16,16>", [&] { if (run_fwdq<512, 9, 16, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("v<256,9,8>", [&] { run_fwdv<256, 9, 8>(b, st); });
-                    var("v<256,9,4>", [&] { run_fwdv<256, 9, 4>(b, st); });
-                    var("v<512,9,4>", [&] { run_fwdv<512, 9, 4>(b, st); });
-                    var("v<512,9,8>", [&] { run_fwdv<512, 9, 8>(b, st); });
-                    var("v<128,9,8>", [&] { run_fwdv<128, 9, 8>(b, st); });
-                    var("v<256,9,2>", [&] { run_fwdv<256, 9, 2>(b, st); });
-                    var("p<256,9,4,24>", [&] { if (run_fwdp<256, 9, 4, 24>(b, st)) printf("    (n/a)\n"); });
+                    var("r<256,9,6,16,4>", [&] { if (run_fwdr<256, 9, 6, 16, 4>(b, st)) printf("    (n/a)\n"); });
+                    var("r<256,9,4,16,4>", [&] { if (run_fwdr<256, 9, 4, 16, 4>(b, st)) printf("    (n/a)\n"); });
+                    var("r<256,9,4,8,4>", [&] { if (run_fwdr<256, 9, 4, 8, 4>(b, st)) printf("    (n/a)\n"); });
+                    var("r<128,9,4,16,4>", [&] { if (run_fwdr<128, 9, 4, 16, 4>(b, st)) printf("    (n/a)\n"); });
                 } else {
                     var("r<256,3,8,32>", [&] { if (run_fwdr<256, 3, 8, 32>(b, st)) printf("    (n/a)\n"); });
                     var("r<256,3,6,32>", [&] { if (run_fwdr<256, 3, 6, 32>(b, st)) printf("    (n/a)\n"); });
@@ -181,10 +171,13 @@ int main(int argc, char** argv) {
             };
             if (M == 64 && J == 5) {
                 var("r<2,256,5,6,16>", [&] { if (run_dgradr<2, 256, 5, 6, 16>(b, st)) printf("    (n/a)\n"); });
-                var("r<2,256,5,8,16>", [&] { if (run_dgradr<2, 256, 5, 8, 16>(b, st)) printf("    (n/a)\n"); });
-                var("r<2,128,5,6,16>", [&] { if (run_dgradr<2, 128, 5, 6, 16>(b, st)) printf("    (n/a)\n"); });
-                var("r<2,512,5,8,16>", [&] { if (run_dgradr<2, 512, 5, 8, 16>(b, st)) printf("    (n/a)\n"); });
-                var("<64,128,2,2,5>", [&] { run_dgrad<64, 128, 2, 2, 5>(b, st); });
+                var("r<2,256,5,6,16,3>", [&] { if (run_dgradr<2, 256, 5, 6, 16, 3>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,4,16>", [&] { if (run_dgradr<2, 256, 5, 4, 16>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,4,16,3>", [&] { if (run_dgradr<2, 256, 5, 4, 16, 3>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,4,8,3>", [&] { if (run_dgradr<2, 256, 5, 4, 8, 3>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,6,8>", [&] { if (run_dgradr<2, 256, 5, 6, 8>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,128,5,4,16,3>", [&] { if (run_dgradr<2, 128, 5, 4, 16, 3>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,128,5,4,16,4>", [&] { if (run_dgradr<2, 128, 5, 4, 16, 4>(b, st)) printf("    (n/a)\n"); });
             } else if (M == 32 && J == 3) {
                 var("r<1,256,3,6,32>", [&] { if (run_dgradr<1, 256, 3, 6, 32>(b, st)) printf("    (n/a)\n"); });
                 var("r<1,256,3,8,32>", [&] { if (run_dgradr<1, 256, 3, 8, 32>(b, st)) printf("    (n/a)\n"); });
@@ -251,13 +244,10 @@ int main(int argc, char** argv) {
             };
             if (gc && l.KF == 9) {
                 var3("3<9,1,9,6,1> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,1,9,6,1> 32/1024", 32, 1024, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,3,3,16,3> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 16, 3>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,3,3,16,3> 32/1024", 32, 1024, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 16, 3>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,9,6,1,5> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 6, 1, 5>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,3,3,16,3,2> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 16, 3, 2>(g, dy, yact, x, ws, q, st); });
                 var3("3<9,2,9,12,1> 64/512", 64, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 9, 12, 1>(g, dy, yact, x, ws, q, st); });
-                var("2<9,3,3> 512", 512, [&](const WgPlan3& q) { run_wgrad2<9, 3, 3>(g, dy, yact, x, ws, q, st); });
-                var("2<9,3,3> 1024", 1024, [&](const WgPlan3& q) { run_wgrad2<9, 3, 3>(g, dy, yact, x, ws, q, st); });
-                var("2<9,3,3> 2048", 2048, [&](const WgPlan3& q) { run_wgrad2<9, 3, 3>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,2,9,12,1,3> 64/512", 64, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 9, 12, 1, 3>(g, dy, yact, x, ws, q, st); });
             } else if (gc && l.KF == 3) {
                 var3("3<3,1,9,16,1> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1>(g, dy, yact, x, ws, q, st); });
                 var3("3<3,3,3,24,3> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 3, 3, 24, 3>(g, dy, yact, x, ws, q, st); });
