@@ -2276,11 +2276,14 @@ static WgPlan3 plan_wg3r(const C2Geo& g, int GC, int target = 1024) {
     p.lds = ((size_t)4 * GC * p.NR + (size_t)P * 33 + P + (size_t)GC * p.NR * (((p.RL + 3) & ~3))) * sizeof(float);
     return p;
 }
-// the layers c2_wgrad3_kernel<9, 1, 9, 6, 1> serves: 3x9 taps, 32-combo groups, <= 32 rows
+// workgroups per launch (tools/mb/c2_mb sweeps: the wide first strided layers want twice as many
+// splits as the rest)
+static int wg3r_target(const C2Geo& g) { return g.Fo >= 257 ? 1024 : 512; }
+// the layers c2_wgrad3_kernel<9, 1, 9, *, 1> serves: 3x9 taps, 32-combo groups, <= 32 rows
 static bool wg3r_ok(const C2Geo& g) {
     if (g.KF != 9 || (g.Ci * g.KT) % 32 != 0 || g.Co > 32 || g.Fi < 4 || g.pf > 4) return false;
     const WgPlan3 q = plan_wg3r(g, 32, 512);
-    return q.GC * q.NR * (((q.RL + 3) & ~3) >> 2) <= 6 * 9 * 64;
+    return q.GC * q.NR * (((q.RL + 3) & ~3) >> 2) <= 4 * 9 * 64;
 }
 template <int KF, int NTW, int NW, int MQ, int ML, int OCC = 1>
 int run_wgrad3(const C2Geo& g, const float* dy, const float* yact, const float* x, float* ws, const WgPlan3& p,
@@ -2464,7 +2467,7 @@ size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64
     C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
     WgPlan2 p = plan_wg2(g);
     int splits = p.splits;
-    if (wg3r_ok(g)) splits = max(splits, plan_wg3r(g, 32, 512).splits);
+    if (wg3r_ok(g)) splits = max(splits, plan_wg3r(g, 32, wg3r_target(g)).splits);
     if (co1_ok(g)) splits = max(splits, plan_co1(g).splits);
     return (size_t)splits * Co * (Ci * KT * KF + 1) * sizeof(float);
 }
@@ -2495,8 +2498,8 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
         return 0;
     }
     if (wg3r_ok(g)) {  // 9 waves x one 32-column tile each, vectorised staging (c2_wgrad3_kernel)
-        const WgPlan3 q = plan_wg3r(g, 32, 512);
-        if (run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st) == 0) {
+        const WgPlan3 q = plan_wg3r(g, 32, wg3r_target(g));
+        if (run_wgrad3<9, 1, 9, 4, 1, 5>(g, dy, yact, x, ws, q, st) == 0) {
             hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, q.splits, (int)Co,
                                N, dw, db, acc_w, acc_b);
             ENCX_CHECK_LAUNCH();
