@@ -2276,9 +2276,13 @@ static WgPlan3 plan_wg3r(const C2Geo& g, int GC, int target = 1024) {
     p.lds = ((size_t)4 * GC * p.NR + (size_t)P * 33 + P + (size_t)GC * p.NR * (((p.RL + 3) & ~3))) * sizeof(float);
     return p;
 }
-// workgroups per launch (tools/mb/c2_mb sweeps: the wide first strided layers want twice as many
-// splits as the rest)
-static int wg3r_target(const C2Geo& g) { return g.Fo >= 257 ? 1024 : 512; }
+// workgroups per launch: 768 = 3 combo groups x 256 splits, whole rounds over the 256 CUs
+// (tools/mb/c2_mb sweep: 768 within 2 % of the best target on all nine strided layers; targets
+// that leave a partial last round, 512 = 3 x 171, lose up to 35 %)
+static int wg3r_target(const C2Geo& g) {
+    (void)g;
+    return 768;
+}
 // the layers c2_wgrad3_kernel<9, 1, 9, *, 1> serves: 3x9 taps, 32-combo groups, <= 32 rows
 static bool wg3r_ok(const C2Geo& g) {
     if (g.KF != 9 || (g.Ci * g.KT) % 32 != 0 || g.Co > 32 || g.Fi < 4 || g.pf > 4) return false;

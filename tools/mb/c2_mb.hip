@@ -132,10 +132,7 @@ int main(int argc, char** argv) {
             if (l.Co <= 32) {
                 if (l.KF == 9) {
                     var("r<256,9,6,16>", [&] { if (run_fwdr<256, 9, 6, 16>(b, st)) printf("    (n/a)\n"); });
-                    var("r<256,9,6,16,4>", [&] { if (run_fwdr<256, 9, 6, 16, 4>(b, st)) printf("    (n/a)\n"); });
-                    var("r<256,9,4,16,4>", [&] { if (run_fwdr<256, 9, 4, 16, 4>(b, st)) printf("    (n/a)\n"); });
-                    var("r<256,9,4,8,4>", [&] { if (run_fwdr<256, 9, 4, 8, 4>(b, st)) printf("    (n/a)\n"); });
-                    var("r<128,9,4,16,4>", [&] { if (run_fwdr<128, 9, 4, 16, 4>(b, st)) printf("    (n/a)\n"); });
+
                 } else {
                     var("r<256,3,8,32>", [&] { if (run_fwdr<256, 3, 8, 32>(b, st)) printf("    (n/a)\n"); });
                     var("r<256,3,6,32>", [&] { if (run_fwdr<256, 3, 6, 32>(b, st)) printf("    (n/a)\n"); });
@@ -150,7 +147,7 @@ int main(int argc, char** argv) {
             tot_new[0] += best;
         }
         // ---- backward data
-        if (!(l.sf == 1 && l.KF == 9)) {  // the narrow first layer has its own VALU kernel
+        if (!(l.sf == 1 && l.KF == 9) && !getenv("MB_SKIP_DGRAD")) {  // the narrow first layer has its own VALU kernel
             C2Dg a{g, dy, yact, wp, nullptr, dx0, 0, 0, 0, 0, 0, 0};
             const int M = l.Ci * l.sf;
             double t0;
@@ -244,10 +241,11 @@ int main(int argc, char** argv) {
             };
             if (gc && l.KF == 9) {
                 var3("3<9,1,9,6,1> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,1,9,6,1,5> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 6, 1, 5>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,3,3,16,3,2> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 16, 3, 2>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,2,9,12,1> 64/512", 64, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 9, 12, 1>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,2,9,12,1,3> 64/512", 64, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 9, 12, 1, 3>(g, dy, yact, x, ws, q, st); });
+                for (int tg : {384, 512, 640, 768, 896, 1024, 1280, 1536}) {
+                    char nm[48];
+                    snprintf(nm, 48, "3<9,1,9,4,1,5> 32/%d", tg);
+                    var3(nm, 32, tg, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5>(g, dy, yact, x, ws, q, st); });
+                }
             } else if (gc && l.KF == 3) {
                 var3("3<3,1,9,16,1> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1>(g, dy, yact, x, ws, q, st); });
                 var3("3<3,3,3,24,3> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 3, 3, 24, 3>(g, dy, yact, x, ws, q, st); });
