@@ -2,9 +2,10 @@
 
 Encode (SEANet encoder + RVQ argmin) and decode (RVQ gather + SEANet decoder) run the encx
 kernels; each frame's codes are packed / unpacked on the GPU (csrc/bitstream.hip) and only the
-packed bytes cross PCIe. Byte format, metadata keys and error behaviour follow
-compress.py:30-191; `use_lm=True` (the remote-only pretrained LM entropy coder,
-quantization/ac.py) is out of scope and raises.
+packed bytes cross PCIe. With use_lm=True the codes are arithmetic coded under the LM's
+probabilities instead (compress.py:67-89, 128-155): encx.lm runs the LM and the coder on the
+GPU (csrc/lm.hip, csrc/ac.hip). Byte format, metadata keys and error behaviour follow
+compress.py:30-191.
 """
 import io
 import struct
@@ -27,11 +28,6 @@ def _model_device(model):
     return next(model.parameters()).device
 
 
-def _no_lm():
-    raise NotImplementedError('encx: use_lm=True needs the pretrained LM entropy coder '
-                              '(remote-only checkpoint, quantization/ac.py); use use_lm=False')
-
-
 def compress_to_file(model: EncodecModel, wav: torch.Tensor, fo: tp.IO[bytes], use_lm: bool = True):
     """compress.py:30-101: header, then per frame the '!f' scale (normalising models) and the
     frame's codes bit-packed t-major at model.bits_per_codebook bits, flushed per frame."""
@@ -39,7 +35,7 @@ def compress_to_file(model: EncodecModel, wav: torch.Tensor, fo: tp.IO[bytes], u
     if model.name not in MODELS:
         raise ValueError(f"The provided model {model.name} is not supported.")
     if use_lm:
-        _no_lm()
+        lm = model.get_lm_model()
     with torch.no_grad():
         frames = model.encode(wav[None].to(_model_device(model), torch.float32))
     metadata = {
@@ -50,6 +46,14 @@ def compress_to_file(model: EncodecModel, wav: torch.Tensor, fo: tp.IO[bytes], u
         'fr': frames[0][0].shape[2],
     }
     binary.write_ecdc_header(fo, metadata)
+    if use_lm:
+        # compress.py:67-89: one arithmetic coded stream per frame, flushed per frame
+        for frame, scale in frames:
+            if scale is not None:
+                fo.write(struct.pack('!f', scale.cpu().item()))
+            fo.write(lm.encode_streams(frame.contiguous())[0])
+        fo.flush()
+        return
     # pack every frame on the device, then one copy of all payloads (and scales) to the host
     packed = [ops.pack_codes(frame, model.bits_per_codebook) for frame, _ in frames]
     scales = [s.reshape(-1)[:1] for _, s in frames if s is not None]
@@ -81,7 +85,7 @@ def decompress_from_file(model: EncodecModel, fo: tp.IO[bytes], device='cpu') ->
     if model.name not in MODELS:
         raise ValueError(f"The audio was compressed with an unsupported model {model_name}.")
     if use_lm:
-        _no_lm()
+        lm = model.get_lm_model()
     dev = _model_device(model)
     frames: tp.List[EncodedFrame] = []
     segment_stride = model.segment_stride or audio_length
@@ -92,6 +96,14 @@ def decompress_from_file(model: EncodecModel, fo: tp.IO[bytes], device='cpu') ->
             scale = torch.tensor(scale_f, device=dev).view(1)
         else:
             scale = None
+        if use_lm:
+            # compress.py:129-155: the decoder reads the rest of the file and stops where the
+            # reference's does; the file position follows the bytes it consumed
+            start = fo.tell()
+            codes, used = lm.decode_streams([fo.read()], num_codebooks, frame_length)
+            fo.seek(start + used[0])
+            frames.append((codes, scale))
+            continue
         unpacker = binary.BitUnpacker(model.bits_per_codebook, fo, device=dev)
         frames.append((unpacker.pull_frame(num_codebooks, frame_length)[None], scale))
     with torch.no_grad():

@@ -1,7 +1,9 @@
 """EncodecModel (model.py of the reference) on the encx HIP path.
 
 Same constructor, `_get_model` factory, `encode / decode / forward / set_target_bandwidth`
-and state-dict layout. Out of scope here: LMModel, pretrained downloads.
+and state-dict layout, plus `get_lm_model` (model.py:221-240) for the LM entropy coder
+(encx.lm). Pretrained checkpoints are fetched as the reference fetches them (torch.hub, which
+finds a pre-populated hub cache offline); `set_lm_model` installs an LM directly.
 """
 import math
 import random
@@ -132,6 +134,34 @@ class EncodecModel(nn.Module):
             self.last_decoder_input = codes[0][0] if len(codes) == 1 else None
             return self.decode(codes)[:, :, :x.shape[-1]], loss_w, frames
         return self.decode(frames)[:, :, :x.shape[-1]]
+
+    def set_lm_model(self, lm):
+        """Use `lm` (an encx.lm.LMModel) for use_lm=True instead of the pretrained one."""
+        self._lm_model = lm
+
+    def get_lm_model(self):
+        """model.py:221-240: LMModel(n_q, bins, num_layers=5, dim=200, past_context=3.5 s of
+        frames) with the pretrained weights of this model."""
+        from .lm import LMModel
+        lm = getattr(self, '_lm_model', None)
+        if lm is not None:
+            return lm
+        device = next(self.parameters()).device
+        lm = LMModel(self.quantizer.n_q, self.quantizer.bins, num_layers=5, dim=200,
+                     past_context=int(3.5 * self.frame_rate)).to(device)
+        checkpoints = {
+            'encodec_24khz': 'encodec_lm_24khz-1608e3c0.th',
+            'encodec_48khz': 'encodec_lm_48khz-7add9fc3.th',
+        }
+        try:
+            checkpoint_name = checkpoints[self.name]
+        except KeyError:
+            raise RuntimeError("No LM pre-trained for the current Encodec model.")
+        url = 'https://dl.fbaipublicfiles.com/encodec/v0/' + checkpoint_name
+        state = torch.hub.load_state_dict_from_url(url, map_location='cpu', check_hash=True)
+        lm.load_state_dict(state)
+        lm.eval()
+        return lm
 
     def set_target_bandwidth(self, bandwidth: float):
         if bandwidth not in self.target_bandwidths:

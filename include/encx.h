@@ -403,6 +403,76 @@ int encx_crop_collate(const float* pool, const int64_t* offsets, const int64_t* 
                       const int64_t* src_channels, const int64_t* starts, const int64_t* out_len,
                       float* out, int64_t B, int64_t C, int64_t Tmax, encx_stream_t stream);
 
+/* ------------------------------------------------------ LM entropy coding (use_lm=True)
+ * LMModel (model.py:27-65) over StreamingTransformerEncoder (modules/transformer.py:62-119),
+ * inference only, and the arithmetic coder of quantization/ac.py. Activations are [B][T][D]
+ * fp32 (row n = b*T + t). Every kernel computes a row from that row's inputs alone in a fixed
+ * reduction order, so a row's bits do not depend on how many rows share a launch: the encoder
+ * runs a frame's T steps as one pass, the decoder one step at a time, and both see identical
+ * cdfs (the precondition of arithmetic decoding, ac.py:220-224).
+ *
+ * encx_lm_input: the LM input (model.py:59-60: sum_k emb[k][idx], k in order), norm_in
+ * LayerNorm and the sin position embedding of step offset + t (transformer.py:16-27, 104-113).
+ * emb is the K stacked nn.Embedding tables [n_q][card1 = card + 1][D]; idx(b,k,t) =
+ * idx[b*s_b + k*s_k + t*s_t], or with `shifted` (offset 0 only) the teacher-forced input of a
+ * known code sequence, 0 at t = 0 and codes[b][k][t-1] + 1 after (compress.py:74-79). */
+int encx_lm_input(const int64_t* idx, int64_t s_b, int64_t s_k, int64_t s_t, int64_t B, int64_t K,
+                  int64_t T, int shifted, const float* emb, int64_t card1, int64_t D, const float* ln_w,
+                  const float* ln_b, int64_t offset, float max_period, float* x, encx_stream_t stream);
+/* One StreamingTransformerEncoderLayer (transformer.py:30-59; nn.TransformerEncoderLayer with
+ * norm_first=False, GELU, dropout 0): x [B][T][D] -> y. kv [B][L][2D] is the layer's key |
+ * value cache, position s = seq0 + t for row t (seq0 = offset + 1); position 0 is the zero
+ * state every layer starts with (transformer.py:106), written when seq0 == 1. Row t attends
+ * positions [max(0, s - past_context), s] (transformer.py:52-58, 117-118). Weights in
+ * nn.MultiheadAttention / nn.Linear layout; work: encx_lm_layer_workspace(B*T, D, F) bytes. */
+int64_t encx_lm_layer_workspace(int64_t N, int64_t D, int64_t F);
+int encx_lm_layer(const float* x, float* y, int64_t B, int64_t T, float* kv, int64_t L, int64_t seq0,
+                  int64_t past_context, int64_t D, int64_t heads, int64_t F, const float* in_w,
+                  const float* in_b, const float* out_w, const float* out_b, const float* l1_w,
+                  const float* l1_b, const float* l2_w, const float* l2_b, const float* n1_w,
+                  const float* n1_b, const float* n2_w, const float* n2_b, float* work,
+                  encx_stream_t stream);
+/* The first K per-codebook heads (model.py:62-64: linears[k], softmax over the codebook) with
+ * the quantized cdf of every (row, k) fused (ac.py:18-53 as compress.py:84-85 calls it,
+ * check=False). w [>=K][card][D] stacked, bias [>=K][card]; work: encx_lm_heads_workspace.
+ * probas [B][T][K][card] and cdf int32 [B][T][K][card] are each optional (one is required).
+ * With sym (codes, sym[b*s_b + k*s_k + t*s_t]) lohi [B][T][K][2] receives each symbol's coding
+ * interval (cdf[s-1] or 0, cdf[s] - 1) for encx_ac_encode. *err (device, caller-zeroed) |= 1
+ * when a cdf total exceeds 2^total_range_bits (check=True would reject it, ac.py:50; the coder
+ * asserts, ac.py:116), |= 2 for a symbol outside [0, card). */
+int64_t encx_lm_heads_workspace(int64_t N, int64_t K, int64_t card);
+int encx_lm_heads(const float* x, int64_t B, int64_t T, int64_t D, const float* w, const float* bias,
+                  int64_t K, int64_t card, float* work, float* probas, int32_t* cdf, int total_range_bits,
+                  float roundoff, int min_range, const int64_t* sym, int64_t s_b, int64_t s_k, int64_t s_t,
+                  int32_t* lohi, int* err, encx_stream_t stream);
+/* build_stable_quantized_cdf (ac.py:18-53) of `rows` pdfs (row r at pdf + r*ld) -> cdf int32
+ * [rows][card] (values < 2^31 since total_range_bits <= 30). ENCX_EINVAL where the reference
+ * asserts alpha <= 1 or min_range >= 2; *err |= 1 where its check=True would fail. */
+int encx_ac_cdf(const float* pdf, int64_t rows, int64_t card, int64_t ld, int total_range_bits, float roundoff,
+                int min_range, int32_t* cdf, int* err, encx_stream_t stream);
+/* coding interval of sym[r] in cdf row r (ac.py:144-145) -> lohi [rows][2]; *err |= 2 for a
+ * symbol outside [0, card). */
+int encx_ac_lohi(const int32_t* cdf, int64_t ld, const int64_t* sym, int64_t rows, int64_t card, int32_t* lohi,
+                 int* err, encx_stream_t stream);
+/* ArithmeticCoder: push every (lo, hi) of a stream in order, then flush (ac.py:130-167); stream
+ * s reads lohi + s*n*2 and writes out + s*cap. nbytes[s] = bytes of the stream (the BitPacker's
+ * final partial byte included); err[s] = 0, 1 (cdf total above 2^bits: the reference asserts,
+ * ac.py:116), 2 (cap too small; nbytes holds the size needed) or 3 (max_bit > 61, ac.py:157).
+ * encx_ac_encode_capacity(n, bits) bytes always suffice. */
+int64_t encx_ac_encode_capacity(int64_t n_symbols, int total_range_bits);
+int encx_ac_encode(const int32_t* lohi, int64_t streams, int64_t n, int total_range_bits, uint8_t* out,
+                   int64_t cap, int64_t* nbytes, int* err, encx_stream_t stream);
+/* ArithmeticDecoder.pull (ac.py:217-260) of K symbols per stream, symbol k against cdf row
+ * cdf[s][k][:card]. Stream s reads data + s*stride (nbytes[s] bytes); state [streams][5] int64 =
+ * (low, high, current, max_bit, bits consumed), zero with max_bit = -1 for a new stream. The
+ * symbol goes to codes[s*c_s + k*c_k + t*c_t] (codes nullable) and sym + 1 to next_idx[s][k]
+ * (nullable: the LM input of the next step, compress.py:154-155). err[s]: 1 = the stream ran out
+ * (pull returns None), 2 = no interval contains the value (ac.py:238); a failed stream is left
+ * untouched by later calls. Bytes consumed = ceil(bits consumed / 8). */
+int encx_ac_decode(const uint8_t* data, int64_t stride, const int64_t* nbytes, int64_t streams, int64_t* state,
+                   const int32_t* cdf, int64_t K, int64_t card, int total_range_bits, int64_t* codes, int64_t c_s,
+                   int64_t c_k, int64_t c_t, int64_t t, int64_t* next_idx, int* err, encx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -102,3 +102,32 @@ def rvq_certified(emb, embeds, factor=256):
 
 __all__ = ['load', 'T', 'model_state', 'disc_state', 'cfg48k', 'codebooks_from_stats', 'g3_codebooks',
            'certified', 'rvq_certified', 'synth_wave', 'rng']
+
+
+# ---------------------------------------------------------------- g12: LM entropy coder
+def g12_lm_config(name):
+    """The LMConfig + synthetic state of make_goldens.G12_LM[name] (same seeds)."""
+    from oracle.lm_oracle import LMConfig, lm_param_shapes
+    from synth import synth_lm_state
+    c = {'a': dict(n_q=32, card=1024, dim=200, num_heads=8, num_layers=5, past_context=262, seed=121),
+         'b': dict(n_q=4, card=64, dim=64, num_heads=4, num_layers=2, past_context=5, seed=122)}[name]
+    seed = c.pop('seed')
+    cfg = LMConfig(**c)
+    st = {k: T(v) for k, v in synth_lm_state(lm_param_shapes(cfg), seed).items()}
+    return cfg, st
+
+
+def g12_ac_rows(d):
+    """-> list of (card, bits, pdfs [steps][card], cdfs [steps][card], syms [steps], data bytes,
+    eof flag) per coder case of g12_lm.npz."""
+    out, po, so, bo = [], 0, 0, 0
+    for i, (card, steps, bits, uni) in enumerate(d['ac_cases']):
+        n = int(card) * int(steps)
+        pdf = d['ac_pdf'][po:po + n].reshape(steps, card)
+        cdf = d['ac_cdf'][po:po + n].reshape(steps, card).astype(np.int64)
+        sym = d['ac_sym'][so:so + steps]
+        nb = int(d['ac_nbytes'][i])
+        data = d['ac_bytes'][bo:bo + nb].tobytes()
+        out.append((int(card), int(bits), pdf, cdf, sym, data, int(d['ac_eof'][i])))
+        po, so, bo = po + n, so + int(steps), bo + nb
+    return out

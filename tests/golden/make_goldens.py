@@ -17,6 +17,9 @@ Fixture map:
   g10_ecdc.npz     .ecdc: reference BitPacker vectors (bits 1..32), header, compress/decompress
                    bytes + waves for the g1 model and the g9 48 kHz model (one / two segments)
   g11_data.npz     customAudioDataset crop (seeded random) + mono expand + collate_fn
+  g12_lm.npz       LM entropy coder: build_stable_quantized_cdf + ArithmeticCoder/Decoder vectors
+                   (ac.py), LMModel streaming probabilities with synthetic weights (real dims and
+                   a small past_context), and compress(use_lm=True) bytes of the g1 model
   g9_step48k.npz   config-5 analogue: 48 kHz stereo, non-causal, time_group_norm, segment 0.1 s
                    (two frames: 4800 + 48 samples, linear overlap-add), gen-only and GAN steps
 """
@@ -583,8 +586,152 @@ def g11():
     save('g11_data.npz', **out)
 
 
+# ------------------------------------------------------------------------------------ G12
+# (cardinality, steps, total_range_bits, logit scale, symbols): pdf = softmax(scale * randn(card));
+# symbols drawn from the pdf (0, as ac.py:277) or uniformly (1: mostly improbable symbols, long
+# codes, the range straddling a power of two for many steps)
+G12_AC_CASES = [(1024, 32, 24, 3.0, 0), (37, 64, 24, 1.0, 0), (2, 40, 24, 4.0, 0), (3, 6, 24, 1.0, 0),
+                (3000, 8, 24, 6.0, 0), (64, 50, 16, 2.0, 0), (256, 48, 24, 6.0, 1), (1024, 24, 30, 8.0, 1)]
+# LM configs: real dims (model.py:221-226 at 24 kHz) and a small one whose past_context
+# window truncates within the sequence
+G12_LM = {'a': dict(n_q=32, card=1024, dim=200, num_heads=8, num_layers=5, past_context=262,
+                    seed=121, B=1, K=8, T=10),
+          'b': dict(n_q=4, card=64, dim=64, num_heads=4, num_layers=2, past_context=5,
+                    seed=122, B=2, K=3, T=14)}
+
+
+def g12_lm_module(c):
+    from oracle.lm_oracle import LMConfig, lm_param_shapes
+    from synth import synth_lm_state
+    lm = R.model.LMModel(c['n_q'], c['card'], dim=c['dim'], num_heads=c['num_heads'],
+                         num_layers=c['num_layers'], past_context=c['past_context'])
+    cfg = LMConfig(n_q=c['n_q'], card=c['card'], dim=c['dim'], num_heads=c['num_heads'],
+                   num_layers=c['num_layers'], past_context=c['past_context'])
+    shapes = lm_param_shapes(cfg)
+    sd = lm.state_dict()
+    assert set(sd) == set(shapes), set(sd) ^ set(shapes)
+    assert all(tuple(sd[k].shape) == tuple(v) for k, v in shapes.items())
+    lm.load_state_dict({k: t(v) for k, v in synth_lm_state(shapes, c['seed']).items()})
+    lm.eval()
+    return lm
+
+
+def g12():
+    import io
+    import random
+    import compress as ref_compress
+    import quantization.ac as ref_ac
+    out = {}
+    # ---- arithmetic coder vectors (the structure of ac.py:263-288, smaller)
+    pdfs, cdfs, syms, datas, eofs = [], [], [], [], []
+    over_p, over_c, over_b = [], [], []
+    for i, (card, steps, bits, scale, uni) in enumerate(G12_AC_CASES):
+        torch.manual_seed(1234 + i)
+        fo = io.BytesIO()
+        enc = ref_ac.ArithmeticCoder(fo, total_range_bits=bits)
+        cp, cc, cs = [], [], []
+        while len(cs) < steps:
+            pdf = torch.softmax(scale * torch.randn(card), dim=0)
+            # check=False as compress.py:84-85 calls it. A near-certain pdf can round to a
+            # total above 2^bits; check=True rejects it and the coder would then assert
+            # (ac.py:116): such rows are kept apart (ac_over_*) and redrawn
+            q = ref_ac.build_stable_quantized_cdf(pdf, enc.total_range_bits, check=False)
+            if int(q[-1]) > 2 ** bits:
+                over_p.append(pdf.numpy())
+                over_c.append(q.numpy())
+                over_b.append(bits)
+                continue
+            s = torch.multinomial(pdf, 1).item() if not uni else int(torch.randint(card, (1,)))
+            enc.push(s, q)
+            cp.append(pdf.numpy())
+            cc.append(q.numpy())
+            cs.append(s)
+        enc.flush()
+        fo.seek(0)
+        dec = ref_ac.ArithmeticDecoder(fo, total_range_bits=bits)
+        for q, s in zip(cc, cs):
+            assert dec.pull(torch.from_numpy(q)) == s
+        # one pull past the end (ac.py:288): None if the decoder needs bits the stream no
+        # longer has (1), else the binary search over a one-entry zero cdf fails (2)
+        try:
+            eofs.append(1 if dec.pull(torch.zeros(1)) is None else 0)
+        except RuntimeError:
+            eofs.append(2)
+        pdfs.append(np.concatenate(cp))
+        cdfs.append(np.concatenate(cc))
+        syms.append(np.array(cs, np.int64))
+        datas.append(np.frombuffer(fo.getvalue(), np.uint8))
+    out['ac_cases'] = np.array([c[:3] + c[4:] for c in G12_AC_CASES], np.int64)
+    out['ac_scale'] = np.array([c[3] for c in G12_AC_CASES], np.float32)
+    out['ac_pdf'] = np.concatenate(pdfs).astype(np.float32)
+    out['ac_cdf'] = np.concatenate(cdfs).astype(np.int32)
+    out['ac_sym'] = np.concatenate(syms)
+    out['ac_bytes'] = np.concatenate(datas)
+    out['ac_nbytes'] = np.array([len(d) for d in datas], np.int64)
+    out['ac_eof'] = np.array(eofs, np.int64)
+    out['ac_over_pdf'] = np.concatenate(over_p).astype(np.float32)
+    out['ac_over_cdf'] = np.concatenate(over_c).astype(np.int64)
+    out['ac_over_card'] = np.array([len(a) for a in over_p], np.int64)
+    out['ac_over_bits'] = np.array(over_b, np.int64)
+
+    # ---- LM streaming probabilities (compress.py:74-78 call pattern)
+    for name, c in G12_LM.items():
+        lm = g12_lm_module(c)
+        g = rng(c['seed'] + 1000)
+        codes = t(g.integers(0, c['card'], size=(c['B'], c['K'], c['T']), dtype=np.int64))
+        states, offset = None, 0
+        inp = torch.zeros(c['B'], c['K'], 1, dtype=torch.long)
+        probs = []
+        with torch.no_grad():
+            for ti in range(c['T']):
+                p, states, offset = lm(inp, states, offset)
+                inp = 1 + codes[:, :, ti:ti + 1]
+                probs.append(p[:, :, :, 0].permute(0, 2, 1).numpy())   # [B][K][card]
+        out[f'lm_{name}/codes'] = codes.numpy()
+        out[f'lm_{name}/probs'] = np.stack(probs, 1).astype(np.float32)  # [B][T][K][card]
+
+    # ---- compress(use_lm=True) of the g1 model at 1.5 kbps on a 0.2 s clip
+    d1 = np.load(os.path.join(HERE, 'g1_eval24k.npz'))
+    m = R.model.EncodecModel._get_model([1.5, 3., 6., 12., 24.], 24000, 1, causal=True,
+                                        model_norm='weight_norm', audio_normalize=False,
+                                        segment=None, name='encodec_24khz')
+    load_synth(m, 1)
+    fill_codebooks(m, d1['stats'], 77, 2)
+    m.eval()
+    m.set_target_bandwidth(1.5)
+    lm = g12_lm_module(G12_LM['a'])
+    m.get_lm_model = lambda: lm
+    x = t(d1['x'])[0][:, :4800]
+    rec_p, rec_c = [], []
+    orig = ref_compress.build_stable_quantized_cdf
+
+    def recorder(pdf, bits, **kw):
+        q = orig(pdf, bits, **kw)
+        rec_p.append(pdf.numpy().copy())
+        rec_c.append(q.numpy().copy())
+        return q
+    ref_compress.build_stable_quantized_cdf = recorder
+    try:
+        data = ref_compress.compress(m, x, use_lm=True)
+        n_enc = len(rec_p)
+        with torch.no_grad():
+            y, _ = ref_compress.decompress_from_file(m, io.BytesIO(data), device='cpu')
+        assert [a.tolist() for a in rec_c[n_enc:]] == [a.tolist() for a in rec_c[:n_enc]]
+    finally:
+        ref_compress.build_stable_quantized_cdf = orig
+    with torch.no_grad():
+        codes = m.encode(x[None])[0][0]
+    out['e2e_x'] = x.numpy()
+    out['e2e_bytes'] = np.frombuffer(data, np.uint8)
+    out['e2e_codes'] = codes.numpy()
+    out['e2e_pdf'] = np.stack(rec_p[:n_enc]).astype(np.float32)
+    out['e2e_cdf'] = np.stack(rec_c[:n_enc]).astype(np.int32)
+    out['e2e_y'] = y.numpy()
+    save('g12_lm.npz', **out)
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9', 'g10', 'g11']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9', 'g10', 'g11', 'g12']
     for w in which:
         torch.manual_seed(0)
         globals()[w]()

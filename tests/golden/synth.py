@@ -74,3 +74,17 @@ def synth_codebooks(stats, seed):
         cb[i] = (stats[i, 0][None, :].astype(np.float64)
                  + stats[i, 1][None, :].astype(np.float64) * z).astype(np.float32)
     return cb
+
+
+def synth_lm_state(named_shapes, seed, sharp=6.0):
+    """Synthetic LMModel weights (model.py:27-45; the pretrained LM is remote-only,
+    model.py:221-240): synth_state, then LayerNorm gains 1 + u (instead of u) and the
+    per-codebook output projections scaled by `sharp` so the softmax is peaked like a trained
+    model's (the entropy coder then sees both near-certain and rare symbols)."""
+    out = synth_state(named_shapes, seed)
+    for k in list(out):
+        if k.endswith('weight') and ('norm' in k):
+            out[k] = (1.0 + out[k].astype(np.float64)).astype(np.float32)
+        elif k.startswith('linears.') and k.endswith('weight'):
+            out[k] = (out[k] * np.float32(sharp)).astype(np.float32)
+    return out

@@ -215,8 +215,6 @@ def test_gpu_compress_decompress_24k_fixture():
     y, sr = C.decompress(m, d['c24_bytes'].tobytes())
     assert sr == 24000 and y.shape == (1, 24000) and not y.is_cuda
     assert rel(y, d['c24_y']) < 1e-3, rel(y, d['c24_y'])
-    with pytest.raises(NotImplementedError):
-        C.compress(m, x, use_lm=True)
     m.name = 'unset'
     with pytest.raises(ValueError):
         C.compress(m, x)

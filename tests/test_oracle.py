@@ -307,3 +307,76 @@ def test_rvq_bandwidth_rule():
     assert [O.rvq_num_quantizers(b, 75) for b in (1.5, 3., 6., 12., 24.)] == [2, 4, 8, 16, 32]
     assert [O.rvq_num_quantizers(b, 150) for b in (3., 6., 12., 24.)] == [2, 4, 8, 16]
     assert math.isclose(O.Config().frame_rate, 75)
+
+
+# --------------------------------------------------------------------------- g12 LM coder
+def test_oracle_quantized_cdf_and_coder_fixture():
+    from oracle import ac_oracle as A
+    from fixtures import g12_ac_rows
+    d = load('g12_lm.npz')
+    for card, bits, pdf, cdf, sym, data, eof in g12_ac_rows(d):
+        for p, c in zip(pdf, cdf):
+            assert np.array_equal(A.quantized_cdf(p, bits, check=False), c)
+        assert A.encode(sym, cdf, bits) == data
+        dec = A.Decoder(data, bits)
+        assert [dec.pull(c) for c in cdf] == sym.tolist()
+        assert dec.bytes_read == len(data)
+        if eof == 1:
+            assert dec.pull(np.zeros(1, np.int64)) is None
+        else:
+            with pytest.raises(RuntimeError):
+                dec.pull(np.zeros(1, np.int64))
+    # near-certain pdfs whose cdf total exceeds 2^bits: check=True rejects, the coder asserts
+    o = 0
+    for card, bits in zip(d['ac_over_card'], d['ac_over_bits']):
+        p, c = d['ac_over_pdf'][o:o + card], d['ac_over_cdf'][o:o + card]
+        o += card
+        assert np.array_equal(A.quantized_cdf(p, int(bits), check=False), c)
+        assert c[-1] > 2 ** int(bits)
+        with pytest.raises(AssertionError):
+            A.quantized_cdf(p, int(bits), check=True)
+        with pytest.raises(AssertionError):
+            A.encode([card - 1], [c], int(bits))
+
+
+@pytest.mark.parametrize('name', ['a', 'b'])
+def test_oracle_lm_fixture(name):
+    from oracle import lm_oracle as L
+    from fixtures import g12_lm_config
+    d = load('g12_lm.npz')
+    cfg, st = g12_lm_config(name)
+    codes = T(d[f'lm_{name}/codes'])
+    ref = d[f'lm_{name}/probs']                       # [B][T][K][card]
+    B, K, Tn = codes.shape
+    states, offset = None, 0
+    inp = torch.zeros(B, K, 1, dtype=torch.long)
+    got = []
+    for t in range(Tn):
+        p, states, offset = L.lm_step(st, inp, states, offset, cfg)
+        inp = 1 + codes[:, :, t:t + 1]
+        got.append(p[:, :, :, 0].permute(0, 2, 1))
+    close(torch.stack(got, 1), ref, rtol=1e-4, atol=1e-7)
+    # the one-pass form (teacher-forced, phantom zero key) gives the same probabilities
+    allp = L.lm_all(st, codes, cfg).permute(0, 3, 2, 1)   # [B][T][K][card]
+    close(allp, ref, rtol=1e-4, atol=1e-7)
+
+
+def test_oracle_lm_compress_fixture():
+    """compress(use_lm=True) bytes of the reference (g1 model, 1.5 kbps, 0.2 s): the oracle's
+    cdfs from the reference's pdfs and its coder reproduce the payload bit for bit, and the
+    oracle LM reproduces the pdfs."""
+    from oracle import ac_oracle as A, ecdc_oracle as E, lm_oracle as L
+    from fixtures import g12_lm_config
+    d = load('g12_lm.npz')
+    data = d['e2e_bytes'].tobytes()
+    meta, off = E.parse_header(data)
+    codes = d['e2e_codes']                            # [1][K][T]
+    K, Tn = codes.shape[1:]
+    assert meta == {'m': 'encodec_24khz', 'al': 4800, 'nc': int(K), 'lm': True, 'fr': int(Tn)}
+    cdfs = [A.quantized_cdf(p, 24, check=False) for p in d['e2e_pdf']]
+    assert all(np.array_equal(a, b) for a, b in zip(cdfs, d['e2e_cdf']))
+    syms = codes[0].T.reshape(-1)                     # push order: t-major, then codebook
+    assert A.encode(syms, cdfs) == data[off:]
+    cfg, st = g12_lm_config('a')
+    p = L.lm_all(st, T(codes), cfg)                   # [1][card][K][T]
+    close(p[0].permute(2, 1, 0).reshape(-1, cfg.card), d['e2e_pdf'], rtol=1e-4, atol=1e-7)
