@@ -20,6 +20,11 @@
 //   and finds none exactly when that search fails (ac.py:238).
 #include "common.h"
 
+// No mul+add contraction anywhere in this file: the same quantity computed by two kernels (e.g.
+// a score scaled, stored, then offset by the max, against the same expression inline) must round
+// identically, and __fmul_rn alone does not stop clang fusing it into a following add.
+#pragma clang fp contract(off)
+
 namespace {
 
 constexpr int CDF_THREADS = 256;
@@ -145,30 +150,42 @@ __global__ void ac_encode_kernel(const int32_t* __restrict__ lohi, int64_t n, in
     const uint64_t R = 1ull << bits;
     uint64_t low = 0, high = 0;
     int max_bit = -1, e = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const uint64_t rl = (uint64_t)(uint32_t)lh[2 * i], rh = (uint64_t)(uint32_t)lh[2 * i + 1];
-        uint64_t delta = high - low + 1;
-        if (delta < R) {  // ac.py:139-142
-            const int sh = bits - (63 - __builtin_clzll(delta));
-            low <<= sh;
-            high = (high << sh) | lowmask(sh);
-            max_bit += sh;
-            delta = high - low + 1;
+    // the intervals do not depend on the coder state: fetch them 8 symbols at a time (one
+    // memory round trip per 8 pushes instead of one per push)
+    for (int64_t i0 = 0; i0 < n && !e; i0 += 8) {
+        uint32_t iv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int64_t q = 2 * i0 + u;
+            iv[u] = (uint32_t)lh[q < 2 * n ? q : 2 * n - 1];
         }
-        const uint64_t el = (rl * delta + R - 1) >> bits, eh = (rh * delta) >> bits;  // ac.py:146-147
-        high = low + eh;
-        low = low + el;
-        if (high >> (max_bit + 1)) { e = 1; break; }  // ac.py:116
-        const uint64_t x = low ^ high;                  // ac.py:111-128
-        const int hb = x ? 63 - __builtin_clzll(x) : -1;
-        const int nf = max_bit - hb;
-        if (nf > 0) {
-            bo.put_msb_first(low >> (hb + 1), nf);
-            low &= lowmask(hb + 1);
-            high &= lowmask(hb + 1);
-            max_bit = hb;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (i0 + u >= n || e) break;
+            const uint64_t rl = iv[2 * u], rh = iv[2 * u + 1];
+            uint64_t delta = high - low + 1;
+            if (delta < R) {  // ac.py:139-142
+                const int sh = bits - (63 - __builtin_clzll(delta));
+                low <<= sh;
+                high = (high << sh) | lowmask(sh);
+                max_bit += sh;
+                delta = high - low + 1;
+            }
+            const uint64_t el = (rl * delta + R - 1) >> bits, eh = (rh * delta) >> bits;  // ac.py:146-147
+            high = low + eh;
+            low = low + el;
+            if (high >> (max_bit + 1)) { e = 1; break; }  // ac.py:116
+            const uint64_t x = low ^ high;                  // ac.py:111-128
+            const int hb = x ? 63 - __builtin_clzll(x) : -1;
+            const int nf = max_bit - hb;
+            if (nf > 0) {
+                bo.put_msb_first(low >> (hb + 1), nf);
+                low &= lowmask(hb + 1);
+                high &= lowmask(hb + 1);
+                max_bit = hb;
+            }
+            if (max_bit > 61) { e = 3; break; }  // ac.py:157
         }
-        if (max_bit > 61) { e = 3; break; }  // ac.py:157
     }
     if (!e) {
         bo.put_msb_first(low, max_bit + 1);  // flush (ac.py:160-167)
@@ -187,9 +204,10 @@ __global__ __launch_bounds__(64) void ac_decode_kernel(
     const uint8_t* __restrict__ data, int64_t stride, const int64_t* __restrict__ nbytes,
     int64_t* __restrict__ state, const int32_t* __restrict__ cdf, int K, int card, int bits,
     int64_t* __restrict__ codes, int64_t c_s, int64_t c_k, int64_t c_t, int64_t t,
-    int64_t* __restrict__ next_idx, int* __restrict__ err) {
+    const int64_t* __restrict__ dstep, int64_t* __restrict__ next_idx, int* __restrict__ err) {
     const int s = blockIdx.x, lane = threadIdx.x;
     if (err[s]) return;  // the stream already failed; later steps leave it as it is
+    if (dstep) t += *dstep;
     int64_t* stt = state + (int64_t)s * 5;
     uint64_t low = (uint64_t)stt[0], high = (uint64_t)stt[1], cur = (uint64_t)stt[2];
     int max_bit = (int)stt[3];
@@ -203,7 +221,17 @@ __global__ __launch_bounds__(64) void ac_decode_kernel(
         if (delta < R) {  // ac.py:226-233
             const int sh = bits - (63 - __builtin_clzll(delta));
             if (pos + sh > nbits) { e = 1; break; }  // BitUnpacker ran dry: pull returns None
-            for (int i = 0; i < sh; ++i, ++pos) cur = (cur << 1) | ((src[pos >> 3] >> (pos & 7)) & 1);
+            // the sh (<= 31) stream bits from `pos` span at most 5 bytes: load them together
+            const int64_t b0 = pos >> 3, last = (nbits >> 3) - 1;
+            uint64_t win = 0;
+#pragma unroll
+            for (int u = 0; u < 5; ++u) {
+                const int64_t bi = b0 + u <= last ? b0 + u : last;
+                win |= (uint64_t)src[bi] << (8 * u);
+            }
+            const uint64_t chunk = (win >> (pos & 7)) & lowmask(sh);   // stream bit pos at bit 0
+            cur = (cur << sh) | (__builtin_bitreverse64(chunk) >> (64 - sh));
+            pos += sh;
             low <<= sh;
             high = (high << sh) | lowmask(sh);
             max_bit += sh;
@@ -212,14 +240,25 @@ __global__ __launch_bounds__(64) void ac_decode_kernel(
         const int32_t* row = cdf + ((int64_t)s * K + k) * card;
         const uint64_t off = cur - low;
         int found = -1;
-        for (int j = lane; j < card; j += 64) {
-            const int32_t cl = j ? row[j - 1] : 0, ch = row[j];
-            // an empty or negative interval (ch - 1 < cl, e.g. the zero cdf ac.py:288 pulls
-            // with) has effective_high < effective_low and can never hold `current`
-            if (cl < 0 || ch - 1 < cl) continue;
-            const uint64_t rl = (uint64_t)cl, rh = (uint64_t)(ch - 1);
-            const uint64_t el = (rl * delta + R - 1) >> bits, eh = (rh * delta) >> bits;
-            if (off >= el && off <= eh) found = j;
+        for (int j0 = 0; j0 < card; j0 += 64 * 16) {   // 16 entries per lane in flight together
+            int32_t cl[16], ch[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int j = j0 + lane + 64 * u;
+                const int jc = j < card ? j : card - 1;
+                ch[u] = row[jc];
+                cl[u] = jc > 0 ? row[jc - 1] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int j = j0 + lane + 64 * u;
+                // an empty or negative interval (ch - 1 < cl, e.g. the zero cdf ac.py:288 pulls
+                // with) has effective_high < effective_low and can never hold `current`
+                if (j >= card || cl[u] < 0 || ch[u] - 1 < cl[u]) continue;
+                const uint64_t rl = (uint64_t)cl[u], rh = (uint64_t)(ch[u] - 1);
+                const uint64_t el = (rl * delta + R - 1) >> bits, eh = (rh * delta) >> bits;
+                if (off >= el && off <= eh) found = j;
+            }
         }
         const uint64_t hit = __ballot(found >= 0);
         if (!hit) { e = 2; break; }  // ac.py:238 "Binary search failed"
@@ -333,14 +372,15 @@ int encx_ac_encode(const int32_t* lohi, int64_t streams, int64_t n, int total_ra
 
 int encx_ac_decode(const uint8_t* data, int64_t stride, const int64_t* nbytes, int64_t streams, int64_t* state,
                    const int32_t* cdf, int64_t K, int64_t card, int total_range_bits, int64_t* codes, int64_t c_s,
-                   int64_t c_k, int64_t c_t, int64_t t, int64_t* next_idx, int* err, encx_stream_t stream) {
+                   int64_t c_k, int64_t c_t, int64_t t, const int64_t* dev_step, int64_t* next_idx, int* err,
+                   encx_stream_t stream) {
     ENCX_REQUIRE(streams >= 0 && K >= 1 && card >= 1 && card <= INT32_MAX && total_range_bits >= 1 &&
                  total_range_bits <= 30);
     if (streams == 0) return 0;
     ENCX_REQUIRE(data && nbytes && state && cdf && err && streams <= INT32_MAX && K <= INT32_MAX);
     hipLaunchKernelGGL(ac_decode_kernel, dim3((unsigned)streams), dim3(64), 0, (hipStream_t)stream, data, stride,
-                       nbytes, state, cdf, (int)K, (int)card, total_range_bits, codes, c_s, c_k, c_t, t, next_idx,
-                       err);
+                       nbytes, state, cdf, (int)K, (int)card, total_range_bits, codes, c_s, c_k, c_t, t, dev_step,
+                       next_idx, err);
     ENCX_CHECK_LAUNCH();
     return 0;
 }

@@ -127,7 +127,7 @@ class ArithmeticDecoder:
         self._err.zero_()
         call('encx_ac_decode', self._buf.data_ptr(), self._buf.numel(), self._nbytes.data_ptr(), 1,
              self._state.data_ptr(), cdf.data_ptr(), 1, cdf.numel(), self.total_range_bits,
-             self._sym.data_ptr(), 0, 0, 0, 0, None, self._err.data_ptr(), stream())
+             self._sym.data_ptr(), 0, 0, 0, 0, None, None, self._err.data_ptr(), stream())
         e = int(self._err.item())
         used = (int(self._state[0, 4].item()) + 7) // 8
         if hasattr(self.fo, 'seek'):

@@ -121,23 +121,27 @@ class LMModel(nn.Module):
         return LMState(B, len(tr.layers), self.dim, max(int(capacity), 2), self._emb.device)
 
     # ------------------------------------------------------------------ core
-    def _body(self, idx, strides, B, K, T, shifted, state: LMState):
-        """input + transformer over rows [B][T] continuing `state` -> x [B*T][dim]."""
+    def _body(self, idx, strides, B, K, T, shifted, state: LMState, dev_step=None):
+        """input + transformer over rows [B][T] continuing `state` -> x [B*T][dim]. With
+        dev_step (an int64 device counter) the step offset is read on the device and the host
+        offset stays put (a graph-captured decode step; the caller reserved the cache)."""
         tr = self.transformer
         D, Fh = self.dim, tr.hidden
         dev = self._emb.device
         st = stream()
-        state.reserve(state.offset + T + 1)
+        dptr = dev_step.data_ptr() if dev_step is not None else None
+        if dev_step is None:
+            state.reserve(state.offset + T + 1)
         x = torch.empty(B * T, D, device=dev)
         call('encx_lm_input', idx.data_ptr(), strides[0], strides[1], strides[2], B, K, T, int(shifted),
              self._emb.data_ptr(), self.card + 1, D, tr.norm_in.weight.data_ptr(), tr.norm_in.bias.data_ptr(),
-             state.offset, float(tr.max_period), x.data_ptr(), st)
+             state.offset, dptr, float(tr.max_period), x.data_ptr(), st)
         work = torch.empty((int(lib.encx_lm_layer_workspace(B * T, D, Fh)) + 3) // 4, device=dev)
         for i, layer in enumerate(tr.layers):
             y = torch.empty_like(x)
             a = layer.self_attn
             call('encx_lm_layer', x.data_ptr(), y.data_ptr(), B, T, state.kv[i].data_ptr(), state.capacity,
-                 state.offset + 1, tr.past_context, D, tr.num_heads, Fh,
+                 state.offset + 1, dptr, tr.past_context, D, tr.num_heads, Fh,
                  a.in_proj_weight.data_ptr(), a.in_proj_bias.data_ptr(),
                  a.out_proj.weight.data_ptr(), a.out_proj.bias.data_ptr(),
                  layer.linear1.weight.data_ptr(), layer.linear1.bias.data_ptr(),
@@ -145,7 +149,8 @@ class LMModel(nn.Module):
                  layer.norm1.weight.data_ptr(), layer.norm1.bias.data_ptr(),
                  layer.norm2.weight.data_ptr(), layer.norm2.bias.data_ptr(), work.data_ptr(), st)
             x = y
-        state.offset += T
+        if dev_step is None:
+            state.offset += T
         return x
 
     def _heads(self, x, B, T, K, probas=None, cdf=None, sym=None, lohi=None, err=None):
@@ -218,10 +223,15 @@ class LMModel(nn.Module):
         return [host[b, :nb[b]].numpy().tobytes() for b in range(B)]
 
     @torch.no_grad()
-    def decode_streams(self, datas: tp.Sequence[bytes], K: int, T: int):
+    def decode_streams(self, datas: tp.Sequence[bytes], K: int, T: int, graph: bool = True):
         """compress.py:128-155 (use_lm=True) for B streams of K codebooks x T steps: ->
         (codes int64 [B, K, T] on the GPU, bytes consumed per stream). Raises EOFError where
-        the reference's decoder runs dry, RuntimeError where its binary search fails."""
+        the reference's decoder runs dry, RuntimeError where its binary search fails.
+
+        One step = LM input, 5 layers, heads + cdf, arithmetic decode of the K codes (whose
+        + 1 is the next step's input, compress.py:154-155). With graph=True the step's ~40
+        launches are captured once into a HIP graph (offsets from a device-side step counter)
+        and replayed T times, with one host sync at the end."""
         self._packed()
         self._check_device()
         if K > self.n_q:
@@ -242,13 +252,28 @@ class LMModel(nn.Module):
         idx = torch.zeros(B, K, dtype=torch.int64, device=dev)      # step input, 0 at t = 0
         cdf = torch.empty(B, 1, K, self.card, device=dev, dtype=torch.int32)
         state = self.new_state(B, T + 1)
-        st = stream()
-        for t in range(T):
-            x = self._body(idx, (K, 1, 1), B, K, 1, False, state)
+        step = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        def one_step(t, dstep):
+            st = stream()
+            x = self._body(idx, (K, 1, 1), B, K, 1, False, state, dev_step=dstep)
             self._heads(x, B, 1, K, cdf=cdf)
             call('encx_ac_decode', data.data_ptr(), stride, nbytes.data_ptr(), B, dstate.data_ptr(),
                  cdf.data_ptr(), K, self.card, TOTAL_RANGE_BITS, codes.data_ptr(), K * T, T, 1, t,
-                 idx.data_ptr(), err.data_ptr(), st)
+                 dstep.data_ptr() if dstep is not None else None, idx.data_ptr(), err.data_ptr(), st)
+            if dstep is not None:
+                call('encx_lm_step_advance', dstep.data_ptr(), 1, st)
+
+        if graph and T > 2:
+            one_step(0, step)                    # eager first step (loads every kernel)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                one_step(0, step)
+            for _ in range(T - 1):
+                g.replay()
+        else:
+            for t in range(T):
+                one_step(t, None)
         e = err.cpu().tolist()
         if any(v == 1 for v in e):
             raise EOFError("The stream ended sooner than expected.")

@@ -418,16 +418,17 @@ int encx_crop_collate(const float* pool, const int64_t* offsets, const int64_t* 
  * known code sequence, 0 at t = 0 and codes[b][k][t-1] + 1 after (compress.py:74-79). */
 int encx_lm_input(const int64_t* idx, int64_t s_b, int64_t s_k, int64_t s_t, int64_t B, int64_t K,
                   int64_t T, int shifted, const float* emb, int64_t card1, int64_t D, const float* ln_w,
-                  const float* ln_b, int64_t offset, float max_period, float* x, encx_stream_t stream);
+                  const float* ln_b, int64_t offset, const int64_t* dev_step, float max_period, float* x,
+                  encx_stream_t stream);
 /* One StreamingTransformerEncoderLayer (transformer.py:30-59; nn.TransformerEncoderLayer with
  * norm_first=False, GELU, dropout 0): x [B][T][D] -> y. kv [B][L][2D] is the layer's key |
- * value cache, position s = seq0 + t for row t (seq0 = offset + 1); position 0 is the zero
- * state every layer starts with (transformer.py:106), written when seq0 == 1. Row t attends
+ * value cache, position s = seq0 + t for row t (seq0 = offset + 1); position 0, the zero state
+ * every layer starts with (transformer.py:106), is read from the in_proj bias. Row t attends
  * positions [max(0, s - past_context), s] (transformer.py:52-58, 117-118). Weights in
  * nn.MultiheadAttention / nn.Linear layout; work: encx_lm_layer_workspace(B*T, D, F) bytes. */
 int64_t encx_lm_layer_workspace(int64_t N, int64_t D, int64_t F);
 int encx_lm_layer(const float* x, float* y, int64_t B, int64_t T, float* kv, int64_t L, int64_t seq0,
-                  int64_t past_context, int64_t D, int64_t heads, int64_t F, const float* in_w,
+                  const int64_t* dev_step, int64_t past_context, int64_t D, int64_t heads, int64_t F, const float* in_w,
                   const float* in_b, const float* out_w, const float* out_b, const float* l1_w,
                   const float* l1_b, const float* l2_w, const float* l2_b, const float* n1_w,
                   const float* n1_b, const float* n2_w, const float* n2_b, float* work,
@@ -471,7 +472,12 @@ int encx_ac_encode(const int32_t* lohi, int64_t streams, int64_t n, int total_ra
  * untouched by later calls. Bytes consumed = ceil(bits consumed / 8). */
 int encx_ac_decode(const uint8_t* data, int64_t stride, const int64_t* nbytes, int64_t streams, int64_t* state,
                    const int32_t* cdf, int64_t K, int64_t card, int total_range_bits, int64_t* codes, int64_t c_s,
-                   int64_t c_k, int64_t c_t, int64_t t, int64_t* next_idx, int* err, encx_stream_t stream);
+                   int64_t c_k, int64_t c_t, int64_t t, const int64_t* dev_step, int64_t* next_idx, int* err,
+                   encx_stream_t stream);
+/* *dev_step += by on the stream. encx_lm_input / encx_lm_layer / encx_ac_decode add *dev_step
+ * (nullable) to their offset / seq0 / t, so one captured decode step (a hipGraph) replays for
+ * every step; the caller guarantees seq0 + *dev_step + T <= L. */
+int encx_lm_step_advance(int64_t* dev_step, int64_t by, encx_stream_t stream);
 
 #ifdef __cplusplus
 }

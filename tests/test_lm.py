@@ -188,9 +188,11 @@ def test_gpu_lm_coder_round_trip_and_oracle_bytes():
     codes[1] = codes[0]                     # two identical streams code identically
     datas = lm.encode_streams(codes)
     assert datas[0] == datas[1] and datas[0] != datas[2]
-    back, used = lm.decode_streams(datas, K, Tn)
+    back, used = lm.decode_streams(datas, K, Tn)              # HIP-graph replayed steps
     assert torch.equal(back, codes)
     assert used == [len(x) for x in datas]
+    back_e, used_e = lm.decode_streams(datas, K, Tn, graph=False)   # eager steps
+    assert torch.equal(back_e, codes) and used_e == used
     # the integer path against the oracle, on the GPU's own probabilities
     full = torch.zeros_like(codes)
     full[:, :, 1:] = codes[:, :, :-1] + 1
