@@ -55,7 +55,7 @@ def test_lm_host_checks():
     assert lib.encx_lm_layer_workspace(10, 200, 800) == 10 * (5 * 200 + 800) * 4
     # argument validation happens before any device call
     assert lib.encx_ac_cdf(None, 1, 1024, 1024, 10, 1e-8, 2, None, None, None) == 9001   # alpha > 1
-    assert lib.encx_lm_layer(*([None] * 2 + [1, 1, None, 4, 0, 0, 200, 7, 800] + [None] * 14)) == 9001
+    assert lib.encx_lm_layer(*([None] * 2 + [1, 1, None, 4, 0, None, 0, 200, 7, 800] + [None] * 14)) == 9001
     lm = LMModel(4, 64, dim=64, num_heads=4, num_layers=1)
     with pytest.raises(RuntimeError, match='no CPU fallback'):
         lm(torch.zeros(1, 4, 1, dtype=torch.long))
