@@ -251,3 +251,51 @@ def test_gpu_compress_use_lm_fixture():
     p, _, _ = lm(full)
     np.testing.assert_allclose(p[0].permute(2, 1, 0).reshape(-1, cfg.card).cpu().numpy(), d['e2e_pdf'],
                                rtol=2e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_compress_use_lm_48k_segments():
+    """48 kHz stereo, normalised, 0.1 s segments (the g9/g10 model, n_q 2), use_lm=True: every
+    segment is its own scale + arithmetic coded stream (compress.py:67-89) and the decoder stops
+    where the reference's does, so the next segment's scale is read from the right offset; the
+    decoded wave equals the use_lm=False one bit for bit. Two segments hit the reference's
+    short-last-segment quirk (every segment decoded with the first's frame count,
+    compress.py:126): the decoder runs dry -> EOFError, as for use_lm=False."""
+    from test_ecdc import _model48
+    from encx import compress as C
+    from encx.lm import LMModel
+    from oracle.lm_oracle import LMConfig, lm_param_shapes
+    from synth import synth_lm_state
+    m = _model48()
+    cfg = LMConfig(n_q=m.quantizer.n_q, past_context=int(3.5 * m.frame_rate))
+    lm = LMModel(cfg.n_q, 1024, dim=200, num_layers=5, past_context=cfg.past_context)
+    lm.load_state_dict({k: T(v) for k, v in synth_lm_state(lm_param_shapes(cfg), 131).items()})
+    m.set_lm_model(lm.to(DEV).eval())
+    d = load('g10_ecdc.npz')
+    w = T(d['c48_x'])
+    one = C.compress(m, w[:, :4752], use_lm=True)
+    y_lm, _ = C.decompress(m, one)
+    y_plain, _ = C.decompress(m, C.compress(m, w[:, :4752], use_lm=False))
+    assert torch.equal(y_lm, y_plain)
+    two = C.compress(m, w, use_lm=True)
+    with pytest.raises(EOFError):
+        C.decompress(m, two)
+    # the same two segments, each decoded with its own length: the first stream ends exactly
+    # where the second segment's scale begins
+    import io as _io
+    from encx import binary
+    fo = _io.BytesIO(two)
+    meta = binary.read_ecdc_header(fo)
+    K = meta['nc']
+    lengths = [f.shape[-1] for f, _ in m.encode(w[None].to(DEV))]
+    codes = []
+    for Tn in lengths:
+        fo.read(4)                                   # the segment's '!f' scale
+        start = fo.tell()
+        c, used = lm.decode_streams([fo.read()], K, Tn)
+        fo.seek(start + used[0])
+        codes.append(c)
+    assert fo.tell() == len(two)
+    ref = [f for f, _ in m.encode(w[None].to(DEV))]
+    for a, b in zip(codes, ref):
+        assert torch.equal(a, b)
