@@ -803,9 +803,11 @@ ENCX_DEV float feat_term(const C2Dg& a, float c, int64_t o) {
 }
 
 // dx element o (+ masks / feature term) for the epilogues below
+// (the grad of the input map is completed by the feature term first; xact then turns it into
+// the grad of the input's pre-activation, so the producing layer reads dy without its mask)
 ENCX_DEV float dg_out(const C2Dg& a, float fc, int64_t o, float v) {
-    if (a.xact) v *= lrelu_grad(a.xact[o]);
     if (a.ffr) v += feat_term(a, fc, o);
+    if (a.xact) v *= lrelu_grad(a.xact[o]);
     return a.accumulate ? a.dx[o] + v : v;
 }
 typedef float f32x2u __attribute__((ext_vector_type(2), aligned(4)));
@@ -884,7 +886,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
                     const bool ok = rq[q] < nrows && pos >= 0 && pos < g.Fo;
                     const int o = ok ? e[q].x + wq[q] : 0;
                     const float t = dyb[o];
-                    ym[q] = ysrc[o];
+                    if (yab) ym[q] = ysrc[o];
                     v[q] = ok ? t : 0.f;
                 }
 #pragma unroll
@@ -965,8 +967,8 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
                 if (f < 0 || f >= g.Fi) continue;
                 const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
                 float v = acc[i][j][r];
-                if (a.xact) v *= lrelu_grad(a.xact[o]);
                 if (a.ffr) v += feat_term(a, feat_coef(a), o);
+                if (a.xact) v *= lrelu_grad(a.xact[o]);
                 a.dx[o] = a.accumulate ? a.dx[o] + v : v;
             }
         }
@@ -977,7 +979,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
 // (t, u), reduction (co, kt) pairs x JC taps; the staged B image is dy * LeakyReLU'(y), both
 // read as aligned quads (dy columns [base, base + RLp), base = the window start rounded down to
 // a multiple of 4) and masked in the commit.
-template <int TM, int BN, int JC, int MQ, int CKM, int OCC = 1>
+template <int TM, int BN, int JC, int MQ, int CKM, int OCC = 1, int DB = 0, bool YM = true>
 __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
     constexpr int BM = 32 * TM, TN = BN / 128, MW = (JC * CKM * BM / 4 + NT - 1) / NT;
     extern __shared__ float smem[];
@@ -985,9 +987,13 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
     const int CK = a.CK, NR = a.NR, RL = a.RL, U = a.U, S = g.sf;
     const int RLp = (RL + 3) & ~3, NQ = RLp >> 2;
     const int VC = g.Co * g.KT, XR = NR * RLp, M = g.Ci * S, WQ = JC * CK * BM / 4;
+    // DB: two LDS images; chunk i + 1 is committed into the idle one while chunk i is
+    // multiplied, so one barrier per chunk instead of two
     float* Xs = smem;                     // [CK][NR][RLp]
     float* As = smem + CK * XR;           // [CK][JC][BM]
-    int2* rtab = (int2*)(As + JC * CK * BM);  // [VC*NR]
+    float* Xs2 = As + JC * CK * BM;       // DB: second image
+    float* As2 = Xs2 + CK * XR;
+    int2* rtab = (int2*)(DB ? As2 + JC * CK * BM : Xs2);  // [VC*NR]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, l32 = lane & 31;
     const TileId tile = xcd_tile();
@@ -1014,7 +1020,7 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
     const int64_t plane = (int64_t)g.T2 * g.Fo;
     const float* dyb = a.dy + (int64_t)b * g.Co * plane;
-    const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane : dyb;
+    const float* yab = YM ? a.yact + (int64_t)b * g.Co * plane : dyb;
     const int64_t left = (int64_t)(g.B - b) * g.Co * plane;  // floats from dyb to the tensor end
     const float fc = feat_coef(a);
     for (int gr = tid; gr < VC * NR; gr += NT) {
@@ -1040,7 +1046,7 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
             int off = any ? e.x + 4 * q : 0;
             if (off > left - 4) off = (int)left - 4;
             xv[u] = ld4u(dyb + off);
-            yv[u] = ld4u(yab + off);
+            if (YM) yv[u] = ld4u(yab + off);
             const int sh = (any ? e.x + 4 * q : 0) - off;
             xmask[u] = any ? (min(g.Fo - col, 4) | (sh << 4)) : 0;
             xdst[u] = r < rows ? r * RLp + 4 * q : -1;
@@ -1061,9 +1067,7 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
             if (!ok) wv[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
         }
     };
-    fetch(0);
-    for (int c0 = 0; c0 < VC; c0 += CK) {
-        __syncthreads();
+    auto commit = [&](int c0, float* X, float* A) {
 #pragma unroll
         for (int u = 0; u < MQ; ++u) {
             const int m = xmask[u], nv = m & 15, sh = m >> 4;
@@ -1077,8 +1081,8 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = k < nv ? (a.yact ? v[k] * lrelu_grad(y[k]) : v[k]) : 0.f;
-            if (xdst[u] >= 0) *(f32x4*)(Xs + xdst[u]) = v;
+            for (int k = 0; k < 4; ++k) v[k] = k < nv ? (YM ? v[k] * lrelu_grad(y[k]) : v[k]) : 0.f;
+            if (xdst[u] >= 0) *(f32x4*)(X + xdst[u]) = v;
         }
 #pragma unroll
         for (int u = 0; u < MW; ++u) {
@@ -1086,14 +1090,42 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
             if (j < WQ && rr < (VC - c0) * JC && m0 + col + 3 >= M)
                 for (int k = 0; k < 4; ++k)
                     wv[u][k] = m0 + col + k < M ? a.wp[((int64_t)c0 * JC + rr) * M + m0 + col + k] : 0.f;
-            if (j < WQ) *(f32x4*)(As + rr * BM + col) = wv[u];
+            if (j < WQ) *(f32x4*)(A + rr * BM + col) = wv[u];
         }
-        __syncthreads();
-        if (c0 + CK < VC) fetch(c0 + CK);
+    };
+    auto compute = [&](const float* X, const float* A) {
+        if (DB & 2) {  // operands of the next k-pair group read before this group's MFMAs
+            float ca[TM], cb[TN], na[TM], nb[TN];
+            auto rd = [&](int cp, int q, float* va, float* vb) {
+                const float* aq = A + (cp + h) * JC * BM + l32;
+                const float* xq = X + (cp + h) * XR;
+#pragma unroll
+                for (int i = 0; i < TM; ++i) va[i] = aq[q * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) vb[j] = xq[boff[j] - q];
+            };
+            rd(0, 0, ca, cb);
+            for (int cp = 0; cp < CK; cp += 2) {
+#pragma unroll
+                for (int q = 0; q < JC; ++q) {
+                    if (q + 1 < JC) rd(cp, q + 1, na, nb);
+                    else if (cp + 2 < CK) rd(cp + 2, 0, na, nb);
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(ca[i], cb[j], acc[i][j]);
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) ca[i] = na[i];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) cb[j] = nb[j];
+                }
+            }
+            return;
+        }
 #pragma unroll 2
         for (int cp = 0; cp < CK; cp += 2) {
-            const float* aq = As + (cp + h) * JC * BM + l32;
-            const float* xq = Xs + (cp + h) * XR;
+            const float* aq = A + (cp + h) * JC * BM + l32;
+            const float* xq = X + (cp + h) * XR;
 #pragma unroll
             for (int q = 0; q < JC; ++q) {
                 float av[TM], bv[TN];
@@ -1106,6 +1138,31 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
             }
+        }
+    };
+    fetch(0);
+    if (DB) {
+        commit(0, Xs, As);
+        if (CK < VC) fetch(CK);
+        __syncthreads();
+        int i = 0;
+        for (int c0 = 0; c0 < VC; c0 += CK, ++i) {
+            float* Xc = (i & 1) ? Xs2 : Xs;
+            float* Ac = (i & 1) ? As2 : As;
+            if (c0 + CK < VC) {  // the idle image was last read before the previous barrier
+                commit(c0 + CK, (i & 1) ? Xs : Xs2, (i & 1) ? As : As2);
+                if (c0 + 2 * CK < VC) fetch(c0 + 2 * CK);
+            }
+            compute(Xc, Ac);
+            __syncthreads();
+        }
+    } else {
+        for (int c0 = 0; c0 < VC; c0 += CK) {
+            __syncthreads();
+            commit(c0, Xs, As);
+            __syncthreads();
+            if (c0 + CK < VC) fetch(c0 + CK);
+            compute(Xs, As);
         }
     }
 #pragma unroll
@@ -1126,16 +1183,18 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
                     const int64_t o = (((int64_t)b * g.Ci + (m >> 1)) * g.T2 + tr) * g.Fi + f;
                     float v0 = acc[i][j][r], v1 = acc[i][j][r + 1];
                     if (f >= 0 && f + 1 < g.Fi) {
-                        if (a.xact) {
-                            const f32x2u t = *(const f32x2u*)(a.xact + o);
-                            v0 *= lrelu_grad(t[0]);
-                            v1 *= lrelu_grad(t[1]);
-                        }
+                        f32x2u xa;
                         if (a.ffr) {
                             const f32x2u x2 = *(const f32x2u*)(a.ffx + o), r2 = *(const f32x2u*)(a.ffr + o);
                             const float d0 = x2[0] - r2[0], d1 = x2[1] - r2[1];
                             v0 += d0 > 0.f ? fc : (d0 < 0.f ? -fc : 0.f);
                             v1 += d1 > 0.f ? fc : (d1 < 0.f ? -fc : 0.f);
+                            xa = x2;
+                        }
+                        if (a.xact) {
+                            if (!(a.ffr && a.ffx == a.xact)) xa = *(const f32x2u*)(a.xact + o);
+                            v0 *= lrelu_grad(xa[0]);
+                            v1 *= lrelu_grad(xa[1]);
                         }
                         if (a.accumulate) {
                             const f32x2u t = *(const f32x2u*)(a.dx + o);
@@ -1171,7 +1230,7 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
 // CI x 4 accumulators for 4 adjacent f and slides a 4+KF-1 window over its LDS row per tap;
 // the weights are wave-uniform (scalar loads).
 constexpr int DN_ROWS = 16, DN_COLS = 64, DN_FPT = 4, DN_CC = 8, DN_MAXHALO = 4;
-template <int CI, int KT, int KF>
+template <int CI, int KT, int KF, bool YM = true>
 __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
     constexpr int RC = (DN_COLS + KF - 1 + 3) & ~3;  // LDS row length (float4 aligned)
     constexpr int WIN4 = (DN_FPT + KF - 1 + 3) / 4;
@@ -1183,7 +1242,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
     const int tbase = t0 + g.pt - halo, fbase = f0 + g.pf - (KF - 1);
     const int64_t plane = (int64_t)g.T2 * g.Fo;
     const float* dyb = a.dy + (int64_t)b * g.Co * plane;
-    const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane : dyb;
+    const float* yab = YM ? a.yact + (int64_t)b * g.Co * plane : dyb;
     const int items = DN_CC * NRW * RC;
     float acc[CI][DN_FPT];
 #pragma unroll
@@ -1202,13 +1261,13 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
                 const bool ok = i < items && tr >= 0 && tr < g.T2 && fc >= 0 && fc < g.Fo;
                 const int64_t o = ok ? (int64_t)(c0 + cl) * plane + (int64_t)tr * g.Fo + fc : 0;
                 const float t = dyb[o];
-                ym[q] = yab[o];
+                if (YM) ym[q] = yab[o];
                 v[q] = ok ? t : 0.f;
             }
 #pragma unroll
             for (int q = 0; q < DPER; ++q) {
                 const int i = i0 + q * NT + tid;
-                if (i < items) Xs[i] = a.yact ? v[q] * lrelu_grad(ym[q]) : v[q];
+                if (i < items) Xs[i] = YM ? v[q] * lrelu_grad(ym[q]) : v[q];
             }
         }
         __syncthreads();
@@ -1248,8 +1307,8 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
             if (f >= g.Fi) continue;
             const int64_t o = (((int64_t)b * CI + c) * g.T2 + t) * g.Fi + f;
             float v = acc[c][e];
-            if (a.xact) v *= lrelu_grad(a.xact[o]);
             if (a.ffr) v += feat_term(a, feat_coef(a), o);
+            if (a.xact) v *= lrelu_grad(a.xact[o]);
             a.dx[o] = a.accumulate ? a.dx[o] + v : v;
         }
 }
@@ -1264,7 +1323,7 @@ struct C2Wg {
     int BT, NR, RL, NCmax, items, per_split, chunks;
 };
 
-template <int BM, int BN, int WM, int WN, int WK>
+template <int BM, int BN, int WM, int WN, int WK, bool YM = true>
 __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     static_assert(WM * WN * WK == 4, "4 waves");
@@ -1315,7 +1374,7 @@ __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
         const int tf = p0 / g.Fo, f0 = p0 - tf * g.Fo;
         const int nr = (pend - 1) / g.Fo - tf + 1;
         const float* dyb = a.dy + (int64_t)b * g.Co * plane_y;
-        const float* yab = a.yact ? a.yact + (int64_t)b * g.Co * plane_y : nullptr;
+        const float* yab = YM ? a.yact + (int64_t)b * g.Co * plane_y : nullptr;
         const float* xb = a.x + (int64_t)b * g.Ci * plane_x;
         __syncthreads();
         const float* ysrc = yab ? yab : dyb;
@@ -1328,7 +1387,7 @@ __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
                 const bool ok = i < BT * BM && p < pend && co < g.Co;
                 const int64_t o = ok ? (int64_t)co * plane_y + p : 0;
                 const float t = dyb[o];
-                ym[q] = ysrc[o];
+                if (YM) ym[q] = ysrc[o];
                 v[q] = ok ? t : 0.f;
             }
 #pragma unroll
@@ -1336,7 +1395,7 @@ __global__ __launch_bounds__(NT) void c2_wgrad_kernel(C2Wg a) {
                 const int i = i0 + q * NT + tid;
                 if (i < BT * BM) {
                     const int tl = i % BT, col = i / BT;
-                    Ls[tl * BM + col] = yab ? v[q] * lrelu_grad(ym[q]) : v[q];
+                    Ls[tl * BM + col] = YM ? v[q] * lrelu_grad(ym[q]) : v[q];
                 }
             }
         }
@@ -1611,8 +1670,10 @@ struct C2Wg3 {
     float* ws;  // [splits][Co][N], N = VC*KF + 1
     int NR, RL, GC, items, per_split, chunks;
 };
-template <int KF, int NTW, int NW, int MQ, int ML, int OCC = 1>
+template <int KF, int NTW, int NW, int MQ, int ML, int OCC = 1, int PF = 0, bool YM = true>
 __global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
+    // PF: the next chunk's global loads are issued before this chunk's MFMA loop (register
+    // pipelining, as c2_dgradr_kernel), so their latency hides under the 32 k-pairs
     constexpr int NTH = NW * 64, P = W3_P, LDA = 33, PQ = P / 4;
     extern __shared__ float smem[];
     const C2Geo g = a.g;
@@ -1652,16 +1713,16 @@ __global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
     const int dr = NTH / NQ, dq = NTH - dr * NQ, r_init = tid / NQ, q_init = tid - r_init * NQ;
     const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
     __syncthreads();
-    for (int it = it_beg; it < it_end; ++it) {
+    f32x4 dv[ML], yv[ML], xv[MQ];
+    int dmask[ML], xmask[MQ];
+    // ---- loads of chunk it: dy / y quads along positions, x window quads
+    auto load = [&](int it) {
         const int b = it / a.chunks, p0 = (it - b * a.chunks) * P;
         const int pend = min(Nall, p0 + P);
         const int tf = p0 / g.Fo, f0 = p0 - tf * g.Fo;
         const int nr = (pend - 1) / g.Fo - tf + 1;
         const int base0 = (f0 * S - g.pf) & ~3;
         const int64_t yb = (int64_t)b * g.Co * plane_y, xbo = (int64_t)b * g.Ci * plane_x;
-        // ---- loads: dy / y quads along positions, x window quads
-        f32x4 dv[ML], yv[ML], xv[MQ];
-        int dmask[ML], xmask[MQ];
 #pragma unroll
         for (int u = 0; u < ML; ++u) {
             const int i = u * NTH + tid, co = i / PQ, k = i - co * PQ, p = p0 + 4 * k;
@@ -1669,31 +1730,35 @@ __global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
             int64_t off = any ? yb + (int64_t)co * plane_y + p : 0;
             const int64_t offc = off > ytot - 4 ? ytot - 4 : off;
             dv[u] = ld4u(a.dy + offc);
-            yv[u] = ld4u((a.yact ? a.yact : a.dy) + offc);
+            if (YM) yv[u] = ld4u(a.yact + offc);
             dmask[u] = any ? (min(pend - p, 4) | ((int)(off - offc) << 4)) : 0;
         }
-        {
-            int r = r_init, q = q_init;
+        int r = r_init, q = q_init;
 #pragma unroll
-            for (int u = 0; u < MQ; ++u) {
-                const int rr = r < GC * NR ? r : 0;
-                const int4 e = rtab[rr];
-                const int base = e.z ? baseN : base0, col = base + 4 * q;
-                const int row = tf + e.y;
-                const bool any = r < GC * NR && e.w && e.z < nr && row >= 0 && row < g.T2 && col >= 0 && col < g.Fi;
-                int64_t off = any ? xbo + e.x + (int64_t)tf * g.Fi + col : 0;
-                const int64_t offc = off > xtot - 4 ? xtot - 4 : off;
-                xv[u] = ld4u(a.x + offc);
-                xmask[u] = any ? (min(g.Fi - col, 4) | ((int)(off - offc) << 4)) : 0;
-                q += dq;
-                r += dr;
-                if (q >= NQ) {
-                    q -= NQ;
-                    ++r;
-                }
+        for (int u = 0; u < MQ; ++u) {
+            const int rr = r < GC * NR ? r : 0;
+            const int4 e = rtab[rr];
+            const int base = e.z ? baseN : base0, col = base + 4 * q;
+            const int row = tf + e.y;
+            const bool any = r < GC * NR && e.w && e.z < nr && row >= 0 && row < g.T2 && col >= 0 && col < g.Fi;
+            int64_t off = any ? xbo + e.x + (int64_t)tf * g.Fi + col : 0;
+            const int64_t offc = off > xtot - 4 ? xtot - 4 : off;
+            xv[u] = ld4u(a.x + offc);
+            xmask[u] = any ? (min(g.Fi - col, 4) | ((int)(off - offc) << 4)) : 0;
+            q += dq;
+            r += dr;
+            if (q >= NQ) {
+                q -= NQ;
+                ++r;
             }
         }
-        __syncthreads();  // the previous chunk's MFMAs are done with Ls / Rs
+    };
+    // ---- LDS image of chunk it from the loaded registers
+    auto store = [&](int it) {
+        const int b = it / a.chunks, p0 = (it - b * a.chunks) * P;
+        const int pend = min(Nall, p0 + P);
+        const int tf = p0 / g.Fo, f0 = p0 - tf * g.Fo;
+        const int base0 = (f0 * S - g.pf) & ~3;
 #pragma unroll
         for (int u = 0; u < ML; ++u) {
             const int i = u * NTH + tid, co = i / PQ, k = i - co * PQ;
@@ -1710,29 +1775,27 @@ __global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
                 }
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    Ls[(4 * k + c) * LDA + co] = c < nv ? (a.yact ? v[c] * lrelu_grad(y[c]) : v[c]) : 0.f;
+                    Ls[(4 * k + c) * LDA + co] = c < nv ? (YM ? v[c] * lrelu_grad(y[c]) : v[c]) : 0.f;
             }
         }
-        {
-            int r = r_init, q = q_init;
+        int r = r_init, q = q_init;
 #pragma unroll
-            for (int u = 0; u < MQ; ++u) {
-                const int m = xmask[u], nv = m & 15, sh = m >> 4;
-                f32x4 v = xv[u];
-                if (sh) {
-                    const f32x4 t = v;
+        for (int u = 0; u < MQ; ++u) {
+            const int m = xmask[u], nv = m & 15, sh = m >> 4;
+            f32x4 v = xv[u];
+            if (sh) {
+                const f32x4 t = v;
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) v[c] = c + sh < 4 ? (c + sh == 1 ? t[1] : c + sh == 2 ? t[2] : t[3]) : 0.f;
-                }
+                for (int c = 0; c < 4; ++c) v[c] = c + sh < 4 ? (c + sh == 1 ? t[1] : c + sh == 2 ? t[2] : t[3]) : 0.f;
+            }
 #pragma unroll
-                for (int c = 0; c < 4; ++c) v[c] = c < nv ? v[c] : 0.f;
-                if (r < GC * NR) *(f32x4*)(Rs + r * RLp + 4 * q) = v;
-                q += dq;
-                r += dr;
-                if (q >= NQ) {
-                    q -= NQ;
-                    ++r;
-                }
+            for (int c = 0; c < 4; ++c) v[c] = c < nv ? v[c] : 0.f;
+            if (r < GC * NR) *(f32x4*)(Rs + r * RLp + 4 * q) = v;
+            q += dq;
+            r += dr;
+            if (q >= NQ) {
+                q -= NQ;
+                ++r;
             }
         }
         for (int tl = tid; tl < P; tl += NTH) {
@@ -1744,7 +1807,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
             }
             poff[tl] = off;
         }
+    };
+    if (PF && it_beg < it_end) load(it_beg);
+    for (int it = it_beg; it < it_end; ++it) {
+        if (!PF) load(it);
+        __syncthreads();  // the previous chunk's MFMAs are done with Ls / Rs
+        store(it);
         __syncthreads();
+        if (PF && it + 1 < it_end) load(it + 1);
 #pragma unroll 4
         for (int kp = 0; kp < P / 2; ++kp) {
             const int tl = 2 * kp + h;
@@ -2026,8 +2096,8 @@ __global__ __launch_bounds__(256) void c2_co1_dgrad(C2Dg a) {
         }
     }
     const int64_t i = (int64_t)bc * xplane + p;
-    if (a.xact) acc *= lrelu_grad(a.xact[i]);
     if (a.ffr) acc += feat_term(a, feat_coef(a), i);
+    if (a.xact) acc *= lrelu_grad(a.xact[i]);
     a.dx[i] = a.accumulate ? a.dx[i] + acc : acc;
 }
 
@@ -2203,7 +2273,7 @@ int run_fwdr(C2Fwd a, hipStream_t st) {
     return 0;
 }
 
-template <int TM, int BN, int JC, int MQ, int CKM, int OCC = 1>
+template <int TM, int BN, int JC, int MQ, int CKM, int OCC = 1, int DB = 0>
 int run_dgradr(C2Dg a, hipStream_t st) {
     a.J = (int)cdiv(a.g.KF, a.g.sf);
     a.U = (a.g.Fi - 1 + a.g.pf) / a.g.sf + 1;
@@ -2212,10 +2282,11 @@ int run_dgradr(C2Dg a, hipStream_t st) {
     a.CK = fwdq_ck(a.g.Co * a.g.KT, a.NR, a.RL, MQ, CKM);
     if (a.J != JC || a.CK < 2 || a.g.Fo < 4 || JC > 5 || a.g.Ci * a.g.sf > 32 * TM) return ENCX_EINVAL;
     const int RLp = (a.RL + 3) & ~3;
-    const size_t lds = ((size_t)a.CK * a.NR * RLp + (size_t)JC * a.CK * 32 * TM + (size_t)2 * a.g.Co * a.g.KT * a.NR) *
-                       sizeof(float);
+    const size_t lds = ((size_t)(DB ? 2 : 1) * ((size_t)a.CK * a.NR * RLp + (size_t)JC * a.CK * 32 * TM) +
+                        (size_t)2 * a.g.Co * a.g.KT * a.NR) * sizeof(float);
     dim3 grid((unsigned)cdiv((int64_t)a.g.T2 * a.U, BN), 1, (unsigned)a.g.B);
-    hipLaunchKernelGGL((c2_dgradr_kernel<TM, BN, JC, MQ, CKM, OCC>), grid, dim3(NT), lds, st, a);
+    if (a.yact) hipLaunchKernelGGL((c2_dgradr_kernel<TM, BN, JC, MQ, CKM, OCC, DB, true>), grid, dim3(NT), lds, st, a);
+    else hipLaunchKernelGGL((c2_dgradr_kernel<TM, BN, JC, MQ, CKM, OCC, DB, false>), grid, dim3(NT), lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
@@ -2289,14 +2360,21 @@ static bool wg3r_ok(const C2Geo& g) {
     const WgPlan3 q = plan_wg3r(g, 32, 512);
     return q.GC * q.NR * (((q.RL + 3) & ~3) >> 2) <= 4 * 9 * 64;
 }
-template <int KF, int NTW, int NW, int MQ, int ML, int OCC = 1>
+// the narrow first layer (Ci*KT <= 14 combos, 3x9 taps): all combos in one column group of
+// 2 or 4 waves (tools/mb/c2_mb: 1536 workgroups, 4 waves/SIMD cap; 1.5x the generic kernel)
+static bool wg3n_ok(const C2Geo& g) {
+    return g.KF == 9 && g.Ci * g.KT <= 14 && g.Co <= 32 && g.Fi >= 4 && g.pf <= 4;
+}
+static WgPlan3 plan_wg3n(const C2Geo& g) { return plan_wg3r(g, g.Ci * g.KT, 1536); }
+template <int KF, int NTW, int NW, int MQ, int ML, int OCC = 1, int PF = 0>
 int run_wgrad3(const C2Geo& g, const float* dy, const float* yact, const float* x, float* ws, const WgPlan3& p,
                hipStream_t st) {
     const int quads = p.GC * p.NR * (((p.RL + 3) & ~3) >> 2);
     if (quads > MQ * NW * 64 || 32 * (W3_P / 4) > ML * NW * 64 || g.Co > 32 || g.Fi < 4 || g.pf > 4) return ENCX_EINVAL;
     C2Wg3 a{g, dy, yact, x, ws, p.NR, p.RL, p.GC, p.items, p.per_split, p.chunks};
     dim3 grid((unsigned)cdiv(g.Ci * g.KT, p.GC), (unsigned)p.splits);
-    hipLaunchKernelGGL((c2_wgrad3_kernel<KF, NTW, NW, MQ, ML, OCC>), grid, dim3(NW * 64), p.lds, st, a);
+    if (yact) hipLaunchKernelGGL((c2_wgrad3_kernel<KF, NTW, NW, MQ, ML, OCC, PF, true>), grid, dim3(NW * 64), p.lds, st, a);
+    else hipLaunchKernelGGL((c2_wgrad3_kernel<KF, NTW, NW, MQ, ML, OCC, PF, false>), grid, dim3(NW * 64), p.lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
@@ -2453,8 +2531,10 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
     if (M <= 32 && KF == 3 && sf == 1 && run_dgradr<1, 256, 3, 6, 32>(a, st) == 0) return 0;
     if (sf == 1 && KT == 3 && KF == 9 && (Ci == 2 || Ci == 4) && Co % DN_CC == 0 && (KT - 1) * dt <= DN_MAXHALO) {
         dim3 grid((unsigned)cdiv(Fi, DN_COLS), (unsigned)cdiv(T2, DN_ROWS), (unsigned)B);
-        if (Ci == 2) hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((c2_dgrad_narrow<4, 3, 9>), grid, dim3(NT), 0, st, a);
+        if (Ci == 2 && yact) hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9, true>), grid, dim3(NT), 0, st, a);
+        else if (Ci == 2) hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9, false>), grid, dim3(NT), 0, st, a);
+        else if (yact) hipLaunchKernelGGL((c2_dgrad_narrow<4, 3, 9, true>), grid, dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((c2_dgrad_narrow<4, 3, 9, false>), grid, dim3(NT), 0, st, a);
         ENCX_CHECK_LAUNCH();
         return 0;
     }
@@ -2473,6 +2553,7 @@ size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64
     int splits = p.splits;
     if (wg3r_ok(g)) splits = max(splits, plan_wg3r(g, 32, wg3r_target(g)).splits);
     if (co1_ok(g)) splits = max(splits, plan_co1(g).splits);
+    if (wg3n_ok(g)) splits = max(splits, plan_wg3n(g).splits);
     return (size_t)splits * Co * (Ci * KT * KF + 1) * sizeof(float);
 }
 
@@ -2510,17 +2591,30 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
             return 0;
         }
     }
+    if (wg3n_ok(g)) {
+        const WgPlan3 q = plan_wg3n(g);
+        const int rc = Ci * KT <= 7 ? run_wgrad3<9, 1, 2, 2, 4, 4>(g, dy, yact, x, ws, q, st)
+                                    : run_wgrad3<9, 1, 4, 2, 2, 4>(g, dy, yact, x, ws, q, st);
+        if (rc == 0) {
+            hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, q.splits, (int)Co,
+                               N, dw, db, acc_w, acc_b);
+            ENCX_CHECK_LAUNCH();
+            return 0;
+        }
+    }
     WgPlan2 p = plan_wg2(g);
     C2Wg a{g, dy, yact, x, ws, p.BT, p.NR, p.RL, p.NCmax, p.items, p.per_split, p.chunks};
     const size_t lds = ((size_t)4 * p.NCmax * p.NR + (size_t)p.BT * 32 + (size_t)p.NCmax * p.NR * p.RL) * sizeof(float) +
                        p.BT * sizeof(int);
     if (p.narrow) {
         const size_t red = (size_t)4 * 16 * 64 * sizeof(float);  // all 4 waves' tiles
-        hipLaunchKernelGGL((c2_wgrad_kernel<32, 64, 1, 2, 2>), dim3((unsigned)cdiv(N, 64), (unsigned)cdiv(Co, 32), p.splits),
-                           dim3(NT), lds > red ? lds : red, st, a);
+        const dim3 grid((unsigned)cdiv(N, 64), (unsigned)cdiv(Co, 32), p.splits);
+        if (yact) hipLaunchKernelGGL((c2_wgrad_kernel<32, 64, 1, 2, 2, true>), grid, dim3(NT), lds > red ? lds : red, st, a);
+        else hipLaunchKernelGGL((c2_wgrad_kernel<32, 64, 1, 2, 2, false>), grid, dim3(NT), lds > red ? lds : red, st, a);
     } else {
-        hipLaunchKernelGGL((c2_wgrad_kernel<32, 128, 1, 4, 1>), dim3((unsigned)cdiv(N, 128), (unsigned)cdiv(Co, 32), p.splits),
-                           dim3(NT), lds, st, a);
+        const dim3 grid((unsigned)cdiv(N, 128), (unsigned)cdiv(Co, 32), p.splits);
+        if (yact) hipLaunchKernelGGL((c2_wgrad_kernel<32, 128, 1, 4, 1, true>), grid, dim3(NT), lds, st, a);
+        else hipLaunchKernelGGL((c2_wgrad_kernel<32, 128, 1, 4, 1, false>), grid, dim3(NT), lds, st, a);
     }
     ENCX_CHECK_LAUNCH();
     hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, p.splits, (int)Co, N,

@@ -9,11 +9,9 @@ namespace {
 
 constexpr int NT = 256;
 
-__global__ __launch_bounds__(NT) void wn_fwd_kernel(const float* v, const float* g, float* wf,
-                                                    float* wp, int A0, int A1, int K, int s,
-                                                    int J) {
-    __shared__ float red[16];
-    const int a0 = blockIdx.x, cols = A1 * K;
+ENCX_DEV void wn_fwd_row(const float* v, const float* g, float* wf, float* wp, int A0, int A1, int K, int s,
+                         int J, int a0, float* red) {
+    const int cols = A1 * K;
     const float* vr = v + (int64_t)a0 * cols;
     float scale = 1.f;
     if (g) {
@@ -37,10 +35,36 @@ __global__ __launch_bounds__(NT) void wn_fwd_kernel(const float* v, const float*
     }
 }
 
-__global__ __launch_bounds__(NT) void wn_bwd_kernel(const float* v, const float* g, const float* dw,
-                                                    float* dv, float* dg, int cols, int acc) {
+__global__ __launch_bounds__(NT) void wn_fwd_kernel(const float* v, const float* g, float* wf,
+                                                    float* wp, int A0, int A1, int K, int s,
+                                                    int J) {
     __shared__ float red[16];
-    const int r = blockIdx.x;
+    wn_fwd_row(v, g, wf, wp, A0, A1, K, s, J, blockIdx.x, red);
+}
+
+// layer of global row r: the last descriptor with row0 <= r (row0 ascending)
+template <typename D>
+ENCX_DEV int wn_find(const D* d, int n, int64_t r) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (d[mid].row0 <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(NT) void wn_fwd_batch_kernel(const encx_wn_fwd_desc* d, int n) {
+    __shared__ float red[16];
+    const int li = wn_find(d, n, blockIdx.x);
+    const encx_wn_fwd_desc e = d[li];
+    const int J = (int)((e.K + e.stride - 1) / e.stride);
+    wn_fwd_row(e.v, e.g, e.wf, e.wp, (int)e.A0, (int)e.A1, (int)e.K, (int)e.stride, J,
+               (int)(blockIdx.x - e.row0), red);
+}
+
+ENCX_DEV void wn_bwd_row(const float* v, const float* g, const float* dw, float* dv, float* dg, int cols, int acc,
+                         int r, float* red) {
     const float* vr = v + (int64_t)r * cols;
     const float* dr = dw + (int64_t)r * cols;
     float ss = 0.f, dot = 0.f;
@@ -60,6 +84,19 @@ __global__ __launch_bounds__(NT) void wn_bwd_kernel(const float* v, const float*
         float val = sc * (dr[i] - vr[i] * proj);  // (g/||v||)(dw - v * dot/||v||^2)
         o[i] = acc ? o[i] + val : val;
     }
+}
+
+__global__ __launch_bounds__(NT) void wn_bwd_kernel(const float* v, const float* g, const float* dw,
+                                                    float* dv, float* dg, int cols, int acc) {
+    __shared__ float red[16];
+    wn_bwd_row(v, g, dw, dv, dg, cols, acc, blockIdx.x, red);
+}
+
+__global__ __launch_bounds__(NT) void wn_bwd_batch_kernel(const encx_wn_bwd_desc* d, int n) {
+    __shared__ float red[16];
+    const int li = wn_find(d, n, blockIdx.x);
+    const encx_wn_bwd_desc e = d[li];
+    wn_bwd_row(e.v, e.g, e.dw, e.dv, e.dg, (int)e.cols, (int)e.accumulate, (int)(blockIdx.x - e.row0), red);
 }
 
 }  // namespace
@@ -83,6 +120,26 @@ int encx_weightnorm_bwd(const float* v, const float* g, const float* dw, float* 
     encx_prof_scope ps((hipStream_t)stream, 4.0 * rows * cols, 4.0 * rows * cols * (accumulate ? 4 : 3), "weightnorm_bwd", false);
     hipLaunchKernelGGL(wn_bwd_kernel, dim3(rows), dim3(NT), 0, (hipStream_t)stream, v, g, dw, dv,
                        dg, (int)cols, accumulate);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_weightnorm_fwd_batch(const encx_wn_fwd_desc* layers, int64_t n_layers, int64_t rows_total,
+                              encx_stream_t stream) {
+    ENCX_REQUIRE(layers && n_layers > 0 && rows_total > 0);
+    encx_prof_scope ps((hipStream_t)stream, 0.0, 0.0, "weightnorm_batch", false);
+    hipLaunchKernelGGL(wn_fwd_batch_kernel, dim3((unsigned)rows_total), dim3(NT), 0, (hipStream_t)stream, layers,
+                       (int)n_layers);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_weightnorm_bwd_batch(const encx_wn_bwd_desc* layers, int64_t n_layers, int64_t rows_total,
+                              encx_stream_t stream) {
+    ENCX_REQUIRE(layers && n_layers > 0 && rows_total > 0);
+    encx_prof_scope ps((hipStream_t)stream, 0.0, 0.0, "weightnorm_bwd_batch", false);
+    hipLaunchKernelGGL(wn_bwd_batch_kernel, dim3((unsigned)rows_total), dim3(NT), 0, (hipStream_t)stream, layers,
+                       (int)n_layers);
     ENCX_CHECK_LAUNCH();
     return 0;
 }

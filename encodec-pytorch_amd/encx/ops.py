@@ -3,6 +3,7 @@
 Each Function below replaces the device work of one reference module (file:line in the
 docstrings); the nn.Module mirrors in encx.modules / encx.quantization / encx.losses call these.
 """
+import contextlib
 import math
 
 import numpy as np
@@ -70,9 +71,136 @@ def convtr_geometry(T, K, s, causal, trim_right_ratio=1.0):
     return pl, (T - 1) * s + K - pl - pr
 
 
+# ---------------------------------------------------------------------------- batched weight norm
+class WnBatch:
+    """Weight norm (conv.py:25-34) of every layer of the models a Trainer steps, as ONE launch
+    per forward group and one per flushed backward set (encx_weightnorm_{fwd,bwd}_batch) instead
+    of a launch per layer.
+
+    Forward: inside `forward(group)` every weight prep (Conv1d / ConvTranspose1d / Conv2d) is
+    looked up by (parameter, layout); the group's batched launch at scope entry has already
+    written the current weights into the layer's persistent operand buffers. A layer met for the
+    first time is computed on its own into new persistent buffers and joins the group (its
+    descriptor table is rebuilt when the scope closes, so a HIP-graph capture of a later step
+    sees a stable table and stable pointers).
+    Backward: with `backward()` active, a layer whose grads go straight into flat-buffer grad
+    views writes its weight grad dw into a persistent per-layer buffer and is queued; flush()
+    (run by the decoder-bucket all-reduce hook and when the backward scope closes, on the
+    stream the step is launched / captured on) turns the queued dw into dv/dg in one launch.
+    Per row the arithmetic is the single-layer kernels'."""
+
+    FWD_FIELDS = 9  # encx_wn_fwd_desc: v, g, wf, wp, A0, A1, K, stride, row0 (8 bytes each)
+    BWD_FIELDS = 9  # encx_wn_bwd_desc: v, g, dw, dv, dg, rows, cols, row0, accumulate
+
+    def __init__(self):
+        self.groups = {}      # group -> {'entries': {key: entry}, 'desc': tensor|None, 'rows': int, 'dirty'}
+        self.active = None    # group whose forward scope is open
+        self.dw = {}          # id(v) -> persistent dw buffer
+        self.pending = []     # [(v, g)] queued for the batched backward
+        self.bwd_tables = {}  # tuple of ids -> (desc tensor, rows, keep-alive refs)
+        self.in_bwd = False
+
+    # ---- forward
+    @contextlib.contextmanager
+    def forward(self, group):
+        grp = self.groups.setdefault(group, {'entries': {}, 'desc': None, 'rows': 0, 'dirty': False})
+        if grp['desc'] is not None:
+            call('encx_weightnorm_fwd_batch', ptr(grp['desc']), len(grp['entries']), grp['rows'], stream())
+        global _WN
+        prev, _WN = _WN, self
+        self.active = grp
+        try:
+            yield
+        finally:
+            _WN = prev
+            self.active = None
+            if grp['dirty']:
+                self._build_fwd(grp)
+
+    def prep(self, v, g, A0, A1, K, s, want_f, want_p, like):
+        grp = self.active
+        key = (id(v), A0, A1, K, s, want_f, want_p)
+        e = grp['entries'].get(key)
+        if e is None:
+            J = -(-K // s)
+            wf = _f32(A1 * K * A0, like) if want_f else None
+            wp = _f32(A0 * J * A1 * s, like) if want_p else None
+            call('encx_weightnorm_fwd', ptr(v), ptr(g), ptr(wf), ptr(wp), A0, A1, K, s, stream())
+            e = grp['entries'][key] = (v, g, wf, wp, A0, A1, K, s)
+            grp['dirty'] = True
+        return e[2], e[3]
+
+    def _build_fwd(self, grp):
+        rows, tab = 0, []
+        for v, g, wf, wp, A0, A1, K, s in grp['entries'].values():
+            tab.append([v.data_ptr(), ptr(g) or 0, ptr(wf) or 0, ptr(wp) or 0, A0, A1, K, s, rows])
+            rows += A0
+        grp['desc'] = torch.tensor(np.array(tab, dtype=np.int64)).to(next(iter(grp['entries'].values()))[0].device)
+        grp['rows'], grp['dirty'] = rows, False
+
+    # ---- backward
+    @contextlib.contextmanager
+    def backward(self):
+        global _WNB
+        prev, _WNB = _WNB, self
+        self.in_bwd = True
+        try:
+            yield
+        finally:
+            _WNB = prev
+            self.in_bwd = False
+            self.flush()
+
+    def dw_buffer(self, v):
+        """-> (persistent dw buffer of v, accumulate). A layer met twice before a flush (the
+        discriminator's real and fake graphs share its weights) adds its second weight grad into
+        the queued one: the batched backward then runs once on the summed dw, which is the
+        order of the reference's autograd (grad of w summed over its uses, then weight norm)."""
+        b = self.dw.get(id(v))
+        if b is None:
+            b = self.dw[id(v)] = torch.empty(v.shape, device=v.device, dtype=torch.float32)
+        return b, any(p is v for p, _ in self.pending)
+
+    def queue(self, v, g):
+        if any(p is v for p, _ in self.pending):
+            return
+        self.pending.append((v, g))
+
+    def flush(self):
+        if not self.pending:
+            return
+        key = tuple(id(v) for v, _ in self.pending)
+        ent = self.bwd_tables.get(key)
+        if ent is None:
+            rows, tab = 0, []
+            for v, g in self.pending:
+                cols = v[0].numel()
+                tab.append([v.data_ptr(), g.data_ptr(), self.dw[id(v)].data_ptr(), v.grad.data_ptr(),
+                            g.grad.data_ptr(), v.shape[0], cols, rows, 1])
+                rows += v.shape[0]
+            desc = torch.tensor(np.array(tab, dtype=np.int64)).to(self.pending[0][0].device)
+            ent = self.bwd_tables[key] = (desc, rows, [(v, g, v.grad, g.grad) for v, g in self.pending])
+        else:
+            for (v, g), (v0, g0, vg, gg) in zip(self.pending, ent[2]):
+                if v.grad is not vg or g.grad is not gg:
+                    raise RuntimeError('encx: a flat grad view moved; rebuild the WnBatch')
+        call('encx_weightnorm_bwd_batch', ptr(ent[0]), len(self.pending), ent[1], stream())
+        self.pending = []
+
+
+_WN = None   # WnBatch with an open forward scope
+_WNB = None  # WnBatch collecting weight-norm backwards
+
+
+def _wn_fwd(v, g, wf_or_none, wp_or_none, A0, A1, K, s):
+    call('encx_weightnorm_fwd', ptr(v), ptr(g), ptr(wf_or_none), ptr(wp_or_none), A0, A1, K, s, stream())
+
+
 def _weight_prep(v, g, K, s, want_f, want_p):
     """w = v*(g/||v||) (weight_norm, conv.py:25-34) written in the kernels' operand layouts."""
     A0, A1 = v.shape[0], v.shape[1]
+    if _WN is not None:
+        return _WN.prep(v, g, A0, A1, K, s, want_f, want_p, v)
     J = -(-K // s)
     wf = _f32(A1 * K * A0, v) if want_f else None
     wp = _f32(A0 * J * A1 * s, v) if want_p else None
@@ -94,6 +222,14 @@ def _direct(p):
     return p is None or (getattr(p, '_encx_flat', False) and p.grad is not None)
 
 
+def _dw_buffer(v, g, b, shape, like):
+    """Weight-grad output of a conv backward -> (buffer, accumulate): the WnBatch's persistent
+    per-layer buffer when a batched weight-norm backward will consume it, else a fresh tensor."""
+    if _WNB is not None and g is not None and _direct(v) and _direct(g) and _direct(b):
+        return _WNB.dw_buffer(v)
+    return torch.empty(shape, device=like.device, dtype=torch.float32), 0
+
+
 def _param_grads(v, g, b, dw, bias_src, Bn, C, T):
     """dw (natural layout) + the bias-grad source -> grads of (v, g, b). For parameters that
     live in a FlatAdam buffer the kernels accumulate straight into the (pre-zeroed) flat grad
@@ -102,6 +238,8 @@ def _param_grads(v, g, b, dw, bias_src, Bn, C, T):
     if _direct(v) and _direct(g) and _direct(b):
         if g is None:
             call('encx_axpby', ptr(dw), ptr(v.grad), dw.numel(), 1.0, None, 1.0, st)
+        elif _WNB is not None and dw is _WNB.dw.get(id(v)):
+            _WNB.queue(v, g)  # dv/dg in the batched launch (a second use of v added into dw)
         else:
             call('encx_weightnorm_bwd', ptr(v), ptr(g), ptr(dw), ptr(v.grad), ptr(g.grad),
                  v.shape[0], v[0].numel(), 1, st)
@@ -177,7 +315,7 @@ class Conv1dFn(torch.autograd.Function):
             if park:
                 link.grad, dx = dx, None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
-            dw = torch.empty(Cout, Cin, K, device=x.device, dtype=torch.float32)
+            dw, acc_w = _dw_buffer(v, g, b, (Cout, Cin, K), x)
             ws = _f32(lib.encx_conv1d_bwd_weight_workspace(B, Cin, Cout, tout, K) // 4 + 1, x)
             # the bias grad comes out of the same launch (the GEMM's ones column): straight into
             # the flat grad view (accumulate) or into a fresh tensor
@@ -187,7 +325,7 @@ class Conv1dFn(torch.autograd.Function):
                 db = torch.empty(Cout, device=x.device, dtype=torch.float32)
             dbp = ptr(b.grad) if direct_b else ptr(db)
             call('encx_conv1d_bwd_weight_bias', ptr(dy), ptr(x), ptr(dw), dbp, ptr(ws), B, Cin, T,
-                 Cout, tout, K, s, d, pl, e, mode, act, 0, int(direct_b), st)
+                 Cout, tout, K, s, d, pl, e, mode, act, acc_w, int(direct_b), st)
             dv, dg, _ = _param_grads(v, g, None, dw, dy, B, Cout, tout)
             if direct_b and dv is not None:
                 raise RuntimeError('encx: bias grad went to the flat view but the weight grads did not')
@@ -247,10 +385,10 @@ class ConvTr1dFn(torch.autograd.Function):
             call('encx_convtr1d_bwd_data', ptr(dy), ptr(wf), ptr(x), ptr(dx), ptr(ws), B, Cin, T,
                  Cout, tout, K, s, trim_left, act, 0, st)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
-            dw = torch.empty(Cin, Cout, K, device=x.device, dtype=torch.float32)
+            dw, acc_w = _dw_buffer(v, g, b, (Cin, Cout, K), x)
             ws = _f32(lib.encx_convtr1d_bwd_weight_workspace(B, Cin, Cout, T, K) // 4 + 1, x)
             call('encx_convtr1d_bwd_weight', ptr(x), ptr(dy), ptr(dw), None, ptr(ws), B, Cin, T,
-                 Cout, tout, K, s, trim_left, act, 0, st)
+                 Cout, tout, K, s, trim_left, act, acc_w, st)
             dv, dg, db = _param_grads(v, g, b, dw, dy, B, Cout, tout)
         return dx, dv, dg, db, None, None, None, None, None, None
 
@@ -607,8 +745,13 @@ class DiscGradMode:
     discriminator phase w.r.t. its weights only (input=False: no gradient into the
     spectrogram, as the reference's disc(output.detach()), train_multi_gpu.py:114-116)."""
 
-    def __init__(self, params=True, input=True):
+    def __init__(self, params=True, input=True, premask=False):
         self.params, self.input = params, input
+        # premask: the graph's owner guarantees that the feature maps are read only by the next
+        # Conv2d and by FeatFn (no other autograd consumer). Each Conv2d then hands its input's
+        # producer the grad of that producer's pre-activation (the LeakyReLU' mask applied in the
+        # bwd-data epilogue), so the producer's bwd-data and bwd-weight never read its output map.
+        self.premask = premask
 
     def set(self, params, input):
         self.params, self.input = params, input
@@ -636,7 +779,7 @@ class Conv2dFn(torch.autograd.Function):
     the layer that reads the spectrogram (first=True)."""
 
     @staticmethod
-    def forward(ctx, x, v, g, b, geo, act, mode=_ALL_GRADS, first=False, feat_slot=None):
+    def forward(ctx, x, v, g, b, geo, act, mode=_ALL_GRADS, first=False, feat_slot=None, out_slot=None):
         _check(x)
         x = x.contiguous()
         B, Ci, T2, Fi = x.shape
@@ -645,8 +788,11 @@ class Conv2dFn(torch.autograd.Function):
         st = stream()
         ent = mode.cache.get(id(v)) if mode.reuse else None
         if ent is None:
-            wf = _f32(Co * Ci * KT * KF, x)
-            call('encx_weightnorm_fwd', ptr(v), ptr(g), ptr(wf), None, Co, Ci * KT, KF, 1, st)
+            if _WN is not None:
+                wf = _WN.prep(v, g, Co, Ci * KT, KF, 1, True, False, x)[0]
+            else:
+                wf = _f32(Co * Ci * KT * KF, x)
+                call('encx_weightnorm_fwd', ptr(v), ptr(g), ptr(wf), None, Co, Ci * KT, KF, 1, st)
             wp = None
             if mode.reuse:
                 wp = _wpoly(wf, Co, Ci, KT, KF, sf, x)
@@ -659,6 +805,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.save_for_backward(x, y, wf)
         ctx.wp = wp
         ctx.feat_slot = feat_slot
+        ctx.out_slot = out_slot
         ctx.params = (v, g, b)
         ctx.geo, ctx.act = geo, act
         ctx.mode, ctx.first = mode, first
@@ -668,7 +815,7 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         if dy is None:
-            return (None,) * 9
+            return (None,) * 10
         x, y, wf = ctx.saved_tensors
         slot = ctx.feat_slot
         feat = slot.pending if slot is not None else None
@@ -680,18 +827,31 @@ class Conv2dFn(torch.autograd.Function):
         B, Ci, T2, Fi = x.shape
         Co = v.shape[0]
         st = stream()
-        yact = y if ctx.act else None
+        # dy arrives already multiplied by LeakyReLU'(y) when the one layer reading y applied it
+        # in its bwd-data epilogue (FeatSlot.premasked); the flag is consumed here
+        out = ctx.out_slot
+        premasked = out is not None and out.premasked
+        if out is not None:
+            out.premasked = False
+        yact = y if ctx.act and not premasked else None
         dims = (B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf)
         dx = dv = dg = db = None
         mode = ctx.mode
         if ctx.needs_input_grad[0] and (mode.input or not ctx.first):
             wp = ctx.wp if ctx.wp is not None else _wpoly(wf, Co, Ci, KT, KF, sf, x)
             dx = torch.empty_like(x)
+            # hand the producer of x the grad of its pre-activation when this layer is the only
+            # path by which x receives a gradient
+            xact = None
+            if slot is not None:
+                slot.premasked = (mode.premask and slot.act and slot.readers == 1
+                                  and not slot.autograd_feat)
+                xact = x if slot.premasked else None
             if feat is None:
-                call('encx_conv2d_bwd_data', ptr(dy), ptr(yact), ptr(wp), None, ptr(dx), 0, *dims, st)
+                call('encx_conv2d_bwd_data', ptr(dy), ptr(yact), ptr(wp), ptr(xact), ptr(dx), 0, *dims, st)
             else:  # + FeatFn's grad of this input map, in the epilogue
                 fr, den, fg, fscale = feat
-                call('encx_conv2d_bwd_data_feat', ptr(dy), ptr(yact), ptr(wp), None, ptr(dx), 0, ptr(fr),
+                call('encx_conv2d_bwd_data_feat', ptr(dy), ptr(yact), ptr(wp), ptr(xact), ptr(dx), 0, ptr(fr),
                      ptr(x), ptr(den), ptr(fg), float(fscale), *dims, st)
         elif feat is not None:
             raise RuntimeError('encx: a feature-matching grad was handed to a Conv2d whose input grad '
@@ -702,6 +862,11 @@ class Conv2dFn(torch.autograd.Function):
             if direct and g is None:   # plain weight: straight into the flat grad views
                 call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(v.grad), ptr(b.grad), 1, 1,
                      ptr(ws), *dims, st)
+            elif direct and _WNB is not None:  # dv/dg in the batched weight-norm backward
+                dw, acc_w = _WNB.dw_buffer(v)
+                call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(dw), ptr(b.grad), acc_w, 1,
+                     ptr(ws), *dims, st)
+                _WNB.queue(v, g)
             elif direct:
                 dw = torch.empty(v.shape, device=x.device, dtype=torch.float32)
                 call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(dw), ptr(b.grad), 0, 1,
@@ -714,7 +879,7 @@ class Conv2dFn(torch.autograd.Function):
                 call('encx_conv2d_bwd_weight', ptr(dy), ptr(yact), ptr(x), ptr(dw), ptr(db), 0, 0,
                      ptr(ws), *dims, st)
                 dv, dg = _weight_bwd(v, g, dw)
-        return dx, dv, dg, db, None, None, None, None, None
+        return dx, dv, dg, db, None, None, None, None, None, None
 
 
 class FeatSlot:
@@ -723,11 +888,17 @@ class FeatSlot:
     the map adds it in its bwd-data epilogue (encx_conv2d_bwd_data_feat), so the map's grad is
     never materialised twice and autograd does no add. FeatFn runs before every Conv2d of its
     graph in a traversal (it is the loss node), and the consumer clears the slot."""
-    __slots__ = ('pending', 'consumer_out')
+    __slots__ = ('pending', 'consumer_out', 'act', 'readers', 'autograd_feat', 'premasked')
 
-    def __init__(self):
+    def __init__(self, act=False):
         self.pending = None
         self.consumer_out = None  # the slot of the map the reading Conv2d produces
+        self.act = act            # the map is a LeakyReLU output (its sign is the pre-activation's)
+        self.readers = 0          # Conv2d layers reading the map
+        self.autograd_feat = False  # FeatFn returns this map's grad through autograd
+        # set by the reading Conv2d's backward when its dx is already the grad of the producing
+        # layer's pre-activation (dy * LeakyReLU'(map)); read and cleared by the producer
+        self.premasked = False
 
 
 def _wpoly(wf, Co, Ci, KT, KF, sf, like):
@@ -742,10 +913,12 @@ def conv2d(x, v, g, b, kernel, stride=(1, 1), dilation=(1, 1), padding=(0, 0), a
            first=False):
     geo = conv2d_geometry(x.shape[-1], kernel, stride, dilation, padding)
     in_slot = getattr(x, '_encx_feat_slot', None)
-    y = Conv2dFn.apply(x, v, g, b, geo, act, mode, first, in_slot)
-    y._encx_feat_slot = FeatSlot()
+    out_slot = FeatSlot(act=bool(act))
+    y = Conv2dFn.apply(x, v, g, b, geo, act, mode, first, in_slot, out_slot)
+    y._encx_feat_slot = out_slot
     if in_slot is not None:
-        in_slot.consumer_out = y._encx_feat_slot
+        in_slot.consumer_out = out_slot
+        in_slot.readers += 1
     return y
 
 
@@ -833,6 +1006,9 @@ class FeatFn(torch.autograd.Function):
         slots = [getattr(f, '_encx_feat_slot', None) for f in maps[n_pairs:]]
         live = {id(sl) for sl in slots if sl is not None}
         ctx.slots = [sl if sl is not None and id(sl.consumer_out) in live else None for sl in slots]
+        for sl, parked in zip(slots, ctx.slots):
+            if sl is not None and parked is None:
+                sl.autograd_feat = True  # a second gradient path into the map: its reader must not premask
         return out
 
     @staticmethod

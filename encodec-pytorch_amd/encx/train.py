@@ -18,6 +18,8 @@ Documented deviations: #7 a single combined backward (ide
 world_size 1; at world_size > 1 the commit-loss grads are all-reduced too, true DP);
 #9 the discriminator is trained with an explicit probability instead of eval(bool).
 """
+import contextlib
+import os
 import random
 
 import torch
@@ -26,7 +28,7 @@ from .balancer import Balancer
 from . import distrib
 from .losses import total_loss, disc_loss
 from .model import EncodecModel
-from .ops import DiscGradMode
+from .ops import DiscGradMode, WnBatch
 from .optim import FlatAdam
 from .scheduler import WarmupCosineLrScheduler
 
@@ -58,7 +60,14 @@ class Trainer:
                 self.sched_d = WarmupCosineLrScheduler(self.opt_d, max_iter=max_iter, eta_ratio=0.1,
                                                        warmup_iter=warmup_iter, warmup_ratio=1e-4)
         self.disc_prob = disc_prob
-        self.disc_mode = DiscGradMode()
+        # the step feeds the feature maps to the losses only (FeatFn), so the Conv2d backward may
+        # pass pre-activation grads between layers (DiscGradMode.premask). Off by default: on
+        # MI355X the producer's extra read of its input map in the discriminator phase costs more
+        # than the skipped reads of the output map save (A/B, config 3: 620 vs 634 audio-s/s)
+        self.disc_mode = DiscGradMode(premask=os.environ.get('ENCX_PREMASK', '0') == '1')
+        # every weight norm of a step as one launch per model forward and per backward
+        # (ops.WnBatch); ENCX_WN_BATCH=0 keeps the per-layer launches
+        self.wn = WnBatch() if os.environ.get('ENCX_WN_BATCH', '1') != '0' else None
         self.graphs = graphs
         self._graphs = {}
         dec = [p for p in model.decoder.parameters() if p.requires_grad]
@@ -112,23 +121,34 @@ class Trainer:
         c = {}
         dist = distrib.is_distributed()
 
+        wn = self.wn
+        fwd = (lambda grp: wn.forward(grp)) if wn is not None else (lambda grp: contextlib.nullcontext())
+        bwd = (lambda: wn.backward()) if wn is not None else contextlib.nullcontext
+
+        def dec_bucket(a, b):
+            if wn is not None:
+                wn.flush()  # the decoder's queued weight-norm backwards complete its grads
+            self.opt.all_reduce_bucket(a, b)
+
         def seg_a():
             self.opt.zero_grad()
-            y, loss_w, _ = self.model(x, bandwidth=bw)
+            with fwd('gen'):
+                y, loss_w, _ = self.model(x, bandwidth=bw)
             c['y'], c['loss_w'] = y, loss_w
             if overlap and dist:
                 q = self.model.last_decoder_input
                 if q is not None and q.requires_grad:
                     a, b = self._dec_span
-                    q.register_hook(lambda g: self.opt.all_reduce_bucket(a, b))
+                    q.register_hook(lambda g: dec_bucket(a, b))
             if self.disc is not None:
                 # generator phase: the balancer's autograd.grad calls differentiate the shared
                 # discriminator graph w.r.t. the fake audio only
                 self.disc_mode.set(params=False, input=True)
                 self.disc_mode.reuse_weights(True)  # same weights for both forwards
                 yd = y.detach().requires_grad_()
-                c['logits_real'], fmap_real = self.disc(x, mode=self.disc_mode)
-                c['logits_fake'], fmap_fake = self.disc(yd, mode=self.disc_mode)
+                with fwd('disc'):
+                    c['logits_real'], fmap_real = self.disc(x, mode=self.disc_mode)
+                    c['logits_fake'], fmap_fake = self.disc(yd, mode=self.disc_mode)
                 self.disc_mode.reuse_weights(False)
                 losses = total_loss(fmap_real, c['logits_fake'], fmap_fake, x, yd, self.sample_rate)
                 wrt = yd
@@ -141,7 +161,8 @@ class Trainer:
         def seg_b():
             out_grad = self.balancer.combine_finish()
             y, loss_w = c.pop('y'), c['loss_w']
-            torch.autograd.backward([y, loss_w], [out_grad, torch.ones_like(loss_w)])
+            with bwd():
+                torch.autograd.backward([y, loss_w], [out_grad, torch.ones_like(loss_w)])
 
         def seg_c():
             if dist:
@@ -154,7 +175,8 @@ class Trainer:
                 self.disc_mode.set(params=True, input=False)
                 self.opt_d.zero_grad()
                 out['l_d'] = disc_loss(c['logits_real'], c['logits_fake'])
-                out['l_d'].backward()
+                with bwd():
+                    out['l_d'].backward()
             c.clear()
             c['out'] = out
 

@@ -63,6 +63,23 @@ int encx_weightnorm_fwd(const float* v, const float* g, float* wf, float* wp, in
  * rows = A0, cols = A1*K. accumulate: 0 overwrite, 1 add into dv/dg. */
 int encx_weightnorm_bwd(const float* v, const float* g, const float* dw, float* dv, float* dg,
                         int64_t rows, int64_t cols, int accumulate, encx_stream_t stream);
+/* Batched forms: every weight-normed layer of a model in ONE launch (one workgroup per row
+ * over all layers; same arithmetic per row as the single-layer calls, so bit-identical). The
+ * descriptor arrays live in device memory (caller-owned, built once per model: the pointers
+ * are the persistent parameter / operand buffers); row0 = first row of the layer in the
+ * concatenation (ascending), rows_total = sum of the layers' rows. */
+typedef struct {
+    const float* v; const float* g; float* wf; float* wp;
+    int64_t A0, A1, K, stride, row0;
+} encx_wn_fwd_desc;
+typedef struct {
+    const float* v; const float* g; const float* dw; float* dv; float* dg;
+    int64_t rows, cols, row0, accumulate;
+} encx_wn_bwd_desc;
+int encx_weightnorm_fwd_batch(const encx_wn_fwd_desc* layers, int64_t n_layers, int64_t rows_total,
+                              encx_stream_t stream);
+int encx_weightnorm_bwd_batch(const encx_wn_bwd_desc* layers, int64_t n_layers, int64_t rows_total,
+                              encx_stream_t stream);
 
 /* ---------------------------------------------------------------- Conv1d
  * SConv1d.forward (modules/conv.py:195-210): pad1d (:79-96, reflect or zero, `short_ext` =
@@ -308,8 +325,11 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
 /* polyphase weight layout for the backward-data: wp[(co,kt)][ceil(KF/sf)][ci*sf + r] */
 int encx_conv2d_wpoly(const float* wf, float* wp, int64_t Co, int64_t Ci, int64_t KT, int64_t KF, int64_t sf,
                       encx_stream_t stream);
-/* dx (+)= d/dx, from dy masked by LeakyReLU'(yact) (yact NULL: no output activation) and
- * multiplied by LeakyReLU'(xact) (xact NULL: the input had no activation). */
+/* dx (+)= d/dx, from dy masked by LeakyReLU'(yact) (yact NULL: no output activation, or dy
+ * already carries the mask) and multiplied by LeakyReLU'(xact) (xact NULL: the input had no
+ * activation, or the caller wants the grad of the post-activation input map). With xact the
+ * result is the grad of the input's PRE-activation, which the producing layer then passes as its
+ * dy with yact NULL (its bwd-data and bwd-weight skip reading its output map). */
 int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
                          int accumulate, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
                          int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
@@ -317,7 +337,8 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
 /* encx_conv2d_bwd_data + the feature-matching loss's grad of this layer's input map added in the
  * epilogue (FeatFn's d l_feat / d ff, losses.py:53, fused instead of a grad tensor and an add):
  * dx += c * sign(feat_fake - feat_real), c = feat_g[0] * feat_scale / feat_denom[0] (feat_g NULL:
- * 1); feat_fake is this layer's input map, feat_real its real-audio counterpart. */
+ * 1); feat_fake is this layer's input map, feat_real its real-audio counterpart. The feature
+ * term is added before the xact mask: dx (+)= (d/dx + feature term) * LeakyReLU'(xact). */
 int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
                               int accumulate, const float* feat_real, const float* feat_fake,
                               const float* feat_denom, const float* feat_g, double feat_scale, int64_t B,

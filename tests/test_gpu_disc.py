@@ -233,3 +233,36 @@ def test_conv2d_vs_torch_fp64(li, T2, Fi):
     bscale = float(dyl.abs().sum(dim=(0, 2, 3)).max())
     berr = float((b.grad.double().cpu() - b64.grad).abs().max())
     assert rel(b.grad, b64.grad) < 1e-5 or berr <= 1e-7 * bscale, (rel(b.grad, b64.grad), berr, bscale)
+
+
+@pytest.mark.parametrize('params,inp', [(False, True), (True, False), (True, True)])
+def test_premask_bit_identical(params, inp):
+    """DiscGradMode.premask (the Trainer's setting: each Conv2d's bwd-data hands its input's
+    producer the grad of that producer's pre-activation) changes where the LeakyReLU' mask is
+    applied, not its value: grads of l_g + l_feat and of the hinge disc loss w.r.t. the fake
+    audio and every discriminator parameter are bit-identical to the unmasked protocol."""
+    from encx.ops import DiscGradMode
+    from encx.msstftd import adversarial_losses, hinge_disc_loss
+    disc, _ = make_disc(11)
+    g = torch.Generator().manual_seed(5)
+    x = (0.1 * torch.randn(2, 1, 24000, generator=g)).to(DEV)
+    y0 = (0.1 * torch.randn(2, 1, 24000, generator=g)).to(DEV)
+    outs = []
+    for premask in (False, True):
+        y = y0.clone().requires_grad_(True)
+        mode = DiscGradMode(params=params, input=inp, premask=premask)
+        lr, fr = disc(x, mode=mode)
+        lf, ff = disc(y, mode=mode)
+        l_g, l_feat = adversarial_losses(fr, lf, ff)
+        l_d = hinge_disc_loss(lr, lf)
+        wrt = ([y] if inp else []) + ([q for q in disc.parameters()] if params else [])
+        res = []
+        for loss in (l_g, l_feat, l_g + l_feat, l_d):
+            gs = torch.autograd.grad(loss, wrt, retain_graph=True, allow_unused=True)
+            res.append([t.clone() if t is not None else None for t in gs])
+        outs.append(res)
+    for a, b in zip(*outs):
+        for ta, tb in zip(a, b):
+            assert (ta is None) == (tb is None)
+            if ta is not None:
+                assert torch.equal(ta, tb)

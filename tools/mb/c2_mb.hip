@@ -111,8 +111,9 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(c2_wpoly_kernel, dim3((unsigned)cdiv((int64_t)l.Co * l.KT * J * l.Ci * l.sf, 256)), dim3(256), 0,
                            st, wf, wp, l.Co, l.Ci, l.KT, l.KF, l.sf, J);
         printf("== %s  T2=%d Fo=%d  %.2f GFLOP per call\n", l.name, l.T2, Fo, flops * 1e-9);
+        const char* only = getenv("MB_ONLY");  // fwd | dgrad | wgrad
         // ---- forward
-        {
+        if (!only || !strcmp(only, "fwd")) {
             C2Fwd a{g, x, wf, bias, y0, 1, 0, 0, 0};
             auto old = [&] { run_fwd<32, 128, 1, 4>(a, st); };
             double t0 = time_ms(old);
@@ -147,7 +148,7 @@ int main(int argc, char** argv) {
             tot_new[0] += best;
         }
         // ---- backward data
-        if (!(l.sf == 1 && l.KF == 9) && !getenv("MB_SKIP_DGRAD")) {  // the narrow first layer has its own VALU kernel
+        if (!(l.sf == 1 && l.KF == 9) && !getenv("MB_SKIP_DGRAD") && (!only || !strcmp(only, "dgrad"))) {  // the narrow first layer has its own VALU kernel
             C2Dg a{g, dy, yact, wp, nullptr, dx0, 0, 0, 0, 0, 0, 0};
             const int M = l.Ci * l.sf;
             double t0;
@@ -167,23 +168,25 @@ int main(int argc, char** argv) {
                 if (e <= 1e-5 && t < best) best = t;
             };
             if (M == 64 && J == 5) {
-                var("r<2,256,5,6,16>", [&] { if (run_dgradr<2, 256, 5, 6, 16>(b, st)) printf("    (n/a)\n"); });
-                var("r<2,256,5,6,16,3>", [&] { if (run_dgradr<2, 256, 5, 6, 16, 3>(b, st)) printf("    (n/a)\n"); });
-                var("r<2,256,5,4,16>", [&] { if (run_dgradr<2, 256, 5, 4, 16>(b, st)) printf("    (n/a)\n"); });
-                var("r<2,256,5,4,16,3>", [&] { if (run_dgradr<2, 256, 5, 4, 16, 3>(b, st)) printf("    (n/a)\n"); });
                 var("r<2,256,5,4,8,3>", [&] { if (run_dgradr<2, 256, 5, 4, 8, 3>(b, st)) printf("    (n/a)\n"); });
-                var("r<2,256,5,6,8>", [&] { if (run_dgradr<2, 256, 5, 6, 8>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,4,8,3,SP>", [&] { if (run_dgradr<2, 256, 5, 4, 8, 3, 2>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,4,8,2,SP>", [&] { if (run_dgradr<2, 256, 5, 4, 8, 2, 2>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,4,16,2,SP>", [&] { if (run_dgradr<2, 256, 5, 4, 16, 2, 2>(b, st)) printf("    (n/a)\n"); });
                 var("r<2,128,5,4,16,3>", [&] { if (run_dgradr<2, 128, 5, 4, 16, 3>(b, st)) printf("    (n/a)\n"); });
-                var("r<2,128,5,4,16,4>", [&] { if (run_dgradr<2, 128, 5, 4, 16, 4>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,128,5,4,16,3,SP>", [&] { if (run_dgradr<2, 128, 5, 4, 16, 3, 2>(b, st)) printf("    (n/a)\n"); });
+                b.yact = nullptr;
+                var("r<2,256,5,4,8,3> noY", [&] { if (run_dgradr<2, 256, 5, 4, 8, 3>(b, st)) printf("    (n/a)\n"); });
+                var("r<2,256,5,4,8,3,SP> noY", [&] { if (run_dgradr<2, 256, 5, 4, 8, 3, 2>(b, st)) printf("    (n/a)\n"); });
+                b.yact = a.yact;
             } else if (M == 32 && J == 3) {
                 var("r<1,256,3,6,32>", [&] { if (run_dgradr<1, 256, 3, 6, 32>(b, st)) printf("    (n/a)\n"); });
-                var("r<1,256,3,8,32>", [&] { if (run_dgradr<1, 256, 3, 8, 32>(b, st)) printf("    (n/a)\n"); });
-                var("<32,256,1,4,3>", [&] { run_dgrad<32, 256, 1, 4, 3>(b, st); });
+                var("r<1,256,3,6,32,1,SP>", [&] { if (run_dgradr<1, 256, 3, 6, 32, 1, 2>(b, st)) printf("    (n/a)\n"); });
+                var("r<1,256,3,6,16,2,SP>", [&] { if (run_dgradr<1, 256, 3, 6, 16, 2, 2>(b, st)) printf("    (n/a)\n"); });
             }
             tot_new[1] += best;
         }
         // ---- weight grad (+ bias column)
-        {
+        if (!only || !strcmp(only, "wgrad")) {
             const int N = l.Ci * l.KT * l.KF + 1;
             float* dw0 = dev_zero((size_t)l.Co * N);
             float* db0 = dev_zero(l.Co);
@@ -240,17 +243,26 @@ int main(int argc, char** argv) {
                 if (e <= 1e-5 && t < best) best = t;
             };
             if (gc && l.KF == 9) {
-                var3("3<9,1,9,6,1> 32/512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 6, 1>(g, dy, yact, x, ws, q, st); });
-                for (int tg : {384, 512, 640, 768, 896, 1024, 1280, 1536}) {
-                    char nm[48];
-                    snprintf(nm, 48, "3<9,1,9,4,1,5> 32/%d", tg);
-                    var3(nm, 32, tg, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5>(g, dy, yact, x, ws, q, st); });
-                }
+                var3("3<9,1,9,4,1,5,PF0> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5, 0>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,9,4,1,5,PF1> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,9,4,1,4,PF1> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 4, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,9,4,1,6,PF1> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 6, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,9,4,1,5,PF1> 512", 32, 512, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,9,4,1,5,PF1> 1024", 32, 1024, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,9,4,1,5,PF1> 1536", 32, 1536, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5, 1>(g, dy, yact, x, ws, q, st); });
+            } else if (l.Ci == 2 && l.KF == 9) {  // first layer: all 6 combos in one group, 54 of 64 columns
+                var3("3<9,1,2,2,4,4> 6/768", 6, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 2, 2, 4, 4>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,2,2,4,8> 6/768", 6, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 2, 2, 4, 8>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,2,2,4,4> 6/1536", 6, 1536, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 2, 2, 4, 4>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,2,1,4,8,4> 6/768", 6, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 1, 4, 8, 4>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,2,1,4,8,8> 6/1536", 6, 1536, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 1, 4, 8, 8>(g, dy, yact, x, ws, q, st); });
+                var3("3<9,1,2,2,4,4> 6/768 noY", 6, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 2, 2, 4, 4>(g, dy, nullptr, x, ws, q, st); });
             } else if (gc && l.KF == 3) {
-                var3("3<3,1,9,16,1> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1>(g, dy, yact, x, ws, q, st); });
-                var3("3<3,3,3,24,3> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 3, 3, 24, 3>(g, dy, yact, x, ws, q, st); });
-                var("2<3,3,3> 512", 512, [&](const WgPlan3& q) { run_wgrad2<3, 3, 3>(g, dy, yact, x, ws, q, st); });
-                var("2<3,3,3> 1024", 1024, [&](const WgPlan3& q) { run_wgrad2<3, 3, 3>(g, dy, yact, x, ws, q, st); });
+                var3("3<3,1,9,16,1,1,PF0> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1, 1, 0>(g, dy, yact, x, ws, q, st); });
+                var3("3<3,1,9,16,1,1,PF1> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1, 1, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<3,1,9,16,1,2,PF1> 96/768", 96, 768, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1, 2, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<3,3,3,24,3,1,PF1> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 3, 3, 24, 3, 1, 1>(g, dy, yact, x, ws, q, st); });
+                var3("3<3,3,3,24,3,2,PF1> 96/768", 96, 768, [&](const WgPlan3& q) { return run_wgrad3<3, 3, 3, 24, 3, 2, 1>(g, dy, yact, x, ws, q, st); });
             }
             tot_new[2] += best;
             CK(hipFree(dw0)); CK(hipFree(db0)); CK(hipFree(dw1)); CK(hipFree(db1)); CK(hipFree(ws));
