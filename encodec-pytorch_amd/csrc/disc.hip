@@ -1230,7 +1230,7 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
 // CI x 4 accumulators for 4 adjacent f and slides a 4+KF-1 window over its LDS row per tap;
 // the weights are wave-uniform (scalar loads).
 constexpr int DN_ROWS = 16, DN_COLS = 64, DN_FPT = 4, DN_CC = 8, DN_MAXHALO = 4;
-template <int CI, int KT, int KF, bool YM = true>
+template <int CI, int KT, int KF, bool YM = true, bool VQ = true>
 __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
     constexpr int RC = (DN_COLS + KF - 1 + 3) & ~3;  // LDS row length (float4 aligned)
     constexpr int WIN4 = (DN_FPT + KF - 1 + 3) / 4;
@@ -1249,8 +1249,55 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
     for (int c = 0; c < CI; ++c)
 #pragma unroll
         for (int e = 0; e < DN_FPT; ++e) acc[c][e] = 0.f;
+    // VQ: the tile is staged as quads along f (ld4u; lanes outside [0, Fo) or outside the
+    // tensor masked), one index split per 4 elements instead of per element
+    constexpr int RQ = RC / 4, QP = 4;
+    const int nq = DN_CC * NRW * RQ;
+    const int64_t left = (int64_t)(g.B - b) * g.Co * plane;  // floats from dyb to the tensor end
     for (int c0 = 0; c0 < g.Co; c0 += DN_CC) {
         __syncthreads();
+        if (VQ) {
+            for (int i0 = 0; i0 < nq; i0 += NT * QP) {
+                f32x4 v[QP], ym[QP];
+                int mk[QP];
+#pragma unroll
+                for (int q = 0; q < QP; ++q) {
+                    const int i = i0 + q * NT + tid;
+                    const int cl = i / (NRW * RQ), rem = i - cl * (NRW * RQ), r = rem / RQ, cq = rem - r * RQ;
+                    const int tr = tbase + r, fc = fbase + 4 * cq;
+                    const bool ok = i < nq && c0 + cl < g.Co && tr >= 0 && tr < g.T2 && fc + 4 > 0 && fc < g.Fo;
+                    const int64_t o = ok ? (int64_t)(c0 + cl) * plane + (int64_t)tr * g.Fo + fc : 0;
+                    int64_t oc = o < 0 ? 0 : o;
+                    if (oc > left - 4) oc = left - 4;
+                    v[q] = ld4u(dyb + oc);
+                    if (YM) ym[q] = ld4u(yab + oc);
+                    // lanes [lo, hi) hold columns inside [0, Fo); sh = the shift of a clamped load
+                    const int lo = fc < 0 ? -fc : 0, hi = min(g.Fo - fc, 4), sh = (int)(o - oc);
+                    mk[q] = ok ? (lo | (hi << 4) | ((sh + 4) << 8)) : 0;
+                }
+#pragma unroll
+                for (int q = 0; q < QP; ++q) {
+                    const int i = i0 + q * NT + tid;
+                    if (i >= nq) continue;
+                    const int m = mk[q], lo = m & 15, hi = (m >> 4) & 15, sh = (m >> 8) - 4;
+                    f32x4 t = v[q], ty = ym[q], u;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int src = k + sh;  // lane of the loaded quad holding column fc + k
+                        float dv = 0.f, yv = 0.f;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (src == j) {
+                                dv = t[j];
+                                if (YM) yv = ty[j];
+                            }
+                        const bool in = m && k >= lo && k < hi && src >= 0 && src < 4;
+                        u[k] = in ? (YM ? dv * lrelu_grad(yv) : dv) : 0.f;
+                    }
+                    *(f32x4*)(Xs + i * 4) = u;
+                }
+            }
+        } else
         for (int i0 = 0; i0 < items; i0 += NT * DPER) {
             float v[DPER], ym[DPER];
 #pragma unroll

@@ -844,7 +844,9 @@ class Conv2dFn(torch.autograd.Function):
             # path by which x receives a gradient
             xact = None
             if slot is not None:
-                slot.premasked = (mode.premask and slot.act and slot.readers == 1
+                # only where the epilogue reads x anyway (the feature term): elsewhere the
+                # extra read of x costs more than the producer saves by not reading its map
+                slot.premasked = (mode.premask and feat is not None and slot.act and slot.readers == 1
                                   and not slot.autograd_feat)
                 xact = x if slot.premasked else None
             if feat is None:

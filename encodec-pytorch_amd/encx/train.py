@@ -61,10 +61,9 @@ class Trainer:
                                                        warmup_iter=warmup_iter, warmup_ratio=1e-4)
         self.disc_prob = disc_prob
         # the step feeds the feature maps to the losses only (FeatFn), so the Conv2d backward may
-        # pass pre-activation grads between layers (DiscGradMode.premask). Off by default: on
-        # MI355X the producer's extra read of its input map in the discriminator phase costs more
-        # than the skipped reads of the output map save (A/B, config 3: 620 vs 634 audio-s/s)
-        self.disc_mode = DiscGradMode(premask=os.environ.get('ENCX_PREMASK', '0') == '1')
+        # pass pre-activation grads between layers (DiscGradMode.premask) wherever the bwd-data
+        # epilogue reads the input map anyway (the feature-matching term); ENCX_PREMASK=0 off
+        self.disc_mode = DiscGradMode(premask=os.environ.get('ENCX_PREMASK', '1') != '0')
         # every weight norm of a step as one launch per model forward and per backward
         # (ops.WnBatch); ENCX_WN_BATCH=0 keeps the per-layer launches
         self.wn = WnBatch() if os.environ.get('ENCX_WN_BATCH', '1') != '0' else None

@@ -139,3 +139,25 @@ def test_hip_graph_steps_match_eager(case):
     assert_same(runs[0][1], runs[1][1])
     g = runs[1][2]._graphs
     assert any(isinstance(v, tuple) for v in g.values())
+
+
+def test_weight_norm_batch_matches_per_layer():
+    """ops.WnBatch (every weight norm of a step as one launch per model forward / backward)
+    against the per-layer launches: generator grads bit-identical (the same per-row arithmetic);
+    discriminator grads within fp32 rounding (its layers serve the real and the fake graph, and
+    the batched backward normalises the summed weight grad once, as the reference's autograd
+    does, instead of each use's grad separately)."""
+    import encx.ops as ops
+    x = batches(1)[0]
+    grads = []
+    for batched in (False, True):
+        tr = make_trainer()
+        if not batched:
+            tr.wn = None
+        tr.step(x)
+        grads.append((tr.opt.flat_grad.clone(), tr.opt_d.flat_grad.clone(), tr.opt.flat.clone()))
+        assert ops._WN is None and ops._WNB is None
+    (g0, d0, p0), (g1, d1, p1) = grads
+    assert torch.equal(g0, g1)
+    assert torch.equal(p0, p1)
+    assert float((d0 - d1).abs().max()) <= 1e-5 * float(d0.abs().max())

@@ -133,6 +133,11 @@ int main(int argc, char** argv) {
             if (l.Co <= 32) {
                 if (l.KF == 9) {
                     var("r<256,9,6,16>", [&] { if (run_fwdr<256, 9, 6, 16>(b, st)) printf("    (n/a)\n"); });
+                    if (l.Ci == 2) {
+                        var("r<256,9,4,16,2>", [&] { if (run_fwdr<256, 9, 4, 16, 2>(b, st)) printf("    (n/a)\n"); });
+                        var("r<256,9,3,16,3>", [&] { if (run_fwdr<256, 9, 3, 16, 3>(b, st)) printf("    (n/a)\n"); });
+                        var("r<128,9,2,16,4>", [&] { if (run_fwdr<128, 9, 2, 16, 4>(b, st)) printf("    (n/a)\n"); });
+                    }
 
                 } else {
                     var("r<256,3,8,32>", [&] { if (run_fwdr<256, 3, 8, 32>(b, st)) printf("    (n/a)\n"); });
@@ -184,6 +189,23 @@ int main(int argc, char** argv) {
                 var("r<1,256,3,6,16,2,SP>", [&] { if (run_dgradr<1, 256, 3, 6, 16, 2, 2>(b, st)) printf("    (n/a)\n"); });
             }
             tot_new[1] += best;
+        }
+        // ---- first-layer backward data (VALU kernel): element vs quad staging
+        if (l.sf == 1 && l.KF == 9 && l.Ci == 2 && (!only || !strcmp(only, "dgrad"))) {
+            C2Dg a{g, dy, yact, wp, nullptr, dx0, 0, 0, 0, 0, 0, 0};
+            dim3 grid((unsigned)cdiv(l.Fi, DN_COLS), (unsigned)cdiv(l.T2, DN_ROWS), (unsigned)B);
+            double t0 = time_ms([&] { hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9, true, false>), grid, dim3(NT), 0, st, a); });
+            printf("  dgrad narrow elem            %8.1f us  %6.1f TF/s\n", t0 * 1e3, flops / t0 * 1e-9);
+            C2Dg b = a;
+            b.dx = dx1;
+            CK(hipMemset(dx1, 0, nx * 4));
+            double t1 = time_ms([&] { hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9, true, true>), grid, dim3(NT), 0, st, b); });
+            double e = rel_err(dx1, dx0, nx);
+            printf("  dgrad narrow quad            %8.1f us  %6.1f TF/s  err %.1e%s\n", t1 * 1e3, flops / t1 * 1e-9, e,
+                   e > 1e-6 ? "  MISMATCH" : "");
+            b.yact = nullptr;
+            double t2 = time_ms([&] { hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9, false, true>), grid, dim3(NT), 0, st, b); });
+            printf("  dgrad narrow quad noY        %8.1f us  %6.1f TF/s\n", t2 * 1e3, flops / t2 * 1e-9);
         }
         // ---- weight grad (+ bias column)
         if (!only || !strcmp(only, "wgrad")) {
