@@ -1081,7 +1081,155 @@ static int fwd_flat_slabs(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, in
     return gemm_slabs(Kred, gemm_splits((int)Cout, (int)(B * Tout), Kred));
 }
 
+// ---------------------------------------------------------------------------- 1x1 convs
+// The pointwise convs of the residual blocks (seanet.py:59-60, kernel 1, stride 1, no padding)
+// as a batched GEMM: C[b][m][n] = sum_k A[k][m] Bm[b][k][n], A the weight in k-major layout
+// (forward: wf [Cin][Cout]; backward-data: wp [Cout][Cin]) and Bm the [B][C][T] activation
+// (forward: ELU(x) when pre-activated; backward-data: dy). Both operands are staged as float4
+// quads along their contiguous dim (m for A, n = t for Bm), register-prefetched one BK slice
+// ahead; the epilogue is fwd_store's (bias, act'(xact), residual, accumulate).
+struct PwArgs {
+    const float* w;     // A [K][M]
+    const float* x;     // Bm [B][K][N]
+    const float* bias;  // [M] or null
+    const float* res;   // [B][M][N] (PW_RES)
+    const float* xact;  // [B][M][N] (PW_XACT): y *= act'(xact)
+    float* y;           // [B][M][N]
+    int M, K, N, in_act, epi_act;
+};
+enum { PW_RES = 1, PW_XACT = 2, PW_ACC = 4 };
+typedef float f32x4u_pw __attribute__((ext_vector_type(4), aligned(4)));
+
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(256) void pw_kernel(PwArgs a) {
+    constexpr int BK = 32, TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int QA = BM * BK / 4 / 256, QB = BN * BK / 4 / 256;  // quads per thread
+    static_assert(QA * 1024 == BM * BK && QB * 1024 == BN * BK, "tile / thread mismatch");
+    __shared__ float As[BK][BM + 4];
+    __shared__ float Bs[BK][BN + 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const TileId tile = xcd_tile();
+    const int n0 = tile.x * BN, m0 = tile.y * BM, b = tile.z;
+    const int h = lane >> 5, l32 = lane & 31;
+    const float* xb = a.x + (int64_t)b * a.K * a.N;
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    f32x4 ra[QA], rb[QB];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int e = 0; e < QA; ++e) {
+            const int i = tid + e * 256, k = i / (BM / 4), mq = (i - k * (BM / 4)) * 4;
+            const bool ok = k0 + k < a.K && m0 + mq < a.M;  // M % 4 == 0: whole quads
+            ra[e] = *(const f32x4u_pw*)(a.w + (ok ? (int64_t)(k0 + k) * a.M + m0 + mq : 0));
+            if (!ok) ra[e] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int e = 0; e < QB; ++e) {
+            const int i = tid + e * 256, k = i / (BN / 4), nq = (i - k * (BN / 4)) * 4;
+            const bool ok = k0 + k < a.K && n0 + nq < a.N;  // N % 4 == 0
+            rb[e] = *(const f32x4u_pw*)(xb + (ok ? (int64_t)(k0 + k) * a.N + n0 + nq : 0));
+            if (!ok) rb[e] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    fetch(0);
+    for (int k0 = 0; k0 < a.K; k0 += BK) {
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < QA; ++e) {
+            const int i = tid + e * 256, k = i / (BM / 4), mq = (i - k * (BM / 4)) * 4;
+            *(f32x4*)&As[k][mq] = ra[e];
+        }
+#pragma unroll
+        for (int e = 0; e < QB; ++e) {
+            const int i = tid + e * 256, k = i / (BN / 4), nq = (i - k * (BN / 4)) * 4;
+            f32x4 v = rb[e];
+            if (a.in_act == ENCX_ACT_ELU)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) v[c] = elu(v[c]);  // elu(0) = 0 keeps the padding
+            *(f32x4*)&Bs[k][nq] = v;
+        }
+        __syncthreads();
+        if (k0 + BK < a.K) fetch(k0 + BK);
+#pragma unroll
+        for (int kp = 0; kp < BK; kp += 2) {
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) av[i] = As[kp + h][wm0 + i * 32 + l32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bv[j] = Bs[kp + h][wn0 + j * 32 + l32];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 32 + l32;
+            if (n >= a.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (m >= a.M) continue;
+                const int64_t o = ((int64_t)b * a.M + m) * a.N + n;
+                float v = acc[i][j][r];
+                if (a.bias) v += a.bias[m];
+                if (EPI & PW_XACT) v *= act_grad(a.epi_act, a.xact[o]);
+                if (EPI & PW_RES) v += a.res[o];
+                if (EPI & PW_ACC) v += a.y[o];
+                a.y[o] = v;
+            }
+        }
+}
+
+template <int EPI>
+static void pw_launch_epi(const PwArgs& a, int B, hipStream_t st) {
+    // largest tile that still gives >= 640 workgroups (2.5 rounds over 256 CUs)
+    const int64_t nb128 = cdiv(a.N, 128), nb64 = cdiv(a.N, 64);
+    if (a.M > 64 && cdiv(a.M, 128) * nb128 * B >= 640) {
+        hipLaunchKernelGGL((pw_kernel<128, 128, 2, 2, EPI>), dim3(nb128, cdiv(a.M, 128), B), dim3(256), 0, st, a);
+    } else if (a.M > 64 && cdiv(a.M, 128) * nb64 * B >= 640) {
+        hipLaunchKernelGGL((pw_kernel<128, 64, 2, 2, EPI>), dim3(nb64, cdiv(a.M, 128), B), dim3(256), 0, st, a);
+    } else if (a.M > 32 && cdiv(a.M, 64) * nb128 * B >= 640) {
+        hipLaunchKernelGGL((pw_kernel<64, 128, 2, 2, EPI>), dim3(nb128, cdiv(a.M, 64), B), dim3(256), 0, st, a);
+    } else if (a.M > 32) {
+        hipLaunchKernelGGL((pw_kernel<64, 64, 2, 2, EPI>), dim3(nb64, cdiv(a.M, 64), B), dim3(256), 0, st, a);
+    } else {
+        hipLaunchKernelGGL((pw_kernel<32, 128, 1, 4, EPI>), dim3(nb128, cdiv(a.M, 32), B), dim3(256), 0, st, a);
+    }
+}
+static int pw_launch(const PwArgs& a, int B, int epi, hipStream_t st) {
+    switch (epi) {
+        case 0: pw_launch_epi<0>(a, B, st); break;
+        case PW_RES: pw_launch_epi<PW_RES>(a, B, st); break;
+        case PW_XACT: pw_launch_epi<PW_XACT>(a, B, st); break;
+        case PW_ACC: pw_launch_epi<PW_ACC>(a, B, st); break;
+        case PW_XACT | PW_ACC: pw_launch_epi<PW_XACT | PW_ACC>(a, B, st); break;
+        case PW_RES | PW_ACC: pw_launch_epi<PW_RES | PW_ACC>(a, B, st); break;
+        default: return ENCX_EINVAL;
+    }
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+// the 1x1 layers the pointwise kernel serves (ENCX_PW=0 keeps the implicit-GEMM path)
+static bool pw_ok(int K, int s, int d, int pl, int pr, int e, int Tin, int Tout, int Cin, int Cout) {
+    static const int on = [] { const char* v = getenv("ENCX_PW"); return v ? atoi(v) : 1; }();
+    return on && K == 1 && s == 1 && d == 1 && pl == 0 && pr == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 &&
+           Cin % 4 == 0 && Cout % 4 == 0;
+}
+
 int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
+    if (pw_ok(a.K, a.s, a.d, a.pl, 0, a.e, a.Tin, a.Tout, a.Cin, a.Cout) && !a.part) {
+        PwArgs p{a.wf, a.x, a.bias, a.res, a.xact, a.y, a.Cout, a.Cin, a.Tout, a.act, a.epi_act};
+        const int epi = (a.res ? PW_RES : 0) | (a.xact ? PW_XACT : 0) | (a.accumulate ? PW_ACC : 0);
+        if (pw_launch(p, a.B, epi, st) == 0) return 0;
+    }
     if (fwd_flat(a.Cout, a.Tout)) {
         const int Kred = a.Cin * a.K, N = a.B * a.Tout;
         const int splits = gemm_splits(a.Cout, N, Kred);
@@ -1349,6 +1497,13 @@ int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float
     encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
                        4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout), "conv_dgrad");
     ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
+    if (pw_ok((int)K, (int)stride, 1, (int)pad_left, (int)pad_right, (int)short_ext, (int)Tin, (int)Tout, (int)Cin,
+              (int)Cout)) {
+        // dx[b][ci][t] = sum_co wp[co][ci] dy[b][co][t], * act'(x), (+ dx)
+        PwArgs p{wp, dy, nullptr, nullptr, x, dx, (int)Cin, (int)Cout, (int)Tout, ENCX_ACT_NONE, pre_act};
+        const int epi = (pre_act != ENCX_ACT_NONE ? PW_XACT : 0) | (accumulate ? PW_ACC : 0);
+        if (pw_launch(p, (int)B, epi, st) == 0) return 0;
+    }
     int rc = poly_run(a, ncols, part, st);
     if (rc) return rc;
     if (pad_left + pad_right > 0 && pad_mode == ENCX_PAD_REFLECT) {
