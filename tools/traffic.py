@@ -15,7 +15,7 @@ import json
 import re
 
 # kernels launched by the conv / convtr / conv2d ABI entry points (csrc/conv1d.hip, disc.hip)
-FAMILY = re.compile(r'conv_fwd_kernel|conv_poly_kernel|conv_wgrad|wgrad_reduce|conv_fwd_reduce|'
+FAMILY = re.compile(r'conv_fwd_kernel|pw_kernel|conv_poly_kernel|conv_wgrad|wgrad_reduce|conv_fwd_reduce|'
                     r'conv_poly_reduce|conv_fold_edges|LdConvFlat|LdPolyFlat|c2_')
 
 
