@@ -95,10 +95,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # ENCX_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- a one-GPU rehearsal of the
+    # N-rank path (collectives, barriers, max-over-ranks timing); the real runs use RCCL
+    rehearse = os.environ.get('ENCX_BENCH_REHEARSE', '0') == '1'
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        torch.distributed.init_process_group('nccl', device_id=dev)
+        if rehearse:
+            torch.distributed.init_process_group('gloo')
+        else:
+            torch.distributed.init_process_group('nccl', device_id=dev)
     import encx
     from encx.model import EncodecModel
     from encx.train import Trainer

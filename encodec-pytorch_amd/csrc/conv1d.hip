@@ -1217,11 +1217,14 @@ static int pw_launch(const PwArgs& a, int B, int epi, hipStream_t st) {
     ENCX_CHECK_LAUNCH();
     return 0;
 }
-// the 1x1 layers the pointwise kernel serves (ENCX_PW=0 keeps the implicit-GEMM path)
+// the 1x1 layers the pointwise kernel serves (ENCX_PW=0 keeps the implicit-GEMM path): the
+// short, wide ones (T <= 1024). tools/mb/conv_mb: 256x256 at T 600 101 -> 59 us, 128x256 53 -> 42
+// us; the long, HBM-bound ones (T >= 3000) stay on conv_fwd_kernel, whose epilogue streams
+// the residual better (64x64 at T 12000: 108 us there, 145 here)
 static bool pw_ok(int K, int s, int d, int pl, int pr, int e, int Tin, int Tout, int Cin, int Cout) {
     static const int on = [] { const char* v = getenv("ENCX_PW"); return v ? atoi(v) : 1; }();
     return on && K == 1 && s == 1 && d == 1 && pl == 0 && pr == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 &&
-           Cin % 4 == 0 && Cout % 4 == 0;
+           Tout <= 1024 && Cin % 4 == 0 && Cout % 4 == 0;
 }
 
 int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {

@@ -316,8 +316,6 @@ __global__ __launch_bounds__(NT) void c2_fwdp_kernel(C2Fwd a) {
 
 // 4 floats from a dword-aligned global address (one global_load_dwordx4: the HSA target runs in
 // unaligned-access mode)
-typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
-ENCX_DEV f32x4 ld4u(const float* p) { return *(const f32x4u*)p; }
 
 // One window row of the LDS image, as float4 quads: src = global offset of window column 0,
 // pos0 = its input column (-2^30 when the row lies outside the input), lim = input width.
@@ -1928,7 +1926,8 @@ __global__ void c2_wpoly_kernel(const float* wf, float* wp, int Co, int Ci, int 
 
 // ---------------------------------------------------------------------------- spectrogram
 struct LdSpecD {  // A(m = (bc, fr), k) = x[bc][fr*hop + k]; B = DFT table [n][2nb]
-    static constexpr bool A_K_FAST = true, B_N_FAST = true;
+    // (scalar staging: the quad form measured 4 % slower here)
+    static constexpr bool A_K_FAST = true, B_N_FAST = true, VEC = false;
     const float* x;
     const float* bt;
     int T, Fr, hop, nb2;
@@ -1938,6 +1937,11 @@ struct LdSpecD {  // A(m = (bc, fr), k) = x[bc][fr*hop + k]; B = DFT table [n][2
         return x[(int64_t)bc * T + (int64_t)fr * hop + k];
     }
     ENCX_DEV float b(int k, int n) const { return bt[(int64_t)k * nb2 + n]; }
+    ENCX_DEV f32x4 a4(int m, int k) const {  // k..k+3 of one frame (k + 3 < n_fft)
+        const int bc = (int)fdiv((uint32_t)m, fFr), fr = m - bc * Fr;
+        return ld4u(x + (int64_t)bc * T + (int64_t)fr * hop + k);
+    }
+    ENCX_DEV f32x4 b4(int k, int n) const { return ld4u(bt + (int64_t)k * nb2 + n); }
 };
 struct EpSpecD {  // z[b][ch][fr][k], ch = c (re) or C + c (im)
     float* z;
@@ -1950,7 +1954,7 @@ struct EpSpecD {  // z[b][ch][fr][k], ch = c (re) or C + c (im)
     }
 };
 struct LdSpecDB {  // A(m = (bc, fr), col) = dz at col; B(col, t) = bt[t][col]
-    static constexpr bool A_K_FAST = true, B_N_FAST = false;
+    static constexpr bool A_K_FAST = true, B_N_FAST = false, VEC = true;
     const float* dz;
     const float* bt;
     int C, Fr, nb, nb2;
@@ -1961,6 +1965,19 @@ struct LdSpecDB {  // A(m = (bc, fr), col) = dz at col; B(col, t) = bt[t][col]
         return dz[(((int64_t)b * 2 * C + ch) * Fr + fr) * nb + k] * inv;
     }
     ENCX_DEV float b(int col, int t) const { return bt[(int64_t)t * nb2 + col]; }
+    ENCX_DEV f32x4 a4(int m, int col) const {
+        if (col < nb && col + 3 >= nb) {  // the quad straddles the re / im boundary
+            f32x4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = a(m, col + q);
+            return v;
+        }
+        const int bc = m / Fr, fr = m - bc * Fr, b = bc / C, c = bc - b * C;
+        const int im = col >= nb, k = im ? col - nb : col, ch = im ? C + c : c;
+        const f32x4 v = ld4u(dz + (((int64_t)b * 2 * C + ch) * Fr + fr) * nb + k);
+        return (f32x4){v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv};
+    }
+    ENCX_DEV f32x4 b4(int col, int t) const { return ld4u(bt + (int64_t)t * nb2 + col); }
 };
 struct EpFrames {
     float* out;

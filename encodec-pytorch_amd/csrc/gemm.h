@@ -21,6 +21,15 @@ struct ep_npre { static constexpr int value = 0; };
 template <class EP>
 struct ep_npre<EP, decltype((void)EP::NPRE)> { static constexpr int value = EP::NPRE; };
 
+// loaders that can hand over 4 consecutive elements along their fast dim declare
+// `static constexpr bool VEC = true` and a4(m, k) / b4(k, n) (f32x4 of (m..m+3 or k..k+3) /
+// (k..k+3 or n..n+3)); the kernel then stages quads (one loader call per 4 elements) and takes
+// the scalar path only for quads that cross the matrix edge
+template <class LD, class = void>
+struct ld_vec { static constexpr bool value = false; };
+template <class LD>
+struct ld_vec<LD, decltype((void)LD::VEC)> { static constexpr bool value = LD::VEC; };
+
 template <int BM, int BN, int WM, int WN, int BK, class LD, class EP>
 __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, int Kred, int kchunk) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -45,7 +54,63 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
     // a bounds test around each loader call compiles to an exec-masked branch per element, and
     // a loader that transforms the loaded value (ELU, |X|^2, ...) then waits for each load
     // before issuing the next (one memory round trip per element instead of one per fetch).
+    constexpr bool VEC = ld_vec<LD>::value;
+    static_assert(!VEC || (EA % 4 == 0 && EB % 4 == 0), "quad staging");
+    // quad e of this thread: its first element (m, k) and the fast dim
+    auto quad_a = [&](int e, int& m, int& k) {
+        const int i = tid + e * 256;
+        if (LD::A_K_FAST) { m = i / (BK / 4); k = (i - m * (BK / 4)) * 4; }
+        else { k = i / (BM / 4); m = (i - k * (BM / 4)) * 4; }
+    };
+    auto quad_b = [&](int e, int& k, int& n) {
+        const int i = tid + e * 256;
+        if (LD::B_N_FAST) { k = i / (BN / 4); n = (i - k * (BN / 4)) * 4; }
+        else { n = i / (BK / 4); k = (i - n * (BK / 4)) * 4; }
+    };
     auto fetch = [&](int k0) {
+        if constexpr (VEC) {
+#pragma unroll
+            for (int e = 0; e < EA / 4; ++e) {
+                int m, k;
+                quad_a(e, m, k);
+                const int gm = m0 + m, gk = k0 + k;
+                const bool whole = LD::A_K_FAST ? (gm < M && gk + 3 < kend) : (gm + 3 < M && gk < kend);
+                f32x4 v;
+                if (whole) {
+                    v = ld.a4(gm, gk);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int mm = LD::A_K_FAST ? gm : gm + c, kk = LD::A_K_FAST ? gk + c : gk;
+                        const float t = ld.a(mm < M ? mm : M - 1, kk < kend ? kk : kend - 1);
+                        v[c] = (mm < M && kk < kend) ? t : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ra[4 * e + c] = v[c];
+            }
+#pragma unroll
+            for (int e = 0; e < EB / 4; ++e) {
+                int k, n;
+                quad_b(e, k, n);
+                const int gn = n0 + n, gk = k0 + k;
+                const bool whole = LD::B_N_FAST ? (gk < kend && gn + 3 < N) : (gk + 3 < kend && gn < N);
+                f32x4 v;
+                if (whole) {
+                    v = ld.b4(gk, gn);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int nn = LD::B_N_FAST ? gn + c : gn, kk = LD::B_N_FAST ? gk : gk + c;
+                        const float t = ld.b(kk < kend ? kk : kend - 1, nn < N ? nn : N - 1);
+                        v[c] = (nn < N && kk < kend) ? t : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) rb[4 * e + c] = v[c];
+            }
+            return;
+        }
 #pragma unroll
         for (int e = 0; e < EA; ++e) {
             const int i = tid + e * 256;
@@ -72,6 +137,28 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
     if (kbeg < kend) fetch(kbeg);
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
         __syncthreads();
+        if constexpr (VEC) {
+#pragma unroll
+            for (int e = 0; e < EA / 4; ++e) {
+                int m, k;
+                quad_a(e, m, k);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (LD::A_K_FAST) As[k + c][m] = ra[4 * e + c];
+                    else As[k][m + c] = ra[4 * e + c];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < EB / 4; ++e) {
+                int k, n;
+                quad_b(e, k, n);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (LD::B_N_FAST) Bs[k][n + c] = rb[4 * e + c];
+                    else Bs[k + c][n] = rb[4 * e + c];
+                }
+            }
+        } else {
 #pragma unroll
         for (int e = 0; e < EA; ++e) {
             const int i = tid + e * 256;
@@ -87,6 +174,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(LD ld, EP ep, int M, int N, i
             if (LD::B_N_FAST) { k = i / BN; n = i - k * BN; }
             else { n = i / BK; k = i - n * BK; }
             Bs[k][n] = rb[e];
+        }
         }
         __syncthreads();
         if (k0 + BK < kend) fetch(k0 + BK);
