@@ -1227,6 +1227,154 @@ static bool pw_ok(int K, int s, int d, int pl, int pr, int e, int Tin, int Tout,
            Tout <= 1024 && Cin % 4 == 0 && Cout % 4 == 0;
 }
 
+// weight grad of the short, wide 1x1 convs: dW[m=co][n=ci] = sum_{b,t} dy[b][co][t] act(x[b][ci][t])
+// over positions k = b*T + t (T % 4 == 0: a quad never straddles two clips), split over k into
+// slabs [S][M][N] (+ bias slabs [S][M] = sum dy, from the staged A operand) that wgrad_reduce
+// adds in a fixed order
+struct PwWgArgs {
+    const float* dy;  // [B][M][T]
+    const float* x;   // [B][N][T]
+    float* ws;        // [S][M][N], then [S][M]
+    int M, N, T, Ktot, kchunk, in_act, do_bias, S;
+};
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs a) {
+    constexpr int BK = 32, TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int QA = BM * BK / 4 / 256, QB = BN * BK / 4 / 256;
+    static_assert(QA * 1024 == BM * BK && QB * 1024 == BN * BK, "tile / thread mismatch");
+    __shared__ float As[BK][BM + 1];
+    __shared__ float Bs[BK][BN + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, z = blockIdx.z;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int kbeg = z * a.kchunk, kend = min(a.Ktot, kbeg + a.kchunk);
+    const bool bias_wave = a.do_bias && blockIdx.x == 0 && (wave % WN) == 0;
+    f32x16 acc[TM][TN];
+    float bsum[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        bsum[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    }
+    f32x4 ra[QA], rb[QB];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int e = 0; e < QA; ++e) {
+            const int i = tid + e * 256, m = i / (BK / 4), k4 = (i - m * (BK / 4)) * 4, gk = k0 + k4;
+            const bool ok = m0 + m < a.M && gk < kend;
+            const int b = gk / a.T, t = gk - b * a.T;
+            ra[e] = ld4u(a.dy + (ok ? ((int64_t)b * a.M + m0 + m) * a.T + t : 0));
+            if (!ok) ra[e] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int e = 0; e < QB; ++e) {
+            const int i = tid + e * 256, n = i / (BK / 4), k4 = (i - n * (BK / 4)) * 4, gk = k0 + k4;
+            const bool ok = n0 + n < a.N && gk < kend;
+            const int b = gk / a.T, t = gk - b * a.T;
+            rb[e] = ld4u(a.x + (ok ? ((int64_t)b * a.N + n0 + n) * a.T + t : 0));
+            if (!ok) rb[e] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    if (kbeg < kend) fetch(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < QA; ++e) {
+            const int i = tid + e * 256, m = i / (BK / 4), k4 = (i - m * (BK / 4)) * 4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) As[k4 + c][m] = ra[e][c];
+        }
+#pragma unroll
+        for (int e = 0; e < QB; ++e) {
+            const int i = tid + e * 256, n = i / (BK / 4), k4 = (i - n * (BK / 4)) * 4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) Bs[k4 + c][n] = a.in_act == ENCX_ACT_ELU ? elu(rb[e][c]) : rb[e][c];
+        }
+        __syncthreads();
+        if (k0 + BK < kend) fetch(k0 + BK);
+#pragma unroll
+        for (int kp = 0; kp < BK; kp += 2) {
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) av[i] = As[kp + h][wm0 + i * 32 + l32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bv[j] = Bs[kp + h][wn0 + j * 32 + l32];
+            if (bias_wave)
+#pragma unroll
+                for (int i = 0; i < TM; ++i) bsum[i] += av[i];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+        }
+    }
+    float* slab = a.ws + (int64_t)z * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 32 + l32;
+            if (n >= a.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                if (m < a.M) slab[(int64_t)m * a.N + n] = acc[i][j][r];
+            }
+        }
+    if (bias_wave) {
+        float* bslab = a.ws + (int64_t)a.S * a.M * a.N + (int64_t)z * a.M;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const float v = bsum[i] + __shfl_xor(bsum[i], 32, 64);
+            const int m = m0 + wm0 + i * 32 + l32;
+            if (h == 0 && m < a.M) bslab[m] = v;
+        }
+    }
+}
+
+struct PwWgPlan {
+    int BM, BN, S, kchunk;
+};
+static PwWgPlan plan_pw_wgrad(int64_t B, int64_t M, int64_t N, int64_t T) {
+    PwWgPlan p;
+    p.BM = M >= 128 ? 128 : 64;
+    p.BN = N >= 128 ? 128 : 64;
+    const int64_t tiles = cdiv(M, p.BM) * cdiv(N, p.BN), Ktot = B * T;
+    int64_t S = cdiv(768, tiles);
+    const int64_t cap = Ktot / 128;  // >= 4 k-stages per workgroup
+    if (S > cap) S = cap;
+    if (S < 1) S = 1;
+    p.kchunk = (int)(cdiv(cdiv(Ktot, S), 32) * 32);
+    p.S = (int)cdiv(Ktot, p.kchunk);
+    return p;
+}
+static size_t pw_wgrad_ws_bytes(int64_t B, int64_t M, int64_t N, int64_t T) {
+    const PwWgPlan p = plan_pw_wgrad(B, M, N, T);
+    return (size_t)p.S * M * (N + 1) * sizeof(float);
+}
+// the layers pw_wgrad serves: 1x1, T <= 3000, at least 64 x 64
+static bool pw_wgrad_ok(int64_t K, int64_t s, int64_t d, int64_t pl, int64_t e, int64_t Tin, int64_t Tout, int64_t Cin,
+                        int64_t Cout) {
+    static const int on = [] { const char* v = getenv("ENCX_PW"); return v ? atoi(v) : 1; }();
+    return on && K == 1 && s == 1 && d == 1 && pl == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 && Tout <= 3000 &&
+           Cin >= 64 && Cout >= 64 && Cin % 4 == 0 && Cout % 4 == 0;
+}
+static void pw_wgrad_run(const float* dy, const float* x, float* dw, float* db, float* ws, int64_t B, int64_t M,
+                         int64_t N, int64_t T, int in_act, int acc_w, int acc_b, hipStream_t st) {
+    const PwWgPlan p = plan_pw_wgrad(B, M, N, T);
+    PwWgArgs a{dy, x, ws, (int)M, (int)N, (int)T, (int)(B * T), p.kchunk, in_act, db != nullptr, p.S};
+    const dim3 grid((unsigned)cdiv(N, p.BN), (unsigned)cdiv(M, p.BM), (unsigned)p.S);
+    if (p.BM == 128 && p.BN == 128) hipLaunchKernelGGL((pw_wgrad_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, a);
+    else if (p.BM == 128) hipLaunchKernelGGL((pw_wgrad_kernel<128, 64, 2, 2>), grid, dim3(256), 0, st, a);
+    else if (p.BN == 128) hipLaunchKernelGGL((pw_wgrad_kernel<64, 128, 2, 2>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((pw_wgrad_kernel<64, 64, 2, 2>), grid, dim3(256), 0, st, a);
+    const int64_t AN = M * N;
+    hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)(cdiv(AN, 64) + (db ? cdiv(M, 64) : 0))), dim3(256), 0, st, ws, dw,
+                       AN, p.S, acc_w, ws + (int64_t)p.S * AN, db, (int)M, acc_b);
+}
+
 int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
     if (pw_ok(a.K, a.s, a.d, a.pl, 0, a.e, a.Tin, a.Tout, a.Cin, a.Cout) && !a.part) {
         PwArgs p{a.wf, a.x, a.bias, a.res, a.xact, a.y, a.Cout, a.Cin, a.Tout, a.act, a.epi_act};
@@ -1536,6 +1684,11 @@ int encx_conv1d_bwd_weight_bias(const float* dy, const float* x, float* dw, floa
     hipStream_t st = (hipStream_t)stream;
     encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K, 4.0 * (B * Cout * Tout + B * Cin * Tin + Cin * K * Cout), "conv_wgrad");
     ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
+    if (pw_wgrad_ok(K, stride, dilation, pad_left, short_ext, Tin, Tout, Cin, Cout)) {
+        pw_wgrad_run(dy, x, dw, db, ws, B, Cout, Cin, Tout, pre_act, acc_w, acc_b, st);
+        ENCX_CHECK_LAUNCH();
+        return 0;
+    }
     const bool fused = db && wgrad_bias_ok(B, Cout, Tout, Cin, K);
     int rc = wgrad_run(dy, x, dw, ws, B, Cout, Tout, Cin, Tin, K, stride, dilation, pad_left, short_ext, pad_mode,
                        ENCX_ACT_NONE, pre_act, acc_w, st, fused ? db : nullptr, acc_b);
@@ -1545,7 +1698,8 @@ int encx_conv1d_bwd_weight_bias(const float* dy, const float* x, float* dw, floa
 
 size_t encx_conv1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout,
                                         int64_t K) {
-    return maxz(wgrad_ws_bytes(B, Cout, Tout, Cin, K), encx_channel_sum_workspace(Cout));
+    return maxz(maxz(wgrad_ws_bytes(B, Cout, Tout, Cin, K), encx_channel_sum_workspace(Cout)),
+                K == 1 ? pw_wgrad_ws_bytes(B, Cout, Cin, Tout) : 0);
 }
 
 size_t encx_convtr1d_fwd_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K,

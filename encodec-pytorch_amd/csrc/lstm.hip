@@ -293,7 +293,7 @@ __global__ void lstm_out_skip(const float* Y, const float* x, float* out, int B,
 // ------------------------------------------------------------------------- weight grads
 // dwcat_l[j][n] = sum_m DA_l[m][j] Z(m, n), Z = [x_l(m, :) | h_l(m-1, :) (0 at t = 0) | 1]
 struct LdWcat {
-    static constexpr bool A_K_FAST = false, B_N_FAST = true;
+    static constexpr bool A_K_FAST = false, B_N_FAST = true, VEC = true;
     const float* DA;
     const float* in;
     const float* Yl;
@@ -308,6 +308,21 @@ struct LdWcat {
         const float v = (rec ? Yl : in)[(int64_t)mm * H + u];
         const int t = m - (int)fdiv((uint32_t)m, fT) * T;
         return n == 2 * H ? 1.f : (rec && t == 0 ? 0.f : v);
+    }
+    // quads (H % 4 == 0, so a quad never straddles the x | h boundary; the ones column n = 2H
+    // only ever sits in the scalar edge quad)
+    ENCX_DEV f32x4 a4(int j, int m) const { return ld4u(DA + (int64_t)m * 4 * H + j); }
+    ENCX_DEV f32x4 b4(int m, int n) const {
+        if (n + 3 >= 2 * H) {
+            f32x4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = b(m, n + q);
+            return v;
+        }
+        const bool rec = n >= H;
+        const int t = m - (int)fdiv((uint32_t)m, fT) * T;
+        const f32x4 v = ld4u(rec ? Yl + (int64_t)(m > 0 ? m - 1 : 0) * H + (n - H) : in + (int64_t)m * H + n);
+        return rec && t == 0 ? (f32x4){0.f, 0.f, 0.f, 0.f} : v;
     }
 };
 struct EpSlabs {  // split-K partial slabs [z][M][N]
