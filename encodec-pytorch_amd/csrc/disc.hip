@@ -2131,18 +2131,20 @@ __global__ __launch_bounds__(256) void c2_co1_fwd(C2Fwd a) {
 // dx[b][ci][ti][fi] = sum_{kt,kf} W[ci][kt][kf] * dy'[b][ti - kt*dt + pt][(fi - kf + pf)/S]
 // (terms whose output column is fractional or out of range drop), dy' = dy * LeakyReLU'(yact).
 // Block = 64 columns x 4 rows of one (b, ci) plane.
-template <int KT, int KF, int S>
+// CPT input channels per thread share the KT*KF loads of dy' (blockIdx.y = (b, channel group));
+// per channel the taps are summed in the same order as one channel per thread.
+template <int KT, int KF, int S, int CPT = 1>
 __global__ __launch_bounds__(256) void c2_co1_dgrad(C2Dg a) {
     const C2Geo g = a.g;
     const int xplane = g.T2 * g.Fi, p = blockIdx.x * 256 + threadIdx.x;
     if (p >= xplane) return;
     const int ti = p / g.Fi, fi = p - ti * g.Fi;
-    const int bc = blockIdx.y, b = bc / g.Ci, ci = bc - b * g.Ci;
+    const int groups = g.Ci / CPT, b = blockIdx.y / groups, ci0 = (blockIdx.y - b * groups) * CPT;
     const int64_t plane = (int64_t)g.T2 * g.Fo;
     const float* dyb = a.dy + (int64_t)b * plane;
     const float* yab = a.yact ? a.yact + (int64_t)b * plane : dyb;
     const int M = g.Ci * S;
-    float acc = 0.f;
+    float dv[KT * KF];
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) {
         const int to = ti - kt * g.dt + g.pt;
@@ -2155,14 +2157,24 @@ __global__ __launch_bounds__(256) void c2_co1_dgrad(C2Dg a) {
             const int64_t o = ok ? (int64_t)to * g.Fo + fo : 0;
             float d = dyb[o];
             if (a.yact) d *= lrelu_grad(yab[o]);
-            const float w = a.wp[(kt * a.J + kf / S) * M + ci * S + kf % S];
-            acc = fmaf(w, ok ? d : 0.f, acc);
+            dv[kt * KF + kf] = ok ? d : 0.f;
         }
     }
-    const int64_t i = (int64_t)bc * xplane + p;
-    if (a.ffr) acc += feat_term(a, feat_coef(a), i);
-    if (a.xact) acc *= lrelu_grad(a.xact[i]);
-    a.dx[i] = a.accumulate ? a.dx[i] + acc : acc;
+    const float fc = feat_coef(a);
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        const int ci = ci0 + c;
+        float acc = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf)
+                acc = fmaf(a.wp[(kt * a.J + kf / S) * M + ci * S + kf % S], dv[kt * KF + kf], acc);
+        const int64_t i = ((int64_t)b * g.Ci + ci) * xplane + p;
+        if (a.ffr) acc += feat_term(a, fc, i);
+        if (a.xact) acc *= lrelu_grad(a.xact[i]);
+        a.dx[i] = a.accumulate ? a.dx[i] + acc : acc;
+    }
 }
 
 // ws[s][0][n], s = (b, row chunk): n = (ci*KT + kt)*KF + kf -> sum over the chunk's output
@@ -2581,7 +2593,11 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
     const int M = (int)(Ci * sf);
     if (Co == 1 && KT == 3 && KF == 3 && (sf == 1 || sf == 2)) {
         dim3 grid((unsigned)cdiv(T2 * Fi, 256), (unsigned)(B * Ci));
-        if (sf == 1) hipLaunchKernelGGL((c2_co1_dgrad<3, 3, 1>), grid, dim3(256), 0, st, a);
+        if (Ci % 4 == 0) {
+            const dim3 g4((unsigned)cdiv(T2 * Fi, 256), (unsigned)(B * Ci / 4));
+            if (sf == 1) hipLaunchKernelGGL((c2_co1_dgrad<3, 3, 1, 4>), g4, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((c2_co1_dgrad<3, 3, 2, 4>), g4, dim3(256), 0, st, a);
+        } else if (sf == 1) hipLaunchKernelGGL((c2_co1_dgrad<3, 3, 1>), grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((c2_co1_dgrad<3, 3, 2>), grid, dim3(256), 0, st, a);
         ENCX_CHECK_LAUNCH();
         return 0;

@@ -89,6 +89,10 @@ MODEL_LAYERS = [
     ('conv', 32, 1, 7, 1, True, 4800),
     ('convtr', 512, 256, 16, 8, True, 15), ('convtr', 256, 128, 10, 5, True, 120),
     ('convtr', 128, 64, 8, 4, True, 600), ('convtr', 64, 32, 4, 2, True, 2400),
+    # the 1x1 layers on the pointwise GEMM kernels (fwd / bwd-data for T <= 1024, weight grad
+    # for T <= 3000 at >= 64 channels) at their real widths and lengths
+    ('conv', 256, 256, 1, 1, True, 600), ('conv', 128, 256, 1, 1, False, 600),
+    ('conv', 64, 128, 1, 1, True, 3000), ('conv', 128, 128, 1, 1, True, 1000),
 ]
 
 
