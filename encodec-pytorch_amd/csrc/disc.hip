@@ -1865,7 +1865,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
             const int tl = 2 * kp + h;
             const int po = poff[tl];
             const float av = Ls[tl * LDA + l32];
-            if (do_bias) bsum += av;
+            bsum += av;  // every wave (no branch in the loop); only the bias wave stores it
             float bv[NTW];
 #pragma unroll
             for (int j = 0; j < NTW; ++j) bv[j] = Rs[cbase[j] + po];

@@ -266,10 +266,6 @@ int main(int argc, char** argv) {
             };
             if (gc && l.KF == 9) {
                 var3("3<9,1,9,4,1,5,PF0> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5, 0>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,3,3,12,3,2> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 12, 3, 2>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,3,3,12,3,3> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 12, 3, 3>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,3,3,12,3,2> 1536", 32, 1536, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 12, 3, 2>(g, dy, yact, x, ws, q, st); });
-                var3("3<9,3,3,16,3,2> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 3, 3, 16, 3, 2>(g, dy, yact, x, ws, q, st); });
             } else if (l.Ci == 2 && l.KF == 9) {  // first layer: all 6 combos in one group, 54 of 64 columns
                 var3("3<9,1,2,2,4,4> 6/768", 6, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 2, 2, 4, 4>(g, dy, yact, x, ws, q, st); });
                 var3("3<9,1,2,2,4,8> 6/768", 6, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 2, 2, 4, 8>(g, dy, yact, x, ws, q, st); });
