@@ -1889,6 +1889,16 @@ __global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
     }
 }
 
+// part[g][i] = sum of slabs s in [g*G, (g+1)*G) of ws[s][i], ascending: the first stage of a
+// two-stage slab sum when the slabs far outnumber the outputs (c2_wg_reduce alone would run a
+// few dozen workgroups, each adding hundreds of slabs in sequence)
+__global__ __launch_bounds__(256) void c2_slab_group_sum(const float* ws, int S, int G, int64_t n, float* part) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int g = blockIdx.y, s0 = g * G, cnt = min(G, S - s0);
+    part[(int64_t)g * n + i] = sum_strided(ws + (int64_t)s0 * n + i, cnt, n);
+}
+
 // dw[co][n] (+)= sum_s ws[s][co][n] for n < Nw; db[co] (+)= sum_s ws[s][co][Nw]. Fixed order
 // (slab_sum_256: 64 outputs per block, 4 split slices).
 __global__ __launch_bounds__(256) void c2_wg_reduce(const float* ws, int S, int Co, int N, float* dw, float* db,
@@ -2633,7 +2643,7 @@ size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64
     int splits = p.splits;
     if (wg3r_ok(g)) splits = max(splits, plan_wg3r(g, 32, wg3r_target(g)).splits);
     if (co1_ok(g)) splits = max(splits, plan_co1(g).splits);
-    if (wg3n_ok(g)) splits = max(splits, plan_wg3n(g).splits);
+    if (wg3n_ok(g)) splits = max(splits, plan_wg3n(g).splits + (int)cdiv(plan_wg3n(g).splits, 32));
     return (size_t)splits * Co * (Ci * KT * KF + 1) * sizeof(float);
 }
 
@@ -2676,8 +2686,14 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
         const int rc = Ci * KT <= 7 ? run_wgrad3<9, 1, 2, 2, 4, 4>(g, dy, yact, x, ws, q, st)
                                     : run_wgrad3<9, 1, 4, 2, 2, 4>(g, dy, yact, x, ws, q, st);
         if (rc == 0) {
-            hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, q.splits, (int)Co,
-                               N, dw, db, acc_w, acc_b);
+            // ~1500 slabs of Co x N outputs: groups of 32 slabs first, then the fixed-order sum
+            const int G = 32, S2 = (int)cdiv(q.splits, G);
+            const int64_t n = Co * N;
+            float* part = ws + (int64_t)q.splits * n;
+            hipLaunchKernelGGL(c2_slab_group_sum, dim3((unsigned)cdiv(n, 256), (unsigned)S2), dim3(256), 0, st, ws,
+                               q.splits, G, n, part);
+            hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(n, 64)), dim3(256), 0, st, part, S2, (int)Co, N, dw,
+                               db, acc_w, acc_b);
             ENCX_CHECK_LAUNCH();
             return 0;
         }
