@@ -273,6 +273,32 @@ int main(int argc, char** argv) {
                 var3("3<9,2,1,4,8,4> 6/768", 6, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 1, 4, 8, 4>(g, dy, yact, x, ws, q, st); });
                 var3("3<9,2,1,4,8,8> 6/1536", 6, 1536, [&](const WgPlan3& q) { return run_wgrad3<9, 2, 1, 4, 8, 8>(g, dy, yact, x, ws, q, st); });
                 var3("3<9,1,2,2,4,4> 6/768 noY", 6, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 2, 2, 4, 4>(g, dy, nullptr, x, ws, q, st); });
+            } else if (gc && l.KF == 3 && getenv("MB_L4_BN64")) {
+                // the 3x3 layer on 64-column tiles (5 tiles for its 289 columns instead of 3 x 128)
+                for (int tgt : {1024, 2048}) {
+                    WgPlan2 p2 = plan_wg2(g);
+                    p2.narrow = 1;
+                    p2.NCmax = 63 / l.KF + 2;
+                    const int tiles = (int)(cdiv(N, 64) * cdiv(l.Co, 32));
+                    int sp = (int)cdiv(tgt, tiles);
+                    if (sp > p2.items) sp = p2.items;
+                    p2.per_split = (int)cdiv(p2.items, sp);
+                    p2.splits = (int)cdiv(p2.items, p2.per_split);
+                    C2Wg a2{g, dy, yact, x, ws, p2.BT, p2.NR, p2.RL, p2.NCmax, p2.items, p2.per_split, p2.chunks};
+                    const size_t lds = ((size_t)4 * p2.NCmax * p2.NR + (size_t)p2.BT * 32 + (size_t)p2.NCmax * p2.NR * p2.RL) *
+                                           sizeof(float) + p2.BT * sizeof(int);
+                    const size_t red = (size_t)4 * 16 * 64 * sizeof(float);
+                    CK(hipMemset(dw1, 0, (size_t)l.Co * N * 4));
+                    double t = time_ms([&] {
+                        hipLaunchKernelGGL((c2_wgrad_kernel<32, 64, 1, 2, 2>), dim3((unsigned)cdiv(N, 64), 1, p2.splits),
+                                           dim3(NT), lds > red ? lds : red, st, a2);
+                        hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 64)), dim3(256), 0, st, ws, p2.splits,
+                                           l.Co, N, dw1, db1, 0, 0);
+                    });
+                    double e = fmax(rel_err(dw1, dw0, (size_t)l.Co * (N - 1)), rel_err(db1, db0, l.Co));
+                    printf("  wgrad <32,64,1,2,2> %d      %8.1f us  %6.1f TF/s  err %.1e%s  (splits %d)\n", tgt, t * 1e3,
+                           flops / t * 1e-9, e, e > 1e-5 ? "  MISMATCH" : "", p2.splits);
+                }
             } else if (gc && l.KF == 3) {
                 var3("3<3,1,9,16,1,1,PF0> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1, 1, 0>(g, dy, yact, x, ws, q, st); });
                 var3("3<3,1,9,16,1,1,PF1> 96/512", 96, 512, [&](const WgPlan3& q) { return run_wgrad3<3, 1, 9, 16, 1, 1, 1>(g, dy, yact, x, ws, q, st); });
