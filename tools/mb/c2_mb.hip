@@ -134,6 +134,9 @@ int main(int argc, char** argv) {
                 if (l.KF == 9) {
                     var("r<256,9,6,16>", [&] { if (run_fwdr<256, 9, 6, 16>(b, st)) printf("    (n/a)\n"); });
                     if (l.Ci == 2) {
+                        var("<32,128,1,4,KF9>", [&] { run_fwd<32, 128, 1, 4, 9>(b, st); });
+                        var("<32,256,1,4>", [&] { run_fwd<32, 256, 1, 4>(b, st); });
+                        var("<32,256,1,4,KF9>", [&] { run_fwd<32, 256, 1, 4, 9>(b, st); });
                         var("r<256,9,4,16,2>", [&] { if (run_fwdr<256, 9, 4, 16, 2>(b, st)) printf("    (n/a)\n"); });
                         var("r<256,9,3,16,3>", [&] { if (run_fwdr<256, 9, 3, 16, 3>(b, st)) printf("    (n/a)\n"); });
                         var("r<128,9,2,16,4>", [&] { if (run_fwdr<128, 9, 2, 16, 4>(b, st)) printf("    (n/a)\n"); });
