@@ -2612,10 +2612,11 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
         ENCX_CHECK_LAUNCH();
         return 0;
     }
-    // tile choice from tools/mb/c2_mb sweeps: 128-column tiles for the narrow late layers, 8-combo
+    // tile choice from tools/mb/c2_mb sweeps: 128-column tiles for the narrowest layers (Fo 33;
+    // at Fo 65 the 256-column tile is 4-7 % faster), 8-combo
     // chunks + a 3-waves/SIMD register cap for the wide ones
     if (M == 64 && KF == 9 && sf == 2) {
-        if (Fo <= 65 ? run_dgradr<2, 128, 5, 4, 16, 3>(a, st) == 0 : run_dgradr<2, 256, 5, 4, 8, 3>(a, st) == 0)
+        if (Fo <= 33 ? run_dgradr<2, 128, 5, 4, 16, 3>(a, st) == 0 : run_dgradr<2, 256, 5, 4, 8, 3>(a, st) == 0)
             return 0;
     }
     if (M <= 32 && KF == 3 && sf == 1 && run_dgradr<1, 256, 3, 6, 32>(a, st) == 0) return 0;
