@@ -140,6 +140,17 @@ struct BitOut {
     }
 };
 
+// The reference's coder state is Python ints (ac.py:56-260): within a push, low / high grow by
+// up to total_range_bits (<= 30) bits past max_bit (<= 61 after every flush, ac.py:157), so
+// they are held in 128 bits here (never more than 93 used); every interval width (delta, at
+// most 2^(bits+1)) and every product of a cdf value with it fits in 64.
+typedef unsigned __int128 u128;
+ENCX_DEV u128 lowmask128(int n) { return n <= 0 ? (u128)0 : (n >= 128 ? ~(u128)0 : (((u128)1 << n) - 1)); }
+ENCX_DEV int hibit128(u128 x) {  // index of the highest set bit, -1 for 0
+    const uint64_t h = (uint64_t)(x >> 64), l = (uint64_t)x;
+    return h ? 127 - __builtin_clzll(h) : (l ? 63 - __builtin_clzll(l) : -1);
+}
+
 __global__ void ac_encode_kernel(const int32_t* __restrict__ lohi, int64_t n, int S, int bits,
                                  uint8_t* __restrict__ out, int64_t cap, int64_t* __restrict__ nbytes,
                                  int* __restrict__ err) {
@@ -148,7 +159,7 @@ __global__ void ac_encode_kernel(const int32_t* __restrict__ lohi, int64_t n, in
     const int32_t* lh = lohi + (int64_t)s * n * 2;
     BitOut bo{out + (int64_t)s * cap, cap, 0, 0ull, 0};
     const uint64_t R = 1ull << bits;
-    uint64_t low = 0, high = 0;
+    u128 low = 0, high = 0;
     int max_bit = -1, e = 0;
     // the intervals do not depend on the coder state: fetch them 8 symbols at a time (one
     // memory round trip per 8 pushes instead of one per push)
@@ -163,32 +174,33 @@ __global__ void ac_encode_kernel(const int32_t* __restrict__ lohi, int64_t n, in
         for (int u = 0; u < 8; ++u) {
             if (i0 + u >= n || e) break;
             const uint64_t rl = iv[2 * u], rh = iv[2 * u + 1];
-            uint64_t delta = high - low + 1;
+            uint64_t delta = (uint64_t)(high - low) + 1;  // < 2^62 (both < 2^(max_bit+1))
             if (delta < R) {  // ac.py:139-142
                 const int sh = bits - (63 - __builtin_clzll(delta));
                 low <<= sh;
-                high = (high << sh) | lowmask(sh);
+                high = (high << sh) | lowmask128(sh);
                 max_bit += sh;
-                delta = high - low + 1;
+                delta = (uint64_t)(high - low) + 1;
             }
             const uint64_t el = (rl * delta + R - 1) >> bits, eh = (rh * delta) >> bits;  // ac.py:146-147
             high = low + eh;
             low = low + el;
             if (high >> (max_bit + 1)) { e = 1; break; }  // ac.py:116
-            const uint64_t x = low ^ high;                  // ac.py:111-128
-            const int hb = x ? 63 - __builtin_clzll(x) : -1;
+            const int hb = hibit128(low ^ high);           // ac.py:111-128
             const int nf = max_bit - hb;
             if (nf > 0) {
-                bo.put_msb_first(low >> (hb + 1), nf);
-                low &= lowmask(hb + 1);
-                high &= lowmask(hb + 1);
+                const u128 pre = low >> (hb + 1);  // the nf-bit common prefix, pushed msb first
+                if (nf > 64) bo.put_msb_first((uint64_t)(pre >> 64), nf - 64);
+                bo.put_msb_first((uint64_t)pre, nf > 64 ? 64 : nf);
+                low &= lowmask128(hb + 1);
+                high &= lowmask128(hb + 1);
                 max_bit = hb;
             }
             if (max_bit > 61) { e = 3; break; }  // ac.py:157
         }
     }
     if (!e) {
-        bo.put_msb_first(low, max_bit + 1);  // flush (ac.py:160-167)
+        bo.put_msb_first((uint64_t)low, max_bit + 1);  // flush (ac.py:160-167); max_bit <= 61
         if (bo.nb) {
             if (bo.pos < cap) bo.o[bo.pos] = (uint8_t)(bo.acc & 0xff);
             ++bo.pos;
@@ -199,7 +211,8 @@ __global__ void ac_encode_kernel(const int32_t* __restrict__ lohi, int64_t n, in
     err[s] = e;
 }
 
-// decoder state per stream: low, high, current, max_bit, bits consumed
+// decoder state per stream (ENCX_AC_STATE int64 words): low, high, current (128 bits each,
+// low word first), max_bit, bits consumed
 __global__ __launch_bounds__(64) void ac_decode_kernel(
     const uint8_t* __restrict__ data, int64_t stride, const int64_t* __restrict__ nbytes,
     int64_t* __restrict__ state, const int32_t* __restrict__ cdf, int K, int card, int bits,
@@ -208,16 +221,20 @@ __global__ __launch_bounds__(64) void ac_decode_kernel(
     const int s = blockIdx.x, lane = threadIdx.x;
     if (err[s]) return;  // the stream already failed; later steps leave it as it is
     if (dstep) t += *dstep;
-    int64_t* stt = state + (int64_t)s * 5;
-    uint64_t low = (uint64_t)stt[0], high = (uint64_t)stt[1], cur = (uint64_t)stt[2];
-    int max_bit = (int)stt[3];
-    int64_t pos = stt[4];
+    int64_t* stt = state + (int64_t)s * ENCX_AC_STATE;
+    auto ld128 = [&](int i) { return ((u128)(uint64_t)stt[2 * i + 1] << 64) | (u128)(uint64_t)stt[2 * i]; };
+    u128 low = ld128(0), high = ld128(1), cur = ld128(2);
+    int max_bit = (int)stt[6];
+    int64_t pos = stt[7];
     const int64_t nbits = nbytes[s] * 8;
     const uint8_t* src = data + (int64_t)s * stride;
     const uint64_t R = 1ull << bits;
     int e = 0;
     for (int k = 0; k < K; ++k) {
-        uint64_t delta = high - low + 1;
+        // the reference decoder has no bound on max_bit (ac.py:217-260); a stream its encoder
+        // wrote keeps it <= 61 after every pull, so past 96 the stream is not one it could write
+        if (max_bit > 96) { e = 3; break; }
+        uint64_t delta = (uint64_t)(high - low) + 1;
         if (delta < R) {  // ac.py:226-233
             const int sh = bits - (63 - __builtin_clzll(delta));
             if (pos + sh > nbits) { e = 1; break; }  // BitUnpacker ran dry: pull returns None
@@ -230,15 +247,15 @@ __global__ __launch_bounds__(64) void ac_decode_kernel(
                 win |= (uint64_t)src[bi] << (8 * u);
             }
             const uint64_t chunk = (win >> (pos & 7)) & lowmask(sh);   // stream bit pos at bit 0
-            cur = (cur << sh) | (__builtin_bitreverse64(chunk) >> (64 - sh));
+            cur = (cur << sh) | (u128)(__builtin_bitreverse64(chunk) >> (64 - sh));
             pos += sh;
             low <<= sh;
-            high = (high << sh) | lowmask(sh);
+            high = (high << sh) | lowmask128(sh);
             max_bit += sh;
-            delta = high - low + 1;
+            delta = (uint64_t)(high - low) + 1;
         }
         const int32_t* row = cdf + ((int64_t)s * K + k) * card;
-        const uint64_t off = cur - low;
+        const uint64_t off = (uint64_t)(cur - low);  // < delta when the stream is consistent
         int found = -1;
         for (int j0 = 0; j0 < card; j0 += 64 * 16) {   // 16 entries per lane in flight together
             int32_t cl[16], ch[16];
@@ -268,12 +285,11 @@ __global__ __launch_bounds__(64) void ac_decode_kernel(
         const uint64_t el = (rl * delta + R - 1) >> bits, eh = (rh * delta) >> bits;
         high = low + eh;
         low = low + el;
-        const uint64_t x = low ^ high;  // ac.py:201-215
-        const int hb = x ? 63 - __builtin_clzll(x) : -1;
+        const int hb = hibit128(low ^ high);  // ac.py:201-215
         if (max_bit > hb) {
-            low &= lowmask(hb + 1);
-            high &= lowmask(hb + 1);
-            cur &= lowmask(hb + 1);
+            low &= lowmask128(hb + 1);
+            high &= lowmask128(hb + 1);
+            cur &= lowmask128(hb + 1);
             max_bit = hb;
         }
         if (lane == 0) {
@@ -282,11 +298,14 @@ __global__ __launch_bounds__(64) void ac_decode_kernel(
         }
     }
     if (lane == 0) {
-        stt[0] = (int64_t)low;
-        stt[1] = (int64_t)high;
-        stt[2] = (int64_t)cur;
-        stt[3] = max_bit;
-        stt[4] = pos;
+        const u128 w[3] = {low, high, cur};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            stt[2 * i] = (int64_t)(uint64_t)w[i];
+            stt[2 * i + 1] = (int64_t)(uint64_t)(w[i] >> 64);
+        }
+        stt[6] = max_bit;
+        stt[7] = pos;
         err[s] = e;
     }
 }

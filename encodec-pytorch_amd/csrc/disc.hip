@@ -773,6 +773,162 @@ __global__ __launch_bounds__(NT, OCC) void c2_fwdr_kernel(C2Fwd a) {
     }
 }
 
+// A quad meant to start at element offset o of a tensor whose last quad starts at `last` is
+// loaded from min(max(o, 0), last) (never outside the tensor); quad_abs moves it into place:
+// o[e] = v[e + sh], sh = o - clamped, zero where e + sh leaves the quad. Only the tensor's first
+// and last quads are ever clamped, and there |sh| < 4 matters: the rest is padding, masked by
+// the caller. Two select layers on the bits of |sh| (a select chain on sh == k compiles to
+// branches).
+ENCX_DEV f32x4 quad_abs(f32x4 v, int o, int last) {
+    const int sh = o < 0 ? o : (o > last ? o - last : 0);
+    const int n = sh < 0 ? -sh : sh;
+    const bool b1 = n & 1, b2 = n & 2;
+    f32x4 r;
+    if (sh >= 0) {  // down: r[e] = v[e + n]
+        const float t0 = b1 ? v[1] : v[0], t1 = b1 ? v[2] : v[1], t2 = b1 ? v[3] : v[2], t3 = b1 ? 0.f : v[3];
+        r[0] = b2 ? t2 : t0;
+        r[1] = b2 ? t3 : t1;
+        r[2] = b2 ? 0.f : t2;
+        r[3] = b2 ? 0.f : t3;
+    } else {  // up: r[e] = v[e - n]
+        const float t0 = b1 ? 0.f : v[0], t1 = b1 ? v[0] : v[1], t2 = b1 ? v[1] : v[2], t3 = b1 ? v[2] : v[3];
+        r[0] = b2 ? 0.f : t0;
+        r[1] = b2 ? 0.f : t1;
+        r[2] = b2 ? t0 : t2;
+        r[3] = b2 ? t1 : t3;
+    }
+    return r;
+}
+
+// Forward, register-window form. The 32 x (Ci*KT*KF) weights of the layer are staged ONCE per
+// workgroup into LDS ([(ci,kt)][kf][32 co], the wf layout), then each wave loops over tiles of
+// 32 output-position QUADS (128 positions; rows padded to whole quads, F4 = ceil(Fo/4) quads
+// per row). Lane l of a wave owns quad l: its 4 consecutive output columns f0..f0+3 are the
+// MFMA columns of its 4 accumulators (jb = 0..3). The MFMA's two k slots are two input channels
+// (ci = 2c + h), so per (c, kt) step each lane loads ONE contiguous input window
+// x[ci][t + kt*dt - pt][S*f0 - pf .. + 3S + KF - 1] (WQ quads, straight from global memory into
+// registers) which holds the operand of all KF taps x 4 columns: 4 * KF MFMAs per step, each
+// with no address arithmetic, the A operand (weights) one ds_read_b32 per tap shared by the 4
+// columns. The next step's window is loaded before this step's MFMAs. Window elements outside
+// the input (padding, rows outside [0, T2), the tensor's ends) are zeroed by a per-lane
+// element mask, only in waves that have such a lane. Bias + LeakyReLU(0.2) in the epilogue.
+struct C2FwdR {
+    C2Geo g;
+    const float* x;
+    const float* wf;  // [(ci,kt)][kf][co]
+    const float* bias;
+    float* y;
+    int act;
+    int F4;     // quads per output row
+    int tiles;  // ceil(B * T2 * F4 / 32)
+};
+template <int KF, int S, int WQ, int NWV>
+__global__ __launch_bounds__(NWV * 64, 2) void c2_fwd_rw_kernel(C2FwdR a) {
+    constexpr int NE = 4 * WQ, KT = 3;  // window elements per lane; kernel rows (host-checked)
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    float* Ws = smem;                          // [Ci*KT][KF][32]
+    float* Bs = smem + g.Ci * KT * KF * 32;    // [32] bias
+    for (int i = threadIdx.x; i < g.Ci * KT * KF * 32; i += NWV * 64) {
+        const int co = i & 31, r = i >> 5;
+        Ws[i] = co < g.Co ? a.wf[r * g.Co + co] : 0.f;
+    }
+    if (threadIdx.x < 32) Bs[threadIdx.x] = (a.bias && (int)threadIdx.x < g.Co) ? a.bias[threadIdx.x] : 0.f;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l = lane & 31;
+    // element offsets fit in 32 bits (checked on the host)
+    const int quads = g.B * g.T2 * a.F4;
+    const int plane = g.T2 * g.Fi, xlast = g.B * g.Ci * plane - 4;
+    const int CP = g.Ci >> 1;  // channel pairs
+    const int cstride = 2 * plane;
+    for (int tile = blockIdx.x * NWV + wave; tile < a.tiles; tile += gridDim.x * NWV) {
+        const int qd = min(tile * 32 + l, quads - 1);
+        const int fq = qd % a.F4, bt = qd / a.F4;
+        const int t = bt % g.T2, b = bt / g.T2;
+        const int f0 = 4 * fq, col0 = S * f0 - g.pf;
+        // window element e of step (c, kt) is x[b][2c + h][row(kt)][col0 + e]
+        uint32_t cmask = 0;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) cmask |= (col0 + e >= 0 && col0 + e < g.Fi) ? (1u << e) : 0u;
+        int rb[KT];
+        uint32_t msk[KT];
+        bool clean = true;  // every element of every window of this lane is in the input
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+            const int row = t + kt * g.dt - g.pt;
+            const bool ok = row >= 0 && row < g.T2;
+            rb[kt] = (b * g.Ci + h) * plane + (ok ? row : 0) * g.Fi + col0;
+            msk[kt] = ok ? cmask : 0u;
+            clean = clean && msk[kt] == (1u << NE) - 1;
+        }
+        const bool fix = !__all(clean);  // wave-uniform
+        auto load = [&](f32x4* w, int c, int kt) {
+            const int base = rb[kt] + c * cstride;
+#pragma unroll
+            for (int q = 0; q < WQ; ++q) w[q] = ld4u(a.x + min(max(base + 4 * q, 0), xlast));
+        };
+        f32x16 acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = (f32x16){0};
+        // three register windows, one per kt: step (c, kt) multiplies window kt while the next
+        // step's window is in flight (the prefetch is unconditional, so every wait is exact)
+        f32x4 wb[KT][WQ];
+        load(wb[0], 0, 0);
+        for (int c = 0; c < CP; ++c) {
+#pragma unroll
+            for (int kt = 0; kt < KT; ++kt) {
+                if (kt + 1 < KT) load(wb[kt + 1], c, kt + 1);
+                else load(wb[0], min(c + 1, CP - 1), 0);
+                f32x4* w = wb[kt];
+                if (fix) {
+                    const int base = rb[kt] + c * cstride;
+#pragma unroll
+                    for (int q = 0; q < WQ; ++q) {
+                        const int o = base + 4 * q;
+                        if (__any(o < 0 || o > xlast)) w[q] = quad_abs(w[q], o, xlast);  // tensor ends
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (!((msk[kt] >> (4 * q + e)) & 1u)) w[q][e] = 0.f;
+                    }
+                }
+                const float* wk = Ws + ((2 * c + h) * KT + kt) * KF * 32 + l;
+#pragma unroll
+                for (int kf = 0; kf < KF; ++kf) {
+                    const float av = wk[kf * 32];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = S * j + kf;
+                        acc[j] = mfma32(av, w[r >> 2][r & 3], acc[j]);
+                    }
+                }
+            }
+        }
+        // ---- epilogue: rows co, columns f0 + j of this lane's quad
+        if (tile * 32 + l < quads) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = mfma_row(r, lane);
+                if (co >= g.Co) continue;
+                const float bco = Bs[co];
+                f32x4 v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float u = acc[j][r] + bco;
+                    v[j] = a.act ? lrelu(u) : u;
+                }
+                float* dst = a.y + (((int64_t)b * g.Co + co) * g.T2 + t) * g.Fo + f0;
+                if (f0 + 4 <= g.Fo) {
+                    *(f32x4u*)dst = v;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (f0 + j < g.Fo) dst[j] = v[j];
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------ backward data
 struct C2Dg {
     C2Geo g;
@@ -1220,6 +1376,193 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
         }
 }
 
+
+// Backward-data, register-window form (c2_fwd_rw_kernel's scheme on c2_dgradr_kernel's
+// polyphase GEMM): rows m = (ci, r) (M = Ci*S: TM tiles of 32), columns = output-column QUADS
+// of the polyphase grid (t, u), rows padded to whole quads (U4 per row); lane l of a wave owns
+// quad l, its 4 accumulators per row tile are the columns u0..u0+3. The k slots are two output
+// channels (co = 2c + h): per (c, kt) step each lane loads ONE window of the output grad
+// dy[co][t + pt - kt*dt][u0 - J + 1 .. u0 + 3] (+ the same window of y for LeakyReLU'(y)),
+// which holds the operand of all J taps x 4 columns: J * 4 * TM MFMAs per step, the polyphase
+// weights (staged once per workgroup in LDS, wp layout) one ds_read_b32 per tap and row tile.
+// Epilogue: the feature-matching term, LeakyReLU'(x), accumulate, as c2_dgradr_kernel; the
+// 2S consecutive input columns a lane holds per ci are written as quads.
+struct C2DgR {
+    C2Dg d;
+    int U4;     // quads per polyphase row
+    int tiles;  // ceil(B * T2 * U4 / 32)
+};
+template <int J, int S, int TM, int WQ, bool YM, int NWV>
+__global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
+    constexpr int NE = 4 * WQ, KT = 3, M = 32 * TM;
+    const C2Dg& a = R.d;
+    extern __shared__ float smem[];
+    const C2Geo g = a.g;
+    float* As = smem;  // [(co,kt)][J][M]: the wp layout (M == Ci*S, host-checked)
+    for (int i = threadIdx.x; i < g.Co * KT * J * M; i += NWV * 64) As[i] = a.wp[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l = lane & 31;
+    // element offsets fit in 32 bits (checked on the host)
+    const int quads = g.B * g.T2 * R.U4;
+    const int plane = g.T2 * g.Fo, ylast = g.B * g.Co * plane - 4;
+    const int CP = g.Co >> 1, cstride = 2 * plane;
+    const float fc = feat_coef(a);
+    for (int tile = blockIdx.x * NWV + wave; tile < R.tiles; tile += gridDim.x * NWV) {
+        const int qd = min(tile * 32 + l, quads - 1);
+        const int uq = qd % R.U4, bt = qd / R.U4;
+        const int t = bt % g.T2, b = bt / g.T2;
+        const int u0 = 4 * uq, e0 = u0 - (J - 1);  // dy column of window element 0
+        uint32_t cmask = 0;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) cmask |= (e0 + e >= 0 && e0 + e < g.Fo) ? (1u << e) : 0u;
+        int rb[KT];
+        uint32_t msk[KT];
+        bool clean = true;
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+            const int row = t + g.pt - kt * g.dt;
+            const bool ok = row >= 0 && row < g.T2;
+            rb[kt] = (b * g.Co + h) * plane + (ok ? row : 0) * g.Fo + e0;
+            msk[kt] = ok ? cmask : 0u;
+            clean = clean && msk[kt] == (1u << NE) - 1;
+        }
+        const bool fix = !__all(clean);  // wave-uniform
+        f32x4 wb[KT][WQ], yb[KT][WQ];
+        auto load = [&](int k, int c, int kt) {
+            const int base = rb[kt] + c * cstride;
+#pragma unroll
+            for (int q = 0; q < WQ; ++q) {
+                const int o = min(max(base + 4 * q, 0), ylast);
+                wb[k][q] = ld4u(a.dy + o);
+                if (YM) yb[k][q] = ld4u(a.yact + o);
+            }
+        };
+        f32x16 acc[TM][4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){0};
+        load(0, 0, 0);
+        for (int c = 0; c < CP; ++c) {
+#pragma unroll
+            for (int kt = 0; kt < KT; ++kt) {
+                if (kt + 1 < KT) load(kt + 1, c, kt + 1);
+                else load(0, min(c + 1, CP - 1), 0);
+                f32x4* w = wb[kt];
+                if (YM) {
+#pragma unroll
+                    for (int q = 0; q < WQ; ++q)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) w[q][e] *= lrelu_grad(yb[kt][q][e]);
+                }
+                if (fix) {
+                    const int base = rb[kt] + c * cstride;
+#pragma unroll
+                    for (int q = 0; q < WQ; ++q) {
+                        const int o = base + 4 * q;
+                        if (__any(o < 0 || o > ylast)) w[q] = quad_abs(w[q], o, ylast);  // tensor ends
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (!((msk[kt] >> (4 * q + e)) & 1u)) w[q][e] = 0.f;
+                    }
+                }
+                const float* ak = As + ((2 * c + h) * KT + kt) * J * M + l;
+#pragma unroll
+                for (int q = 0; q < J; ++q) {
+                    float av[TM];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) av[i] = ak[q * M + i * 32];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = j - q + J - 1;  // window element of column u0 + j, tap q
+#pragma unroll
+                        for (int i = 0; i < TM; ++i) acc[i][j] = mfma32(av[i], w[r >> 2][r & 3], acc[i][j]);
+                    }
+                }
+            }
+        }
+        // ---- epilogue
+        if (tile * 32 + l >= quads) continue;
+        if (S == 2) {
+            // registers r, r + 1 are phases 0 / 1 of one ci: with the 4 columns, 8 consecutive f
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                    const int ci = (i * 32 + mfma_row(r, lane)) >> 1;
+                    const int f = 2 * u0 - g.pf;
+                    const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
+                    float v[8];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        v[2 * j] = acc[i][j][r];
+                        v[2 * j + 1] = acc[i][j][r + 1];
+                    }
+                    if (f >= 0 && f + 8 <= g.Fi) {
+#pragma unroll
+                        for (int hq = 0; hq < 2; ++hq) {
+                            f32x4 x4, r4, d4;
+                            if (a.ffr) {
+                                x4 = ld4u(a.ffx + o + 4 * hq);
+                                r4 = ld4u(a.ffr + o + 4 * hq);
+                            }
+                            if (a.xact && !(a.ffr && a.ffx == a.xact)) x4 = ld4u(a.xact + o + 4 * hq);
+                            if (a.accumulate) d4 = ld4u(a.dx + o + 4 * hq);
+                            f32x4 s4;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                float u = v[4 * hq + e];
+                                if (a.ffr) {
+                                    const float d = x4[e] - r4[e];
+                                    u += d > 0.f ? fc : (d < 0.f ? -fc : 0.f);
+                                }
+                                if (a.xact) u *= lrelu_grad(x4[e]);
+                                s4[e] = a.accumulate ? d4[e] + u : u;
+                            }
+                            *(f32x4u*)(a.dx + o + 4 * hq) = s4;
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            if (f + e >= 0 && f + e < g.Fi) a.dx[o + e] = dg_out(a, fc, o + e, v[e]);
+                    }
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int ci = i * 32 + mfma_row(r, lane);
+                    const int f = u0 - g.pf;
+                    const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
+                    if (f >= 0 && f + 4 <= g.Fi) {
+                        f32x4 x4, r4, d4, s4;
+                        if (a.ffr) {
+                            x4 = ld4u(a.ffx + o);
+                            r4 = ld4u(a.ffr + o);
+                        }
+                        if (a.xact && !(a.ffr && a.ffx == a.xact)) x4 = ld4u(a.xact + o);
+                        if (a.accumulate) d4 = ld4u(a.dx + o);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float u = acc[i][e][r];
+                            if (a.ffr) {
+                                const float d = x4[e] - r4[e];
+                                u += d > 0.f ? fc : (d < 0.f ? -fc : 0.f);
+                            }
+                            if (a.xact) u *= lrelu_grad(x4[e]);
+                            s4[e] = a.accumulate ? d4[e] + u : u;
+                        }
+                        *(f32x4u*)(a.dx + o) = s4;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (f + e >= 0 && f + e < g.Fi) a.dx[o + e] = dg_out(a, fc, o + e, acc[i][e][r]);
+                    }
+                }
+        }
+    }
+}
 
 // Narrow backward-data (M = Ci <= 4 rows, stride 1 along f: the first layer's grad into the
 // spectrogram). A 32-row MFMA tile would carry 2 useful rows, so this runs on the vector ALU:
@@ -1889,6 +2232,170 @@ __global__ __launch_bounds__(NW * 64, OCC) void c2_wgrad3_kernel(C2Wg3 a) {
     }
 }
 
+// Weight grad, register-window form: no LDS, no staging. The GEMM's reduction index is the
+// output position, and the MFMA's two k slots are two positions, so the 32 x 32 tile of one tap
+// (kt, kf) is D[co][ci] = sum_p dy'[co][p] x[ci][row(p, kt)][S p + kf - pf]. A wave owns 9 taps
+// (one kt of a 3x9 layer, or all of a 3x3 layer) and walks (b, t, 8-position chunk) items; half
+// h of the wave takes positions f0 + 4h .. f0 + 4h + 3 of a chunk, so
+//   A: lane (h, co) needs dy'[co][t][f0 + 4h + q], q < 4: ONE quad load (+ the y quad for
+//      LeakyReLU'(y)),
+//   B: lane (h, ci) needs, for all 9 taps and the 4 positions, x[ci][row][S (f0 + 4h) - pf + r],
+//      r < 3S + KF: one contiguous window of WQ quads per kt row,
+// and a chunk is 9 taps x 4 positions = 36 MFMAs on 9 accumulator chains (one per tap), with
+// no LDS read and no address arithmetic between them. The next item's quads are loaded before the
+// current item's MFMAs (register double buffer). Each wave writes its 32 x 32 x 9 partial to
+// the split slab ws[split][co][n] (c2_wg_reduce sums the slabs in a fixed order).
+struct C2WgR {
+    C2Geo g;
+    const float* dy;
+    const float* yact;
+    const float* x;
+    float* ws;      // [splits][Co][N], N = Ci*KT*KF + 1
+    int NC;         // 8-position chunks per output row
+    int items;      // B * T2 * NC
+    int per_split;  // items per wave
+    int ktg;        // kt groups (tasks per split per ci block): KT for KF = 9, 1 for KF = 3
+    int cib;        // 32-channel ci blocks
+};
+template <int KTW, int WQ>
+struct RwStage {  // one item's operands, loaded a whole item ahead of their MFMAs
+    f32x4 av, yv, xw[KTW][WQ];
+    int p, col0;  // this lane's first position / first input column (for the edge masks)
+    int sha;      // the dy / y quad's shift (nonzero only at the very end of the tensor)
+    int xo[KTW];  // this lane's first window element offset per kt row (unclamped)
+    bool edge;    // wave-uniform: some element of this item lies outside its row
+    bool rok[KTW];
+};
+template <int KF, int S, int KTW, int WQ, bool YM>
+__global__ __launch_bounds__(64, 2) void c2_wgrad_rw_kernel(C2WgR a) {
+    constexpr int NTAP = KTW * KF;
+    const C2Geo g = a.g;
+    const int lane = threadIdx.x, h = lane >> 5, l = lane & 31;
+    const int id = xcd_linear_id();
+    const int kg = id % a.ktg, rest = id / a.ktg, cb = rest % a.cib, split = rest / a.cib;
+    const int kt0 = kg * KTW, ci = cb * 32 + l;
+    const bool ci_ok = ci < g.Ci, co_ok = l < g.Co;
+    const bool full = g.Co >= 32 && (cb + 1) * 32 <= g.Ci;  // every lane's row and column exist
+    const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
+    // element offsets fit in 32 bits (checked on the host)
+    const int plane_y = g.T2 * g.Fo, plane_x = g.T2 * g.Fi;
+    const int ylast = g.B * g.Co * plane_y - 4, xlast = g.B * g.Ci * plane_x - 4;
+    f32x16 acc[NTAP];
+#pragma unroll
+    for (int j = 0; j < NTAP; ++j) acc[j] = (f32x16){0};
+    float bsum = 0.f;
+    // ---- issue the loads of item it; nothing waits for them until compute(). Every quad is one
+    // (unaligned) load at its own address, so every item issues the same loads: elements past a
+    // row's ends read the neighbouring row (in bounds) and compute() zeroes them; only a quad
+    // past the END of the tensor is read from a clamped address and shifted.
+    auto load = [&](RwStage<KTW, WQ>& st, int it) {
+        const int c = it % a.NC, bt = it / a.NC, t = bt % g.T2, b = bt / g.T2;
+        const int f0 = c * 8, p = f0 + 4 * h;
+        const int oa = (b * g.Co + (co_ok ? l : 0)) * plane_y + t * g.Fo + p;
+        const int oac = min(oa, ylast);
+        st.av = ld4u(a.dy + oac);
+        if (YM) st.yv = ld4u(a.yact + oac);
+        st.sha = oa - oac;
+        const int col0 = S * p - g.pf;
+        const int xb = (b * g.Ci + (ci_ok ? ci : 0)) * plane_x + col0;
+#pragma unroll
+        for (int k = 0; k < KTW; ++k) {
+            const int row = t + (kt0 + k) * g.dt - g.pt;
+            st.rok[k] = row >= 0 && row < g.T2;
+            const int rb = xb + (st.rok[k] ? row : 0) * g.Fi;
+#pragma unroll
+            for (int w = 0; w < WQ; ++w) st.xw[k][w] = ld4u(a.x + min(max(rb + 4 * w, 0), xlast));
+            st.xo[k] = rb;
+        }
+        st.p = p;
+        st.col0 = col0;
+        st.edge = f0 + 8 > g.Fo || S * f0 - g.pf < 0 || S * (f0 + 4) - g.pf + 4 * WQ > g.Fi;
+    };
+    // ---- the 9 taps x 4 positions of one item
+    auto compute = [&](RwStage<KTW, WQ>& st) {
+        if (st.edge) {
+            if (__any(st.sha != 0)) {
+                st.av = quad_abs(st.av, ylast + st.sha, ylast);
+                if (YM) st.yv = quad_abs(st.yv, ylast + st.sha, ylast);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (st.p + e >= g.Fo) st.av[e] = 0.f;
+#pragma unroll
+            for (int w = 0; w < WQ; ++w) {
+#pragma unroll
+                for (int k = 0; k < KTW; ++k) {  // the tensor's first / last quad
+                    const int o = st.xo[k] + 4 * w;
+                    if (__any(o < 0 || o > xlast)) st.xw[k][w] = quad_abs(st.xw[k][w], o, xlast);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int col = st.col0 + 4 * w + e;
+                    if (col < 0 || col >= g.Fi) {
+#pragma unroll
+                        for (int k = 0; k < KTW; ++k) st.xw[k][w][e] = 0.f;
+                    }
+                }
+            }
+        }
+        if (!full) {
+            if (!co_ok) st.av = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < KTW; ++k)
+#pragma unroll
+                for (int w = 0; w < WQ; ++w)
+                    if (!ci_ok) st.xw[k][w] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+        f32x4 ca = st.av;
+        if (YM) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ca[e] *= lrelu_grad(st.yv[e]);
+        }
+        bsum += (ca[0] + ca[1]) + (ca[2] + ca[3]);
+#pragma unroll
+        for (int k = 0; k < KTW; ++k) {
+            if (!st.rok[k]) continue;  // a kt row outside the input contributes zero
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int kf = 0; kf < KF; ++kf) {
+                    const int r = S * q + kf;
+                    acc[k * KF + kf] = mfma32(ca[q], st.xw[k][r >> 2][r & 3], acc[k * KF + kf]);
+                }
+        }
+    };
+    // two register stages, alternating: item it + 1 is in flight while item it computes
+    // The prefetches are unconditional (past the end they re-load the last item and are never
+    // used), so every path issues the same loads and each wait is for exactly the older item.
+    RwStage<KTW, WQ> s0, s1;
+    if (it_beg < it_end) load(s0, it_beg);
+    for (int it = it_beg; it < it_end; it += 2) {
+        load(s1, min(it + 1, it_end - 1));
+        compute(s0);
+        if (it + 1 >= it_end) break;
+        load(s0, min(it + 2, it_end - 1));
+        compute(s1);
+    }
+    // ---- the partial: D[co][ci] of tap (kt0 + k, kf) -> ws[split][co][(ci*KT + kt)*KF + kf]
+    const int N = g.Ci * g.KT * KF + 1;
+    float* wsb = a.ws + (int64_t)split * g.Co * N;
+    if (ci_ok) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = mfma_row(r, lane);
+            if (co < g.Co) {
+                float* dst = wsb + (int64_t)co * N + (ci * g.KT + kt0) * KF;
+#pragma unroll
+                for (int j = 0; j < NTAP; ++j) dst[j] = acc[j][r];
+            }
+        }
+    }
+    if (kg == 0 && cb == 0) {
+        bsum += __shfl_xor(bsum, 32, 64);
+        if (h == 0 && co_ok) wsb[(int64_t)l * N + N - 1] = bsum;
+    }
+}
+
 // part[g][i] = sum of slabs s in [g*G, (g+1)*G) of ws[s][i], ascending: the first stage of a
 // two-stage slab sum when the slabs far outnumber the outputs (c2_wg_reduce alone would run a
 // few dozen workgroups, each adding hundreds of slabs in sequence)
@@ -2344,6 +2851,63 @@ int run_fwdq(C2Fwd a, hipStream_t st) {
     return 0;
 }
 
+// register-window backward-data (c2_dgrad_rw_kernel): 3x9 stride 2 (M = 64) and 3x3 stride 1
+// (M = 32) layers with even Co; the polyphase weights in LDS
+static bool dgr_ok(const C2Geo& g) {
+    if ((g.Co & 1) || g.KT != 3 || g.Fi < 4 || g.Fo < 4) return false;
+    if (!((g.KF == 9 && g.sf == 2 && g.Ci == 32) || (g.KF == 3 && g.sf == 1 && g.Ci == 32))) return false;
+    if ((int64_t)g.B * g.Co * g.T2 * g.Fo >= (1ll << 31) - 64) return false;
+    const int J = (g.KF + g.sf - 1) / g.sf;
+    return (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float) <= 150 * 1024;
+}
+static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st) {
+    const C2Geo& g = d.g;
+    if (!dgr_ok(g)) return ENCX_EINVAL;
+    constexpr int NWV = 8;
+    C2DgR R{d, 0, 0};
+    R.d.U = (g.Fi - 1 + g.pf) / g.sf + 1;
+    R.U4 = (int)cdiv(R.d.U, 4);
+    R.tiles = (int)cdiv((int64_t)g.B * g.T2 * R.U4, 32);
+    const int J = (g.KF + g.sf - 1) / g.sf;
+    const size_t lds = (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float);
+    const int grid = (int)min((int64_t)wgs, cdiv(R.tiles, NWV));
+    const bool ym = d.yact != nullptr;
+    if (g.KF == 9) {
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV>), dim3(grid), dim3(NWV * 64), lds, st, R);
+    } else {
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV>), dim3(grid), dim3(NWV * 64), lds, st, R);
+    }
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+// register-window forward (c2_fwd_rw_kernel): 32-wide output-channel tile, even Ci, KT <= 3,
+// the layer's weights in LDS (<= 128 KB)
+static bool fwr_ok(const C2Geo& g) {
+    if (g.Co > 32 || (g.Ci & 1) || g.KT != 3 || g.Fo < 1 || g.Fi < 4) return false;
+    if ((int64_t)g.B * g.Ci * g.T2 * g.Fi >= (1ll << 31) || (int64_t)g.B * g.T2 * cdiv(g.Fo, 4) >= (1ll << 31) - 64)
+        return false;
+    if (!((g.KF == 9 && (g.sf == 2 || g.sf == 1)) || (g.KF == 3 && g.sf == 1))) return false;
+    return (size_t)g.Ci * g.KT * g.KF * 32 * sizeof(float) <= 128 * 1024;
+}
+static int run_fwd_rw(const C2Fwd& f, int wgs, hipStream_t st) {
+    const C2Geo& g = f.g;
+    if (!fwr_ok(g)) return ENCX_EINVAL;
+    constexpr int NWV = 8;
+    C2FwdR a{g, f.x, f.wf, f.bias, f.y, f.act, (int)cdiv(g.Fo, 4), 0};
+    a.tiles = (int)cdiv((int64_t)g.B * g.T2 * a.F4, 32);
+    const size_t lds = ((size_t)g.Ci * g.KT * g.KF * 32 + 32) * sizeof(float);
+    const int grid = (int)min((int64_t)wgs, cdiv(a.tiles, NWV));
+    if (g.KF == 9 && g.sf == 2)
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 2, 4, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
+    else if (g.KF == 9)
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 1, 3, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
+    else
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<3, 1, 2, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
 template <int BN, int KFC, int MQ, int CKM, int OCC = 1>
 int run_fwdr(C2Fwd a, hipStream_t st) {
     a.NR = c2_rows(BN, a.g.Fo);
@@ -2466,6 +3030,46 @@ int run_wgrad3(const C2Geo& g, const float* dy, const float* yact, const float* 
 }
 
 
+// register-window weight grad (c2_wgrad_rw_kernel): 3x9 stride-2 and 3x3 stride-1 layers with
+// 32-channel blocks of input channels and <= 32 output channels
+struct WgPlanR {
+    int NC, items, ktg, cib, splits, per_split;
+};
+static bool wgr_ok(const C2Geo& g) {
+    if (g.Co > 32 || g.Ci < 16 || g.KT != 3 || g.Fo < 4 || g.Fi < 4) return false;
+    if ((int64_t)g.B * g.Ci * g.T2 * g.Fi >= (1ll << 31) - 64 || (int64_t)g.B * g.Co * g.T2 * g.Fo >= (1ll << 31) - 64)
+        return false;
+    return (g.KF == 9 && g.sf == 2) || (g.KF == 3 && g.sf == 1);
+}
+static WgPlanR plan_wgr(const C2Geo& g, int waves = 2048) {
+    WgPlanR p;
+    p.NC = (int)cdiv(g.Fo, 8);
+    p.items = g.B * g.T2 * p.NC;
+    p.ktg = g.KF == 9 ? g.KT : 1;
+    p.cib = (int)cdiv(g.Ci, 32);
+    const int per = p.ktg * p.cib;
+    int sp = (int)cdiv(waves, per);
+    if (sp > p.items) sp = p.items;
+    p.per_split = (int)cdiv(p.items, sp);
+    p.splits = (int)cdiv(p.items, p.per_split);
+    return p;
+}
+static int run_wgrad_rw(const C2Geo& g, const float* dy, const float* yact, const float* x, float* ws,
+                        const WgPlanR& p, hipStream_t st) {
+    if (!wgr_ok(g)) return ENCX_EINVAL;
+    C2WgR a{g, dy, yact, x, ws, p.NC, p.items, p.per_split, p.ktg, p.cib};
+    const dim3 grid((unsigned)(p.splits * p.ktg * p.cib)), blk(64);
+    if (g.KF == 9) {
+        if (yact) hipLaunchKernelGGL((c2_wgrad_rw_kernel<9, 2, 1, 4, true>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((c2_wgrad_rw_kernel<9, 2, 1, 4, false>), grid, blk, 0, st, a);
+    } else {
+        if (yact) hipLaunchKernelGGL((c2_wgrad_rw_kernel<3, 1, 3, 2, true>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((c2_wgrad_rw_kernel<3, 1, 3, 2, false>), grid, blk, 0, st, a);
+    }
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
 static int c2_ck(int VC, int per_ch, int budget) {
     int ck = budget / per_ch;
     if (ck > 32) ck = 32;
@@ -2550,6 +3154,9 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + B * Co * T2 * Fo), "c2_fwd");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
+    // register-window form (c2_fwd_rw_kernel); ENCX_FWR = workgroups (0: off)
+    static const int fw_wgs = [] { const char* v = getenv("ENCX_FWR"); return v ? atoi(v) : 256; }();
+    if (fw_wgs > 0 && fwr_ok(g) && run_fwd_rw(a, fw_wgs, st) == 0) return 0;
     if (Co == 1 && KT == 3 && KF == 3 && (sf == 1 || sf == 2)) {
         dim3 grid((unsigned)cdiv(T2 * Fo, 64), (unsigned)B);
         if (sf == 1) hipLaunchKernelGGL((c2_co1_fwd<3, 3, 1>), grid, dim3(256), 0, st, a);
@@ -2612,6 +3219,9 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
         ENCX_CHECK_LAUNCH();
         return 0;
     }
+    // register-window form (c2_dgrad_rw_kernel); ENCX_DGR = workgroups (0: off)
+    static const int dg_wgs = [] { const char* v = getenv("ENCX_DGR"); return v ? atoi(v) : 256; }();
+    if (dg_wgs > 0 && dgr_ok(g) && run_dgrad_rw(a, dg_wgs, st) == 0) return 0;
     // tile choice from tools/mb/c2_mb sweeps: 128-column tiles for the narrowest layers (Fo 33;
     // at Fo 65 the 256-column tile is 4-7 % faster), 8-combo
     // chunks + a 3-waves/SIMD register cap for the wide ones
@@ -2643,6 +3253,7 @@ size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64
     WgPlan2 p = plan_wg2(g);
     int splits = p.splits;
     if (wg3r_ok(g)) splits = max(splits, plan_wg3r(g, 32, wg3r_target(g)).splits);
+    if (wgr_ok(g)) splits = max(splits, plan_wgr(g, 4096).splits);  // ENCX_WGR up to 4096 waves
     if (co1_ok(g)) splits = max(splits, plan_co1(g).splits);
     if (wg3n_ok(g)) splits = max(splits, plan_wg3n(g).splits + (int)cdiv(plan_wg3n(g).splits, 32));
     return (size_t)splits * Co * (Ci * KT * KF + 1) * sizeof(float);
@@ -2672,6 +3283,16 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
                            acc_w, acc_b);
         ENCX_CHECK_LAUNCH();
         return 0;
+    }
+    static const int rw_waves = [] { const char* v = getenv("ENCX_WGR"); return v ? min(atoi(v), 4096) : 2048; }();
+    if (rw_waves > 0 && wgr_ok(g)) {  // register-window form (c2_wgrad_rw_kernel); ENCX_WGR=0 off
+        const WgPlanR q = plan_wgr(g, rw_waves);
+        if (run_wgrad_rw(g, dy, yact, x, ws, q, st) == 0) {
+            hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, q.splits, (int)Co,
+                               N, dw, db, acc_w, acc_b);
+            ENCX_CHECK_LAUNCH();
+            return 0;
+        }
     }
     if (wg3r_ok(g)) {  // 9 waves x one 32-column tile each, vectorised staging (c2_wgrad3_kernel)
         const WgPlan3 q = plan_wg3r(g, 32, wg3r_target(g));

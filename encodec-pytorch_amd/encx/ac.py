@@ -18,7 +18,7 @@ import typing as tp
 
 import torch
 
-from ._lib import call, lib, stream, ensure_device
+from ._lib import call, lib, stream, ensure_device, ENCX_AC_STATE, ENCX_AC_MAXBIT, ENCX_AC_POS
 
 
 def _dev_tensor(x, dtype):
@@ -90,11 +90,20 @@ class ArithmeticCoder:
             raise IndexError('symbol outside the quantized cdf')
         if e == 1:
             raise AssertionError('quantized cdf total above 2^total_range_bits (ac.py:116)')
+        if e == 3:
+            raise AssertionError('coder max_bit above 61 after a flush (ac.py:157)')
         if e:
             raise RuntimeError(f'encx arithmetic coder failed ({e})')
         self.fo.write(out[:int(nbytes.item())].cpu().numpy().tobytes())
         self.fo.flush()
         self._lohi = []
+
+
+def new_decoder_state(streams, dev):
+    """Zeroed arithmetic-decoder states [streams][ENCX_AC_STATE] (max_bit = -1), encx_ac_decode."""
+    st = torch.zeros(streams, ENCX_AC_STATE, dtype=torch.int64, device=dev)
+    st[:, ENCX_AC_MAXBIT] = -1
+    return st
 
 
 class ArithmeticDecoder:
@@ -114,8 +123,7 @@ class ArithmeticDecoder:
         buf = torch.frombuffer(bytearray(self._data or b'\0'), dtype=torch.uint8)
         self._buf = buf.to(dev)
         self._nbytes = torch.tensor([len(self._data)], dtype=torch.int64).to(dev)
-        self._state = torch.zeros(1, 5, dtype=torch.int64, device=dev)
-        self._state[0, 3] = -1
+        self._state = new_decoder_state(1, dev)
         self._err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._sym = torch.zeros(1, dtype=torch.int64, device=dev)
 
@@ -129,11 +137,14 @@ class ArithmeticDecoder:
              self._state.data_ptr(), cdf.data_ptr(), 1, cdf.numel(), self.total_range_bits,
              self._sym.data_ptr(), 0, 0, 0, 0, None, None, self._err.data_ptr(), stream())
         e = int(self._err.item())
-        used = (int(self._state[0, 4].item()) + 7) // 8
+        used = (int(self._state[0, ENCX_AC_POS].item()) + 7) // 8
         if hasattr(self.fo, 'seek'):
             self.fo.seek(self._start + used)
         if e == 1:
             return None
         if e == 2:
             raise RuntimeError("Binary search failed")
+        if e:
+            raise RuntimeError(f'encx arithmetic decoder failed ({e}): the stream is not one the '
+                               'reference coder can have written')
         return int(self._sym.item())

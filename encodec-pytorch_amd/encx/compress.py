@@ -89,23 +89,38 @@ def decompress_from_file(model: EncodecModel, fo: tp.IO[bytes], device='cpu') ->
     dev = _model_device(model)
     frames: tp.List[EncodedFrame] = []
     segment_stride = model.segment_stride or audio_length
+    if use_lm:
+        # compress.py:129-155: the rest of the file is read and uploaded ONCE; each segment's
+        # decoder starts where the previous one stopped (the reference's decoder reads lazily
+        # and stops there too), and a seekable file is left at that position at the end
+        start = fo.tell() if hasattr(fo, 'tell') else 0
+        rest = fo.read()
+        rest_dev = torch.frombuffer(bytearray(rest or b'\0'), dtype=torch.uint8).to(dev)
+        pos = 0
     for offset in range(0, audio_length, segment_stride):
         frame_length = metadata['fr']
         if model.normalize:
-            scale_f, = struct.unpack('!f', binary._read_exactly(fo, struct.calcsize('!f')))
+            if use_lm:
+                if pos + 4 > len(rest):
+                    raise EOFError('Impossible to read enough data from the stream, '
+                                   f'{pos + 4 - len(rest)} bytes remaining.')
+                scale_f, = struct.unpack('!f', rest[pos:pos + 4])
+                pos += 4
+            else:
+                scale_f, = struct.unpack('!f', binary._read_exactly(fo, struct.calcsize('!f')))
             scale = torch.tensor(scale_f, device=dev).view(1)
         else:
             scale = None
         if use_lm:
-            # compress.py:129-155: the decoder reads the rest of the file and stops where the
-            # reference's does; the file position follows the bytes it consumed
-            start = fo.tell()
-            codes, used = lm.decode_streams([fo.read()], num_codebooks, frame_length)
-            fo.seek(start + used[0])
+            codes, used = lm.decode_streams(None, num_codebooks, frame_length,
+                                            dev_span=(rest_dev, pos, len(rest) - pos))
+            pos += used[0]
             frames.append((codes, scale))
             continue
         unpacker = binary.BitUnpacker(model.bits_per_codebook, fo, device=dev)
         frames.append((unpacker.pull_frame(num_codebooks, frame_length)[None], scale))
+    if use_lm and hasattr(fo, 'seek'):
+        fo.seek(start + pos)
     with torch.no_grad():
         wav = model.decode(frames)
     return wav[0, :, :audio_length].cpu(), model.sample_rate

@@ -19,7 +19,8 @@ import typing as tp
 import torch
 from torch import nn
 
-from ._lib import call, lib, stream, ensure_device
+from ._lib import call, lib, stream, ensure_device, ENCX_AC_POS
+from .ac import new_decoder_state
 
 TOTAL_RANGE_BITS = 24   # ArithmeticCoder default (ac.py:96), as compress.py uses it
 ROUNDOFF = 1e-8         # build_stable_quantized_cdf defaults (ac.py:18-20)
@@ -223,7 +224,8 @@ class LMModel(nn.Module):
         return [host[b, :nb[b]].numpy().tobytes() for b in range(B)]
 
     @torch.no_grad()
-    def decode_streams(self, datas: tp.Sequence[bytes], K: int, T: int, graph: bool = True):
+    def decode_streams(self, datas: tp.Sequence[bytes], K: int, T: int, graph: bool = True,
+                       dev_span=None):
         """compress.py:128-155 (use_lm=True) for B streams of K codebooks x T steps: ->
         (codes int64 [B, K, T] on the GPU, bytes consumed per stream). Raises EOFError where
         the reference's decoder runs dry, RuntimeError where its binary search fails.
@@ -231,22 +233,33 @@ class LMModel(nn.Module):
         One step = LM input, 5 layers, heads + cdf, arithmetic decode of the K codes (whose
         + 1 is the next step's input, compress.py:154-155). With graph=True the step's ~40
         launches are captured once into a HIP graph (offsets from a device-side step counter)
-        and replayed T times, with one host sync at the end."""
+        and replayed T times, with one host sync at the end.
+        dev_span = (uint8 device tensor, byte offset, byte count): decode ONE stream of that many
+        bytes at that offset of a buffer already on the device (datas is then ignored), so a
+        file's segments are decoded from one upload of the file."""
         self._packed()
         self._check_device()
         if K > self.n_q:
             raise ValueError(f'{K} codebooks for an LM of n_q={self.n_q}')
-        B = len(datas)
         dev = self._emb.device
-        stride = max([len(d) for d in datas] + [1])
-        buf = torch.zeros(B, stride, dtype=torch.uint8)
-        for b, d in enumerate(datas):
-            if len(d):
-                buf[b, :len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8)
-        data = buf.to(dev)
-        nbytes = torch.tensor([len(d) for d in datas], dtype=torch.int64).to(dev)
-        dstate = torch.zeros(B, 5, dtype=torch.int64, device=dev)
-        dstate[:, 3] = -1
+        if dev_span is not None:
+            src, off, count = dev_span
+            if off < 0 or count < 0 or off + count > src.numel():
+                raise ValueError('encx decode_streams: dev_span outside its buffer')
+            B, stride = 1, max(count, 1)
+            data_ptr = src.data_ptr() + off
+            nbytes = torch.tensor([count], dtype=torch.int64).to(dev)
+        else:
+            B = len(datas)
+            stride = max([len(d) for d in datas] + [1])
+            buf = torch.zeros(B, stride, dtype=torch.uint8)
+            for b, d in enumerate(datas):
+                if len(d):
+                    buf[b, :len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8)
+            data = buf.to(dev)
+            data_ptr = data.data_ptr()
+            nbytes = torch.tensor([len(d) for d in datas], dtype=torch.int64).to(dev)
+        dstate = new_decoder_state(B, dev)
         err = torch.zeros(B, dtype=torch.int32, device=dev)
         codes = torch.zeros(B, K, T, dtype=torch.int64, device=dev)
         idx = torch.zeros(B, K, dtype=torch.int64, device=dev)      # step input, 0 at t = 0
@@ -258,7 +271,7 @@ class LMModel(nn.Module):
             st = stream()
             x = self._body(idx, (K, 1, 1), B, K, 1, False, state, dev_step=dstep)
             self._heads(x, B, 1, K, cdf=cdf)
-            call('encx_ac_decode', data.data_ptr(), stride, nbytes.data_ptr(), B, dstate.data_ptr(),
+            call('encx_ac_decode', data_ptr, stride, nbytes.data_ptr(), B, dstate.data_ptr(),
                  cdf.data_ptr(), K, self.card, TOTAL_RANGE_BITS, codes.data_ptr(), K * T, T, 1, t,
                  dstep.data_ptr() if dstep is not None else None, idx.data_ptr(), err.data_ptr(), st)
             if dstep is not None:
@@ -279,4 +292,6 @@ class LMModel(nn.Module):
             raise EOFError("The stream ended sooner than expected.")
         if any(v == 2 for v in e):
             raise RuntimeError("Binary search failed")
-        return codes, [(p + 7) // 8 for p in dstate[:, 4].cpu().tolist()]
+        if any(e):
+            raise RuntimeError(f'encx arithmetic decoder failed: {e}')
+        return codes, [(p + 7) // 8 for p in dstate[:, ENCX_AC_POS].cpu().tolist()]

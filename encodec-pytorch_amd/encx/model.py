@@ -114,10 +114,14 @@ class EncodecModel(nn.Module):
             index = int(t.item())
         return self.target_bandwidths[index]
 
-    def forward(self, x: torch.Tensor, bandwidth: tp.Optional[float] = None):
+    def forward(self, x: torch.Tensor, bandwidth: tp.Optional[float] = None, split: bool = False):
         """model.py:195-213. Train mode -> (output, loss_w, frames); eval -> output.
         `bandwidth` (train mode, not in the reference) fixes the step's target bandwidth instead
-        of drawing it here: the HIP-graph trainer draws it on the host before replaying."""
+        of drawing it here: the HIP-graph trainer draws it on the host before replaying.
+        `split` (train mode, one segment; not in the reference): the decoder reads a detached leaf
+        copy of the quantized latent, so the backward runs as two calls -- output -> decoder
+        weights + the leaf's grad, then (quantized, loss_w) -> encoder -- and the data-parallel
+        trainer all-reduces the decoder's grads between them (self.last_split = (quantized, leaf))."""
         frames = self.encode(x)
         if self.training:
             bw = self._pick_bandwidth(x.device) if bandwidth is None else bandwidth
@@ -129,9 +133,12 @@ class EncodecModel(nn.Module):
                 loss_w = pen if loss_w is None else loss_w + pen
                 codes.append((qv.quantized, scale))
             self.last_codes = [qv.codes]
-            # the decoder's input: its gradient is ready once every decoder weight grad is (the
-            # trainer's overlapped all-reduce of the decoder bucket hooks it)
-            self.last_decoder_input = codes[0][0] if len(codes) == 1 else None
+            self.last_split = None
+            if split and len(codes) == 1:
+                q, scale = codes[0]
+                leaf = q.detach().requires_grad_()
+                self.last_split = (q, leaf)
+                codes = [(leaf, scale)]
             return self.decode(codes)[:, :, :x.shape[-1]], loss_w, frames
         return self.decode(frames)[:, :, :x.shape[-1]]
 

@@ -552,6 +552,38 @@ def rvq_to_rows(res):
     return out
 
 
+_CB_DEFER = None  # list collecting CodebookSync entries while defer_codebook_sync is active
+
+
+class CodebookSync:
+    """The data-parallel EMA codebook sync of one RVQ forward: `sums` [n_q, K, D+1] holds each
+    layer's per-code sums (sum of x over the rows assigned to a code, and their count); after
+    an all-reduce (SUM) of `sums` over the ranks, apply() runs each layer's EMA update from them
+    (core_vq.py:227-235), so every rank applies the same update."""
+
+    def __init__(self, sums, codebooks, decay, eps):
+        self.sums, self.codebooks, self.decay, self.eps = sums, codebooks, decay, eps
+
+    def apply(self):
+        n_q, Kc, D1 = self.sums.shape
+        for i, cb in enumerate(self.codebooks):
+            call('encx_rvq_ema_from_sums', ptr(self.sums[i]), ptr(cb.cluster_size), ptr(cb.embed_avg),
+                 ptr(cb.embed), D1 - 1, Kc, self.decay, self.eps, stream())
+
+
+@contextlib.contextmanager
+def defer_codebook_sync(pending: list):
+    """Inside this scope a synced RVQ forward leaves its CodebookSync in `pending` instead of
+    all-reducing and applying it, so a HIP-graph trainer can run the collective eagerly between
+    two captured segments and apply() it in a later one."""
+    global _CB_DEFER
+    prev, _CB_DEFER = _CB_DEFER, pending
+    try:
+        yield pending
+    finally:
+        _CB_DEFER = prev
+
+
 class RVQTrainFn(torch.autograd.Function):
     """ResidualVectorQuantization.forward in train mode (core_vq.py:337-355) over
     VectorQuantization.forward (:301-324) + the EMA codebook update (:212-237), one fused
@@ -583,7 +615,10 @@ class RVQTrainFn(torch.autograd.Function):
         sums = None
         if sync and codebooks[0].training and torch.distributed.is_initialized() \
                 and torch.distributed.get_world_size() > 1:
-            sums = torch.empty(Kc, D + 1, device=emb.device, dtype=torch.float32)
+            # every layer's sums, all-reduced in ONE collective after the layer loop: layer i's
+            # EMA update is read by no later layer of this forward (each quantizes with its own
+            # codebook), so deferring it is value-identical to updating inside the loop
+            sums = torch.empty(n_q, Kc, D + 1, device=emb.device, dtype=torch.float32)
         for i, cb in enumerate(codebooks):
             x = res[i % 2]
             cb.init_embed_(x)
@@ -593,14 +628,18 @@ class RVQTrainFn(torch.autograd.Function):
             call('encx_rvq_apply', ptr(x), ptr(res[(i + 1) % 2]), ptr(cb.embed), ptr(codes[i]),
                  ptr(out), ptr(cdir), ptr(parts[i]), B, D, T, int(i == 0), 1, st)
             if cb.training and sums is not None:
-                call('encx_rvq_code_sums', ptr(x), ptr(codes[i]), ptr(sums), ptr(bws), B, D, T, Kc, st)
-                torch.distributed.all_reduce(sums)  # 1024 x 129 fp32 = 528 KB per layer
-                call('encx_rvq_ema_from_sums', ptr(sums), ptr(cb.cluster_size), ptr(cb.embed_avg),
-                     ptr(cb.embed), D, Kc, float(decay), float(eps), st)
+                call('encx_rvq_code_sums', ptr(x), ptr(codes[i]), ptr(sums[i]), ptr(bws), B, D, T, Kc, st)
             elif cb.training:
                 call('encx_rvq_ema', ptr(x), ptr(codes[i]), ptr(cb.cluster_size), ptr(cb.embed_avg),
                      ptr(cb.embed), ptr(bws), B, D, T, cb.embed.shape[0], float(decay), float(eps), st)
             call('encx_reduce_sum', ptr(parts[i]), P, 1.0 / numel, ptr(commits[i:i + 1]), 0, st)
+        if sums is not None:
+            sync_ent = CodebookSync(sums, list(codebooks), float(decay), float(eps))
+            if _CB_DEFER is not None:  # the Trainer runs the collective between graph segments
+                _CB_DEFER.append(sync_ent)
+            else:
+                torch.distributed.all_reduce(sums)  # n_q x 1024 x 129 fp32 = 528 KB per layer
+                sync_ent.apply()
         penalty = torch.empty(1, device=emb.device, dtype=torch.float32)
         call('encx_reduce_sum', ptr(commits), n_q, 1.0 / n_q, ptr(penalty), 0, st)
         ctx.save_for_backward(cdir)

@@ -32,7 +32,6 @@ class FlatAdam(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros(n, device=dev, dtype=torch.float32)
         self.hp = torch.zeros(8, device=dev, dtype=torch.float32)  # per-step scalars (encx_adam_hyper)
         self.n_step = 0
-        self._pending = []  # async all-reduce handles of buckets launched during backward
         o = 0
         self._views = []
         self.offsets = []
@@ -71,28 +70,19 @@ class FlatAdam(torch.optim.Optimizer):
             raise ValueError('encx FlatAdam.span: params are not contiguous in the flat buffer')
         return a, b
 
-    def all_reduce_bucket(self, a, b):
-        """Start the RCCL sum of flat_grad[a:b] now (async on the communicator's stream, ordered
-        after the work already queued on the current stream), so it overlaps the rest of the
-        backward. all_reduce_grads() reduces the remainder and waits."""
-        if distrib.is_distributed():
-            work = torch.distributed.all_reduce(self.flat_grad[a:b], async_op=True)
-            self._pending.append((a, b, work))
+    def reduce_async(self, a=0, b=None):
+        """Start the RCCL sum of flat_grad[a:b] over the ranks and return its work handle. The
+        collective runs on the communicator's stream, ordered after the work already queued on
+        the current stream, so it overlaps whatever the current stream does next (the rest of
+        the backward, the discriminator phase); work.wait() orders the current stream after it."""
+        return torch.distributed.all_reduce(self.flat_grad[a:b], async_op=True)
 
     def all_reduce_grads(self, scale=True):
-        """Sum flat_grad over ranks (buckets already started by all_reduce_bucket included), then
-        divide by the world size unless scale=False (the caller folds it in later)."""
+        """Sum flat_grad over ranks in one collective, then divide by the world size unless
+        scale=False."""
         if not distrib.is_distributed():
             return
-        done = sorted((a, b) for a, b, _ in self._pending)
-        o = 0
-        for a, b in done + [(self.flat_grad.numel(), None)]:
-            if a > o:
-                torch.distributed.all_reduce(self.flat_grad[o:a])
-            o = b if b is not None else o
-        for _, _, work in self._pending:
-            work.wait()
-        self._pending = []
+        self.reduce_async().wait()
         if scale:
             self.flat_grad.div_(distrib.world_size())
 

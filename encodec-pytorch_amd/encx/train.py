@@ -28,7 +28,7 @@ from .balancer import Balancer
 from . import distrib
 from .losses import total_loss, disc_loss
 from .model import EncodecModel
-from .ops import DiscGradMode, WnBatch
+from .ops import DiscGradMode, WnBatch, defer_codebook_sync
 from .optim import FlatAdam
 from .scheduler import WarmupCosineLrScheduler
 
@@ -38,8 +38,12 @@ DEFAULT_WEIGHTS = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}  # config/config
 class Trainer:
     def __init__(self, model: EncodecModel, disc=None, lr=3e-4, disc_lr=3e-4, betas=(0.5, 0.9),
                  weights=None, max_iter=100000, warmup_iter=0, disc_prob=1.0, sample_rate=24000,
-                 scheduler=True, balancer_kwargs=None, graphs=False):
+                 scheduler=True, balancer_kwargs=None, graphs=False, ddp_commit_local=False):
         self.model = model
+        # ddp_commit_local: the reference's exact DDP semantics (train_multi_gpu.py:86-95, SURVEY
+        # quirk 7): the commit loss's grads are added AFTER the all-reduce, so they stay rank-local
+        # and the ranks' weights drift apart. Off (default): one backward, true data parallelism.
+        self.ddp_commit_local = ddp_commit_local
         self.disc = disc
         self.sample_rate = sample_rate
         if distrib.is_distributed():
@@ -69,23 +73,36 @@ class Trainer:
         self.wn = WnBatch() if os.environ.get('ENCX_WN_BATCH', '1') != '0' else None
         self.graphs = graphs
         self._graphs = {}
+        self._pool = None  # one HIP-graph memory pool shared by every captured key
+        self.max_graph_keys = 8  # keys past this many run eagerly (their pool memory is bounded)
         dec = [p for p in model.decoder.parameters() if p.requires_grad]
         self._dec_span = self.opt.span(dec) if dec else None
 
     # ------------------------------------------------------------------ step
     # step() = host part (draw the bandwidth and the discriminator coin, advance the optimiser step
     # counts and write their scalars) + device part. The device part is a list of segments with
-    # the cross-rank collectives between them:
-    #   A  forward, discriminator, losses, per-loss grads, balancer statistics
-    #   -- all-reduce balancer statistics (world > 1)
-    #   B  balancer scales + combine, the one backward (decoder-grad bucket all-reduce overlaps
-    #      the encoder backward when eager)
-    #   -- all-reduce generator grads
-    #   C  generator Adam; discriminator loss + weight-grad backward
-    #   -- all-reduce discriminator grads
-    #   D  discriminator Adam
+    # the cross-rank collectives between them (world > 1; at world 1 every collective is None):
+    #   gen     zero grads, generator forward (synced codebooks: the per-code sums, deferred)
+    #     -- start the all-reduce of the codebook sums (async)
+    #   losses  discriminator on real / fake, losses, per-loss grads, balancer statistics
+    #     -- all-reduce the balancer statistics (nl + 1 floats)
+    #   dec     balancer scales + combine; backward output -> decoder weights and the decoder
+    #           input's grad (the whole backward when the model is segmented or world is 1)
+    #     -- start the all-reduce of the decoder's grad bucket (async)
+    #   enc     backward (quantized, loss_w) -> encoder
+    #     -- start the all-reduce of the encoder's grad bucket (async)
+    #   disc    discriminator loss + its weight-grad backward (independent of the generator
+    #           update, so the generator's buckets reduce underneath it)
+    #     -- start the discriminator's all-reduce; wait for every collective of the step
+    #   opt     codebook EMA from the reduced sums, generator Adam, discriminator Adam
+    # The reference's order is generator Adam, then the discriminator phase (train_multi_gpu.py
+    # :95, :112-124); the discriminator phase reads neither the generator's weights nor its
+    # grads, so running its backward first changes no value.
     # With graphs=True each (bandwidth, coin, shape) key runs eagerly once, is then captured into
-    # HIP graphs (one per segment; world 1: the whole step is one graph), and is replayed after.
+    # HIP graphs (one per segment between collectives; world 1: the whole step is one graph), and
+    # is replayed after. All keys share one memory pool: replays never overlap, and every tensor
+    # a replay reads is written earlier in the same replay (inputs are copied into a buffer
+    # outside the pool; losses are copied out of it on return).
     def step(self, x):
         model, disc = self.model, self.disc
         model.train()
@@ -97,10 +114,10 @@ class Trainer:
         if train_d:
             self.opt_d.prepare()
         key = (bw, train_d, tuple(x.shape))
-        if self.graphs and self._graph_ok():
+        if self.graphs and self._graph_ok(key):
             out = self._graph_step(key, x)
         else:
-            out = self._run(x, bw, train_d, overlap=True)
+            out = self._run(x, bw, train_d)
         if self.sched is not None:
             self.sched.step()
         if self.sched_d is not None:
@@ -108,6 +125,10 @@ class Trainer:
         return out
 
     def _pick_train_d(self, device):
+        """train_multi_gpu.py:105-110. disc_prob None = the reference's short-circuit (the flag
+        off, or a warmup epoch): no random draw, so Python's RNG stream stays the reference's."""
+        if self.disc_prob is None:
+            return False
         train_d = random.random() < self.disc_prob
         if distrib.is_distributed() and self.disc_prob < 1.0:
             t = torch.tensor([train_d], device=device)
@@ -115,30 +136,33 @@ class Trainer:
             train_d = bool(t.item())
         return train_d
 
-    def _segments(self, x, bw, train_d, overlap):
+    def _segments(self, x, bw, train_d):
         """The device part as (segment, collective) pairs; state flows through `c`."""
         c = {}
         dist = distrib.is_distributed()
+        split = dist and self._dec_span is not None and self.model.segment is None
+        local = dist and self.ddp_commit_local
+        if local and not split:
+            raise ValueError('encx Trainer: ddp_commit_local needs an unsegmented model')
+        works = []
 
         wn = self.wn
         fwd = (lambda grp: wn.forward(grp)) if wn is not None else (lambda grp: contextlib.nullcontext())
         bwd = (lambda: wn.backward()) if wn is not None else contextlib.nullcontext
 
-        def dec_bucket(a, b):
-            if wn is not None:
-                wn.flush()  # the decoder's queued weight-norm backwards complete its grads
-            self.opt.all_reduce_bucket(a, b)
-
-        def seg_a():
+        def seg_gen():
             self.opt.zero_grad()
-            with fwd('gen'):
-                y, loss_w, _ = self.model(x, bandwidth=bw)
+            c['cb'] = []
+            with fwd('gen'), defer_codebook_sync(c['cb']):
+                y, loss_w, _ = self.model(x, bandwidth=bw, split=split)
             c['y'], c['loss_w'] = y, loss_w
-            if overlap and dist:
-                q = self.model.last_decoder_input
-                if q is not None and q.requires_grad:
-                    a, b = self._dec_span
-                    q.register_hook(lambda g: dec_bucket(a, b))
+            c['split'] = self.model.last_split
+
+        def coll_gen():
+            works.extend(torch.distributed.all_reduce(e.sums, async_op=True) for e in c['cb'])
+
+        def seg_losses():
+            y = c['y']
             if self.disc is not None:
                 # generator phase: the balancer's autograd.grad calls differentiate the shared
                 # discriminator graph w.r.t. the fake audio only
@@ -157,53 +181,89 @@ class Trainer:
             c['losses'] = losses
             self.balancer.combine_start(self.balancer.grads(losses, wrt))
 
-        def seg_b():
+        def seg_dec():
             out_grad = self.balancer.combine_finish()
             y, loss_w = c.pop('y'), c['loss_w']
             with bwd():
-                torch.autograd.backward([y, loss_w], [out_grad, torch.ones_like(loss_w)])
+                if c['split'] is not None:
+                    torch.autograd.backward([y], [out_grad])
+                else:
+                    torch.autograd.backward([y, loss_w], [out_grad, torch.ones_like(loss_w)])
 
-        def seg_c():
-            if dist:
-                self.opt.flat_grad.div_(distrib.world_size())
-            self.opt.launch()
-            out = dict(c['losses'])
+        def coll_dec():
+            works.append(self.opt.reduce_async(*self._dec_span))
+
+        def seg_enc():
+            q, leaf = c.pop('split')
+            loss_w = c['loss_w']
+            with bwd():
+                if local:  # the balanced grads only; the commit backward follows the all-reduce
+                    torch.autograd.backward([q], [leaf.grad], retain_graph=True)
+                else:
+                    torch.autograd.backward([q, loss_w], [leaf.grad, torch.ones_like(loss_w)])
+
+        def coll_enc():
+            a = self._dec_span[0] if split else self.opt.flat_grad.numel()
+            if a > 0:
+                works.append(self.opt.reduce_async(0, a))
+
+        def seg_disc():
+            out = dict(c.pop('losses'))
             out['loss_w'] = c['loss_w']
             if train_d:
                 # discriminator phase on the same graph: weight grads only (train_multi_gpu.py:112-124)
                 self.disc_mode.set(params=True, input=False)
                 self.opt_d.zero_grad()
-                out['l_d'] = disc_loss(c['logits_real'], c['logits_fake'])
+                out['l_d'] = disc_loss(c.pop('logits_real'), c.pop('logits_fake'))
                 with bwd():
                     out['l_d'].backward()
-            c.clear()
             c['out'] = out
 
-        def seg_d():
+        def coll_disc():
+            if train_d:
+                works.append(self.opt_d.reduce_async())
+            for w in works:
+                w.wait()
+            works.clear()
+
+        def seg_opt():
+            for e in c['cb']:
+                e.apply()  # the EMA codebook update from the rank-summed code sums
+            if dist:
+                self.opt.flat_grad.div_(distrib.world_size())
+            if local:  # loss_w.backward() (train_multi_gpu.py:94): rank-local commit grads
+                loss_w = c['loss_w']
+                with bwd():
+                    torch.autograd.backward([loss_w], [torch.ones_like(loss_w)])
+            self.opt.launch()
             if train_d:
                 if dist:
                     self.opt_d.flat_grad.div_(distrib.world_size())
                 self.opt_d.launch()
 
-        return [(seg_a, self.balancer.reduce_stats),
-                (seg_b, lambda: self.opt.all_reduce_grads(scale=False)),
-                (seg_c, (lambda: self.opt_d.all_reduce_grads(scale=False)) if train_d else None),
-                (seg_d, None)], c
+        if not dist:
+            segs = [seg_gen, seg_losses, seg_dec, seg_disc, seg_opt]
+            return [(lambda: [s() for s in segs], None)], c
+        return [(seg_gen, coll_gen if self.model.quantizer.sync_codebooks else None),
+                (seg_losses, self.balancer.reduce_stats),
+                (seg_dec, coll_dec if split else None),
+                (seg_enc if split else (lambda: None), coll_enc),
+                (seg_disc, coll_disc),
+                (seg_opt, None)], c
 
-    def _run(self, x, bw, train_d, overlap=False):
-        segs, c = self._segments(x, bw, train_d, overlap)
+    def _run(self, x, bw, train_d):
+        segs, c = self._segments(x, bw, train_d)
         for seg, coll in segs:
             seg()
             if coll is not None:
                 coll()
         return c['out']
 
-    def _graph_ok(self):
+    def _graph_ok(self, key):
         from ._lib import lib
         if lib.encx_prof_enabled() or self.balancer.monitor:
             return False  # profiler events / the monitor's host read are not capturable
-        q = getattr(self.model, 'quantizer', None)
-        return not (distrib.is_distributed() and q is not None and getattr(q, 'sync_codebooks', False))
+        return key in self._graphs or len(self._graphs) < self.max_graph_keys
 
     def _graph_step(self, key, x):
         ent = self._graphs.get(key)
@@ -214,27 +274,29 @@ class Trainer:
             return self._run(x, key[0], key[1])
         if ent == 'warm':  # second occurrence: capture, which also runs this step
             ent = self._graphs[key] = self._capture(key, x)
-            return ent[3]
-        graphs, colls, xs, out = ent
-        xs.copy_(x)
-        for g, coll in zip(graphs, colls):
-            g.replay()
-            if coll is not None:
-                coll()
-        return out
+        else:
+            graphs, colls, xs, out = ent
+            xs.copy_(x)
+            for g, coll in zip(graphs, colls):
+                g.replay()
+                if coll is not None:
+                    coll()
+        out = ent[3]
+        # the replayed graphs rewrite `out` in place: hand the caller a copy of this step's values
+        names = list(out)
+        vals = torch.cat([out[k].detach().reshape(-1)[:1] for k in names])
+        return {k: vals[i] for i, k in enumerate(names)}
 
     def _capture(self, key, x):
         xs = x.detach().clone()
-        segs, c = self._segments(xs, key[0], key[1], overlap=False)
-        if not distrib.is_distributed():  # no collectives: the whole step is one graph
-            parts = [s for s, _ in segs]
-            segs = [(lambda: [s() for s in parts], None)]
+        segs, c = self._segments(xs, key[0], key[1])
         torch.cuda.synchronize()
-        pool = torch.cuda.graph_pool_handle()
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
         graphs, colls = [], []
         for seg, coll in segs:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=self._pool):
                 seg()
             graphs.append(g)
             colls.append(coll)

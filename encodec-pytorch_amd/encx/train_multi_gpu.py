@@ -123,8 +123,10 @@ def train_one_step(epoch, trainer, dataset, config, rank=0, world=1):
     """train_multi_gpu.py:32-143: one epoch; the discriminator trains from warmup_epoch on, with
     probability eval(train_discriminator) per step (:105-107)."""
     td = config.model.train_discriminator
-    prob = float(td) if isinstance(td, (bool, int, float)) else float(eval(str(td)))
-    trainer.disc_prob = prob if epoch >= config.lr_scheduler.warmup_epoch else 0.0
+    if td and epoch >= config.lr_scheduler.warmup_epoch:
+        trainer.disc_prob = float(td) if isinstance(td, (bool, int, float)) else float(eval(str(td)))
+    else:
+        trainer.disc_prob = None  # the reference's `and` short-circuits before random.random()
     batches = shard_order(len(dataset), rank, world, config.datasets.batch_size, world > 1)
     last = {}
     for idx, ids in enumerate(batches, 1):

@@ -485,12 +485,17 @@ int64_t encx_ac_encode_capacity(int64_t n_symbols, int total_range_bits);
 int encx_ac_encode(const int32_t* lohi, int64_t streams, int64_t n, int total_range_bits, uint8_t* out,
                    int64_t cap, int64_t* nbytes, int* err, encx_stream_t stream);
 /* ArithmeticDecoder.pull (ac.py:217-260) of K symbols per stream, symbol k against cdf row
- * cdf[s][k][:card]. Stream s reads data + s*stride (nbytes[s] bytes); state [streams][5] int64 =
- * (low, high, current, max_bit, bits consumed), zero with max_bit = -1 for a new stream. The
+ * cdf[s][k][:card]. Stream s reads data + s*stride (nbytes[s] bytes); state [streams][ENCX_AC_STATE]
+ * int64 = (low, high, current as 128-bit values, low word first; max_bit; bits consumed), zero
+ * with max_bit (word ENCX_AC_MAXBIT) = -1 for a new stream. The
  * symbol goes to codes[s*c_s + k*c_k + t*c_t] (codes nullable) and sym + 1 to next_idx[s][k]
  * (nullable: the LM input of the next step, compress.py:154-155). err[s]: 1 = the stream ran out
- * (pull returns None), 2 = no interval contains the value (ac.py:238); a failed stream is left
+ * (pull returns None), 2 = no interval contains the value (ac.py:238), 3 = max_bit past 96 (a
+ * stream the reference's encoder cannot have written, ac.py:157); a failed stream is left
  * untouched by later calls. Bytes consumed = ceil(bits consumed / 8). */
+#define ENCX_AC_STATE 8
+#define ENCX_AC_MAXBIT 6
+#define ENCX_AC_POS 7
 int encx_ac_decode(const uint8_t* data, int64_t stride, const int64_t* nbytes, int64_t streams, int64_t* state,
                    const int32_t* cdf, int64_t K, int64_t card, int total_range_bits, int64_t* codes, int64_t c_s,
                    int64_t c_k, int64_t c_t, int64_t t, const int64_t* dev_step, int64_t* next_idx, int* err,

@@ -100,7 +100,12 @@ def rvq_certified(emb, embeds, factor=256):
     return torch.stack(codes), torch.stack(certs)
 
 
-__all__ = ['load', 'T', 'model_state', 'disc_state', 'cfg48k', 'codebooks_from_stats', 'g3_codebooks',
+def g13_samples(n, count=64):
+    """The evenly spaced element indices of an n-element tensor that g13_ddp.npz stores."""
+    return np.unique(np.linspace(0, n - 1, min(n, count)).round().astype(np.int64))
+
+
+__all__ = ['load', 'g13_samples', 'T', 'model_state', 'disc_state', 'cfg48k', 'codebooks_from_stats', 'g3_codebooks',
            'certified', 'rvq_certified', 'synth_wave', 'rng']
 
 

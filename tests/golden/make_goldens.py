@@ -22,6 +22,7 @@ Fixture map:
                    a small past_context), and compress(use_lm=True) bytes of the g1 model
   g9_step48k.npz   config-5 analogue: 48 kHz stereo, non-causal, time_group_norm, segment 0.1 s
                    (two frames: 4800 + 48 samples, linear overlap-add), gen-only and GAN steps
+  g13_ddp.npz      the reference's train_one_step under DDP, 2 ranks over gloo (G13 below)
 """
 import os
 import sys
@@ -730,8 +731,130 @@ def g12():
     save('g12_lm.npz', **out)
 
 
+# ------------------------------------------------------------------------------------ G13
+# The reference's OWN data-parallel step: train_multi_gpu.train_one_step (:32-142) on models
+# wrapped as train() wraps them (DDP, broadcast_buffers=False, :310-325), 2 ranks over gloo on
+# the CPU, one batch of G13_B clips per rank, bandwidth fixed (n_q 2), the discriminator trained
+# (p = 1). Recorded per rank, by wrapping (not editing) the reference's objects:
+#   g_bal  : the generator grads right after balancer.backward (DDP-averaged, equal on both ranks)
+#   commit : the grads loss_w.backward() (:94) then adds (rank-local under DDP)
+#   disc   : the discriminator grads at optimizer_disc.step (DDP-averaged)
+#   the losses, the post-Adam parameters and codebook buffers (sync off: each rank's own EMA)
+# Generator tensors are stored as per-tensor sums / abs-sums / squared sums plus G13_S evenly
+# spaced elements of every parameter (the 14.85 M-element vectors themselves are 59 MB each).
+G13_B, G13_T = 2, 4800
+from fixtures import g13_samples  # noqa: E402  (64 evenly spaced elements per tensor)
+
+
+def _g13_rank(rank, world, port, outdir):
+    import random
+    import types as _types
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.distributed.init_process_group('gloo', rank=rank, world_size=world)
+    torch.set_num_threads(4)
+    # off-path imports of train_multi_gpu.py absent from this image: hydra (the CLI decorator),
+    # tensorboard (the logging writer; a no-op one is passed in), audioread (datasets)
+    for name in ('hydra', 'audioread', 'torch.utils.tensorboard'):
+        mod = _types.ModuleType(name)
+        mod.main = lambda **kw: (lambda f: f)
+        mod.SummaryWriter = object
+        sys.modules.setdefault(name, mod)
+    import train_multi_gpu as tmg
+    torch.manual_seed(0)
+    random.seed(0)
+    m = R.model.EncodecModel._get_model([1.5], 24000, 1, causal=True, model_norm='weight_norm',
+                                        audio_normalize=True, segment=None, name='x')
+    load_synth(m, 71)
+    stats = np.load(os.path.join(HERE, 'g7_step.npz'))['gan/stats']
+    fill_codebooks(m, stats, 73, 2)
+    d = R.msstftd.MultiScaleSTFTDiscriminator(filters=32)
+    load_synth(d, 74)
+    x = t(synth_wave((world * G13_B, 1, G13_T), 131))[rank * G13_B:(rank + 1) * G13_B]
+    names = [k for k, p in m.named_parameters() if p.requires_grad]
+    gparams = [p for p in m.parameters() if p.requires_grad]
+    rec = {}
+
+    def snap(ps):
+        return [p.grad.detach().clone() for p in ps]
+
+    class RecBalancer(R.balancer.Balancer):
+        def backward(self, losses, input, retain_graph=False):
+            super().backward(losses, input, retain_graph=retain_graph)
+            rec['g_bal'] = snap(gparams)
+            rec['losses'] = {k: float(v) for k, v in losses.items()}
+
+    class RecAdam(torch.optim.Adam):
+        def __init__(self, *a, tag, **kw):
+            super().__init__(*a, **kw)
+            self.tag = tag
+
+        def step(self, closure=None):
+            rec[self.tag] = snap([p for grp in self.param_groups for p in grp['params']])
+            return super().step(closure)
+
+    model = torch.nn.parallel.DistributedDataParallel(m, broadcast_buffers=False, find_unused_parameters=False)
+    disc = torch.nn.parallel.DistributedDataParallel(d, broadcast_buffers=False, find_unused_parameters=False)
+    opt = RecAdam([{'params': gparams, 'lr': 3e-4}], betas=(0.5, 0.9), tag='g_total')
+    optd = RecAdam([{'params': [p for p in d.parameters() if p.requires_grad], 'lr': 3e-4}], betas=(0.5, 0.9),
+                   tag='g_disc')
+    sched = R.scheduler.WarmupCosineLrScheduler(opt, max_iter=100, eta_ratio=0.1, warmup_iter=0, warmup_ratio=1e-4)
+    dsched = R.scheduler.WarmupCosineLrScheduler(optd, max_iter=100, eta_ratio=0.1, warmup_iter=0, warmup_ratio=1e-4)
+    ns = _types.SimpleNamespace
+    config = ns(common=ns(amp=False, log_interval=1), model=ns(train_discriminator='1.0', sample_rate=24000),
+                lr_scheduler=ns(warmup_epoch=0), distributed=ns(data_parallel=True))
+    writer = ns(add_scalar=lambda *a, **kw: None)
+    bal = RecBalancer({'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3})
+    tmg.train_one_step(1, opt, optd, model, disc, [x], config, sched, dsched, writer=writer, balancer=bal)
+    out = {}
+    for i, (k, p) in enumerate(zip(names, gparams)):
+        idx = g13_samples(p.numel())
+        for tag, v in (('bal', rec['g_bal'][i]), ('commit', rec['g_total'][i] - rec['g_bal'][i]),
+                       ('total', rec['g_total'][i]), ('param', p.detach())):
+            v = v.double().reshape(-1)
+            out[f'{tag}/{k}'] = v[torch.from_numpy(idx)].numpy()
+            out[f'{tag}_sum/{k}'] = np.array([v.sum().item(), v.abs().sum().item(), v.pow(2).sum().item()])
+    out['disc_grad'] = torch.cat([g.reshape(-1) for g in rec['g_disc']]).numpy()
+    for k, p in d.named_parameters():
+        if p.requires_grad:
+            out[f'dparam/{k}'] = p.detach().reshape(-1)[torch.from_numpy(g13_samples(p.numel()))].numpy()
+    for k, v in rec['losses'].items():
+        out[f'loss/{k}'] = np.array(v)
+    sd = m.state_dict()
+    for i in range(2):
+        pre = f'quantizer.vq.layers.{i}._codebook.'
+        out[f'cb{i}/cluster_size'] = sd[pre + 'cluster_size'].numpy()
+        out[f'cb{i}/embed_avg_rows'] = sd[pre + 'embed_avg'][::16].numpy()
+        out[f'cb{i}/embed_rows'] = sd[pre + 'embed'][::16].numpy()
+    np.savez(os.path.join(outdir, f'r{rank}.npz'), **out)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def g13():
+    import socket
+    import tempfile
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    outdir = tempfile.mkdtemp(prefix='g13_')
+    mp.spawn(_g13_rank, args=(2, port, outdir), nprocs=2, join=True)
+    r = [dict(np.load(os.path.join(outdir, f'r{i}.npz'))) for i in range(2)]
+    for k in r[0]:
+        if k.startswith(('bal', 'disc_grad', 'dparam')):  # DDP-averaged: one value for both ranks
+            assert np.array_equal(r[0][k], r[1][k]), k
+    out = {'stats': np.load(os.path.join(HERE, 'g7_step.npz'))['gan/stats']}
+    for k, v in r[0].items():
+        if k.startswith(('bal', 'disc_grad', 'dparam')):
+            out[k] = v
+        else:
+            out['r0/' + k] = v
+            out['r1/' + k] = r[1][k]
+    save('g13_ddp.npz', **out)
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9', 'g10', 'g11', 'g12']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9', 'g10', 'g11', 'g12', 'g13']
     for w in which:
         torch.manual_seed(0)
         globals()[w]()

@@ -1,0 +1,143 @@
+"""One Trainer step against the CPU oracle's step from the SAME state, element by element.
+
+Test infrastructure (GPU tests only). Before a HIP step the trainer's state -- parameters, Adam
+moments and step count, codebook buffers, balancer statistics, learning rate -- is copied to
+the host; the oracle (oracle/encodec_oracle.py train_step, pinned to the reference's g7 / g9
+fixtures by tests/test_oracle.py) then runs the same step from that state in fp64, and once more
+in fp32. The HIP step is compared with the fp64 step:
+
+  * grads, per tensor: max |g - g64| / max |g64| within 4x what the plain fp32 oracle achieves
+    on the same tensor (floor 1e-6): the HIP path must be as accurate as a straightforward fp32
+    implementation of the reference's arithmetic, tensor by tensor. The table of achieved errors
+    is returned (and printed).
+  * post-Adam parameters, element-wise: an element whose fp64 grad is within 4 x the tensor's
+    grad error of zero can take either sign in fp32 (Adam then steps it either way by ~lr): it is
+    "undecided" and skipped. Every decided element must match within
+    4 * lr * err / |g64| + 2e-6, Adam's sensitivity to the grad error at that element, plus fp32
+    rounding of the parameter. At least 97 % of the elements must be decided.
+  * codebook EMA buffers (cluster_size, embed_avg, embed): element-wise within 1e-5 of the
+    buffer's largest magnitude.
+No global slack: every bound is per element or per tensor.
+"""
+import numpy as np
+import torch
+
+from oracle import encodec_oracle as O
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+def _flat_views(opt, names):
+    out = {}
+    for k, (p, _), (o, n) in zip(names, opt._views, opt.offsets):
+        out[k] = (p, opt.flat_grad[o:o + n].view_as(p), opt.exp_avg[o:o + n].view_as(p),
+                  opt.exp_avg_sq[o:o + n].view_as(p))
+    return out
+
+
+def snapshot(tr):
+    """The trainer's state before a step, on the host."""
+    s = {}
+    for tag, mod, opt in (('gen', tr.model, tr.opt), ('disc', tr.disc, tr.opt_d)):
+        if mod is None:
+            continue
+        names = [k for k, p in mod.named_parameters() if p.requires_grad]
+        v = _flat_views(opt, names)
+        s[tag] = {'p': {k: t[0].detach().cpu().clone() for k, t in v.items()},
+                  'm': {k: t[2].detach().cpu().clone() for k, t in v.items()},
+                  'v': {k: t[3].detach().cpu().clone() for k, t in v.items()},
+                  'step': opt.n_step, 'lr': float(opt.param_groups[0]['lr'])}
+    s['cbs'] = [{k: getattr(layer._codebook, k).detach().cpu().clone()
+                 for k in ('inited', 'cluster_size', 'embed', 'embed_avg')}
+                for layer in tr.model.quantizer.vq.layers]
+    st = tr.balancer._state
+    s['bal'] = None if st is None else (list(st['names']), st['total'].cpu().tolist(), st['fix'].cpu().tolist())
+    return s
+
+
+def oracle_step(snap, x, cfg, bandwidth, weights, dtype):
+    """O.train_step from the snapshot in `dtype` -> (out, params, codebooks, disc params)."""
+    p = {k: v.to(dtype) for k, v in snap['gen']['p'].items()}
+    adam = {k: {'step': snap['gen']['step'], 'm': snap['gen']['m'][k].to(dtype),
+                'v': snap['gen']['v'][k].to(dtype)} for k in p}
+    cbs = [{k: v.to(dtype) for k, v in cb.items()} for cb in snap['cbs']]
+    bal = O.Balancer(weights)
+    if snap['bal'] is not None:
+        for name, t, f in zip(*snap['bal']):
+            bal.total[name], bal.fix[name] = t, f
+    dp = dadam = dlr = None
+    if 'disc' in snap:
+        d = snap['disc']
+        dp = {k: v.to(dtype) for k, v in d['p'].items()}
+        dadam = {k: {'step': d['step'], 'm': d['m'][k].to(dtype), 'v': d['v'][k].to(dtype)} for k in dp}
+        dlr = d['lr']
+    out = O.train_step(x.detach().cpu().to(dtype), p, cbs, cfg, bandwidth, bal, adam, snap['gen']['lr'],
+                       disc_p=dp, disc_adam_state=dadam, disc_lr=dlr)
+    return out, p, cbs, dp
+
+
+def _check_opt(tag, mod, opt, g64, g32, p64, lr, table):
+    names = [k for k, p in mod.named_parameters() if p.requires_grad]
+    decided_n = total_n = 0
+    for k, (p, g, _, _) in _flat_views(opt, names).items():
+        if k not in g64:
+            continue
+        e = _rel(g, g64[k])
+        e32 = _rel(g32[k], g64[k])
+        bound = max(4 * e32, 1e-6)
+        table.append((f'{tag}:{k}', e, e32, bound))
+        assert e <= bound, (tag, k, e, e32)
+        gd = g64[k].double()
+        err = float((g.detach().double().cpu() - gd).abs().max())
+        decided = gd.abs() > 4 * err
+        decided_n += int(decided.sum())
+        total_n += gd.numel()
+        tol = 4 * lr * err / gd.abs().clamp_min(1e-30) + 2e-6
+        diff = (p.detach().double().cpu() - p64[k].double()).abs()
+        bad = decided & (diff > tol)
+        assert not bool(bad.any()), (tag, k, float(diff[decided].max()), int(bad.sum()))
+    assert decided_n >= 0.97 * total_n, (tag, decided_n, total_n)
+
+
+def check_grads(mine, g64, g32, what, floor=1e-6):
+    """Per tensor: rel err of `mine` vs fp64 within 4x the fp32 oracle's (floor `floor`).
+    mine / g64 / g32: name -> tensor. Returns the table [(name, err, err_fp32, bound)]."""
+    table = []
+    for k in g64:
+        e, e32 = _rel(mine[k], g64[k]), _rel(g32[k], g64[k])
+        bound = max(4 * e32, floor)
+        table.append((k, e, e32, bound))
+        assert e <= bound, (what, k, e, e32)
+    worst = max(table, key=lambda r: r[1] / r[3])
+    print(f'{what}: {len(table)} tensors, worst err {max(r[1] for r in table):.2e}; '
+          f'tightest {worst[0]} {worst[1]:.2e} vs fp32 oracle {worst[2]:.2e}')
+    return table
+
+
+def check_step(tr, x, cfg, bandwidth, weights, verbose=True):
+    """tr.step(x) against the oracle's step from the same state; returns (out, table)."""
+    snap = snapshot(tr)
+    out = tr.step(x)
+    torch.cuda.synchronize()
+    o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64)
+    o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32)
+    table = []
+    _check_opt('gen', tr.model, tr.opt, o64['grads'], o32['grads'], p64, snap['gen']['lr'], table)
+    if tr.disc is not None and 'disc_grads' in o64:
+        _check_opt('disc', tr.disc, tr.opt_d, o64['disc_grads'], o32['disc_grads'], dp64, snap['disc']['lr'], table)
+    for i, layer in enumerate(tr.model.quantizer.vq.layers):
+        cb = layer._codebook
+        for k in ('cluster_size', 'embed_avg', 'embed'):
+            e = _rel(getattr(cb, k), cbs64[i][k])
+            table.append((f'codebook{i}:{k}', e, float('nan'), 1e-5))
+            assert e <= 1e-5, (i, k, e)
+    for k in weights:
+        np.testing.assert_allclose(float(out[k]), o64[k], rtol=2e-5, err_msg=k)
+    if verbose:
+        worst = max(table, key=lambda r: r[1] / r[3])
+        print(f'step vs oracle: {len(table)} tensors, worst grad err {max(r[1] for r in table):.2e}, '
+              f'tightest {worst[0]} {worst[1]:.2e} / bound {worst[3]:.2e}')
+    return out, table

@@ -1,6 +1,6 @@
 """world_size-2 `gloo` tests of the data-parallel plumbing (CPU; the GPU run uses RCCL through
 the same calls): parameter broadcast at Trainer start, the flat-grad all-reduce of FlatAdam,
-distrib.py's helpers (distrib.py:55-124 of the reference)."""
+the bucketed async reduction of the training step, distrib.py's broadcast (distrib.py:55-72)."""
 import os
 import socket
 
@@ -68,20 +68,23 @@ def _body_broadcast(rank, world):
     return (ts[0].tolist(), ts[1].flatten().tolist(), int(ts[2]))
 
 
-def _body_metrics(rank, world):
+def _body_buckets(rank, world):
+    """The Trainer's bucketed exchange: the decoder span reduced async first, the rest (the
+    encoder span) async second, both waited for together -- equals one all-reduce."""
+    from encx.optim import FlatAdam
     from encx import distrib
-    m = distrib.average_metrics({'a': float(rank), 'b': 2.0 * rank}, count=rank + 1)
-    return m
-
-
-def _body_sync(rank, world):
-    from encx import distrib
-    buf = [torch.full((3,), float(rank))]
-    distrib.sync_buffer(buf, average=True)
-    p = torch.nn.Parameter(torch.zeros(2))
-    p.grad = torch.full((2,), float(rank * 4))
-    distrib.sync_grad([p])
-    return buf[0].tolist(), p.grad.tolist(), distrib.rank(), distrib.world_size()
+    torch.manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(6)), torch.nn.Parameter(torch.randn(4, 2)),
+              torch.nn.Parameter(torch.randn(3))]
+    opt = FlatAdam(params, lr=1e-3)
+    g = torch.arange(opt.flat_grad.numel(), dtype=torch.float32) * (rank + 1)
+    opt.flat_grad.copy_(g)
+    a, b = opt.span(params[1:])
+    works = [opt.reduce_async(a, b), opt.reduce_async(0, a)]
+    for w in works:
+        w.wait()
+    want = torch.arange(opt.flat_grad.numel(), dtype=torch.float32) * sum(r + 1 for r in range(world))
+    return bool(torch.equal(opt.flat_grad, want)), (a, b), distrib.rank(), distrib.world_size()
 
 
 def test_flat_grad_all_reduce_mean():
@@ -97,16 +100,8 @@ def test_broadcast_tensors_from_rank0():
         assert out[r][2] == r
 
 
-def test_average_metrics_weighted():
-    out = _run('_body_metrics')
-    # weights 1 and 2: a = (0*1 + 1*2) / 3
+def test_bucketed_async_reduce():
+    out = _run('_body_buckets')
     for r in range(2):
-        assert out[r]['a'] == pytest.approx(2 / 3)
-        assert out[r]['b'] == pytest.approx(4 / 3)
-
-
-def test_sync_buffer_and_grad():
-    out = _run('_body_sync')
-    for r in range(2):
-        buf, g, rk, ws = out[r]
-        assert buf == [0.5] * 3 and g == [2.0, 2.0] and rk == r and ws == 2
+        ok, span, rk, ws = out[r]
+        assert ok and span == (6, 17) and rk == r and ws == 2

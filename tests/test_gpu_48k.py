@@ -36,9 +36,11 @@ def build48k(d, pre):
 
 @pytest.mark.parametrize('gan', [False, True])
 def test_train_step_48k_fixture(gan):
-    """Two train steps of the 48 kHz stereo model (two segments, 4800 + 48 samples) against
-    the reference's losses and post-Adam parameter checksums (g9)."""
+    """Two train steps of the 48 kHz stereo model (two segments, 4800 + 48 samples): losses
+    against the reference's (g9), and each step element by element against the oracle's step
+    from the same state (tests/steputil.py)."""
     from encx.train import Trainer
+    from steputil import check_step
     d = load('g9_step48k.npz')
     pre = 'gan/' if gan else 'gen/'
     m, p, cbs, cfg = build48k(d, pre)
@@ -54,32 +56,16 @@ def test_train_step_48k_fixture(gan):
     tr = Trainer(m, disc, lr=1e-4, disc_lr=1e-4, scheduler=False, weights=weights, sample_rate=48000)
     x = T(d[pre + 'x']).to(DEV)
     for it in range(2):
-        out = tr.step(x)
+        out, _ = check_step(tr, x, cfg, 3.0, weights)
         for k in weights:
             np.testing.assert_allclose(float(out[k]), float(d[f'{pre}it{it}_{k}'].reshape(-1)[0]), rtol=2e-4,
                                        err_msg=f'it{it} {k}')
+        # loss_w: the commit loss of residuals ~10x smaller than the latent (see the 24 kHz
+        # test); step 0 against the fp32 reference, step 1 after its own Adam sign flips
         np.testing.assert_allclose(float(out['loss_w']), float(d[f'{pre}it{it}_loss_w'].reshape(-1)[0]),
-                                   rtol=5e-3, atol=1e-6)
+                                   rtol=1e-4 if it == 0 else 5e-3, atol=1e-6)
         if gan:
             np.testing.assert_allclose(float(out['l_d']), float(d[f'{pre}it{it}_l_d'].reshape(-1)[0]), rtol=1e-4)
-    flips = 20 * 2 * 1e-4 * 2
-    for k, v in m.state_dict().items():
-        ref = d[pre + 'p/' + k]
-        mine = np.array([v.double().sum().item(), v.double().abs().sum().item()])
-        # codebook buffers: the second step's codes come from weights that already differ by
-        # Adam sign flips, so a near-tie code may flip; one flip moves two embed_avg rows by
-        # 0.01 * |x| (~1e-4 of the buffer's abs-sum here)
-        r = 1e-3 if '_codebook.' in k else 1e-4
-        assert abs(mine[1] - ref[1]) <= r * ref[1] + flips, (k, mine, ref)
-        assert abs(mine[0] - ref[0]) <= r * ref[1] + flips, (k, mine, ref)
-    if gan:
-        for k, v in disc.state_dict().items():
-            if k.endswith('spec_transform.window'):
-                continue
-            ref = d['gan/d/' + k]
-            mine = np.array([v.double().sum().item(), v.double().abs().sum().item()])
-            assert abs(mine[1] - ref[1]) <= 1e-4 * ref[1] + flips, (k, mine, ref)
-            assert abs(mine[0] - ref[0]) <= 1e-5 * ref[1] + flips, (k, mine, ref)
 
 
 def test_forward_48k_vs_oracle_fp64():
@@ -98,14 +84,14 @@ def test_forward_48k_vs_oracle_fp64():
     y64, lw64, _, _, _ = O.encodec_forward_train(T(d['gen/x']).double(), p64, cbs64, cfg, 3.0)
     torch.autograd.backward([y64, lw64], [gy.cpu().double(), torch.ones_like(lw64)])
     assert rel(y, y64) < 1e-4, rel(y, y64)
-    worst, where = 0.0, ''
+    from steputil import check_grads
+    p32 = {k: v.float().requires_grad_(True) for k, v in p.items()}
+    cbs32 = [{k: v.float() for k, v in cb.items()} for cb in cbs]
+    y32, lw32, _, _, _ = O.encodec_forward_train(T(d['gen/x']).float(), p32, cbs32, cfg, 3.0)
+    torch.autograd.backward([y32, lw32], [gy.cpu(), torch.ones_like(lw32)])
     params = dict(m.named_parameters())
-    for k, v in p64.items():
-        e = rel(params[k].grad, v.grad)
-        if e > worst:
-            worst, where = e, k
-    print(f'worst grad rel err {worst:.3e} at {where}')
-    assert worst < 1e-3, (worst, where)
+    check_grads({k: params[k].grad for k in p64}, {k: v.grad for k, v in p64.items()},
+                {k: v.grad for k, v in p32.items()}, '48 kHz grads vs fp64')
 
 
 @pytest.mark.parametrize('B,C,T_,tl,tr', [(2, 32, 4800, 0, 0), (3, 64, 37, 0, 0), (1, 512, 1, 0, 0),

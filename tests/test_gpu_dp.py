@@ -79,8 +79,13 @@ CASES = {
     # encoder backward) vs HIP graphs (segments captured between the eager collectives)
     'gan_eager3': (True, False, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 3, False),
     'gan_graph3': (True, False, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 3, True),
+    # the same with the codebook sums all-reduced (deferred to one collective between segments)
+    'gan_sync_eager3': (True, True, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 3, False),
+    'gan_sync_graph3': (True, True, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 3, True),
 }
-MULTI_STEP = ('gan_eager3', 'gan_graph3')
+MULTI_STEP = ('gan_eager3', 'gan_graph3', 'gan_sync_eager3', 'gan_sync_graph3')
+# config 4's partition count: 8 ranks x B/8 against 1 rank x B (the same cases as the 2-rank run)
+CASES8 = ('gen_sync', 'gan_sync_plain')
 
 
 def _run_case(name, x):
@@ -107,26 +112,72 @@ def _run_case(name, x):
     return out
 
 
-def _rank_main(rank, world, port, outdir):
+def _run_g13(rank, local):
+    """The G13 step (tests/golden/make_goldens.py:g13): the reference's train_one_step under DDP,
+    2 ranks x 2 clips of 4800 samples, n_q 2, all four losses balanced, the discriminator trained,
+    warm-cosine LR at its first step. local: Trainer(ddp_commit_local=True), the reference's
+    rank-local commit grads."""
+    from oracle import encodec_oracle as O
+    from fixtures import model_state, codebooks_from_stats, disc_state, load
+    from synth import synth_wave
+    from encx.model import EncodecModel
+    from encx.msstftd import MultiScaleSTFTDiscriminator
+    from encx.train import Trainer
+    d = load('g13_ddp.npz')
+    cfg = O.Config(target_bandwidths=(1.5,), audio_normalize=True)
+    m = EncodecModel._get_model([1.5], 24000, 1, causal=True, model_norm='weight_norm', audio_normalize=True)
+    sd = dict(model_state(cfg, 71))
+    for i, cb in enumerate(codebooks_from_stats(d['stats'], 73, 2, cfg.n_q)):
+        for k, v in cb.items():
+            sd[f'quantizer.vq.layers.{i}._codebook.{k}'] = v
+    m.load_state_dict(sd)
+    m = m.to(DEV)
+    disc = MultiScaleSTFTDiscriminator(filters=32)
+    disc.load_state_dict(disc_state(74), strict=False)
+    disc = disc.to(DEV)
+    tr = Trainer(m, disc, lr=3e-4, disc_lr=3e-4, max_iter=100, warmup_iter=0, ddp_commit_local=local)
+    x = torch.from_numpy(synth_wave((4, 1, 4800), 131))[2 * rank:2 * rank + 2].to(DEV)
+    out = tr.step(x)
+    torch.cuda.synchronize()
+    res = {'loss/' + k: float(v) for k, v in out.items()}
+    names = [k for k, p in m.named_parameters() if p.requires_grad]
+    for (p, g), k in zip(tr.opt._views, names):
+        res['grad/' + k] = g.detach().cpu().clone()
+        res['param/' + k] = p.detach().cpu().clone()
+    res['disc_grad'] = tr.opt_d.flat_grad.cpu()
+    dn = [k for k, p in disc.named_parameters() if p.requires_grad]
+    for (p, _), k in zip(tr.opt_d._views, dn):
+        res['dparam/' + k] = p.detach().cpu().clone()
+    for i in range(2):
+        cb = m.quantizer.vq.layers[i]._codebook
+        for k in ('cluster_size', 'embed', 'embed_avg'):
+            res[f'cb{i}/{k}'] = getattr(cb, k).detach().cpu().clone()
+    return res
+
+
+def _rank_main(rank, world, port, outdir, cases, g13):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     torch.distributed.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        x = _batch()[rank * B:(rank + 1) * B]
-        for name in CASES:
+        b = 2 * B // world
+        x = _batch()[rank * b:(rank + 1) * b]
+        for name in cases:
             torch.save(_run_case(name, x), os.path.join(outdir, f'{name}_r{rank}.pt'))
+        if g13:
+            for local in (False, True):
+                torch.save(_run_g13(rank, local), os.path.join(outdir, f'g13_{int(local)}_r{rank}.pt'))
         torch.distributed.barrier()
     finally:
         torch.distributed.destroy_process_group()
 
 
-@pytest.fixture(scope='module')
-def runs():
+def _spawn(world, cases, g13=False):
     import torch.multiprocessing as mp
     outdir = tempfile.mkdtemp(prefix='encx_dp_')
     ctx = mp.get_context('spawn')
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, outdir)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, outdir, cases, g13)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -135,13 +186,29 @@ def runs():
     for p in procs:
         if p.is_alive():
             p.kill()
-    assert codes == [0, 0], f'rank processes exited with {codes}'
+    assert codes == [0] * world, f'rank processes exited with {codes}'
+    return outdir
+
+
+@pytest.fixture(scope='module')
+def runs():
+    outdir = _spawn(2, list(CASES), g13=True)
     two = {n: [torch.load(os.path.join(outdir, f'{n}_r{r}.pt'), weights_only=True) for r in range(2)]
            for n in CASES}
+    for local in (0, 1):
+        two[f'g13_{local}'] = [torch.load(os.path.join(outdir, f'g13_{local}_r{r}.pt'), weights_only=True)
+                               for r in range(2)]
     x = _batch()
     one = {n: _run_case(n, x) for n in CASES if n != 'gen_nosync' and n not in MULTI_STEP}
     halves = [_run_case('gen_nosync', x[r * B:(r + 1) * B]) for r in range(2)]
     return two, one, halves
+
+
+@pytest.fixture(scope='module')
+def runs8(runs):
+    outdir = _spawn(8, list(CASES8))
+    return {n: [torch.load(os.path.join(outdir, f'{n}_r{r}.pt'), weights_only=True) for r in range(8)]
+            for n in CASES8}
 
 
 def close(a, b, rtol):
@@ -233,9 +300,140 @@ def test_balanced_grads_half_plus_commit(runs):
 
 def test_graph_steps_match_eager_two_ranks(runs):
     """3 data-parallel GAN steps replayed from HIP graphs (collectives eager between the captured
-    segments) equal the eager run with the overlapped decoder-bucket all-reduce, bit for bit."""
+    segments: the decoder bucket's all-reduce overlapping the encoder backward, the encoder's
+    overlapping the discriminator phase) equal the eager run, bit for bit; with the codebook sums
+    all-reduced too (sync_codebooks)."""
     two, _, _ = runs
-    for r in range(2):
-        a, b = two['gan_eager3'][r], two['gan_graph3'][r]
-        for k in a:
-            assert torch.equal(a[k], b[k]), (r, k)
+    for eager, graph in (('gan_eager3', 'gan_graph3'), ('gan_sync_eager3', 'gan_sync_graph3')):
+        for r in range(2):
+            a, b = two[eager][r], two[graph][r]
+            for k in a:
+                assert torch.equal(a[k], b[k]), (eager, r, k)
+        for k in ('cb0.embed', 'cb7.cluster_size', 'gen_param'):
+            assert torch.equal(two[graph][0][k], two[graph][1][k]), k
+
+
+# ---------------------------------------------------------------- G13: the reference's DDP step
+def _g13_stats(v):
+    v = v.double().reshape(-1)
+    return np.array([v.sum().item(), v.abs().sum().item(), v.pow(2).sum().item()])
+
+
+def _g13_close(mine, want, what, rtol):
+    """per tensor: the sampled elements within rtol of the tensor's sampled scale, and the
+    abs-sum / squared sum of the whole tensor within rtol."""
+    from fixtures import g13_samples
+    worst = 0.0
+    for k, (ws, wsum) in want.items():
+        t = mine[k].double().reshape(-1)
+        s = t[torch.from_numpy(g13_samples(t.numel()))].numpy()
+        scale = max(np.abs(ws).max(), 1e-30)
+        e = float(np.abs(s - ws).max() / scale)
+        ms = _g13_stats(t)
+        e = max(e, abs(ms[1] - wsum[1]) / max(wsum[1], 1e-30), abs(ms[2] - wsum[2]) / max(wsum[2], 1e-30))
+        worst = max(worst, e)
+        assert e <= rtol, (what, k, e)
+    return worst
+
+
+def _g13_want(d, tag, rank=None):
+    pre = '' if rank is None else f'r{rank}/'
+    names = [k[len(pre + tag + '/'):] for k in d.files if k.startswith(pre + tag + '/')]
+    return {k: (d[f'{pre}{tag}/{k}'], d[f'{pre}{tag}_sum/{k}']) for k in names}
+
+
+def test_g13_reference_ddp_exact(runs):
+    """Trainer(ddp_commit_local=True) on 2 ranks against the reference's own DDP step (G13,
+    train_multi_gpu.py:56-124 under DDP :310-325): per rank, the generator grads Adam sees (the
+    DDP-averaged balanced grads + that rank's own commit grads), the post-Adam parameters (which
+    differ between the ranks, as the reference's do), the losses, each rank's codebook EMA
+    buffers, and the DDP-averaged discriminator grads."""
+    from fixtures import load
+    d = load('g13_ddp.npz')
+    two, _, _ = runs
+    r = two['g13_1']
+    for rank in range(2):
+        mine = {k[5:]: v for k, v in r[rank].items() if k.startswith('grad/')}
+        _g13_close(mine, _g13_want(d, 'total', rank), f'grad r{rank}', 2e-4)
+        for k in ('l_t', 'l_f', 'l_g', 'l_feat'):
+            want = float(d[f'r{rank}/loss/{k}'])
+            assert abs(r[rank]['loss/' + k] - want) <= 2e-5 * abs(want), (rank, k, r[rank]['loss/' + k], want)
+        for i in range(2):
+            assert close(r[rank][f'cb{i}/cluster_size'], torch.from_numpy(d[f'r{rank}/cb{i}/cluster_size']), 1e-6)
+            assert close(r[rank][f'cb{i}/embed_avg'][::16], torch.from_numpy(d[f'r{rank}/cb{i}/embed_avg_rows']), 1e-5)
+            assert close(r[rank][f'cb{i}/embed'][::16], torch.from_numpy(d[f'r{rank}/cb{i}/embed_rows']), 1e-5)
+        _g13_params(r[rank], d, rank)
+    # the commit grads stay rank-local: the ranks' encoder weights differ after the step
+    k = 'encoder.model.0.conv.conv.weight_v'
+    assert not torch.equal(r[0]['param/' + k], r[1]['param/' + k])
+    assert close(r[0]['disc_grad'], torch.from_numpy(d['disc_grad']), 2e-4)
+
+
+def _g13_params(res, d, rank):
+    """Post-Adam parameters (first Adam step: p - lr * g / (|g| + eps) up to bias correction)
+    at the sampled elements, element-wise; where the grad is so small that fp32 rounding can flip
+    its sign (|g| below 1e-3 of the tensor's largest sampled grad), Adam's step direction is
+    rounding, and the element is skipped."""
+    from fixtures import g13_samples
+    for k, want in _g13_want(d, 'param', rank).items():
+        p = res['param/' + k].double().reshape(-1)
+        idx = torch.from_numpy(g13_samples(p.numel()))
+        g = d[f'r{rank}/total/{k}']
+        live = np.abs(g) > 1e-3 * max(np.abs(g).max(), 1e-30)
+        diff = np.abs(p[idx].numpy() - want[0])
+        assert float(diff[live].max(initial=0.0)) <= 2e-6, (rank, k, float(diff[live].max()))
+
+
+def test_g13_true_data_parallel(runs):
+    """The default Trainer (one combined backward, deviation #7) on the G13 step: both ranks
+    hold the same grads = the reference's DDP-averaged balanced grads + the MEAN of the two ranks'
+    commit grads, and the same parameters."""
+    from fixtures import load
+    d = load('g13_ddp.npz')
+    two, _, _ = runs
+    r = two['g13_0']
+    bal = _g13_want(d, 'bal')
+    c0, c1 = _g13_want(d, 'commit', 0), _g13_want(d, 'commit', 1)
+    for rank in range(2):
+        mine = {k[5:]: v.double() for k, v in r[rank].items() if k.startswith('grad/')}
+        worst = 0.0
+        for k, (bs, _) in bal.items():
+            from fixtures import g13_samples
+            t = mine[k].reshape(-1)
+            s = t[torch.from_numpy(g13_samples(t.numel()))].numpy()
+            ws = bs + 0.5 * (c0[k][0] + c1[k][0])
+            e = float(np.abs(s - ws).max() / max(np.abs(ws).max(), 1e-30))
+            worst = max(worst, e)
+            assert e <= 2e-4, (rank, k, e)
+    for k in r[0]:
+        if k.startswith(('grad/', 'param/')):
+            assert torch.equal(r[0][k], r[1][k]), k
+
+
+# ---------------------------------------------------------------- config 4's partition count
+def test_eight_ranks_identical(runs8):
+    for name in CASES8:
+        r0 = runs8[name][0]
+        for r in range(1, 8):
+            assert torch.equal(r0['gen_param'], runs8[name][r]['gen_param']), (name, r)
+            if 'disc_param' in r0:
+                assert torch.equal(r0['disc_param'], runs8[name][r]['disc_param']), (name, r)
+
+
+def test_eight_ranks_match_single_process(runs8, runs):
+    """8 ranks x B4 over gloo (config 4's partition of a batch) against 1 rank x B32: codes,
+    synced codebooks, and (balancer off) the averaged grads; with the balancer, 1/8 of the
+    balanced grad + the commit grad."""
+    _, one, _ = runs
+    r8 = runs8['gan_sync_plain']
+    ref = one['gan_sync_plain']
+    codes = torch.cat([r8[r]['codes'] for r in range(8)], dim=1)
+    assert torch.equal(codes, ref['codes'])
+    for i in range(8):
+        for k in ('cluster_size', 'embed', 'embed_avg'):
+            assert close(r8[0][f'cb{i}.{k}'], ref[f'cb{i}.{k}'], 1e-5), (i, k)
+    assert close(r8[0]['gen_grad'], ref['gen_grad'], 1e-4)
+    assert close(r8[0]['disc_grad'], ref['disc_grad'], 1e-4)
+    g_bal, g_commit = _split_grads(_batch())
+    want = g_bal.double() / 8 + g_commit.double()
+    assert close(runs8['gen_sync'][0]['gen_grad'], want, 1e-4)

@@ -7,7 +7,8 @@ Parity rule (index work is bit-exact): for EVERY segment and EVERY codebook laye
 must equal the fp64 RVQ of the segment's latent on every frame that fp64 certifies
 (fixtures.rvq_certified: a top-2 distance gap beyond the worst-case fp32 rounding of the
 distance, all earlier layers certified too), and on every frame the ~3-sigma statistical
-certificate covers. The decoded waveform is compared unconditionally: the oracle's codes and
+certificate covers; and they must equal the ORACLE's own codes on every frame certified for
+both latents (ours and the oracle's). The decoded waveform is compared unconditionally: the oracle's codes and
 scales are fed to both decoders."""
 import numpy as np
 import pytest
@@ -60,6 +61,14 @@ def check_segments(m, x, p, cbs, cfg, bw):
                 print(f'certified at {factor}: {float(cert.float().mean()):.3f} of the codes')
                 assert cert.any()
                 assert torch.equal(mine[cert], want[cert]), (factor, int((mine[cert] != want[cert]).sum()))
+            # against the ORACLE's own codes (its fp32 latent, its argmin) where the fp64 gap
+            # certifies the code for both latents: then both must have picked the fp64 winner
+            want_o, cert_o = rvq_certified(emb_o, embeds, 256)
+            _, cert_m = rvq_certified(emb, embeds, 256)
+            both = cert_o & cert_m & (want_o == want)
+            co = torch.as_tensor(codes_o).transpose(0, 1).long()
+            assert both.float().mean() > 0.5, float(both.float().mean())
+            assert torch.equal(mine[both], co[both]), int((mine[both] != co[both]).sum())
         y_ref = O.encodec_decode_eval([(c, s) for c, s, _ in ref], p, cbs, cfg, x.shape[-1])
         y_mine = m.decode([(c.to(DEV), None if s is None else s.to(DEV)) for c, s, _ in ref])[:, :, :x.shape[-1]]
     assert rel(y_mine, y_ref) < 1e-3, rel(y_mine, y_ref)

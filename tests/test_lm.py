@@ -92,6 +92,90 @@ def test_gpu_quantized_cdf_matches_reference():
         ac.build_stable_quantized_cdf(torch.full((1024,), 1 / 1024, device=DEV), 10)
 
 
+def straddle_stream(bits=24, rounds=6, seed=0):
+    """Symbols + per-step cdfs that keep the coder's interval straddling the bit-max_bit boundary
+    B = 2^max_bit for as long as ac.py:157 allows (each straddling push picks a 2m+1-wide symbol
+    around B, so nothing flushes and max_bit grows by ~bits - log2(2m+1) per push), then resolve
+    it with the symbol just below B, which flushes the whole carried prefix at once. Returns
+    (symbols, cdfs, the largest max_bit reached before a flush). Big-int arithmetic, as ac.py's."""
+    g = np.random.default_rng(seed)
+    R = 1 << bits
+    low = high = 0
+    max_bit = -1
+    syms, cdfs, peak = [], [], -1
+    for _ in range(rounds):
+        straddle = True
+        while True:
+            lo, hi, mb = low, high, max_bit
+            while hi - lo + 1 < R:
+                lo, hi, mb = 2 * lo, 2 * hi + 1, mb + 1
+            delta = hi - lo + 1
+            B = 1 << mb
+            m = int(g.integers(2, 6))
+            if straddle and lo < B <= hi:
+                t = ((B - lo) * R) // delta
+                rl, rh = max(1, t - m), min(R - 2, t + m)
+                cdf = [rl, rh + 1, R]
+                el = -((-rl * delta) // R)
+                eh = (rh * delta) // R
+                nlo, nhi = lo + el, lo + eh
+                # keep straddling while the push leaves max_bit <= 61 (nothing flushes: ac.py:157)
+                if nlo < B <= nhi and mb <= 61:
+                    syms.append(1)
+                    cdfs.append(cdf)
+                    low, high, max_bit = nlo, nhi, mb
+                    peak = max(peak, mb)
+                    continue
+            # resolve: the symbol whose interval ends just below B (or a random one if none)
+            t = ((B - lo) * R) // delta if lo < B <= hi else R // 2
+            cut = max(2, min(R - 2, t - 1))
+            cdf = [cut, R]
+            el, eh = 0, ((cut - 1) * delta) // R
+            low, high = lo + el, lo + eh
+            max_bit = mb
+            peak = max(peak, mb)
+            syms.append(0)
+            cdfs.append(cdf)
+            while max_bit >= 0 and (low >> max_bit) == (high >> max_bit):
+                b = low >> max_bit
+                low -= b << max_bit
+                high -= b << max_bit
+                max_bit -= 1
+            assert max_bit <= 61
+            break
+    return syms, [np.array(c, np.int32) for c in cdfs], peak
+
+
+def test_ac_oracle_long_straddle():
+    """The crafted stream carries more than 64 undecided bits through a push (the reference's
+    Python ints hold them; a 64-bit coder state would overflow) and round-trips in the oracle."""
+    from oracle import ac_oracle as A
+    syms, cdfs, peak = straddle_stream()
+    assert peak > 64, peak
+    data = A.encode(syms, cdfs, 24)
+    assert A.decode(data, cdfs, 24) == syms
+
+
+@pytest.mark.gpu
+def test_gpu_ac_long_straddle_matches_oracle():
+    """encx_ac_encode / encx_ac_decode on the long-straddle stream: bytes and symbols equal the
+    big-int oracle's (the coder state is 128 bits wide)."""
+    from oracle import ac_oracle as A
+    from encx import ac
+    for seed in range(3):
+        syms, cdfs, peak = straddle_stream(seed=seed)
+        want = A.encode(syms, cdfs, 24)
+        fo = io.BytesIO()
+        enc = ac.ArithmeticCoder(fo, total_range_bits=24)
+        dc = [torch.from_numpy(c).to(DEV) for c in cdfs]
+        for sy, c in zip(syms, dc):
+            enc.push(sy, c)
+        enc.flush()
+        assert fo.getvalue() == want, (seed, peak)
+        dec = ac.ArithmeticDecoder(io.BytesIO(want), total_range_bits=24)
+        assert [dec.pull(c) for c in dc] == syms
+
+
 @pytest.mark.gpu
 def test_gpu_arithmetic_coder_matches_reference_bytes():
     from encx import ac

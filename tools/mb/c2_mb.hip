@@ -130,6 +130,13 @@ int main(int argc, char** argv) {
                        e > 1e-5 ? "  MISMATCH" : "");
                 if (e <= 1e-5 && t < best) best = t;
             };
+            if (fwr_ok(g)) {
+                for (int wgs : {256, 512, 1024}) {
+                    char nm[32];
+                    snprintf(nm, 32, "rw wgs %d", wgs);
+                    var(nm, [&] { if (run_fwd_rw(b, wgs, st)) printf("    (n/a)\n"); });
+                }
+            }
             if (l.Co <= 32) {
                 if (l.KF == 9) {
                     var("r<256,9,6,16>", [&] { if (run_fwdr<256, 9, 6, 16>(b, st)) printf("    (n/a)\n"); });
@@ -175,6 +182,13 @@ int main(int argc, char** argv) {
                        e > 1e-5 ? "  MISMATCH" : "");
                 if (e <= 1e-5 && t < best) best = t;
             };
+            if (dgr_ok(g)) {
+                for (int wgs : {256, 512}) {
+                    char nm[32];
+                    snprintf(nm, 32, "rw wgs %d", wgs);
+                    var(nm, [&] { if (run_dgrad_rw(b, wgs, st)) printf("    (n/a)\n"); });
+                }
+            }
             if (M == 64 && J == 5) {
                 var("r<2,256,5,4,8,3>", [&] { if (run_dgradr<2, 256, 5, 4, 8, 3>(b, st)) printf("    (n/a)\n"); });
                 var("r<2,256,5,4,8,3,SP>", [&] { if (run_dgradr<2, 256, 5, 4, 8, 3, 2>(b, st)) printf("    (n/a)\n"); });
@@ -267,6 +281,23 @@ int main(int argc, char** argv) {
                        flops / t * 1e-9, e, e > 1e-5 ? "  MISMATCH" : "", q.splits, q.lds);
                 if (e <= 1e-5 && t < best) best = t;
             };
+            if (wgr_ok(g)) {
+                for (int waves : {1024, 1536, 2048}) {
+                    const WgPlanR q = plan_wgr(g, waves);
+                    CK(hipMemset(dw1, 0, (size_t)l.Co * N * 4));
+                    double t = time_ms([&] {
+                        run_wgrad_rw(g, dy, yact, x, ws, q, st);
+                        hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(l.Co * N, 64)), dim3(256), 0, st, ws, q.splits,
+                                           l.Co, N, dw1, db1, 0, 0);
+                    });
+                    double tk = time_ms([&] { run_wgrad_rw(g, dy, yact, x, ws, q, st); });
+                    double e = fmax(rel_err(dw1, dw0, (size_t)l.Co * (N - 1)), rel_err(db1, db0, l.Co));
+                    printf("  wgrad rw %-20d %8.1f us  %6.1f TF/s  err %.1e%s  (splits %d, kernel only %.1f us %.1f TF/s)\n",
+                           waves, t * 1e3, flops / t * 1e-9, e, e > 1e-5 ? "  MISMATCH" : "", q.splits, tk * 1e3,
+                           flops / tk * 1e-9);
+                    if (e <= 1e-5 && t < best) best = t;
+                }
+            }
             if (gc && l.KF == 9) {
                 var3("3<9,1,9,4,1,5,PF0> 768", 32, 768, [&](const WgPlan3& q) { return run_wgrad3<9, 1, 9, 4, 1, 5, 0>(g, dy, yact, x, ws, q, st); });
             } else if (l.Ci == 2 && l.KF == 9) {  // first layer: all 6 combos in one group, 54 of 64 columns
