@@ -48,6 +48,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--no-graphs', action='store_true', help='eager steps instead of HIP-graph replay')
+    ap.add_argument('--sync-codebooks', action='store_true',
+                    help='all-reduce the RVQ EMA code sums across ranks (north_star DP; off = reference)')
     return ap.parse_args()
 
 
@@ -119,7 +121,8 @@ def main():
         # config 5 (scripts/train.sbatch:18-33): 48 kHz stereo, non-causal, time_group_norm,
         # 1 s segments (48000 + 480 samples per clip), n_q 16, lr 1e-4, l_g = l_feat = 4
         model = EncodecModel._get_model([24.0], 48000, 2, causal=False, model_norm='time_group_norm',
-                                        audio_normalize=True, segment=1.0, name='encodec_48khz').to(dev)
+                                        audio_normalize=True, segment=1.0, name='encodec_48khz',
+                                        sync_codebooks=args.sync_codebooks).to(dev)
         from encx.msstftd import MultiScaleSTFTDiscriminator
         disc = MultiScaleSTFTDiscriminator(filters=32, in_channels=2, out_channels=2).to(dev)
         trainer = Trainer(model, disc, lr=1e-4, disc_lr=1e-4, max_iter=100000, warmup_iter=500,
@@ -128,7 +131,8 @@ def main():
         shape = (B, 2, 48000)
     else:
         model = EncodecModel._get_model([6.0], 24000, 1, causal=True, model_norm='weight_norm',
-                                        audio_normalize=True, name='my_encodec').to(dev)
+                                        audio_normalize=True, name='my_encodec',
+                                        sync_codebooks=args.sync_codebooks).to(dev)
         disc = None
         if args.config == 'gan':
             from encx.msstftd import MultiScaleSTFTDiscriminator
@@ -233,6 +237,15 @@ def main():
             'roofline': roof,
             'whole_step': whole,
         }
+        if args.sync_codebooks:
+            out['config']['sync_codebooks'] = True
+        if rehearse:
+            # every rank shared ONE physical GPU over gloo: a rehearsal of the N-rank code path,
+            # not an N-GPU measurement
+            out['rehearsal'] = True
+            out['n_gpus'] = 1
+            out['ranks'] = world
+            out['config']['parallelism'] = f'dp{world} rehearsal: {world} ranks on 1 GPU over gloo'
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(args.config, min(16, os.cpu_count() or 1))
         print(json.dumps(out), flush=True)

@@ -822,8 +822,15 @@ struct C2FwdR {
     int F4;     // quads per output row
     int tiles;  // ceil(B * T2 * F4 / 32)
 };
-template <int KF, int S, int WQ, int NWV>
-__global__ __launch_bounds__(NWV * 64, 2) void c2_fwd_rw_kernel(C2FwdR a) {
+// Slot order of the persistent register-window loops (one NWV-wave workgroup per CU): item j of
+// a round goes to wave j / gridDim.x of the j % gridDim.x-th workgroup in XCD order. A partial last
+// round thus hands out one item per SIMD (waves w and w + 4 share one) before any SIMD takes a second
+// -- the workgroup-major order piled it onto the first CUs, costing a whole extra round on layers
+// with 1.5x or 2.9x as many items as wave slots -- and neighbouring items still share an XCD's L2.
+ENCX_DEV int rw_first_slot(int wave) { return wave * (int)gridDim.x + xcd_linear_id(); }
+
+template <int KF, int S, int WQ, int NWV, bool APF>
+__global__ __launch_bounds__(NWV * 64) void c2_fwd_rw_kernel(C2FwdR a) {
     constexpr int NE = 4 * WQ, KT = 3;  // window elements per lane; kernel rows (host-checked)
     extern __shared__ float smem[];
     const C2Geo g = a.g;
@@ -841,7 +848,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_fwd_rw_kernel(C2FwdR a) {
     const int plane = g.T2 * g.Fi, xlast = g.B * g.Ci * plane - 4;
     const int CP = g.Ci >> 1;  // channel pairs
     const int cstride = 2 * plane;
-    for (int tile = blockIdx.x * NWV + wave; tile < a.tiles; tile += gridDim.x * NWV) {
+    for (int tile = rw_first_slot(wave); tile < a.tiles; tile += gridDim.x * NWV) {
         const int qd = min(tile * 32 + l, quads - 1);
         const int fq = qd % a.F4, bt = qd / a.F4;
         const int t = bt % g.T2, b = bt / g.T2;
@@ -870,15 +877,26 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_fwd_rw_kernel(C2FwdR a) {
         f32x16 acc[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] = (f32x16){0};
-        // three register windows, one per kt: step (c, kt) multiplies window kt while the next
-        // step's window is in flight (the prefetch is unconditional, so every wait is exact)
+        // three register windows and weight columns, one per kt: step (c, kt) multiplies
+        // window kt with weights kt while the next step's window (global) and weights (LDS) are
+        // in flight (the prefetches are unconditional, so every wait is exact)
         f32x4 wb[KT][WQ];
+        float ab[KT][APF ? KF : 1];
+        auto wcol = [&](int c, int kt) { return Ws + ((2 * c + h) * KT + kt) * KF * 32 + l; };
+        auto load_a = [&](float* av, int c, int kt) {
+            if (!APF) return;
+            const float* wk = wcol(c, kt);
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf) av[APF ? kf : 0] = wk[kf * 32];
+        };
         load(wb[0], 0, 0);
+        load_a(ab[0], 0, 0);
         for (int c = 0; c < CP; ++c) {
 #pragma unroll
             for (int kt = 0; kt < KT; ++kt) {
-                if (kt + 1 < KT) load(wb[kt + 1], c, kt + 1);
-                else load(wb[0], min(c + 1, CP - 1), 0);
+                const int nk = kt + 1 < KT ? kt + 1 : 0, nc = kt + 1 < KT ? c : min(c + 1, CP - 1);
+                load(wb[nk], nc, nk);
+                load_a(ab[nk], nc, nk);
                 f32x4* w = wb[kt];
                 if (fix) {
                     const int base = rb[kt] + c * cstride;
@@ -891,10 +909,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_fwd_rw_kernel(C2FwdR a) {
                             if (!((msk[kt] >> (4 * q + e)) & 1u)) w[q][e] = 0.f;
                     }
                 }
-                const float* wk = Ws + ((2 * c + h) * KT + kt) * KF * 32 + l;
+                const float* wk = wcol(c, kt);
 #pragma unroll
                 for (int kf = 0; kf < KF; ++kf) {
-                    const float av = wk[kf * 32];
+                    const float av = APF ? ab[kt][APF ? kf : 0] : wk[kf * 32];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int r = S * j + kf;
@@ -1392,9 +1410,11 @@ struct C2DgR {
     int U4;     // quads per polyphase row
     int tiles;  // ceil(B * T2 * U4 / 32)
 };
-template <int J, int S, int TM, int WQ, bool YM, int NWV>
-__global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
-    constexpr int NE = 4 * WQ, KT = 3, M = 32 * TM;
+template <int J, int S, int RT, int WQ, bool YM, int NWV, int TM, bool APF>
+__global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
+    // RT row tiles of 32 (M = Ci*S = 32 RT); a work item is (column tile, TM row tiles); APF:
+    // the weight columns of step s + 1 are read from LDS during step s (else just in time)
+    constexpr int NE = 4 * WQ, KT = 3, M = 32 * RT, RG = RT / TM;
     const C2Dg& a = R.d;
     extern __shared__ float smem[];
     const C2Geo g = a.g;
@@ -1407,7 +1427,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
     const int plane = g.T2 * g.Fo, ylast = g.B * g.Co * plane - 4;
     const int CP = g.Co >> 1, cstride = 2 * plane;
     const float fc = feat_coef(a);
-    for (int tile = blockIdx.x * NWV + wave; tile < R.tiles; tile += gridDim.x * NWV) {
+    for (int item = rw_first_slot(wave); item < R.tiles * RG; item += gridDim.x * NWV) {
+        const int tile = item / RG, rt = item - tile * RG;  // rows rt*TM*32 .. + TM*32
         const int qd = min(tile * 32 + l, quads - 1);
         const int uq = qd % R.U4, bt = qd / R.U4;
         const int t = bt % g.T2, b = bt / g.T2;
@@ -1427,7 +1448,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
             clean = clean && msk[kt] == (1u << NE) - 1;
         }
         const bool fix = !__all(clean);  // wave-uniform
-        f32x4 wb[KT][WQ], yb[KT][WQ];
+        // two register buffers (windows + weight columns), alternating over the (c, kt) steps:
+        // step s + 1 is in flight while step s multiplies. The loop body is 2 channel pairs x 3
+        // kt = 6 steps, so every buffer / kt index is a compile-time constant (Co % 4 == 0).
+        f32x4 wb[2][WQ], yb[2][WQ];
+        float ab[2][APF ? J * TM : 1];
+        auto acol = [&](int c, int kt) { return As + ((2 * c + h) * KT + kt) * J * M + rt * TM * 32 + l; };
         auto load = [&](int k, int c, int kt) {
             const int base = rb[kt] + c * cstride;
 #pragma unroll
@@ -1436,6 +1462,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
                 wb[k][q] = ld4u(a.dy + o);
                 if (YM) yb[k][q] = ld4u(a.yact + o);
             }
+            if (APF) {
+                const float* ak = acol(c, kt);
+#pragma unroll
+                for (int q = 0; q < J; ++q)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) ab[k][APF ? q * TM + i : 0] = ak[q * M + i * 32];
+            }
         };
         f32x16 acc[TM][4];
 #pragma unroll
@@ -1443,17 +1476,20 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){0};
         load(0, 0, 0);
-        for (int c = 0; c < CP; ++c) {
+        for (int c0 = 0; c0 < CP; c0 += 2) {
 #pragma unroll
-            for (int kt = 0; kt < KT; ++kt) {
-                if (kt + 1 < KT) load(kt + 1, c, kt + 1);
-                else load(0, min(c + 1, CP - 1), 0);
-                f32x4* w = wb[kt];
+            for (int u = 0; u < 2 * KT; ++u) {
+                const int kt = u % KT, c = c0 + u / KT, k = u & 1;
+                // the next step (past the end: the last one again, never used)
+                const int nu = u + 1 < 2 * KT ? u + 1 : 0;
+                const int nc = u + 1 < 2 * KT ? c0 + nu / KT : min(c0 + 2, CP - 1);
+                load(k ^ 1, nc, nu % KT);
+                f32x4* w = wb[k];
                 if (YM) {
 #pragma unroll
                     for (int q = 0; q < WQ; ++q)
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) w[q][e] *= lrelu_grad(yb[kt][q][e]);
+                        for (int e = 0; e < 4; ++e) w[q][e] *= lrelu_grad(yb[k][q][e]);
                 }
                 if (fix) {
                     const int base = rb[kt] + c * cstride;
@@ -1466,12 +1502,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
                             if (!((msk[kt] >> (4 * q + e)) & 1u)) w[q][e] = 0.f;
                     }
                 }
-                const float* ak = As + ((2 * c + h) * KT + kt) * J * M + l;
+                const float* ak = acol(c, kt);
 #pragma unroll
                 for (int q = 0; q < J; ++q) {
                     float av[TM];
 #pragma unroll
-                    for (int i = 0; i < TM; ++i) av[i] = ak[q * M + i * 32];
+                    for (int i = 0; i < TM; ++i) av[i] = APF ? ab[k][APF ? q * TM + i : 0] : ak[q * M + i * 32];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int r = j - q + J - 1;  // window element of column u0 + j, tap q
@@ -1489,7 +1525,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; r += 2) {
-                    const int ci = (i * 32 + mfma_row(r, lane)) >> 1;
+                    const int ci = ((rt * TM + i) * 32 + mfma_row(r, lane)) >> 1;
                     const int f = 2 * u0 - g.pf;
                     const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
                     float v[8];
@@ -1532,7 +1568,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void c2_dgrad_rw_kernel(C2DgR R) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int ci = i * 32 + mfma_row(r, lane);
+                    const int ci = (rt * TM + i) * 32 + mfma_row(r, lane);
                     const int f = u0 - g.pf;
                     const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
                     if (f >= 0 && f + 4 <= g.Fi) {
@@ -2852,36 +2888,49 @@ int run_fwdq(C2Fwd a, hipStream_t st) {
 }
 
 // register-window backward-data (c2_dgrad_rw_kernel): 3x9 stride 2 (M = 64) and 3x3 stride 1
-// (M = 32) layers with even Co; the polyphase weights in LDS
+// (M = 32) layers with Co % 4 == 0; the polyphase weights in LDS
 static bool dgr_ok(const C2Geo& g) {
-    if ((g.Co & 1) || g.KT != 3 || g.Fi < 4 || g.Fo < 4) return false;
+    if ((g.Co & 3) || g.KT != 3 || g.Fi < 4 || g.Fo < 4) return false;
     if (!((g.KF == 9 && g.sf == 2 && g.Ci == 32) || (g.KF == 3 && g.sf == 1 && g.Ci == 32))) return false;
     if ((int64_t)g.B * g.Co * g.T2 * g.Fo >= (1ll << 31) - 64) return false;
     const int J = (g.KF + g.sf - 1) / g.sf;
     return (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float) <= 150 * 1024;
 }
-static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st) {
+template <int NWV, int TM, bool APF>
+static int run_dgrad_rw_n(const C2Dg& d, int wgs, hipStream_t st) {
     const C2Geo& g = d.g;
-    if (!dgr_ok(g)) return ENCX_EINVAL;
-    constexpr int NWV = 8;
     C2DgR R{d, 0, 0};
     R.d.U = (g.Fi - 1 + g.pf) / g.sf + 1;
     R.U4 = (int)cdiv(R.d.U, 4);
     R.tiles = (int)cdiv((int64_t)g.B * g.T2 * R.U4, 32);
     const int J = (g.KF + g.sf - 1) / g.sf;
     const size_t lds = (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float);
-    const int grid = (int)min((int64_t)wgs, cdiv(R.tiles, NWV));
+    const int RT = g.Ci * g.sf / 32, rg = max(1, RT / TM);
+    const int grid = (int)min((int64_t)wgs, cdiv((int64_t)R.tiles * rg, NWV));
     const bool ym = d.yact != nullptr;
     if (g.KF == 9) {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, TM, APF>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, TM, APF>), dim3(grid), dim3(NWV * 64), lds, st, R);
     } else {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV, 1, APF>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV, 1, APF>), dim3(grid), dim3(NWV * 64), lds, st, R);
     }
     ENCX_CHECK_LAUNCH();
     return 0;
 }
+// variant: 0 = 8 waves, both row tiles per item, weights just in time; 1 = 8 waves, one row tile
+// per item, weights prefetched; 2 = 12 waves, one row tile, prefetched; 3 = 8 waves, one row tile,
+// just in time
+static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st, int variant = 0) {
+    if (!dgr_ok(d.g)) return ENCX_EINVAL;
+    switch (variant) {
+        case 1: return run_dgrad_rw_n<8, 1, true>(d, wgs, st);
+        case 2: return run_dgrad_rw_n<12, 1, true>(d, wgs, st);
+        case 3: return run_dgrad_rw_n<8, 1, false>(d, wgs, st);
+        default: return run_dgrad_rw_n<8, 2, false>(d, wgs, st);
+    }
+}
+
 // register-window forward (c2_fwd_rw_kernel): 32-wide output-channel tile, even Ci, KT <= 3,
 // the layer's weights in LDS (<= 128 KB)
 static bool fwr_ok(const C2Geo& g) {
@@ -2891,22 +2940,27 @@ static bool fwr_ok(const C2Geo& g) {
     if (!((g.KF == 9 && (g.sf == 2 || g.sf == 1)) || (g.KF == 3 && g.sf == 1))) return false;
     return (size_t)g.Ci * g.KT * g.KF * 32 * sizeof(float) <= 128 * 1024;
 }
-static int run_fwd_rw(const C2Fwd& f, int wgs, hipStream_t st) {
+template <int NWV, bool APF>
+static int run_fwd_rw_n(const C2Fwd& f, int wgs, hipStream_t st) {
     const C2Geo& g = f.g;
-    if (!fwr_ok(g)) return ENCX_EINVAL;
-    constexpr int NWV = 8;
     C2FwdR a{g, f.x, f.wf, f.bias, f.y, f.act, (int)cdiv(g.Fo, 4), 0};
     a.tiles = (int)cdiv((int64_t)g.B * g.T2 * a.F4, 32);
     const size_t lds = ((size_t)g.Ci * g.KT * g.KF * 32 + 32) * sizeof(float);
     const int grid = (int)min((int64_t)wgs, cdiv(a.tiles, NWV));
     if (g.KF == 9 && g.sf == 2)
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 2, 4, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 2, 4, NWV, APF>), dim3(grid), dim3(NWV * 64), lds, st, a);
     else if (g.KF == 9)
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 1, 3, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 1, 3, NWV, APF>), dim3(grid), dim3(NWV * 64), lds, st, a);
     else
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<3, 1, 2, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<3, 1, 2, NWV, APF>), dim3(grid), dim3(NWV * 64), lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
+}
+// wgs: workgroups (one per CU holds the layer's weights); variant: 0 = 8 waves, weights just in
+// time from LDS; 1 = 8 waves, weights prefetched a step ahead
+static int run_fwd_rw(const C2Fwd& f, int wgs, hipStream_t st, int variant = 0) {
+    if (!fwr_ok(f.g)) return ENCX_EINVAL;
+    return variant == 1 ? run_fwd_rw_n<8, true>(f, wgs, st) : run_fwd_rw_n<8, false>(f, wgs, st);
 }
 template <int BN, int KFC, int MQ, int CKM, int OCC = 1>
 int run_fwdr(C2Fwd a, hipStream_t st) {
@@ -3144,6 +3198,22 @@ int encx_conv2d_wpoly(const float* wf, float* wp, int64_t Co, int64_t Ci, int64_
     return 0;
 }
 
+// Register-window or tiled kernel for a layer. The register-window kernels hand whole 128-position
+// items to SIMDs (rw_first_slot), so their time follows ceil(items / SIMDs) item rounds; the tiled
+// kernels' time follows the positions. Per round / per 128 x SIMDs positions, measured on the
+// config-3 layers (tools/mb/c2_mb, profiles/r03/mb_rw.md): forward 66 vs 87 us, bwd-data 78 vs 92
+// us -- so the register-window form loses on layers whose last round is mostly idle (Fo 65 at
+// T2 90, Fo 65 at T2 184) and wins everywhere else. `ratio` = tiled / register-window cost.
+static bool rw_pays(int64_t items, int64_t positions, double ratio) {
+    static const int simds = [] {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) cus = 256;
+        return 4 * cus;
+    }();
+    const double rounds = std::ceil((double)items / simds), tiled = (double)positions / (128.0 * simds);
+    return rounds < ratio * tiled;
+}
+
 int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y, int64_t B, int64_t Ci,
                     int64_t T2, int64_t Fi, int64_t Co, int64_t Fo, int64_t KT, int64_t KF, int64_t sf,
                     int64_t dt, int64_t pt, int64_t pf, int act, encx_stream_t stream) {
@@ -3156,7 +3226,10 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
     // register-window form (c2_fwd_rw_kernel); ENCX_FWR = workgroups (0: off)
     static const int fw_wgs = [] { const char* v = getenv("ENCX_FWR"); return v ? atoi(v) : 256; }();
-    if (fw_wgs > 0 && fwr_ok(g) && run_fwd_rw(a, fw_wgs, st) == 0) return 0;
+    if (fw_wgs > 0 && fwr_ok(g) &&
+        (Ci * KT < 16 || rw_pays(cdiv(B * T2 * cdiv(Fo, 4), 32), B * T2 * Fo, 87.0 / 66.0)) &&
+        run_fwd_rw(a, fw_wgs, st) == 0)
+        return 0;
     if (Co == 1 && KT == 3 && KF == 3 && (sf == 1 || sf == 2)) {
         dim3 grid((unsigned)cdiv(T2 * Fo, 64), (unsigned)B);
         if (sf == 1) hipLaunchKernelGGL((c2_co1_fwd<3, 3, 1>), grid, dim3(256), 0, st, a);
@@ -3221,7 +3294,9 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
     }
     // register-window form (c2_dgrad_rw_kernel); ENCX_DGR = workgroups (0: off)
     static const int dg_wgs = [] { const char* v = getenv("ENCX_DGR"); return v ? atoi(v) : 256; }();
-    if (dg_wgs > 0 && dgr_ok(g) && run_dgrad_rw(a, dg_wgs, st) == 0) return 0;
+    if (dg_wgs > 0 && dgr_ok(g) && rw_pays(cdiv(B * T2 * cdiv(a.U, 4), 32), B * T2 * a.U, 92.0 / 78.0) &&
+        run_dgrad_rw(a, dg_wgs, st) == 0)
+        return 0;
     // tile choice from tools/mb/c2_mb sweeps: 128-column tiles for the narrowest layers (Fo 33;
     // at Fo 65 the 256-column tile is 4-7 % faster), 8-combo
     // chunks + a 3-waves/SIMD register cap for the wide ones

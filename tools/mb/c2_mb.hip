@@ -131,10 +131,10 @@ int main(int argc, char** argv) {
                 if (e <= 1e-5 && t < best) best = t;
             };
             if (fwr_ok(g)) {
-                for (int wgs : {256, 512, 1024}) {
+                for (int v : {0, 1}) {
                     char nm[32];
-                    snprintf(nm, 32, "rw wgs %d", wgs);
-                    var(nm, [&] { if (run_fwd_rw(b, wgs, st)) printf("    (n/a)\n"); });
+                    snprintf(nm, 32, "rw variant %d", v);
+                    var(nm, [&] { if (run_fwd_rw(b, 256, st, v)) printf("    (n/a)\n"); });
                 }
             }
             if (l.Co <= 32) {
@@ -183,10 +183,10 @@ int main(int argc, char** argv) {
                 if (e <= 1e-5 && t < best) best = t;
             };
             if (dgr_ok(g)) {
-                for (int wgs : {256, 512}) {
+                for (int v : {0, 1, 2, 3}) {
                     char nm[32];
-                    snprintf(nm, 32, "rw wgs %d", wgs);
-                    var(nm, [&] { if (run_dgrad_rw(b, wgs, st)) printf("    (n/a)\n"); });
+                    snprintf(nm, 32, "rw variant %d", v);
+                    var(nm, [&] { if (run_dgrad_rw(b, 256, st, v)) printf("    (n/a)\n"); });
                 }
             }
             if (M == 64 && J == 5) {

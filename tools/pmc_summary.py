@@ -1,8 +1,18 @@
 """Summarise rocprofv3 --pmc CSVs per kernel (last timed step of a bench run):
-python tools/pmc_summary.py gpurun_out/pmc1 [gpurun_out/pmc2 ...]"""
+python tools/pmc_summary.py gpurun_out/pmc1 [gpurun_out/pmc2 ...]
+FETCH_SIZE is doubled only for the kernels whose reads are dwordx4 loads (tools/traffic.py WIDE,
+the width MI355X_MICROARCH.md calibrates); the `x2` column says which rows got it."""
 import collections
 import csv
+import os
+import re
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from traffic import WIDE  # noqa: E402
+
+# non-conv kernels that also read with dwordx4 loads (gemm.h loaders, LSTM, RVQ, mel, Adam)
+WIDE_OTHER = re.compile(r'gemm_kernel|lstm_|rvq_argmin_mfma|adam_kernel|mel_loss_kernel')
 
 
 def load(d):
@@ -31,8 +41,8 @@ def main():
                 if not c.startswith('_'):
                     per[k][c] += x
     rows = sorted(per.items(), key=lambda kv: -kv[1]['_ns'])[:28]
-    print('| kernel | calls | us/call | mfma busy | wait any | wait inst | lds conf | vgpr | lds B | fetch MB/call |')
-    print('|---|---|---|---|---|---|---|---|---|---|')
+    print('| kernel | calls | us/call | mfma busy | wait any | wait inst | lds conf | vgpr | lds B | fetch MB/call | x2 |')
+    print('|---|---|---|---|---|---|---|---|---|---|---|')
     for k, v in rows:
         n = cnt[k]
         wc = v.get('SQ_WAVE_CYCLES', 0) or 1
@@ -40,11 +50,12 @@ def main():
         mb = v.get('SQ_VALU_MFMA_BUSY_CYCLES', 0)
         gui = v.get('GRBM_GUI_ACTIVE', 0)
         busy = mb / (gui / 8 * 256 * 4) if gui else float('nan')
-        fetch = v.get('FETCH_SIZE', 0) / n / 1024 * 2  # KB units x2 (gfx950 half-count), -> MB below
+        wide = bool(WIDE.search(k) or WIDE_OTHER.search(k))
+        fetch = v.get('FETCH_SIZE', 0) / n / 1024 * (2 if wide else 1)  # KB -> MB; x2 gfx950 half-count
         print(f"| `{k}` | {n} | {v['_ns'] / n / 1e3:.1f} | {busy:.2f} | {v.get('SQ_WAIT_ANY', 0) / wc:.2f} | "
               f"{v.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | "
               f"{v.get('SQ_LDS_BANK_CONFLICT', 0) / max(1, v.get('SQ_LDS_IDX_ACTIVE', 0)):.2f} | {v['_vgpr']:.0f} | "
-              f"{v['_lds']:.0f} | {fetch:.1f} |")
+              f"{v['_lds']:.0f} | {fetch:.1f} | {'x2' if wide else '-'} |")
 
 
 if __name__ == '__main__':

@@ -6,8 +6,12 @@
 --fetch / --write: output dirs of `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs (one
 counter block per pass) of `bench.py --steps S --warmup W --no-roofline`; --steps = S + W (every
 train step the profiled process ran). Corrections as in MI355X_MICROARCH.md "HBM": counters are in
-KiB; FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B). The result is per train step
-and per conv-family ABI call (bench.py reads it into roofline.traffic)."""
+KiB; FETCH_SIZE is doubled ONLY for the kernels whose reads are 16-byte-per-lane (dwordx4) loads,
+the access width the guide calibrates (gfx950 tallies their 128-B requests at 64 B); the kernels
+that read with 4-byte loads (the fixed-order slab reductions, the one-channel post conv, the
+first-layer forward) are left uncorrected, as the guide leaves other widths uncalibrated. Both
+lists are written into the output. The result is per train step and per conv-family ABI call
+(bench.py reads it into roofline.traffic)."""
 import argparse
 import collections
 import csv
@@ -31,14 +35,24 @@ def per_dispatch(d, counter):
     return out, names
 
 
-def family_kib(d, counter):
+# conv-family kernels whose operand reads are dwordx4 (ld4u / f32x4) loads
+WIDE = re.compile(r'conv_fwd_kernel|conv_poly_kernel|conv_wgrad_kernel|pw_kernel|pw_wgrad_kernel|'
+                  r'LdConvFlat|LdPolyFlat|c2_fwd_rw|c2_dgrad_rw|c2_wgrad_rw|c2_fwdr|c2_dgradr|c2_wgrad3|'
+                  r'c2_dgrad_narrow')
+
+
+def family_kib(d, counter, split=False):
     vals, names = per_dispatch(d, counter)
-    tot, n = 0.0, 0
+    tot, wide, n = 0.0, 0.0, 0
+    kinds = {'wide': set(), 'narrow': set()}
     for k, v in vals.items():
         if FAMILY.search(names[k]):
             tot += v
             n += 1
-    return tot, n
+            w = bool(WIDE.search(names[k]))
+            wide += v if w else 0.0
+            kinds['wide' if w else 'narrow'].add(re.sub(r'[<(].*', '', names[k]).replace('void ', ''))
+    return (tot, wide, n, kinds) if split else (tot, n)
 
 
 def main():
@@ -51,13 +65,16 @@ def main():
                     help='conv-family ABI calls per step (bench roofline "launches" / steps)')
     ap.add_argument('--out', required=True)
     args = ap.parse_args()
-    f_kib, nf = family_kib(args.fetch, 'FETCH_SIZE')
+    f_kib, f_wide, nf, kinds = family_kib(args.fetch, 'FETCH_SIZE', split=True)
     w_kib, nw = family_kib(args.write, 'WRITE_SIZE')
-    fetch = 2.0 * f_kib * 1024 / args.steps
+    fetch = (f_kib + f_wide) * 1024 / args.steps  # x2 on the wide-load kernels only
     write = w_kib * 1024 / args.steps
     res = {'config': args.config, 'fetch_bytes_per_step': fetch, 'write_bytes_per_step': write,
            'hbm_bytes_per_step': fetch + write, 'kernel_dispatches_per_step': nf / args.steps,
-           'correction': 'FETCH_SIZE x2 (gfx950), KiB -> bytes', 'steps_profiled': args.steps}
+           'fetch_bytes_per_step_uncorrected': f_kib * 1024 / args.steps,
+           'correction': 'FETCH_SIZE x2 on the dwordx4-load kernels only (gfx950), KiB -> bytes',
+           'fetch_x2_kernels': sorted(kinds['wide']), 'fetch_uncorrected_kernels': sorted(kinds['narrow']),
+           'steps_profiled': args.steps}
     if args.calls_per_step:
         res['abi_calls_per_step'] = args.calls_per_step
         res['hbm_bytes_per_call'] = (fetch + write) / args.calls_per_step
