@@ -3204,7 +3204,9 @@ int encx_conv2d_wpoly(const float* wf, float* wp, int64_t Co, int64_t Ci, int64_
 // config-3 layers (tools/mb/c2_mb, profiles/r03/mb_rw.md): forward 66 vs 87 us, bwd-data 78 vs 92
 // us -- so the register-window form loses on layers whose last round is mostly idle (Fo 65 at
 // T2 90, Fo 65 at T2 184) and wins everywhere else. `ratio` = tiled / register-window cost.
+static int g_c2_select = 0;  // encx_conv2d_select
 static bool rw_pays(int64_t items, int64_t positions, double ratio) {
+    if (g_c2_select != 0) return g_c2_select == 1;
     static const int simds = [] {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) cus = 256;
@@ -3212,6 +3214,12 @@ static bool rw_pays(int64_t items, int64_t positions, double ratio) {
     }();
     const double rounds = std::ceil((double)items / simds), tiled = (double)positions / (128.0 * simds);
     return rounds < ratio * tiled;
+}
+
+int encx_conv2d_select(int mode) {
+    const int prev = g_c2_select;
+    if (mode >= 0 && mode <= 2) g_c2_select = mode;
+    return prev;
 }
 
 int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y, int64_t B, int64_t Ci,
@@ -3227,7 +3235,7 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     // register-window form (c2_fwd_rw_kernel); ENCX_FWR = workgroups (0: off)
     static const int fw_wgs = [] { const char* v = getenv("ENCX_FWR"); return v ? atoi(v) : 256; }();
     if (fw_wgs > 0 && fwr_ok(g) &&
-        (Ci * KT < 16 || rw_pays(cdiv(B * T2 * cdiv(Fo, 4), 32), B * T2 * Fo, 87.0 / 66.0)) &&
+        ((Ci * KT < 16 && g_c2_select != 2) || rw_pays(cdiv(B * T2 * cdiv(Fo, 4), 32), B * T2 * Fo, 87.0 / 66.0)) &&
         run_fwd_rw(a, fw_wgs, st) == 0)
         return 0;
     if (Co == 1 && KT == 3 && KF == 3 && (sf == 1 || sf == 2)) {
@@ -3360,7 +3368,7 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
         return 0;
     }
     static const int rw_waves = [] { const char* v = getenv("ENCX_WGR"); return v ? min(atoi(v), 4096) : 2048; }();
-    if (rw_waves > 0 && wgr_ok(g)) {  // register-window form (c2_wgrad_rw_kernel); ENCX_WGR=0 off
+    if (rw_waves > 0 && wgr_ok(g) && g_c2_select != 2) {  // register-window form (c2_wgrad_rw_kernel); ENCX_WGR=0 off
         const WgPlanR q = plan_wgr(g, rw_waves);
         if (run_wgrad_rw(g, dy, yact, x, ws, q, st) == 0) {
             hipLaunchKernelGGL(c2_wg_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, q.splits, (int)Co,

@@ -351,6 +351,11 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
                            int acc_w, int acc_b, float* ws, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co,
                            int64_t Fo, int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
                            encx_stream_t stream);
+/* Kernel family of the Conv2d layers: 0 = chosen per layer by the cost model (default), 1 =
+ * register-window kernels wherever their shape limits allow, 2 = tiled kernels only. Process-wide;
+ * returns the previous setting (any other value only queries). The results of the families agree
+ * to fp32 rounding (different summation orders), so tests exercise each at every size. */
+int encx_conv2d_select(int mode);
 /* Spectrogram(n_fft, hop, win=n_fft, hann, normalized=True, center=False, power=None) of
  * x [B][C][T], written as cat([re, im], 1) in 'b c t w' layout: z [B][2C][Fr][n/2+1]
  * (msstftd.py:97-99). tables: the mel-table buffer of this n_fft (encx_mel_tables_init). */
