@@ -3204,7 +3204,10 @@ int encx_conv2d_wpoly(const float* wf, float* wp, int64_t Co, int64_t Ci, int64_
 // config-3 layers (tools/mb/c2_mb, profiles/r03/mb_rw.md): forward 66 vs 87 us, bwd-data 78 vs 92
 // us -- so the register-window form loses on layers whose last round is mostly idle (Fo 65 at
 // T2 90, Fo 65 at T2 184) and wins everywhere else. `ratio` = tiled / register-window cost.
-static int g_c2_select = 0;  // encx_conv2d_select
+static int g_c2_select = [] {  // encx_conv2d_select; ENCX_C2 sets the initial mode
+    const char* v = getenv("ENCX_C2");
+    return v ? atoi(v) : 0;
+}();
 static bool rw_pays(int64_t items, int64_t positions, double ratio) {
     if (g_c2_select != 0) return g_c2_select == 1;
     static const int simds = [] {

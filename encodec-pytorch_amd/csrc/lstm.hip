@@ -81,23 +81,35 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_wave(const float* xt, const 
     const float cpl = Cl[((int64_t)pb * T + tp) * H + pu];
     const float cpv = t > 0 ? cpl : 0.f;
     float4 wv[G], hv[RT][G];
+    bool okv[G], keepv[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int gi = wave + FW * g;
         const bool okg = gi < NG;
         const int kq = (okg ? gi : 0) * 16 + 4 * kk;  // first k of this lane's float4
-        wv[g] = sel4(okg, ld4(W + (int64_t)j * K + kq));
+        wv[g] = ld4(W + (int64_t)j * K + kq);
         const bool rec = kq >= H;  // recurrent half: h_l(t-1), zero at t = 0
         const float* src = rec ? Yl : xin;
         const int ts = rec ? tp : t;
         const int kc = rec ? kq - H : kq;
-        const bool keep = !rec || t > 0;
+        okv[g] = okg;
+        keepv[g] = !rec || t > 0;
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
             int row = r * 16 + col;
             row = row < B ? row : B - 1;  // rows >= B compute garbage that is never read
-            hv[r][g] = sel4(keep, ld4(src + ((int64_t)row * T + ts) * H + kc));
+            hv[r][g] = ld4(src + ((int64_t)row * T + ts) * H + kc);
         }
+    }
+    // every operand load is issued before the first MFMA and before any select on a loaded value:
+    // one memory round trip per launch (left to itself the scheduler interleaves the loads with
+    // the MFMA chain, G serial round trips)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        wv[g] = sel4(okv[g], wv[g]);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) hv[r][g] = sel4(keepv[g], hv[r][g]);
     }
     f32x4v acc[RT];
 #pragma unroll
@@ -143,17 +155,15 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_wave(const float* xt, const 
 //   dc = dh o (1 - tanh^2 c) + dcn;  da_{i,f,g,o} -> DA_l[b][t];  dcn <- dc f
 // role L: dx[b][u][t0] (+)= sum_s P_0[s][b][u] for the frame t0 layer 0 finished in step k-1.
 // Partial sums over the split index s are added in ascending s (deterministic).
-__global__ __launch_bounds__(256) void lstm_bwd_elem(const float* dout, const float* P, int ns, float* dcn,
-                                                     const float* Cst, const float* Gs, float* DA, float* dx,
-                                                     int acc_x, int B, int T, int H, int L, int k) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= B * H) return;
-    const int role = blockIdx.y;
-    const int b = p / H, u = p - b * H;
+// one (b, u) point of E(k) in `role` (the body of lstm_bwd_elem; the fused step's tail)
+ENCX_DEV void bwd_elem_point(const float* dout, const float* P, int ns, float* dcn, const float* Cst,
+                             const float* Gs, float* DA, float* dx, int acc_x, int B, int T, int H, int L, int k,
+                             int role, int b, int u) {
+    const int p = b * H + u;
     const int64_t N2 = 2 * H, SB = (int64_t)B * N2;
     if (role == L) {
         const int t0 = T - k + L - 1;
-        if (t0 < 0 || t0 >= T) return;
+        if (!dx || t0 < 0 || t0 >= T) return;
         const float s = sum_strided(P + (int64_t)b * N2 + u, ns, SB);
         const int64_t o = ((int64_t)b * H + u) * T + t0;
         dx[o] = acc_x ? dx[o] + s : s;
@@ -165,10 +175,9 @@ __global__ __launch_bounds__(256) void lstm_bwd_elem(const float* dout, const fl
     const int64_t BTH = (int64_t)B * T * H;
     const bool top = l == L - 1;
     // grad from above: dout for the top layer, else the upper layer's input-grad partials
-    const float dtop = dout[((int64_t)b * H + u) * T + t];
-    const float dup = sum_strided(P + (int64_t)(top ? l : l + 1) * ns * SB + (int64_t)b * N2 + u, ns, SB);
-    const float dhr = sum_strided(P + (int64_t)l * ns * SB + (int64_t)b * N2 + H + u, ns, SB);
-    const float dh = (top ? dtop : dup) + (rec ? dhr : 0.f);
+    const float dh = (top ? dout[((int64_t)b * H + u) * T + t]
+                          : sum_strided(P + (int64_t)(l + 1) * ns * SB + (int64_t)b * N2 + u, ns, SB)) +
+                     (rec ? sum_strided(P + (int64_t)l * ns * SB + (int64_t)b * N2 + H + u, ns, SB) : 0.f);
     const int64_t o = ((int64_t)b * T + t) * H + u;
     const float* Cl = Cst + (int64_t)l * BTH;
     const float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)b * T + t) * 4 * H;
@@ -185,56 +194,111 @@ __global__ __launch_bounds__(256) void lstm_bwd_elem(const float* dout, const fl
     dcl[p] = dc * fg;
 }
 
+__global__ __launch_bounds__(256) void lstm_bwd_elem(const float* dout, const float* P, int ns, float* dcn,
+                                                     const float* Cst, const float* Gs, float* DA, float* dx,
+                                                     int acc_x, int B, int T, int H, int L, int k) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= B * H) return;
+    const int b = p / H;
+    bwd_elem_point(dout, P, ns, dcn, Cst, Gs, DA, dx, acc_x, B, T, H, L, k, blockIdx.y, b, p - b * H);
+}
+
 // G(k), grid (2H/16, ns, L): P_l[s][b][n] = sum_{j in split s} DA_l[b][t][j] wcat_l[j][n] for the
 // frame t of layer l in step k (MFMA 16x16x4 over float4 operands from wcatT [2H][4H]; the 4H
 // reduction split over blockIdx.y so the grid covers the CUs, BW waves interleaving k-groups).
-template <int G, int RT>
+//
+// FUSE: the same launch also runs E(k + 1). Every P tile feeds exactly one (role, 16-unit) group
+// of E(k + 1): columns n >= H are the recurrent grad of layer l's units n - H (role l), columns
+// n < H the input grad of layer l, i.e. the grad from above of layer l - 1's units n (role l - 1;
+// dx for l = 0). A group has ns (top layer, dx) or 2 ns producing workgroups. Each workgroup,
+// active or not, publishes its tile (stores drained, workgroup barrier, agent-scope release) and
+// adds 1 to its group's arrival counter; the workgroup whose add completes the group acquires and
+// runs E(k + 1) for the group's B x 16 points, then resets the counter for the next launch. No
+// workgroup ever waits on another, so the launch cannot deadlock.
+template <int G, int RT, bool FUSE>
 __global__ __launch_bounds__(BW * 64) void lstm_bwd_gemm(const float* DA, const float* wcatT, float* P,
-                                                         int B, int T, int H, int L, int k, int gper) {
+                                                         int B, int T, int H, int L, int k, int gper,
+                                                         const float* dout, float* dcn, const float* Cst,
+                                                         const float* Gs, float* DAw, float* dx, int acc_x,
+                                                         int* cnt) {
     const int l = blockIdx.z, t = T - 1 - k + (L - 1 - l);
-    if (t < 0 || t >= T) return;
+    const bool active = t >= 0 && t < T;
+    if (!FUSE && !active) return;
     __shared__ float red[BW][64][17];
+    __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c0 = blockIdx.x * 16, s = blockIdx.y, col = lane & 15, kk = lane >> 4;
     const int K = 4 * H, N2 = 2 * H, g0 = s * gper, ns = gridDim.y;
-    const float* Wt = wcatT + (int64_t)l * N2 * K + (int64_t)(c0 + col) * K;
-    const float* D = DA + (int64_t)l * B * T * K;
-    float4 wv[G], av[RT][G];
+    if (active) {
+        const float* Wt = wcatT + (int64_t)l * N2 * K + (int64_t)(c0 + col) * K;
+        const float* D = DA + (int64_t)l * B * T * K;
+        float4 wv[G], av[RT][G];
+        bool okv[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const int gl = wave + BW * g;
-        const bool ok = gl < gper;
-        const int kq = (g0 + (ok ? gl : 0)) * 16 + 4 * kk;
-        wv[g] = sel4(ok, ld4(Wt + kq));
+        for (int g = 0; g < G; ++g) {
+            const int gl = wave + BW * g;
+            const bool ok = gl < gper;
+            const int kq = (g0 + (ok ? gl : 0)) * 16 + 4 * kk;
+            okv[g] = ok;
+            wv[g] = ld4(Wt + kq);
 #pragma unroll
-        for (int r = 0; r < RT; ++r) {
-            int row = r * 16 + col;
-            row = row < B ? row : B - 1;
-            av[r][g] = ld4(D + ((int64_t)row * T + t) * K + kq);
+            for (int r = 0; r < RT; ++r) {
+                int row = r * 16 + col;
+                row = row < B ? row : B - 1;
+                av[r][g] = ld4(D + ((int64_t)row * T + t) * K + kq);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the MFMA chain (lstm_fwd_wave)
+#pragma unroll
+        for (int g = 0; g < G; ++g) wv[g] = sel4(okv[g], wv[g]);
+        f32x4v acc[RT];
+#pragma unroll
+        for (int r = 0; r < RT; ++r) acc[r] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < RT; ++r) acc[r] = mfma16(at4(av[r][g], q), at4(wv[g], q), acc[r]);
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[wave][r * 16 + kk * 4 + q][col] = acc[r][q];
+        __syncthreads();
+        float* Pl = P + ((int64_t)l * ns + s) * B * N2;
+        for (int p = tid; p < B * 16; p += BW * 64) {
+            const int b = p >> 4, cc = p & 15;
+            float v = red[0][b][cc];
+#pragma unroll
+            for (int w = 1; w < BW; ++w) v += red[w][b][cc];
+            Pl[(int64_t)b * N2 + c0 + cc] = v;
         }
     }
-    f32x4v acc[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int r = 0; r < RT; ++r) acc[r] = mfma16(at4(av[r][g], q), at4(wv[g], q), acc[r]);
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) red[wave][r * 16 + kk * 4 + q][col] = acc[r][q];
+    if (!FUSE) return;
+    // ---- publish the tile, arrive; the last arriver of a group runs E(k + 1) for it
+    const int HX = H >> 4, x = blockIdx.x;
+    const int role = x >= HX ? l : (l >= 1 ? l - 1 : L), ux = x >= HX ? x - HX : x;
+    const int need = (role >= L - 1) ? ns : 2 * ns;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    float* Pl = P + ((int64_t)l * ns + s) * B * N2;
-    for (int p = tid; p < B * 16; p += BW * 64) {
-        const int b = p >> 4, cc = p & 15;
-        float v = red[0][b][cc];
-#pragma unroll
-        for (int w = 1; w < BW; ++w) v += red[w][b][cc];
-        Pl[(int64_t)b * N2 + c0 + cc] = v;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int* c = cnt + role * HX + ux;
+        const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == need - 1;
+        if (last) {
+            __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_last = last;
     }
+    __syncthreads();
+    if (!s_last) return;
+    for (int q = tid; q < B * 16; q += BW * 64)
+        bwd_elem_point(dout, P, ns, dcn, Cst, Gs, DAw, dx, acc_x, B, T, H, L, k + 1, role, q >> 4,
+                       ux * 16 + (q & 15));
 }
 
 // ------------------------------------------------------------------------- layout kernels
@@ -371,23 +435,43 @@ static void fwd_step(int G, int RT, dim3 grid, hipStream_t st, const float* xt, 
     else if (G <= 8) fwd_rt<8>(RT, grid, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k);
     else fwd_rt<16>(RT, grid, st, xt, wcat, bsum, Y, C, Gs, B, T, H, k);
 }
+struct BwdArgs {
+    const float* DA;
+    const float* wcatT;
+    float* P;
+    int B, T, H, L, k, gper;
+    const float* dout;
+    float* dcn;
+    const float* Cst;
+    const float* Gs;
+    float* dx;
+    int acc_x;
+    int* cnt;  // non-NULL: fused with E(k + 1)
+};
+template <int G, int RT>
+static void bwd_launch(dim3 grid, hipStream_t st, const BwdArgs& a) {
+    if (a.cnt)
+        hipLaunchKernelGGL((lstm_bwd_gemm<G, RT, true>), grid, dim3(BW * 64), 0, st, a.DA, a.wcatT, a.P, a.B, a.T, a.H,
+                           a.L, a.k, a.gper, a.dout, a.dcn, a.Cst, a.Gs, (float*)a.DA, a.dx, a.acc_x, a.cnt);
+    else
+        hipLaunchKernelGGL((lstm_bwd_gemm<G, RT, false>), grid, dim3(BW * 64), 0, st, a.DA, a.wcatT, a.P, a.B, a.T,
+                           a.H, a.L, a.k, a.gper, a.dout, a.dcn, a.Cst, a.Gs, (float*)a.DA, a.dx, a.acc_x, a.cnt);
+}
 template <int G>
-static void bwd_rt(int RT, dim3 grid, hipStream_t st, const float* DA, const float* wcatT, float* P, int B,
-                   int T, int H, int L, int k, int gper) {
+static void bwd_rt(int RT, dim3 grid, hipStream_t st, const BwdArgs& a) {
     switch (RT) {
-        case 1: hipLaunchKernelGGL((lstm_bwd_gemm<G, 1>), grid, dim3(BW * 64), 0, st, DA, wcatT, P, B, T, H, L, k, gper); break;
-        case 2: hipLaunchKernelGGL((lstm_bwd_gemm<G, 2>), grid, dim3(BW * 64), 0, st, DA, wcatT, P, B, T, H, L, k, gper); break;
-        case 3: hipLaunchKernelGGL((lstm_bwd_gemm<G, 3>), grid, dim3(BW * 64), 0, st, DA, wcatT, P, B, T, H, L, k, gper); break;
-        default: hipLaunchKernelGGL((lstm_bwd_gemm<G, 4>), grid, dim3(BW * 64), 0, st, DA, wcatT, P, B, T, H, L, k, gper); break;
+        case 1: bwd_launch<G, 1>(grid, st, a); break;
+        case 2: bwd_launch<G, 2>(grid, st, a); break;
+        case 3: bwd_launch<G, 3>(grid, st, a); break;
+        default: bwd_launch<G, 4>(grid, st, a); break;
     }
 }
-static void bwd_gemm(int G, int RT, dim3 grid, hipStream_t st, const float* DA, const float* wcatT, float* P,
-                     int B, int T, int H, int L, int k, int gper) {
-    if (G <= 1) bwd_rt<1>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
-    else if (G <= 2) bwd_rt<2>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
-    else if (G <= 4) bwd_rt<4>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
-    else if (G <= 8) bwd_rt<8>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
-    else bwd_rt<16>(RT, grid, st, DA, wcatT, P, B, T, H, L, k, gper);
+static void bwd_gemm(int G, int RT, dim3 grid, hipStream_t st, const BwdArgs& a) {
+    if (G <= 1) bwd_rt<1>(RT, grid, st, a);
+    else if (G <= 2) bwd_rt<2>(RT, grid, st, a);
+    else if (G <= 4) bwd_rt<4>(RT, grid, st, a);
+    else if (G <= 8) bwd_rt<8>(RT, grid, st, a);
+    else bwd_rt<16>(RT, grid, st, a);
 }
 // k-splits of the backward step GEMM (K = 4H in H/4 groups of 16): <= 4, dividing the groups,
 // >= 8 groups each
@@ -443,7 +527,8 @@ int encx_lstm_fwd(const float* x, const float* wcat, const float* bsum, float* x
 
 size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t L) {
     (void)T;
-    return ((size_t)L * B * H + (size_t)L * bwd_splits(H) * B * 2 * H) * sizeof(float);
+    // dcn [L][B][H], P [L][ns][B][2H], the fused step's arrival counters [(L + 1) * H/16] (int)
+    return ((size_t)L * B * H + (size_t)L * bwd_splits(H) * B * 2 * H + (size_t)(L + 1) * (H / 16)) * sizeof(float);
 }
 
 int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const float* Gs, float* DA, float* dx,
@@ -457,14 +542,31 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
     float* dcn = ws;
     float* P = ws + L * B * H;
     const int ns = bwd_splits(H), gper = (int)(H / 4) / ns, G = (int)cdiv(gper, BW), RT = (int)cdiv(B, 16);
+    int* cnt = (int*)(P + L * ns * B * 2 * H);
     const int BH = (int)(B * H);
     const dim3 egrid((unsigned)cdiv(BH, 256), (unsigned)(L + (dx ? 1 : 0)));
     const dim3 ggrid((unsigned)(2 * H / 16), (unsigned)ns, (unsigned)L);
     const int steps = (int)(T + L);
-    for (int k = 0; k < steps; ++k) {
+    // E(k + 1) fused into G(k) (ENCX_LSTM_FUSE=1; default: separate launches until validated)
+    static const bool fuse = [] { const char* v = getenv("ENCX_LSTM_FUSE"); return v && atoi(v) != 0; }();
+    BwdArgs a{DA, wcatT, P, (int)B, (int)T, (int)H, (int)L, 0, gper, dout, dcn, Cst, Gs, dx, acc_x,
+              fuse ? cnt : nullptr};
+    if (fuse) {
+        const hipError_t e = hipMemsetAsync(cnt, 0, (size_t)(L + 1) * (H / 16) * sizeof(int), st);
+        if (e != hipSuccess) return (int)e;
         hipLaunchKernelGGL(lstm_bwd_elem, egrid, dim3(256), 0, st, dout, P, ns, dcn, Cst, Gs, DA, dx, acc_x,
-                           (int)B, (int)T, (int)H, (int)L, k);
-        if (k < steps - 1) bwd_gemm(G, RT, ggrid, st, DA, wcatT, P, (int)B, (int)T, (int)H, (int)L, k, gper);
+                           (int)B, (int)T, (int)H, (int)L, 0);
+        for (int k = 0; k < steps - 1; ++k) {
+            a.k = k;
+            bwd_gemm(G, RT, ggrid, st, a);
+        }
+    } else {
+        for (int k = 0; k < steps; ++k) {
+            hipLaunchKernelGGL(lstm_bwd_elem, egrid, dim3(256), 0, st, dout, P, ns, dcn, Cst, Gs, DA, dx, acc_x,
+                               (int)B, (int)T, (int)H, (int)L, k);
+            a.k = k;
+            if (k < steps - 1) bwd_gemm(G, RT, ggrid, st, a);
+        }
     }
     ENCX_CHECK_LAUNCH();
     return 0;
