@@ -10,8 +10,8 @@ l_t / l_f / l_g / l_feat through the Balancer, commit loss, Adam, then the discr
 (every step). `--config gen` = config 2 (no discriminator), `--config 48k` = config 5. Inputs are
 resident in HBM before the timed region. Rank 0 prints one JSON line.
 
-Steps replay HIP graphs (encx.train.Trainer(graphs=True): each step's device work captured once
-after one eager step, the collectives eager between segments at N > 1); --no-graphs steps eagerly.
+Steps replay HIP graphs at N = 1 (encx.train.Trainer(graphs=True): the step captured once
+after one eager step); at N > 1 the steps run eagerly (Trainer.step); --no-graphs steps eagerly.
 The warmup covers the eager step and the capture. The roofline / whole-step books come from a
 second, untimed, profiled pass of K eager steps (identical kernels).
 """

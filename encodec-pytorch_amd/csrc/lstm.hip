@@ -81,35 +81,23 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_wave(const float* xt, const 
     const float cpl = Cl[((int64_t)pb * T + tp) * H + pu];
     const float cpv = t > 0 ? cpl : 0.f;
     float4 wv[G], hv[RT][G];
-    bool okv[G], keepv[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int gi = wave + FW * g;
         const bool okg = gi < NG;
         const int kq = (okg ? gi : 0) * 16 + 4 * kk;  // first k of this lane's float4
-        wv[g] = ld4(W + (int64_t)j * K + kq);
+        wv[g] = sel4(okg, ld4(W + (int64_t)j * K + kq));
         const bool rec = kq >= H;  // recurrent half: h_l(t-1), zero at t = 0
         const float* src = rec ? Yl : xin;
         const int ts = rec ? tp : t;
         const int kc = rec ? kq - H : kq;
-        okv[g] = okg;
-        keepv[g] = !rec || t > 0;
+        const bool keep = !rec || t > 0;
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
             int row = r * 16 + col;
             row = row < B ? row : B - 1;  // rows >= B compute garbage that is never read
-            hv[r][g] = ld4(src + ((int64_t)row * T + ts) * H + kc);
+            hv[r][g] = sel4(keep, ld4(src + ((int64_t)row * T + ts) * H + kc));
         }
-    }
-    // every operand load is issued before the first MFMA and before any select on a loaded value:
-    // one memory round trip per launch (left to itself the scheduler interleaves the loads with
-    // the MFMA chain, G serial round trips)
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        wv[g] = sel4(okv[g], wv[g]);
-#pragma unroll
-        for (int r = 0; r < RT; ++r) hv[r][g] = sel4(keepv[g], hv[r][g]);
     }
     f32x4v acc[RT];
 #pragma unroll
@@ -233,14 +221,12 @@ __global__ __launch_bounds__(BW * 64) void lstm_bwd_gemm(const float* DA, const 
         const float* Wt = wcatT + (int64_t)l * N2 * K + (int64_t)(c0 + col) * K;
         const float* D = DA + (int64_t)l * B * T * K;
         float4 wv[G], av[RT][G];
-        bool okv[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int gl = wave + BW * g;
             const bool ok = gl < gper;
             const int kq = (g0 + (ok ? gl : 0)) * 16 + 4 * kk;
-            okv[g] = ok;
-            wv[g] = ld4(Wt + kq);
+            wv[g] = sel4(ok, ld4(Wt + kq));
 #pragma unroll
             for (int r = 0; r < RT; ++r) {
                 int row = r * 16 + col;
@@ -248,9 +234,6 @@ __global__ __launch_bounds__(BW * 64) void lstm_bwd_gemm(const float* DA, const 
                 av[r][g] = ld4(D + ((int64_t)row * T + t) * K + kq);
             }
         }
-        __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the MFMA chain (lstm_fwd_wave)
-#pragma unroll
-        for (int g = 0; g < G; ++g) wv[g] = sel4(okv[g], wv[g]);
         f32x4v acc[RT];
 #pragma unroll
         for (int r = 0; r < RT; ++r) acc[r] = (f32x4v){0.f, 0.f, 0.f, 0.f};
@@ -547,7 +530,10 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
     const dim3 egrid((unsigned)cdiv(BH, 256), (unsigned)(L + (dx ? 1 : 0)));
     const dim3 ggrid((unsigned)(2 * H / 16), (unsigned)ns, (unsigned)L);
     const int steps = (int)(T + L);
-    // E(k + 1) fused into G(k) (ENCX_LSTM_FUSE=1; default: separate launches until validated)
+    // E(k + 1) fused into G(k): opt-in (ENCX_LSTM_FUSE=1). Measured slower in the config-3 step:
+    // 21.7 us per fused launch against 9.0 + 4.9 us for G(k) and E(k + 1) (profiles/r03): each
+    // workgroup's agent-scope release (L2 write-back) and the last arriver's acquire cost more
+    // than the launch they save.
     static const bool fuse = [] { const char* v = getenv("ENCX_LSTM_FUSE"); return v && atoi(v) != 0; }();
     BwdArgs a{DA, wcatT, P, (int)B, (int)T, (int)H, (int)L, 0, gper, dout, dcn, Cst, Gs, dx, acc_x,
               fuse ? cnt : nullptr};

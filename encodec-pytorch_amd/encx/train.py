@@ -114,7 +114,14 @@ class Trainer:
         if train_d:
             self.opt_d.prepare()
         key = (bw, train_d, tuple(x.shape))
-        if self.graphs and self._graph_ok(key):
+        # HIP graphs only for the single-segment step (world 1). At world > 1 the step is cut into
+        # segments around the collectives, and replays of the per-segment graphs were measured
+        # to drift from the eager step (tools/diag/dp_graph_diff.py: the generator grads of the
+        # first replayed step differ at 1e-3..5e-2 whenever the encoder backward and the
+        # discriminator phase are captured into different graphs; fresh pools, device syncs and
+        # synchronous collectives do not change it; cause not found). Eager steps there: config 3
+        # measured 561 audio-s/s eager vs 561 with graphs (profiles/r02), the step is GPU-bound.
+        if self.graphs and not distrib.is_distributed() and self._graph_ok(key):
             out = self._graph_step(key, x)
         else:
             out = self._run(x, bw, train_d)
@@ -208,8 +215,10 @@ class Trainer:
                 works.append(self.opt.reduce_async(0, a))
 
         def seg_disc():
-            out = dict(c.pop('losses'))
-            out['loss_w'] = c['loss_w']
+            # values only: the loss tensors would keep their graphs (the discriminator's
+            # activations) alive for as long as the caller -- or a captured key -- holds them
+            out = {k: v.detach() for k, v in c.pop('losses').items()}
+            out['loss_w'] = c['loss_w'].detach()
             if train_d:
                 # discriminator phase on the same graph: weight grads only (train_multi_gpu.py:112-124)
                 self.disc_mode.set(params=True, input=False)
@@ -293,20 +302,24 @@ class Trainer:
         torch.cuda.synchronize()
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
-        graphs, colls = [], []
+        graphs, colls, pending = [], [], []
         for seg, coll in segs:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._pool):
                 seg()
             graphs.append(g)
             colls.append(coll)
-            if coll is not None:  # capture only records: run the segment for real before the
-                g.replay()        # collective, which the next capture does not depend on
+            pending.append(g)
+            if coll is not None:
+                # capture only records: run every segment captured since the last collective for
+                # real (in order: a segment without a collective of its own still feeds the next),
+                # then the collective, which the next capture does not depend on
+                for pg in pending:
+                    pg.replay()
+                pending.clear()
                 coll()
-        # the segments before the last collective already ran; replay the rest
-        start = max([i + 1 for i, cl in enumerate(colls) if cl is not None], default=0)
-        for g in graphs[start:]:
-            g.replay()
+        for pg in pending:
+            pg.replay()
         return graphs, colls, xs, c['out']
 
     # ------------------------------------------------------------------ checkpoints

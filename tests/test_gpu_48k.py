@@ -56,7 +56,10 @@ def test_train_step_48k_fixture(gan):
     tr = Trainer(m, disc, lr=1e-4, disc_lr=1e-4, scheduler=False, weights=weights, sample_rate=48000)
     x = T(d[pre + 'x']).to(DEV)
     for it in range(2):
-        out, _ = check_step(tr, x, cfg, 3.0, weights)
+        # floor 2e-4 = the LSTM kernels' pinned tolerance vs fp64 (test_lstm_vs_oracle): on the
+        # 48 kHz GAN step the encoder grads below the SLSTM land at 0.9-1.6e-4 against fp64, where
+        # the plain fp32 oracle's lands at 1.2-3e-5 (8 host threads; 4.5e-5 on 16)
+        out, _ = check_step(tr, x, cfg, 3.0, weights, floor=2e-4 if gan else 1e-6)
         for k in weights:
             np.testing.assert_allclose(float(out[k]), float(d[f'{pre}it{it}_{k}'].reshape(-1)[0]), rtol=2e-4,
                                        err_msg=f'it{it} {k}')

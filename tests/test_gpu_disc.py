@@ -282,3 +282,66 @@ def test_premask_bit_identical(params, inp):
             assert (ta is None) == (tb is None)
             if ta is not None:
                 assert torch.equal(ta, tb)
+
+
+def _disc_layer_shapes(B=32, T=24000, C=1):
+    """(n_fft, li, x shape, layer) of every Conv2d of the config-3 MS-STFT discriminator at full
+    size (msstftd.py:131-149: n_fft 1024 / 2048 / 512, hop n/4, 32 filters)."""
+    out = []
+    for n in (1024, 2048, 512):
+        T2, F = (T - n) // (n // 4) + 1, n // 2 + 1
+        for li in range(6):
+            Ci, Co, k, s, d, pad = LAYERS[li]
+            if li == 0:
+                Ci = 2 * C
+            out.append((n, li, (B, Ci, T2, F), (Ci, Co, k, s, d, pad)))
+            F = (F + 2 * pad[1] - k[1]) // s[1] + 1
+    for n in (1024, 2048, 512):  # the first layer of the 48 kHz stereo discriminator (config 5)
+        T2 = (2 * T - n) // (n // 4) + 1
+        out.append((n, 6, (B, 4, T2, n // 2 + 1), LAYERS[6]))
+    return out
+
+
+@pytest.mark.parametrize('family', [1, 2], ids=['regwin', 'tiled'])
+def test_conv2d_full_size_vs_torch_fp64(family):
+    """Every Conv2d of the config-3 discriminator at its real size (B 32, 1 s clips: up to 4.8 M
+    output positions per layer, many work items per wave of the persistent register-window
+    kernels) for one forced kernel family: output, input grad, weight and bias grads against
+    torch's fp64 conv2d on the GPU (test-only checker), relative to the tensor's largest
+    magnitude."""
+    import torch.nn.functional as F
+    from encx import ops
+    from encx._lib import lib
+    def rel(a, b):  # on the device: up to 48 M elements per tensor
+        a, b = a.detach().double(), b.detach().double()
+        return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+    prev = lib.encx_conv2d_select(family)
+    try:
+        bad = []
+        for n, li, xs, (Ci, Co, k, s, d, pad) in _disc_layer_shapes():
+            act = li != 5
+            torch.cuda.empty_cache()
+            g = torch.Generator(device=DEV).manual_seed(li * 100 + n)
+            x64 = torch.randn(xs, generator=g, device=DEV, dtype=torch.float64)
+            v64 = 0.2 * torch.randn((Co, Ci) + k, generator=g, device=DEV, dtype=torch.float64)
+            b64 = 0.1 * torch.randn(Co, generator=g, device=DEV, dtype=torch.float64)
+            x = x64.float().requires_grad_(True)
+            v = v64.float().requires_grad_(True)
+            b = b64.float().requires_grad_(True)
+            y = ops.conv2d(x, v, None, b, k, s, d, pad, act)
+            dy = torch.randn(y.shape, generator=g, device=DEV, dtype=torch.float64)
+            y.backward(dy.float())
+            # the reference in fp64 from the same fp32 operands, with OUR LeakyReLU mask
+            xr, vr, br = (t.detach().double().requires_grad_(True) for t in (x, v, b))
+            p = F.conv2d(xr, vr, br, stride=s, dilation=d, padding=pad)
+            mask = torch.where(y.detach() > 0, 1.0, 0.2).double() if act else 1.0
+            want_y = torch.where(y.detach() > 0, p, 0.2 * p) if act else p
+            gx, gv, gb = torch.autograd.grad(p, (xr, vr, br), dy * mask)
+            errs = {'y': rel(y, want_y), 'dx': rel(x.grad, gx), 'dw': rel(v.grad, gv), 'db': rel(b.grad, gb)}
+            print(f'n {n} layer {li} {tuple(xs)}: ' + ' '.join(f'{k_} {e:.1e}' for k_, e in errs.items()))
+            bad += [(n, li, k_, e) for k_, e in errs.items() if not e < 2e-5]
+            del x64, x, y, dy, p, gx, gv, gb, xr
+        assert not bad, bad
+    finally:
+        lib.encx_conv2d_select(prev)

@@ -67,7 +67,10 @@ def check_segments(m, x, p, cbs, cfg, bw):
             _, cert_m = rvq_certified(emb, embeds, 256)
             both = cert_o & cert_m & (want_o == want)
             co = torch.as_tensor(codes_o).transpose(0, 1).long()
-            assert both.float().mean() > 0.5, float(both.float().mean())
+            # not vacuous: most codes the proof certifies for our latent are certified for the
+            # oracle's latent too (the proof certifies few deep-layer codes: 3-18 % of all)
+            print(f'certified for both latents: {int(both.sum())} of {int(cert_m.sum())} certified for ours')
+            assert both.sum() > 0 and both.sum() >= 0.5 * cert_m.sum(), (int(both.sum()), int(cert_m.sum()))
             assert torch.equal(mine[both], co[both]), int((mine[both] != co[both]).sum())
         y_ref = O.encodec_decode_eval([(c, s) for c, s, _ in ref], p, cbs, cfg, x.shape[-1])
         y_mine = m.decode([(c.to(DEV), None if s is None else s.to(DEV)) for c, s, _ in ref])[:, :, :x.shape[-1]]

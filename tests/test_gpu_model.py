@@ -208,7 +208,7 @@ def test_config3_b32_step_and_input_grads_vs_fp64():
     the fake audio (l_t, l_f, l_g through the discriminator; what the balancer combines) for one
     clip of the B 32 batch against the fp64 oracle run on that clip alone (each loss is a batch
     mean, so clip 0's grad in the batch is 1/32 of its single-clip grad), each within 4x of the
-    fp32 oracle's error."""
+    fp32 oracle's error (the oracle's LeakyReLU slopes taken from our maps)."""
     from encx.train import Trainer
     from encx.msstftd import MultiScaleSTFTDiscriminator
     from encx.losses import total_loss
@@ -234,12 +234,16 @@ def test_config3_b32_step_and_input_grads_vs_fp64():
     losses = total_loss(fr, lf_, ff, x, yd, 24000)
     mine = {k: torch.autograd.grad(losses[k], [yd], retain_graph=True)[0][0] for k in ('l_t', 'l_f', 'l_g')}
     dp = {k: v.detach().cpu() for k, v in disc.state_dict().items() if not k.endswith('spec_transform.window')}
+    # LeakyReLU slopes from OUR fp32 maps of clip 0 (a pre-activation within rounding of 0 may
+    # take either slope in fp32: a discrete, legitimate outcome that a rounding bound cannot
+    # cover; oracle._lrelu), so the comparison measures rounding only
+    masks = [[fm[:1].detach().cpu() > 0 for fm in fms] for fms in ff]
     ref = {}
     for dt in (torch.float64, torch.float32):
         x0 = x[:1].detach().cpu().to(dt)
         y0 = yd[:1].detach().cpu().to(dt).requires_grad_(True)
         pd = {k: v.to(dt) for k, v in dp.items()}
-        lg, _ = O.msstft_forward(y0, pd)
+        lg, _ = O.msstft_forward(y0, pd, masks=masks)
         ls = {'l_t': O.loss_t(x0, y0), 'l_f': O.loss_f(x0, y0, 24000),
               'l_g': sum(torch.relu(1 - l).mean() for l in lg) / len(lg) / len(lg)}
         ref[dt] = {k: torch.autograd.grad(l, [y0], retain_graph=True)[0][0] / 32 for k, l in ls.items()}

@@ -141,6 +141,35 @@ def test_hip_graph_steps_match_eager(case):
     assert any(isinstance(v, tuple) for v in g.values())
 
 
+def test_graph_pool_memory_bounded_across_keys():
+    """Every (bandwidth, coin, shape) key is captured into ONE shared graph pool (steps never
+    overlap; only each key's returned losses stay alive), so capturing three bandwidths reserves
+    little beyond what the first key's capture did; one pool per key would add a whole step's
+    activations per key. Also: past max_graph_keys, keys run eagerly."""
+    tr = make_trainer(graphs=True)
+    x = batches(1)[0]
+    marks, act = [], None
+    for bw in (6.0, 3.0, 1.5):
+        tr.model.target_bandwidths = [bw]
+        for i in range(3):  # eager, capture, replay
+            if act is None:  # one step's activations: the peak of the first eager step
+                torch.cuda.synchronize()
+                a0 = torch.cuda.memory_allocated()
+                torch.cuda.reset_peak_memory_stats()
+            tr.step(x)
+            if act is None:
+                torch.cuda.synchronize()
+                act = torch.cuda.max_memory_allocated() - a0
+        torch.cuda.synchronize()
+        marks.append(torch.cuda.memory_reserved())
+    extra = marks[-1] - marks[0]
+    print(f'one step peaks at +{act / 2**20:.0f} MiB; two more captured keys reserve +{extra / 2**20:.0f} MiB')
+    assert sum(isinstance(v, tuple) for v in tr._graphs.values()) == 3
+    assert extra <= 0.5 * act, (act, extra)
+    tr.max_graph_keys = 3
+    assert not tr._graph_ok((0.75, True, tuple(x.shape)))
+
+
 def test_weight_norm_batch_matches_per_layer():
     """ops.WnBatch (every weight norm of a step as one launch per model forward / backward)
     against the per-layer launches: generator grads bit-identical (the same per-row arithmetic);
