@@ -226,6 +226,7 @@ class Trainer:
                 out['l_d'] = disc_loss(c.pop('logits_real'), c.pop('logits_fake'))
                 with bwd():
                     out['l_d'].backward()
+                out['l_d'] = out['l_d'].detach()
             c['out'] = out
 
         def coll_disc():
