@@ -40,9 +40,10 @@ def main():
             for c, x in v.items():
                 if not c.startswith('_'):
                     per[k][c] += x
-    rows = sorted(per.items(), key=lambda kv: -kv[1]['_ns'])[:28]
-    print('| kernel | calls | us/call | mfma busy | wait any | wait inst | lds conf | vgpr | lds B | fetch MB/call | x2 |')
-    print('|---|---|---|---|---|---|---|---|---|---|---|')
+    rows = sorted(per.items(), key=lambda kv: -kv[1]["_ns"])[:int(os.environ.get("PMC_TOP", "28"))]
+    print('| kernel | calls | us/call | mfma busy | wait any | wait inst | lds conf | vgpr | lds B | fetch MB/call | '
+          'write MB/call | HBM GB/s | x2 |')
+    print('|---|---|---|---|---|---|---|---|---|---|---|---|---|')
     for k, v in rows:
         n = cnt[k]
         wc = v.get('SQ_WAVE_CYCLES', 0) or 1
@@ -52,10 +53,12 @@ def main():
         busy = mb / (gui / 8 * 256 * 4) if gui else float('nan')
         wide = bool(WIDE.search(k) or WIDE_OTHER.search(k))
         fetch = v.get('FETCH_SIZE', 0) / n / 1024 * (2 if wide else 1)  # KB -> MB; x2 gfx950 half-count
+        write = v.get('WRITE_SIZE', 0) / n / 1024
+        gbs = (fetch + write) / max(v['_ns'] / n / 1e3, 1e-9) * 1e3  # MB per us = TB/s -> GB/s
         print(f"| `{k}` | {n} | {v['_ns'] / n / 1e3:.1f} | {busy:.2f} | {v.get('SQ_WAIT_ANY', 0) / wc:.2f} | "
               f"{v.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | "
               f"{v.get('SQ_LDS_BANK_CONFLICT', 0) / max(1, v.get('SQ_LDS_IDX_ACTIVE', 0)):.2f} | {v['_vgpr']:.0f} | "
-              f"{v['_lds']:.0f} | {fetch:.1f} | {'x2' if wide else '-'} |")
+              f"{v['_lds']:.0f} | {fetch:.1f} | {write:.1f} | {gbs:.0f} | {'x2' if wide else '-'} |")
 
 
 if __name__ == '__main__':
