@@ -196,8 +196,9 @@ def main():
         # traffic: HBM bytes per conv-family ABI call from the committed rocprofv3 PMC passes
         # (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic.py); null when no pass exists for the config
         traffic = None
-        tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r02',
-                             f'traffic_{args.config}.json')
+        tpath = next((p for p in (os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', r,
+                                               f'traffic_{args.config}.json') for r in ('r03', 'r02'))
+                      if os.path.exists(p)), '')
         if os.path.exists(tpath) and launches:
             with open(tpath) as fh:
                 traffic = round(json.load(fh)['hbm_bytes_per_step'] / (launches / args.steps))

@@ -19,7 +19,7 @@ import json
 import re
 
 # kernels launched by the conv / convtr / conv2d ABI entry points (csrc/conv1d.hip, disc.hip)
-FAMILY = re.compile(r'conv_fwd_kernel|pw_kernel|conv_poly_kernel|conv_wgrad|wgrad_reduce|conv_fwd_reduce|'
+FAMILY = re.compile(r'conv_fwd_kernel|pw_kernel|pw_wgrad_kernel|conv_poly_kernel|conv_wgrad|wgrad_reduce|conv_fwd_reduce|'
                     r'conv_poly_reduce|conv_fold_edges|LdConvFlat|LdPolyFlat|c2_')
 
 
@@ -51,7 +51,7 @@ def family_kib(d, counter, split=False):
             n += 1
             w = bool(WIDE.search(names[k]))
             wide += v if w else 0.0
-            kinds['wide' if w else 'narrow'].add(re.sub(r'[<(].*', '', names[k]).replace('void ', ''))
+            kinds['wide' if w else 'narrow'].add(re.sub(r'[<(].*', '', names[k].replace('(anonymous namespace)::', '')).replace('void ', ''))
     return (tot, wide, n, kinds) if split else (tot, n)
 
 
