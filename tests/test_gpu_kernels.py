@@ -330,6 +330,18 @@ def test_lstm_vs_oracle(B, H, Tn, L):
         scale = b.abs().max().item() + 1e-12
         close(a, b, rtol=tol, atol=tol * scale, what=what)
 
+    # the same SLSTM in plain fp32 on the host (the oracle's loop): what fp32 arithmetic achieves
+    p32 = {k: v.detach().float().requires_grad_(True) for k, v in p64.items()}
+    x32 = x64.detach().float().requires_grad_(True)
+    y32 = O.slstm(x32, p32, 'm', L)
+    (y32 * r64.float()).sum().backward()
+
+    def err(a, b):
+        b = b.detach().double().cpu()
+        return float((a.detach().double().cpu() - b).abs().max() / (b.abs().max() + 1e-12))
+    rows = [('y', err(y, y64), err(y32, y64)), ('dx', err(x.grad, x64.grad), err(x32.grad, x64.grad))]
+    rows += [(n.split('.')[-1], err(wts[i].grad, w.grad), err(p32[n].grad, w.grad)) for i, (n, w) in enumerate(p64.items())]
+    print('LSTM rel err vs fp64 (encx / plain fp32): ' + ', '.join(f'{n} {a:.1e}/{b:.1e}' for n, a, b in rows))
     rel_close(y, y64, 'y')
     rel_close(x.grad, x64.grad, 'dx')
     for i, (n, w) in enumerate(p64.items()):
