@@ -56,9 +56,10 @@ def test_train_step_48k_fixture(gan):
     tr = Trainer(m, disc, lr=1e-4, disc_lr=1e-4, scheduler=False, weights=weights, sample_rate=48000)
     x = T(d[pre + 'x']).to(DEV)
     for it in range(2):
-        # floor 2e-4 = the LSTM kernels' pinned tolerance vs fp64 (test_lstm_vs_oracle): on the
-        # 48 kHz GAN step the encoder grads below the SLSTM land at 0.9-1.6e-4 against fp64, where
-        # the plain fp32 oracle's lands at 1.2-3e-5 (8 host threads; 4.5e-5 on 16)
+        # floor 2e-4: on the 48 kHz GAN step our encoder grads land at 0.9-1.6e-4 against fp64,
+        # where the plain fp32 oracle's land at 1.2-3e-5 (8 host threads; 4.5e-5 on 16), while
+        # the generator-only step and every decoder / discriminator tensor meet the 4x rule.
+        # The source is not isolated (the SLSTM is within 2.6x of plain fp32, test_lstm_vs_oracle)
         out, _ = check_step(tr, x, cfg, 3.0, weights, floor=2e-4 if gan else 1e-6)
         for k in weights:
             np.testing.assert_allclose(float(out[k]), float(d[f'{pre}it{it}_{k}'].reshape(-1)[0]), rtol=2e-4,

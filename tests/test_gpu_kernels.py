@@ -304,7 +304,8 @@ def test_normalize_and_scale():
 def test_lstm_vs_oracle(B, H, Tn, L):
     """encx LSTM (csrc/lstm.hip, all layers as one diagonal wavefront) forward + backward
     against the oracle's step-by-step restatement of SLSTM (modules/lstm.py:22-28) run in fp64
-    on the CPU, for 1, 2 and 3 layers."""
+    on the CPU, for 1, 2 and 3 layers: every output and grad within 4x the error of the same
+    restatement run in plain fp32."""
     from encx import ops
     gen = torch.Generator().manual_seed(B * 1000 + H)
     k = 1.0 / np.sqrt(H)
@@ -342,6 +343,10 @@ def test_lstm_vs_oracle(B, H, Tn, L):
     rows = [('y', err(y, y64), err(y32, y64)), ('dx', err(x.grad, x64.grad), err(x32.grad, x64.grad))]
     rows += [(n.split('.')[-1], err(wts[i].grad, w.grad), err(p32[n].grad, w.grad)) for i, (n, w) in enumerate(p64.items())]
     print('LSTM rel err vs fp64 (encx / plain fp32): ' + ', '.join(f'{n} {a:.1e}/{b:.1e}' for n, a, b in rows))
+    # as accurate as plain fp32: within 4x of its error (floor 1e-6 of the tensor's magnitude;
+    # measured 0.5-2.6x at (32, 512, 75, 2))
+    bad = [(n, a, b) for n, a, b in rows if not a <= max(4 * b, 1e-6)]
+    assert not bad, bad
     rel_close(y, y64, 'y')
     rel_close(x.grad, x64.grad, 'dx')
     for i, (n, w) in enumerate(p64.items()):
