@@ -165,3 +165,40 @@ def test_full_size_48k_step_runs():
         assert all(np.isfinite(v) for v in vals.values()), vals
     assert m.quantizer.n_q == 16
     assert all(float(m.quantizer.vq.layers[i]._codebook.inited) == 1.0 for i in range(16))
+
+
+def test_stereo_disc_input_grads_vs_fp64():
+    """The generator phase's per-loss grads w.r.t. the fake audio on the 48 kHz stereo GAN
+    fixture (l_t, l_f, l_g, l_feat: what the balancer rescales and combines), against the oracle
+    in fp64 with our LeakyReLU slopes (oracle._lrelu), each within 4x of the plain fp32 oracle's
+    error. Localises the 48 kHz GAN step's encoder-grad excess (test_train_step_48k_fixture)."""
+    from encx.msstftd import MultiScaleSTFTDiscriminator
+    from encx.losses import total_loss
+    from steputil import check_grads
+    d = load('g9_step48k.npz')
+    m, p, cbs, cfg = build48k(d, 'gan/')
+    disc = MultiScaleSTFTDiscriminator(filters=32, in_channels=2, out_channels=2)
+    disc.load_state_dict(disc_state(94, 2, 2), strict=False)
+    disc = disc.to(DEV)
+    x = T(d['gan/x']).to(DEV)
+    m.train()
+    y, _, _ = m(x)
+    yd = y.detach().requires_grad_()
+    _, fr = disc(x)
+    lf_, ff = disc(yd)
+    losses = total_loss(fr, lf_, ff, x, yd, 48000)
+    names = ('l_t', 'l_f', 'l_g', 'l_feat')
+    mine = {k: torch.autograd.grad(losses[k], [yd], retain_graph=True)[0] for k in names}
+    dp = {k: v.detach().cpu() for k, v in disc.state_dict().items() if not k.endswith('spec_transform.window')}
+    mr = [[fm.detach().cpu() > 0 for fm in fms] for fms in fr]
+    mf = [[fm.detach().cpu() > 0 for fm in fms] for fms in ff]
+    ref = {}
+    for dt in (torch.float64, torch.float32):
+        x0 = x.detach().cpu().to(dt)
+        y0 = yd.detach().cpu().to(dt).requires_grad_(True)
+        pd = {k: v.to(dt) for k, v in dp.items()}
+        lr_o, fr_o = O.msstft_forward(x0, pd, masks=mr)
+        lf_o, ff_o = O.msstft_forward(y0, pd, masks=mf)
+        lo = O.total_loss(fr_o, lf_o, ff_o, x0, y0, 48000)
+        ref[dt] = {k: torch.autograd.grad(lo[k].sum(), [y0], retain_graph=True)[0] for k in names}
+    check_grads(mine, ref[torch.float64], ref[torch.float32], '48 kHz stereo GAN input grads')
