@@ -38,8 +38,14 @@ DEFAULT_WEIGHTS = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}  # config/config
 class Trainer:
     def __init__(self, model: EncodecModel, disc=None, lr=3e-4, disc_lr=3e-4, betas=(0.5, 0.9),
                  weights=None, max_iter=100000, warmup_iter=0, disc_prob=1.0, sample_rate=24000,
-                 scheduler=True, balancer_kwargs=None, graphs=False, ddp_commit_local=False):
+                 scheduler=True, balancer_kwargs=None, graphs=False, ddp_commit_local=False,
+                 segmented=None):
         self.model = model
+        # segmented: the device part as the data-parallel list of segments (split backward,
+        # one HIP graph per segment) even at world 1, where the collectives between them are
+        # no-ops. None = segmented exactly when distributed.
+        self.segmented = segmented
+        self._seg_hook = None  # diagnostics: called with the segment index after each segment
         # ddp_commit_local: the reference's exact DDP semantics (train_multi_gpu.py:86-95, SURVEY
         # quirk 7): the commit loss's grads are added AFTER the all-reduce, so they stay rank-local
         # and the ranks' weights drift apart. Off (default): one backward, true data parallelism.
@@ -121,7 +127,8 @@ class Trainer:
         # discriminator phase are captured into different graphs; fresh pools, device syncs and
         # synchronous collectives do not change it; cause not found). Eager steps there: config 3
         # measured 561 audio-s/s eager vs 561 with graphs (profiles/r02), the step is GPU-bound.
-        if self.graphs and not distrib.is_distributed() and self._graph_ok(key):
+        if self.graphs and (not distrib.is_distributed() or os.environ.get('ENCX_DP_GRAPHS') == '1') \
+                and self._graph_ok(key):
             out = self._graph_step(key, x)
         else:
             out = self._run(x, bw, train_d)
@@ -147,7 +154,8 @@ class Trainer:
         """The device part as (segment, collective) pairs; state flows through `c`."""
         c = {}
         dist = distrib.is_distributed()
-        split = dist and self._dec_span is not None and self.model.segment is None
+        seg = dist if self.segmented is None else bool(self.segmented)
+        split = seg and self._dec_span is not None and self.model.segment is None
         local = dist and self.ddp_commit_local
         if local and not split:
             raise ValueError('encx Trainer: ddp_commit_local needs an unsegmented model')
@@ -157,10 +165,15 @@ class Trainer:
         fwd = (lambda grp: wn.forward(grp)) if wn is not None else (lambda grp: contextlib.nullcontext())
         bwd = (lambda: wn.backward()) if wn is not None else contextlib.nullcontext
 
+        # synced codebooks: the EMA sums' all-reduce is deferred to a collective between segments
+        # only for a one-frame model; with segments (48 kHz) frame f + 1 must quantise with the
+        # codebooks synced after frame f, so the RVQ forward all-reduces in place (eager step)
+        defer = (lambda: defer_codebook_sync(c['cb'])) if self.model.segment is None else contextlib.nullcontext
+
         def seg_gen():
             self.opt.zero_grad()
             c['cb'] = []
-            with fwd('gen'), defer_codebook_sync(c['cb']):
+            with fwd('gen'), defer():
                 y, loss_w, _ = self.model(x, bandwidth=bw, split=split)
             c['y'], c['loss_w'] = y, loss_w
             c['split'] = self.model.last_split
@@ -210,9 +223,14 @@ class Trainer:
                     torch.autograd.backward([q, loss_w], [leaf.grad, torch.ones_like(loss_w)])
 
         def coll_enc():
-            a = self._dec_span[0] if split else self.opt.flat_grad.numel()
+            # everything outside the decoder's bucket: [0, dec start) and, should any generator
+            # parameter sit after the decoder in the flat buffer, [dec end, numel)
+            n = self.opt.flat_grad.numel()
+            a, b = self._dec_span if split else (n, n)
             if a > 0:
                 works.append(self.opt.reduce_async(0, a))
+            if b < n:
+                works.append(self.opt.reduce_async(b, n))
 
         def seg_disc():
             # values only: the loss tensors would keep their graphs (the discriminator's
@@ -251,9 +269,12 @@ class Trainer:
                     self.opt_d.flat_grad.div_(distrib.world_size())
                 self.opt_d.launch()
 
-        if not dist:
+        if not seg:
             segs = [seg_gen, seg_losses, seg_dec, seg_disc, seg_opt]
             return [(lambda: [s() for s in segs], None)], c
+        if not dist:  # world 1, segmented on request: the same segments, no collectives
+            return [(seg_gen, None), (seg_losses, None), (seg_dec, None),
+                    (seg_enc if split else (lambda: None), None), (seg_disc, None), (seg_opt, None)], c
         return [(seg_gen, coll_gen if self.model.quantizer.sync_codebooks else None),
                 (seg_losses, self.balancer.reduce_stats),
                 (seg_dec, coll_dec if split else None),
@@ -263,16 +284,20 @@ class Trainer:
 
     def _run(self, x, bw, train_d):
         segs, c = self._segments(x, bw, train_d)
-        for seg, coll in segs:
+        for i, (seg, coll) in enumerate(segs):
             seg()
             if coll is not None:
                 coll()
+            if self._seg_hook is not None:
+                self._seg_hook(i, c)
         return c['out']
 
     def _graph_ok(self, key):
         from ._lib import lib
         if lib.encx_prof_enabled() or self.balancer.monitor:
             return False  # profiler events / the monitor's host read are not capturable
+        if distrib.is_distributed() and self.model.quantizer.sync_codebooks and self.model.segment is not None:
+            return False  # the codebook all-reduce runs inside the forward (seg_gen): not capturable
         return key in self._graphs or len(self._graphs) < self.max_graph_keys
 
     def _graph_step(self, key, x):
@@ -285,13 +310,18 @@ class Trainer:
         if ent == 'warm':  # second occurrence: capture, which also runs this step
             ent = self._graphs[key] = self._capture(key, x)
         else:
-            graphs, colls, xs, out = ent
+            graphs, colls, xs, out, codes = ent
             xs.copy_(x)
-            for g, coll in zip(graphs, colls):
+            for i, (g, coll) in enumerate(zip(graphs, colls)):
                 g.replay()
                 if coll is not None:
                     coll()
+                if self._seg_hook is not None:
+                    self._seg_hook(i, self._cap_c)
         out = ent[3]
+        # this key's graphs rewrite its own codes tensor (held by the entry, so its pool block is
+        # never handed to another key); after another key ran, last_codes must point back at it
+        self.model.last_codes = ent[4]
         # the replayed graphs rewrite `out` in place: hand the caller a copy of this step's values
         names = list(out)
         vals = torch.cat([out[k].detach().reshape(-1)[:1] for k in names])
@@ -303,6 +333,7 @@ class Trainer:
         torch.cuda.synchronize()
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
+        self._cap_c = c
         graphs, colls, pending = [], [], []
         for seg, coll in segs:
             g = torch.cuda.CUDAGraph()
@@ -321,7 +352,9 @@ class Trainer:
                 coll()
         for pg in pending:
             pg.replay()
-        return graphs, colls, xs, c['out']
+        if self._seg_hook is not None:
+            self._seg_hook(len(segs) - 1, c)
+        return graphs, colls, xs, c['out'], self.model.last_codes
 
     # ------------------------------------------------------------------ checkpoints
     def state_dicts(self):

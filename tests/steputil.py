@@ -25,6 +25,8 @@ in fp32. The HIP step is compared with the fp64 step:
     buffer's largest magnitude.
 No global slack: every bound is per element or per tensor.
 """
+import contextlib
+
 import numpy as np
 import torch
 
@@ -79,6 +81,41 @@ def split_masks(store, n_disc):
     per = len(store) // (2 * n_disc)
     grid = [store[i * per:(i + 1) * per] for i in range(2 * n_disc)]
     return {'real': grid[:n_disc], 'fake': grid[n_disc:]}
+
+
+@contextlib.contextmanager
+def lrelu_audit():
+    """Collect (pre-activation, imposed mask) of every masked LeakyReLU the oracle evaluates."""
+    O.LRELU_AUDIT = log = []
+    try:
+        yield log
+    finally:
+        O.LRELU_AUDIT = None
+
+
+def check_masks(a64, a32, what):
+    """Our LeakyReLU slope masks (imposed on the oracle) against the fp64 oracle's OWN signs of
+    the same pre-activations: they may differ only where |z64| is within 4x the largest rounding
+    error the plain fp32 oracle makes on that map (max |z32 - z64|), i.e. where fp32 arithmetic
+    may legitimately land on the other side of 0. A sign error in a HIP epilogue lands far from
+    0 and fails here. a64 / a32: the lrelu_audit logs of the fp64 and fp32 oracle runs."""
+    assert a64 and len(a64) == len(a32), (what, len(a64), len(a32))
+    flips = total = 0
+    worst = 0.0
+    for (z64, m), (z32, _) in zip(a64, a32):
+        z64 = z64.double()
+        bad = m != (z64 > 0)
+        n = int(bad.sum())
+        if n:
+            bound = 4 * float((z32.double() - z64).abs().max())
+            mag = float(z64.abs()[bad].max())
+            assert mag <= bound, (what, 'slope mask off the fp64 sign beyond rounding', mag, bound, n)
+            worst = max(worst, mag / bound)
+        flips += n
+        total += m.numel()
+    print(f'{what}: {flips} of {total} LeakyReLU slopes differ from the fp64 signs, all within '
+          f'rounding of 0 (worst |z64| at {worst:.2f} of its bound)')
+    return flips
 
 
 def oracle_step(snap, x, cfg, bandwidth, weights, dtype, disc_masks=None):
@@ -183,8 +220,12 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6):
     # pre-activation within rounding of 0 may take either slope in fp32, a discrete outcome that
     # no rounding bound covers
     masks = split_masks(store, len(tr.disc.discriminators)) if tr.disc is not None else None
-    o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks)
-    o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks)
+    with lrelu_audit() as a64:
+        o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks)
+    with lrelu_audit() as a32:
+        o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks)
+    if masks is not None:
+        check_masks(a64, a32, 'step slope masks')
     table = []
     _check_opt('gen', tr.model, tr.opt, o64['grads'], o32['grads'], p64, snap['gen']['lr'], table, floor)
     if tr.disc is not None and 'disc_grads' in o64:

@@ -192,13 +192,16 @@ def test_stereo_disc_input_grads_vs_fp64():
     dp = {k: v.detach().cpu() for k, v in disc.state_dict().items() if not k.endswith('spec_transform.window')}
     mr = [[fm.detach().cpu() > 0 for fm in fms] for fms in fr]
     mf = [[fm.detach().cpu() > 0 for fm in fms] for fms in ff]
-    ref = {}
+    from steputil import lrelu_audit, check_masks
+    ref, audit = {}, {}
     for dt in (torch.float64, torch.float32):
         x0 = x.detach().cpu().to(dt)
         y0 = yd.detach().cpu().to(dt).requires_grad_(True)
         pd = {k: v.to(dt) for k, v in dp.items()}
-        lr_o, fr_o = O.msstft_forward(x0, pd, masks=mr)
-        lf_o, ff_o = O.msstft_forward(y0, pd, masks=mf)
+        with lrelu_audit() as audit[dt]:
+            lr_o, fr_o = O.msstft_forward(x0, pd, masks=mr)
+            lf_o, ff_o = O.msstft_forward(y0, pd, masks=mf)
         lo = O.total_loss(fr_o, lf_o, ff_o, x0, y0, 48000)
         ref[dt] = {k: torch.autograd.grad(lo[k].sum(), [y0], retain_graph=True)[0] for k in names}
+    check_masks(audit[torch.float64], audit[torch.float32], '48 kHz stereo slope masks')
     check_grads(mine, ref[torch.float64], ref[torch.float32], '48 kHz stereo GAN input grads')

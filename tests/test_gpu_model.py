@@ -238,13 +238,16 @@ def test_config3_b32_step_and_input_grads_vs_fp64():
     # take either slope in fp32: a discrete, legitimate outcome that a rounding bound cannot
     # cover; oracle._lrelu), so the comparison measures rounding only
     masks = [[fm[:1].detach().cpu() > 0 for fm in fms] for fms in ff]
-    ref = {}
+    from steputil import lrelu_audit, check_masks
+    ref, audit = {}, {}
     for dt in (torch.float64, torch.float32):
         x0 = x[:1].detach().cpu().to(dt)
         y0 = yd[:1].detach().cpu().to(dt).requires_grad_(True)
         pd = {k: v.to(dt) for k, v in dp.items()}
-        lg, _ = O.msstft_forward(y0, pd, masks=masks)
+        with lrelu_audit() as audit[dt]:
+            lg, _ = O.msstft_forward(y0, pd, masks=masks)
         ls = {'l_t': O.loss_t(x0, y0), 'l_f': O.loss_f(x0, y0, 24000),
               'l_g': sum(torch.relu(1 - l).mean() for l in lg) / len(lg) / len(lg)}
         ref[dt] = {k: torch.autograd.grad(l, [y0], retain_graph=True)[0][0] / 32 for k, l in ls.items()}
+    check_masks(audit[torch.float64], audit[torch.float32], 'config-3 B32 clip-0 slope masks')
     check_grads(mine, ref[torch.float64], ref[torch.float32], 'config-3 B32 input grads of clip 0')

@@ -183,6 +183,31 @@ def test_oracle_disc_fixture():
     close(x.grad, d['dx'], rtol=1e-3, atol=1e-5)
 
 
+def test_slope_mask_audit_flags_only_real_sign_errors():
+    """steputil.check_masks: masks taken from a fp32 evaluation pass (flips only within
+    rounding of 0); one mask bit flipped at the map's largest |z| is caught."""
+    import pytest
+    from steputil import lrelu_audit, check_masks
+    d = load('g5_disc.npz')
+    p = disc_state(51)
+    x = T(d['x'])[:1, :, :6000]
+    # the fp32 run's own signs as the imposed masks (what the GPU run's maps provide)
+    _, fm32 = O.msstft_forward(x, p)
+    masks = [[f > 0 for f in fms] for fms in fm32]
+    logs = {}
+    for dt in (torch.float64, torch.float32):
+        with lrelu_audit() as logs[dt]:
+            O.msstft_forward(x.to(dt), {k: v.to(dt) for k, v in p.items()}, masks=masks)
+    check_masks(logs[torch.float64], logs[torch.float32], 'fp32 masks')
+    z64, m = logs[torch.float64][3]
+    i = int(z64.abs().reshape(-1).argmax())
+    bad = m.clone().reshape(-1)
+    bad[i] = ~bad[i]
+    logs[torch.float64][3] = (z64, bad.view_as(m))
+    with pytest.raises(AssertionError):
+        check_masks(logs[torch.float64], logs[torch.float32], 'one flipped slope')
+
+
 # --------------------------------------------------------------------------- G6 balancer
 def test_oracle_balancer_fixture():
     d = load('g6_balancer.npz')

@@ -1,6 +1,7 @@
 """Two ranks on one GPU over gloo: Trainer.step eager vs HIP-graph mode, per step, on the
 test_gpu_dp 'gan_eager3' case; prints where the generator grads / params first differ.
-python tools/diag/dp_graph_diff.py (GPU box)."""
+ENCX_DP_GRAPHS=1 python tools/diag/dp_graph_diff.py (GPU box; the variable lets the Trainer
+capture at world > 1)."""
 import os
 import socket
 import sys
@@ -38,6 +39,13 @@ def rank_main(rank, port, outdir):
             print(f'build_fwd: capturing={torch.cuda.is_current_stream_capturing()}', flush=True)
             return _o(self, grp)
         _ops.WnBatch._build_fwd = build
+    if os.environ.get('DP_RSYNC'):  # a device sync after every graph replay
+        _rep = torch.cuda.CUDAGraph.replay
+
+        def replay(self, _r=_rep):
+            _r(self)
+            torch.cuda.synchronize()
+        torch.cuda.CUDAGraph.replay = replay
     res = {}
     for graphs in (False, True):
         torch.manual_seed(0)

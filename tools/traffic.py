@@ -72,12 +72,16 @@ def main():
     res = {'config': args.config, 'fetch_bytes_per_step': fetch, 'write_bytes_per_step': write,
            'hbm_bytes_per_step': fetch + write, 'kernel_dispatches_per_step': nf / args.steps,
            'fetch_bytes_per_step_uncorrected': f_kib * 1024 / args.steps,
+           # every conv-family kernel's FETCH_SIZE doubled (the upper bound if the narrow-load
+           # kernels' requests are tallied at half size too; their width is uncalibrated)
+           'hbm_bytes_per_step_conservative': 2 * f_kib * 1024 / args.steps + write,
            'correction': 'FETCH_SIZE x2 on the dwordx4-load kernels only (gfx950), KiB -> bytes',
            'fetch_x2_kernels': sorted(kinds['wide']), 'fetch_uncorrected_kernels': sorted(kinds['narrow']),
            'steps_profiled': args.steps}
     if args.calls_per_step:
         res['abi_calls_per_step'] = args.calls_per_step
         res['hbm_bytes_per_call'] = (fetch + write) / args.calls_per_step
+        res['hbm_bytes_per_call_conservative'] = res['hbm_bytes_per_step_conservative'] / args.calls_per_step
     json.dump(res, open(args.out, 'w'), indent=1)
     print(json.dumps(res))
 
