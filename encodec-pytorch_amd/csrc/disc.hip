@@ -1410,7 +1410,7 @@ struct C2DgR {
     int U4;     // quads per polyphase row
     int tiles;  // ceil(B * T2 * U4 / 32)
 };
-template <int J, int S, int RT, int WQ, bool YM, int NWV, int TM, bool APF>
+template <int J, int S, int RT, int WQ, bool YM, int NWV, int TM, bool APF, bool SB = true>
 __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
     // RT row tiles of 32 (M = Ci*S = 32 RT); a work item is (column tile, TM row tiles); APF:
     // the weight columns of step s + 1 are read from LDS during step s (else just in time)
@@ -1484,6 +1484,10 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
                 const int nu = u + 1 < 2 * KT ? u + 1 : 0;
                 const int nc = u + 1 < 2 * KT ? c0 + nu / KT : min(c0 + 2, CP - 1);
                 load(k ^ 1, nc, nu % KT);
+                // keep the next step's loads HERE, a whole step ahead of their use: without the
+                // barrier the scheduler sinks them to the end of the step (one register buffer
+                // instead of two) and every step waits out the load latency
+                if (SB) __builtin_amdgcn_sched_barrier(0);
                 f32x4* w = wb[k];
                 if (YM) {
 #pragma unroll
@@ -2302,11 +2306,18 @@ struct RwStage {  // one item's operands, loaded a whole item ahead of their MFM
     bool edge;    // wave-uniform: some element of this item lies outside its row
     bool rok[KTW];
 };
-template <int KF, int S, int KTW, int WQ, bool YM>
-__global__ __launch_bounds__(64, 2) void c2_wgrad_rw_kernel(C2WgR a) {
+// NW > 1 (c2_wgrad_rwg): NW waves per workgroup share one (kt group, ci block, split) task and
+// take its items interleaved (wave w: items it_beg + w, + NW, ...; neighbouring waves read
+// neighbouring windows), then sum their 32 x 32 x NTAP accumulators through LDS in a fixed
+// order (waves 0..3 store, waves 4..7 add, one pass sums the four) and store ONE task partial,
+// contiguous, in the task-major slab ws[split][kt group][ci block][co][ci][tap] (+ 32 biases),
+// which c2_wgr_reduce sums: NW x fewer slab bytes than the one-wave form, and coalesced.
+template <int KF, int S, int KTW, int WQ, bool YM, int NW = 1>
+__global__ __launch_bounds__(NW * 64, NW == 1 ? 2 : 1) void c2_wgrad_rw_kernel(C2WgR a) {
     constexpr int NTAP = KTW * KF;
+    static_assert(NW == 1 || NW == 8, "one-wave or 8-wave workgroups");
     const C2Geo g = a.g;
-    const int lane = threadIdx.x, h = lane >> 5, l = lane & 31;
+    const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31, wv = threadIdx.x >> 6;
     const int id = xcd_linear_id();
     const int kg = id % a.ktg, rest = id / a.ktg, cb = rest % a.cib, split = rest / a.cib;
     const int kt0 = kg * KTW, ci = cb * 32 + l;
@@ -2404,13 +2415,49 @@ __global__ __launch_bounds__(64, 2) void c2_wgrad_rw_kernel(C2WgR a) {
     // The prefetches are unconditional (past the end they re-load the last item and are never
     // used), so every path issues the same loads and each wait is for exactly the older item.
     RwStage<KTW, WQ> s0, s1;
-    if (it_beg < it_end) load(s0, it_beg);
-    for (int it = it_beg; it < it_end; it += 2) {
-        load(s1, min(it + 1, it_end - 1));
+    const int it0 = it_beg + wv;
+    if (it0 < it_end) load(s0, it0);
+    for (int it = it0; it < it_end; it += 2 * NW) {
+        load(s1, min(it + NW, it_end - 1));
         compute(s0);
-        if (it + 1 >= it_end) break;
-        load(s0, min(it + 2, it_end - 1));
+        if (it + NW >= it_end) break;
+        load(s0, min(it + 2 * NW, it_end - 1));
         compute(s1);
+    }
+    if constexpr (NW > 1) {
+        // ---- fixed-order workgroup sum through LDS, then one contiguous task partial
+        extern __shared__ float red[];  // [4][32 co][32 ci][NTAP] + [NW][32] biases
+        constexpr int TS = 32 * 32 * NTAP;
+        float* bred = red + 4 * TS;
+        bsum += __shfl_xor(bsum, 32, 64);
+        if (h == 0) bred[wv * 32 + l] = bsum;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            if ((wv >> 2) == pass) {
+                float* reg = red + (wv & 3) * TS;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int co = mfma_row(r, lane);
+#pragma unroll
+                    for (int j = 0; j < NTAP; ++j) {
+                        float* q = reg + (co * 32 + l) * NTAP + j;
+                        *q = pass == 0 ? acc[j][r] : *q + acc[j][r];
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        const int64_t SZ = (int64_t)a.ktg * a.cib * TS + 32;
+        float* dst = a.ws + (int64_t)split * SZ + (int64_t)(kg * a.cib + cb) * TS;
+        for (int d = threadIdx.x; d < TS; d += NW * 64)
+            dst[d] = ((red[d] + red[TS + d]) + red[2 * TS + d]) + red[3 * TS + d];
+        if (kg == 0 && cb == 0 && threadIdx.x < 32) {
+            float b = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) b += bred[w * 32 + threadIdx.x];
+            a.ws[(int64_t)split * SZ + (SZ - 32) + threadIdx.x] = b;
+        }
+        return;
     }
     // ---- the partial: D[co][ci] of tap (kt0 + k, kf) -> ws[split][co][(ci*KT + kt)*KF + kf]
     const int N = g.Ci * g.KT * KF + 1;
@@ -2456,6 +2503,41 @@ __global__ __launch_bounds__(256) void c2_wg_reduce(const float* ws, int S, int 
     if (n < Nw) {
         if (dw) {
             float* p = dw + (int64_t)co * Nw + n;
+            *p = acc_w ? *p + v : v;
+        }
+    } else if (db) {
+        db[co] = acc_b ? db[co] + v : v;
+    }
+}
+
+// dw[co][(ci*KT + kt)*KF + kf] (+)= sum_s of the task-major slabs of c2_wgrad_rw_kernel<.., NW > 1>
+// (ws[s][kg][cb][co][ci % 32][k*KF + kf], kt = kg*KTW + k, cb = ci / 32; the biases at SZ - 32 + co),
+// db[co] likewise. Fixed order (slab_sum_256).
+__global__ __launch_bounds__(256) void c2_wgr_reduce(const float* ws, int S, int64_t SZ, int Co, int Ci, int KT,
+                                                     int KF, int KTW, int cib, float* dw, float* db, int acc_w,
+                                                     int acc_b) {
+    __shared__ float red[256];
+    const int N = Ci * KT * KF + 1;
+    const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool valid = i < (int64_t)Co * N;
+    int64_t off = 0;
+    int co = 0, n = 0;
+    if (valid) {
+        co = (int)(i / N);
+        n = (int)(i - (int64_t)co * N);
+        if (n < N - 1) {
+            const int ci = n / (KT * KF), kt = (n / KF) % KT, kf = n % KF;
+            const int kg = kt / KTW, k = kt % KTW, NTAP = KTW * KF;
+            off = ((((int64_t)kg * cib + ci / 32) * 32 + co) * 32 + (ci & 31)) * NTAP + k * KF + kf;
+        } else {
+            off = SZ - 32 + co;
+        }
+    }
+    const float v = slab_sum_256(ws + off, S, SZ, valid, red);
+    if (threadIdx.x >= 64 || !valid) return;
+    if (n < N - 1) {
+        if (dw) {
+            float* p = dw + (int64_t)co * (N - 1) + n;
             *p = acc_w ? *p + v : v;
         }
     } else if (db) {
@@ -2896,7 +2978,7 @@ static bool dgr_ok(const C2Geo& g) {
     const int J = (g.KF + g.sf - 1) / g.sf;
     return (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float) <= 150 * 1024;
 }
-template <int NWV, int TM, bool APF>
+template <int NWV, int TM, bool APF, bool SB = true>
 static int run_dgrad_rw_n(const C2Dg& d, int wgs, hipStream_t st) {
     const C2Geo& g = d.g;
     C2DgR R{d, 0, 0};
@@ -2909,21 +2991,23 @@ static int run_dgrad_rw_n(const C2Dg& d, int wgs, hipStream_t st) {
     const int grid = (int)min((int64_t)wgs, cdiv((int64_t)R.tiles * rg, NWV));
     const bool ym = d.yact != nullptr;
     if (g.KF == 9) {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, TM, APF>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, TM, APF>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, TM, APF, SB>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, TM, APF, SB>), dim3(grid), dim3(NWV * 64), lds, st, R);
     } else {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV, 1, APF>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV, 1, APF>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV, 1, APF, SB>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV, 1, APF, SB>), dim3(grid), dim3(NWV * 64), lds, st, R);
     }
     ENCX_CHECK_LAUNCH();
     return 0;
 }
 // variant: 0 = 8 waves, both row tiles per item, weights just in time; 1 = 8 waves, one row tile
 // per item, weights prefetched; 2 = 12 waves, one row tile, prefetched; 3 = 8 waves, one row tile,
-// just in time
+// just in time; 4 = variant 0 without the scheduling barrier (the window loads sink to the end
+// of the step: the round-3 kernel, for A/B)
 static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st, int variant = 0) {
     if (!dgr_ok(d.g)) return ENCX_EINVAL;
     switch (variant) {
+        case 4: return run_dgrad_rw_n<8, 2, false, false>(d, wgs, st);
         case 1: return run_dgrad_rw_n<8, 1, true>(d, wgs, st);
         case 2: return run_dgrad_rw_n<12, 1, true>(d, wgs, st);
         case 3: return run_dgrad_rw_n<8, 1, false>(d, wgs, st);
@@ -3095,24 +3179,42 @@ static bool wgr_ok(const C2Geo& g) {
         return false;
     return (g.KF == 9 && g.sf == 2) || (g.KF == 3 && g.sf == 1);
 }
-static WgPlanR plan_wgr(const C2Geo& g, int waves = 2048) {
+// waves: the one-wave form's wave count; wgs > 0: the 8-wave workgroup form with at most that
+// many workgroups (one per CU: its 144 KB of reduction LDS), whole rounds over the CUs
+static WgPlanR plan_wgr(const C2Geo& g, int waves = 2048, int wgs = 0) {
     WgPlanR p;
     p.NC = (int)cdiv(g.Fo, 8);
     p.items = g.B * g.T2 * p.NC;
     p.ktg = g.KF == 9 ? g.KT : 1;
     p.cib = (int)cdiv(g.Ci, 32);
     const int per = p.ktg * p.cib;
-    int sp = (int)cdiv(waves, per);
+    int sp = wgs > 0 ? max(1, wgs / per) : (int)cdiv(waves, per);
     if (sp > p.items) sp = p.items;
     p.per_split = (int)cdiv(p.items, sp);
     p.splits = (int)cdiv(p.items, p.per_split);
     return p;
 }
+static int64_t wgr_slab(const C2Geo& g, const WgPlanR& p) {  // task-major slab floats (8-wave form)
+    return (int64_t)p.ktg * p.cib * 32 * 32 * 9 + 32;  // NTAP = 9 taps per task (1 x 9 or 3 x 3)
+}
 static int run_wgrad_rw(const C2Geo& g, const float* dy, const float* yact, const float* x, float* ws,
-                        const WgPlanR& p, hipStream_t st) {
+                        const WgPlanR& p, hipStream_t st, bool wg8 = false) {
     if (!wgr_ok(g)) return ENCX_EINVAL;
     C2WgR a{g, dy, yact, x, ws, p.NC, p.items, p.per_split, p.ktg, p.cib};
-    const dim3 grid((unsigned)(p.splits * p.ktg * p.cib)), blk(64);
+    const dim3 grid((unsigned)(p.splits * p.ktg * p.cib));
+    if (wg8) {
+        const size_t lds = (4 * 32 * 32 * 9 + 8 * 32) * sizeof(float);
+        if (g.KF == 9) {
+            if (yact) hipLaunchKernelGGL((c2_wgrad_rw_kernel<9, 2, 1, 4, true, 8>), grid, dim3(512), lds, st, a);
+            else hipLaunchKernelGGL((c2_wgrad_rw_kernel<9, 2, 1, 4, false, 8>), grid, dim3(512), lds, st, a);
+        } else {
+            if (yact) hipLaunchKernelGGL((c2_wgrad_rw_kernel<3, 1, 3, 2, true, 8>), grid, dim3(512), lds, st, a);
+            else hipLaunchKernelGGL((c2_wgrad_rw_kernel<3, 1, 3, 2, false, 8>), grid, dim3(512), lds, st, a);
+        }
+        ENCX_CHECK_LAUNCH();
+        return 0;
+    }
+    const dim3 blk(64);
     if (g.KF == 9) {
         if (yact) hipLaunchKernelGGL((c2_wgrad_rw_kernel<9, 2, 1, 4, true>), grid, blk, 0, st, a);
         else hipLaunchKernelGGL((c2_wgrad_rw_kernel<9, 2, 1, 4, false>), grid, blk, 0, st, a);
@@ -3305,8 +3407,10 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
     }
     // register-window form (c2_dgrad_rw_kernel); ENCX_DGR = workgroups (0: off)
     static const int dg_wgs = [] { const char* v = getenv("ENCX_DGR"); return v ? atoi(v) : 256; }();
+    // ENCX_DGR_VARIANT: run_dgrad_rw's kernel variant (A/B; default 0)
+    static const int dg_var = [] { const char* v = getenv("ENCX_DGR_VARIANT"); return v ? atoi(v) : 0; }();
     if (dg_wgs > 0 && dgr_ok(g) && rw_pays(cdiv(B * T2 * cdiv(a.U, 4), 32), B * T2 * a.U, 92.0 / 78.0) &&
-        run_dgrad_rw(a, dg_wgs, st) == 0)
+        run_dgrad_rw(a, dg_wgs, st, dg_var) == 0)
         return 0;
     // tile choice from tools/mb/c2_mb sweeps: 128-column tiles for the narrowest layers (Fo 33;
     // at Fo 65 the 256-column tile is 4-7 % faster), 8-combo
@@ -3342,7 +3446,12 @@ size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64
     if (wgr_ok(g)) splits = max(splits, plan_wgr(g, 4096).splits);  // ENCX_WGR up to 4096 waves
     if (co1_ok(g)) splits = max(splits, plan_co1(g).splits);
     if (wg3n_ok(g)) splits = max(splits, plan_wg3n(g).splits + (int)cdiv(plan_wg3n(g).splits, 32));
-    return (size_t)splits * Co * (Ci * KT * KF + 1) * sizeof(float);
+    size_t bytes = (size_t)splits * Co * (Ci * KT * KF + 1) * sizeof(float);
+    if (wgr_ok(g)) {  // the 8-wave form's task-major slabs (ENCX_WGR_WGS up to 1024 workgroups)
+        const WgPlanR q = plan_wgr(g, 0, 1024);
+        bytes = max(bytes, (size_t)q.splits * wgr_slab(g, q) * sizeof(float));
+    }
+    return bytes;
 }
 
 /* dw [Co][Ci][KT][KF] and db [Co] (either may be NULL) of the layer whose output grad is dy,
@@ -3371,6 +3480,18 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
         return 0;
     }
     static const int rw_waves = [] { const char* v = getenv("ENCX_WGR"); return v ? min(atoi(v), 4096) : 2048; }();
+    // 8-wave workgroups summing their partials in LDS (one per CU); ENCX_WGR_WGS=0: one-wave form
+    static const int rw_wgs = [] { const char* v = getenv("ENCX_WGR_WGS"); return v ? min(atoi(v), 1024) : 256; }();
+    if (rw_waves > 0 && rw_wgs > 0 && wgr_ok(g) && g_c2_select != 2) {
+        const WgPlanR q = plan_wgr(g, 0, rw_wgs);
+        if (run_wgrad_rw(g, dy, yact, x, ws, q, st, true) == 0) {
+            hipLaunchKernelGGL(c2_wgr_reduce, dim3((unsigned)cdiv(Co * N, 64)), dim3(256), 0, st, ws, q.splits,
+                               wgr_slab(g, q), (int)Co, (int)Ci, (int)KT, (int)KF, KF == 9 ? 1 : 3, q.cib, dw, db,
+                               acc_w, acc_b);
+            ENCX_CHECK_LAUNCH();
+            return 0;
+        }
+    }
     if (rw_waves > 0 && wgr_ok(g) && g_c2_select != 2) {  // register-window form (c2_wgrad_rw_kernel); ENCX_WGR=0 off
         const WgPlanR q = plan_wgr(g, rw_waves);
         if (run_wgrad_rw(g, dy, yact, x, ws, q, st) == 0) {

@@ -67,30 +67,36 @@ def snapshot(tr):
 
 
 def disc_mask_hooks(disc, store):
-    """Forward hooks collecting the sign (> 0) of every LeakyReLU'd discriminator map of a step,
-    in call order: the Trainer runs the discriminator on the real audio, then on the fake."""
+    """Forward hooks collecting every LeakyReLU'd discriminator map of a step (on the host), in
+    call order: the Trainer runs the discriminator on the real audio, then on the fake."""
     hs = []
     for d in disc.discriminators:
         for layer in d.convs:
-            hs.append(layer.register_forward_hook(lambda mod, inp, out: store.append(out.detach().cpu() > 0)))
+            hs.append(layer.register_forward_hook(lambda mod, inp, out: store.append(out.detach().cpu())))
     return hs
 
 
 def split_masks(store, n_disc):
-    """[real maps..., fake maps...] -> {'real': [disc][layer], 'fake': [disc][layer]}"""
+    """[real maps..., fake maps...] -> {'real': [disc][layer] slope masks (map > 0), 'fake': the
+    same, 'feat': [disc][layer] signs of fake - real (the feature-matching L1's derivative)}"""
     per = len(store) // (2 * n_disc)
     grid = [store[i * per:(i + 1) * per] for i in range(2 * n_disc)]
-    return {'real': grid[:n_disc], 'fake': grid[n_disc:]}
+    real, fake = grid[:n_disc], grid[n_disc:]
+    return {'real': [[m > 0 for m in ms] for ms in real], 'fake': [[m > 0 for m in ms] for ms in fake],
+            'feat': [[torch.sign(f - r) for r, f in zip(rs, fs)] for rs, fs in zip(real, fake)]}
 
 
 @contextlib.contextmanager
-def lrelu_audit():
-    """Collect (pre-activation, imposed mask) of every masked LeakyReLU the oracle evaluates."""
+def lrelu_audit(feat=None):
+    """Collect (pre-activation, imposed mask) of every masked LeakyReLU the oracle evaluates;
+    with a `feat` list also (fake - real, imposed sign) of every feature-matching L1."""
     O.LRELU_AUDIT = log = []
+    O.FEAT_AUDIT = feat
     try:
         yield log
     finally:
         O.LRELU_AUDIT = None
+        O.FEAT_AUDIT = None
 
 
 def check_masks(a64, a32, what):
@@ -104,7 +110,7 @@ def check_masks(a64, a32, what):
     worst = 0.0
     for (z64, m), (z32, _) in zip(a64, a32):
         z64 = z64.double()
-        bad = m != (z64 > 0)
+        bad = m != (z64 > 0) if m.dtype == torch.bool else m.double() != torch.sign(z64)
         n = int(bad.sum())
         if n:
             bound = 4 * float((z32.double() - z64).abs().max())
@@ -113,7 +119,7 @@ def check_masks(a64, a32, what):
             worst = max(worst, mag / bound)
         flips += n
         total += m.numel()
-    print(f'{what}: {flips} of {total} LeakyReLU slopes differ from the fp64 signs, all within '
+    print(f'{what}: {flips} of {total} imposed signs differ from the fp64 signs, all within '
           f'rounding of 0 (worst |z64| at {worst:.2f} of its bound)')
     return flips
 
@@ -220,12 +226,15 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6):
     # pre-activation within rounding of 0 may take either slope in fp32, a discrete outcome that
     # no rounding bound covers
     masks = split_masks(store, len(tr.disc.discriminators)) if tr.disc is not None else None
-    with lrelu_audit() as a64:
+    f64, f32 = [], []
+    with lrelu_audit(f64) as a64:
         o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks)
-    with lrelu_audit() as a32:
+    with lrelu_audit(f32) as a32:
         o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks)
     if masks is not None:
         check_masks(a64, a32, 'step slope masks')
+        if 'l_feat' in weights:
+            check_masks(f64, f32, 'step feature-L1 signs')
     table = []
     _check_opt('gen', tr.model, tr.opt, o64['grads'], o32['grads'], p64, snap['gen']['lr'], table, floor)
     if tr.disc is not None and 'disc_grads' in o64:

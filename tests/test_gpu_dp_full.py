@@ -18,7 +18,7 @@ rows per GPU): every code bit-identical, codebooks within 1e-5.
 Config 5: 2 ranks x B16 of the 48 kHz stereo model (n_q 16, 1 s = two segments, GroupNorm,
 sync_codebooks, l_g = l_feat = 4 as train.sbatch:32-33) vs 1 x B32: codes bit-identical (the
 second segment quantises with the codebooks synced after the first), codebooks within 1e-5,
-ranks identical, and the same grad decomposition.
+ranks identical; and, with rank-local codebooks, the same grad decomposition.
 """
 import os
 import socket
@@ -32,8 +32,9 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda:0'
 W24 = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}
 W48 = {'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4}
-# name: (48 kHz, world, clips per rank)
-CASES = {'c4_8x32': (False, 8, 32), 'c4_2x32': (False, 2, 32), 'c5_2x16': (True, 2, 16)}
+# name: (48 kHz, world, clips per rank, sync_codebooks)
+CASES = {'c4_8x32': (False, 8, 32, True), 'c4_2x32': (False, 2, 32, True), 'c5_2x16': (True, 2, 16, True),
+         'c5_2x16_local': (True, 2, 16, False)}
 
 
 def _free_port():
@@ -97,10 +98,10 @@ def _rank_main(rank, world, port, outdir, name):
     torch.cuda.set_device(0)
     torch.distributed.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        k48, _, b = CASES[name]
+        k48, _, b, sync = CASES[name]
         x = _batch(k48, world * b)[rank * b:(rank + 1) * b].to(DEV)
         torch.manual_seed(0)
-        m, disc = _build(k48)
+        m, disc = _build(k48, sync)
         tr = _trainer(m, disc, k48)
         # every segment's codes (48 kHz: the last segment's are model.last_codes)
         codes = []
@@ -167,7 +168,7 @@ def _decomposed(name):
     from per-rank, per-loss backward passes in this one process (see the module docstring)."""
     from encx.losses import total_loss, disc_loss
     from encx.ops import DiscGradMode
-    k48, world, b = CASES[name]
+    k48, world, b, _ = CASES[name]
     wts = W48 if k48 else W24
     sr = 48000 if k48 else 24000
     x_all = _batch(k48, world * b).to(DEV)
@@ -283,4 +284,15 @@ def test_config5_two_ranks_48k_stereo_vs_one_process():
     _identical(runs, 'c5_2x16')
     _check_vs_single(runs, _single('c5_2x16', 32), 'c5_2x16')
     _check_cluster_sizes(runs, 'c5_2x16')
-    _check_decomposition(runs, 'c5_2x16')
+
+
+def test_config5_two_ranks_48k_stereo_grad_decomposition():
+    """The grad decomposition for the 48 kHz step with rank-local codebooks (the reference's
+    default, core_vq.py:157,175): with two segments the second one quantises with codebooks the
+    first one updated, so the per-rank restatement matches the trainer only when each rank's
+    codebooks follow its own clips."""
+    runs = _spawn('c5_2x16_local')
+    for r, res in enumerate(runs[1:], 1):
+        for k in ('gen_param', 'gen_m', 'disc_param', 'gen_grad', 'disc_grad'):
+            assert torch.equal(runs[0][k], res[k]), (r, k)
+    _check_decomposition(runs, 'c5_2x16_local')

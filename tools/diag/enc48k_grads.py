@@ -22,6 +22,7 @@ from oracle import encodec_oracle as O  # noqa: E402
 from test_gpu_48k import build48k, load, T, DEV, disc_state  # noqa: E402
 
 W = {'l_t': 0.1, 'l_f': 1, 'l_g': 4, 'l_feat': 4}
+FEAT = os.environ.get('ENC48K_FEAT_SIGNS', '1') != '0'  # impose our feature-L1 signs (oracle._l1_feat)
 
 
 def rel(a, b):
@@ -55,7 +56,7 @@ def oracle_gen(snap, x, cfg, bw, masks, dtype):
     y = O.linear_overlap_add(outs, stride)[:, :, :x.shape[-1]]
     lr_, fr = O.msstft_forward(x, dp, masks=masks['real'])
     lf_, ff = O.msstft_forward(y, dp, masks=masks['fake'])
-    losses = O.total_loss(fr, lf_, ff, x, y, cfg.sample_rate)
+    losses = O.total_loss(fr, lf_, ff, x, y, cfg.sample_rate, feat_signs=masks.get('feat') if FEAT else None)
     grads = {k: torch.autograd.grad(l.sum(), [y], retain_graph=True)[0] for k, l in losses.items()}
     bal = O.Balancer(W)
     if snap['bal'] is not None:
