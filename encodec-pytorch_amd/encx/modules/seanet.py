@@ -5,6 +5,7 @@ parameter-free placeholders), so state-dict keys match. forward() walks the list
 every ELU into the conv that consumes it, and each resblock's residual sum into its second
 conv's epilogue: the SEANet stack never materialises an activation tensor on its own.
 """
+import os
 import types
 import typing as tp
 
@@ -12,6 +13,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from .. import ops
 from .conv import SConv1d, SConvTranspose1d
 from .lstm import SLSTM
 
@@ -48,8 +50,22 @@ class SEANetResnetBlock(nn.Module):
         else:
             self.shortcut = SConv1d(dim, dim, kernel_size=1, norm=norm, norm_kwargs=norm_params,
                                     causal=causal, pad_mode=pad_mode)
+        self._fuse = (not true_skip and list(kernel_sizes) == [3, 1] and list(dilations) == [1, 1]
+                      and compress == 2 and dim in (32, 64) and causal and pad_mode == 'reflect'
+                      and norm == 'weight_norm')
+
+    def _fusable(self, x):
+        """The EnCodec block (k3 + 1x1, compress 2, 1x1 shortcut, causal reflect weight_norm
+        convs) at a high rate: one fused kernel per direction (ops.ResBlockFn)."""
+        if not self._fuse or x.dim() != 3 or x.shape[-1] < ops.RESBLOCK_TMIN:
+            return False
+        return os.environ.get('ENCX_RESBLOCK', '1') != '0'
 
     def forward(self, x):
+        if self._fusable(x):
+            c1, c2 = [m for m in self.block if isinstance(m, SConv1d)]
+            ps = [(c.conv.conv.weight_v, c.conv.conv.weight_g, c.conv.conv.bias) for c in (c1, c2, self.shortcut)]
+            return ops.resblock(x, *ps)
         convs = [m for m in self.block if isinstance(m, SConv1d)]
         linkable = (len(convs) > 1 and torch.is_grad_enabled() and x.requires_grad
                     and all(c.conv.norm_type != 'time_group_norm' for c in convs))

@@ -343,6 +343,69 @@ def conv1d(x, v, g, b, K, stride=1, dilation=1, causal=True, pad_mode='reflect',
     return Conv1dFn.apply(x, v, g, b, res, K, stride, dilation, causal, pad_mode, act, link, link_role)
 
 
+# ---------------------------------------------------------------------------- fused residual block
+class ResBlockFn(torch.autograd.Function):
+    """SEANetResnetBlock.forward (modules/seanet.py:46-63) with the EnCodec defaults -- ELU, k3
+    causal reflect-padded conv (C -> C/2), ELU, 1x1 conv (C/2 -> C), plus the 1x1 shortcut conv
+    -- as one kernel per direction (csrc/resblock.hip): the hidden tensor and the shortcut never
+    make a round trip through HBM between three convs. (x, then (v, g, b) of the k3 conv, the
+    second conv and the shortcut.) Saves x and the pre-ELU hidden h for the backward."""
+
+    @staticmethod
+    def forward(ctx, x, v1, g1, b1, v2, g2, b2, vs, gs, bs):
+        _check(x)
+        x = x.contiguous()
+        B, C, T = x.shape
+        w1, _ = _weight_prep(v1, g1, 3, 1, True, False)
+        w2, _ = _weight_prep(v2, g2, 1, 1, True, False)
+        ws, _ = _weight_prep(vs, gs, 1, 1, True, False)
+        h = torch.empty(B, C // 2, T, device=x.device, dtype=torch.float32)
+        y = torch.empty_like(x)
+        call('encx_resblock_fwd', ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(ws), ptr(bs), ptr(h), ptr(y),
+             B, C, T, stream())
+        ctx.save_for_backward(x, h, w1, w2, ws)
+        ctx.params = ((v1, g1, b1), (v2, g2, b2), (vs, gs, bs))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h, w1, w2, ws = ctx.saved_tensors
+        (v1, g1, b1), (v2, g2, b2), (vs, gs, bs) = ctx.params
+        dy = dy.contiguous()
+        B, C, T = x.shape
+        HD = C // 2
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else torch.empty_like(x)
+        bufs = [_dw_buffer(v1, g1, b1, (HD, C, 3), x), _dw_buffer(v2, g2, b2, (C, HD, 1), x),
+                _dw_buffer(vs, gs, bs, (C, C, 1), x)]
+        accs = {a for _, a in bufs}
+        if len(accs) != 1:  # a layer met twice before a flush (never in SEANet): fresh buffers
+            bufs = [(torch.empty(sh, device=x.device, dtype=torch.float32), 0)
+                    for sh in ((HD, C, 3), (C, HD, 1), (C, C, 1))]
+        acc_w = bufs[0][1]
+        direct_b = all(_direct(v) and _direct(g) and _direct(b) for v, g, b in ctx.params)
+        if direct_b:
+            dbs_ = [b1.grad, b2.grad, bs.grad]
+        else:
+            dbs_ = [torch.empty_like(b1), torch.empty_like(b2), torch.empty_like(bs)]
+        wsp = _ws(lib.encx_resblock_bwd_workspace(B, C, T), x)
+        call('encx_resblock_bwd', ptr(dy), ptr(x), ptr(h), ptr(w1), ptr(w2), ptr(ws), ptr(dx),
+             ptr(bufs[0][0]), ptr(dbs_[0]), ptr(bufs[1][0]), ptr(dbs_[1]), ptr(bufs[2][0]), ptr(dbs_[2]),
+             int(acc_w), int(direct_b), ptr(wsp), B, C, T, stream())
+        out = []
+        for (v, g, b), (dw, _), db in zip(ctx.params, bufs, dbs_):
+            dv, dg, _ = _param_grads(v, g, None, dw, None, B, 0, T)
+            out += [dv, dg, None if direct_b else db]
+        return (dx, *out)
+
+
+def resblock(x, p1, p2, ps):
+    """p1 / p2 / ps: (v, g, b) of the block's k3 conv, 1x1 conv and 1x1 shortcut."""
+    return ResBlockFn.apply(x, *p1, *p2, *ps)
+
+
+RESBLOCK_TMIN = 2048  # fused residual block from this many samples up (the HBM-bound stages)
+
+
 # ---------------------------------------------------------------------------- ConvTranspose1d
 class ConvTr1dFn(torch.autograd.Function):
     """SConvTranspose1d.forward (modules/conv.py:230-252) incl. weight_norm (dim 0 = in

@@ -120,14 +120,12 @@ class Trainer:
         if train_d:
             self.opt_d.prepare()
         key = (bw, train_d, tuple(x.shape))
-        # HIP graphs only for the single-segment step (world 1). At world > 1 the step is cut into
-        # segments around the collectives, and replays of the per-segment graphs were measured
-        # to drift from the eager step (tools/diag/dp_graph_diff.py: the generator grads of the
-        # first replayed step differ at 1e-3..5e-2 whenever the encoder backward and the
-        # discriminator phase are captured into different graphs; fresh pools, device syncs and
-        # synchronous collectives do not change it; cause not found). Eager steps there: config 3
-        # measured 561 audio-s/s eager vs 561 with graphs (profiles/r02), the step is GPU-bound.
-        if self.graphs and (not distrib.is_distributed() or os.environ.get('ENCX_DP_GRAPHS') == '1') \
+        # At world > 1 the step is cut into segments around the collectives, one graph each
+        # (ENCX_DP_GRAPHS=0: eager there). The round-3 replay drift does not reproduce: replays
+        # are bit-identical to the eager step at world 2 with the round-3 code and at HEAD, with
+        # and without device syncs, HIP packet capture or the older Conv2d kernels, and at world
+        # 1 for every segmentation (profiles/r04/graph_drift, tests/test_gpu_dp.py).
+        if self.graphs and (not distrib.is_distributed() or os.environ.get('ENCX_DP_GRAPHS', '1') != '0') \
                 and self._graph_ok(key):
             out = self._graph_step(key, x)
         else:

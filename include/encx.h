@@ -148,6 +148,27 @@ int encx_convtr1d_bwd_weight(const float* x, const float* dy, float* dw, float* 
 size_t encx_convtr1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, int64_t Tin,
                                           int64_t K);
 
+/* ---------------------------------------------------------------- fused residual block
+ * SEANetResnetBlock.forward (modules/seanet.py:21-63) with the EnCodec defaults (kernel_sizes
+ * [3, 1], dilations [1, 1], compress 2, true_skip False -> 1x1 shortcut; causal SConv1d with
+ * reflect padding, conv.py:195-210) as ONE kernel per direction for the high-rate stages:
+ *   h = b1 + W1 * ELU(pad_reflect(x, 2, 0))   (k3, C -> C/2),   y = bs + Ws x + b2 + W2 ELU(h).
+ * C in {32, 64}; T >= 3. Weights in the forward layout of encx_weightnorm_fwd (wf [Cin][K][Cout]):
+ * w1 [C][3][C/2], w2 [C/2][C], ws [C][C]. h [B][C/2][T] (pre-ELU) is written for the backward. */
+int encx_resblock_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                      const float* ws, const float* bs, float* h, float* y, int64_t B, int64_t C, int64_t T,
+                      encx_stream_t stream);
+/* Backward of the above: dx = Ws^T dy + ELU'(x) * fold(W1^T * (ELU'(h) * W2^T dy)) (written, not
+ * accumulated) and the weight grads in the natural layouts dw1 [C/2][C][3], dw2 [C][C/2][1],
+ * dws [C][C][1] (+= when acc_w), db1 [C/2], db2 = dbs = sum dy (+= when acc_b); any grad pointer
+ * may be NULL. ws: encx_resblock_bwd_workspace bytes (per-workgroup partials, summed in a
+ * fixed order). */
+size_t encx_resblock_bwd_workspace(int64_t B, int64_t C, int64_t T);
+int encx_resblock_bwd(const float* dy, const float* x, const float* h, const float* w1, const float* w2,
+                      const float* ws, float* dx, float* dw1, float* db1, float* dw2, float* db2, float* dws,
+                      float* dbs, int acc_w, int acc_b, float* wsp, int64_t B, int64_t C, int64_t T,
+                      encx_stream_t stream);
+
 /* ---------------------------------------------------------------- elementwise / reductions */
 /* db[c] = [acc ? db : 0] + sum_{b,t} dy[b,c,t] (the bias grads of every conv); ws: workspace
  * of encx_channel_sum_workspace(C) bytes. */

@@ -77,11 +77,12 @@ CASES = {
     'kmeans_sync': (False, True, True, {'l_t': 0.1, 'l_f': 1}, False),
     # 3 GAN steps, all four losses balanced, eager (decoder-grad bucket all-reduce overlapping the
     # encoder backward) vs HIP graphs (segments captured between the eager collectives)
-    'gan_eager3': (True, False, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 3, False),
-    'gan_graph3': (True, False, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 3, True),
+    # (5 steps: eager, capture, 3 replays)
+    'gan_eager3': (True, False, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 5, False),
+    'gan_graph3': (True, False, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 5, True),
     # the same with the codebook sums all-reduced (deferred to one collective between segments)
-    'gan_sync_eager3': (True, True, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 3, False),
-    'gan_sync_graph3': (True, True, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 3, True),
+    'gan_sync_eager3': (True, True, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 5, False),
+    'gan_sync_graph3': (True, True, True, {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}, True, 5, True),
 }
 MULTI_STEP = ('gan_eager3', 'gan_graph3', 'gan_sync_eager3', 'gan_sync_graph3')
 # config 4's partition count: 8 ranks x B/8 against 1 rank x B (the same cases as the 2-rank run)
@@ -96,12 +97,14 @@ def _run_case(name, x):
     m, disc = _build(gan, sync, inited=inited)
     tr = Trainer(m, disc, lr=3e-4, disc_lr=3e-4, scheduler=False, weights=weights,
                  balancer_kwargs={'rescale_grads': rescale}, graphs=graphs)
+    losses = []
     for i in range(steps):
-        tr.step(x.to(DEV) * (1.0 + 0.1 * i))
+        o = tr.step(x.to(DEV) * (1.0 + 0.1 * i))
+        losses.append(torch.stack([o[k].reshape(()) for k in sorted(o)]).cpu())
     torch.cuda.synchronize()
     captured = any(isinstance(v, tuple) for v in tr._graphs.values())
-    assert not captured or not torch.distributed.is_initialized()
-    out = {'gen_grad': tr.opt.flat_grad.cpu(), 'gen_param': tr.opt.flat.cpu(),
+    assert captured == (graphs and steps >= 2), (name, captured)
+    out = {'gen_grad': tr.opt.flat_grad.cpu(), 'gen_param': tr.opt.flat.cpu(), 'losses': torch.stack(losses),
            'gen_m': tr.opt.exp_avg.cpu(), 'codes': m.last_codes[0].cpu()}
     for i, layer in enumerate(m.quantizer.vq.layers):
         cb = layer._codebook
@@ -299,12 +302,12 @@ def test_balanced_grads_half_plus_commit(runs):
     assert close(two['gen_sync'][0]['gen_grad'], want, 1e-4)
 
 
-def test_graph_trainer_steps_eagerly_at_two_ranks(runs):
-    """Trainer(graphs=True) at world 2 runs its data-parallel steps eagerly (the collectives
-    between segments overlapping the encoder backward and the discriminator phase; per-segment
-    graph replays were measured to drift, encx/train.py Trainer.step): 3 GAN steps equal the
-    eager trainer's bit for bit, with and without the codebook sums all-reduced, and both ranks
-    stay identical."""
+def test_graph_trainer_replays_match_eager_at_two_ranks(runs):
+    """Trainer(graphs=True) at world 2: one HIP graph per segment between the collectives (the
+    decoder's grad bucket all-reduced under the encoder backward, the encoder's under the
+    discriminator phase), captured at step 2 and replayed at steps 3-5. Every step's losses and
+    the final grads, parameters, Adam moments and codebooks equal the eager trainer's bit for
+    bit, with and without the codebook sums all-reduced, and both ranks stay identical."""
     two, _, _ = runs
     for eager, graph in (('gan_eager3', 'gan_graph3'), ('gan_sync_eager3', 'gan_sync_graph3')):
         for r in range(2):

@@ -351,3 +351,71 @@ def test_lstm_vs_oracle(B, H, Tn, L):
     rel_close(x.grad, x64.grad, 'dx')
     for i, (n, w) in enumerate(p64.items()):
         rel_close(wts[i].grad, w.grad, n, tol=5e-4)
+
+
+# --------------------------------------------------------------------------- fused residual block
+@pytest.mark.parametrize('C,T,B', [(32, 2048, 3), (32, 24000, 2), (64, 12000, 2), (64, 3001, 3), (32, 2113, 1)])
+def test_fused_resblock_vs_torch_fp64(C, T, B):
+    """ops.ResBlockFn (csrc/resblock.hip: SEANetResnetBlock, modules/seanet.py:46-63, as one
+    kernel per direction) against torch's fp64 restatement of the block: ELU -> reflect-padded
+    causal k3 conv (C -> C/2) -> ELU -> 1x1 conv (C/2 -> C), plus the 1x1 shortcut, all weight
+    normed. Output, input grad and every weight / bias grad under a seeded output grad, relative to
+    each tensor's largest magnitude; incl. T not a multiple of the 64-position tile."""
+    from encx import ops
+    g = torch.Generator().manual_seed(C * 7 + T)
+    HD = C // 2
+
+    def par(co, ci, k):
+        v = (torch.randn(co, ci, k, generator=g, dtype=torch.float64) / (ci * k) ** 0.5)
+        gg = v.reshape(co, -1).norm(dim=1).reshape(co, 1, 1) * (1 + 0.1 * torch.randn(co, 1, 1, generator=g, dtype=torch.float64))
+        b = 0.1 * torch.randn(co, generator=g, dtype=torch.float64)
+        return [v, gg, b]
+    ps64 = [par(HD, C, 3), par(C, HD, 1), par(C, C, 1)]
+    x64 = 0.5 * torch.randn(B, C, T, generator=g, dtype=torch.float64)
+    dy64 = torch.randn(B, C, T, generator=g, dtype=torch.float64)
+    leaves64 = [x64.requires_grad_(True)] + [t.requires_grad_(True) for p in ps64 for t in p]
+
+    def wn(v, gg):
+        return v * (gg / v.reshape(v.shape[0], -1).norm(dim=1).reshape(-1, 1, 1))
+    (v1, g1, b1), (v2, g2, b2), (vs, gs, bs) = ps64
+    e = F.pad(F.elu(x64), (2, 0), mode='reflect')
+    h = F.conv1d(e, wn(v1, g1), b1)
+    y64 = F.conv1d(F.elu(h), wn(v2, g2), b2) + F.conv1d(x64, wn(vs, gs), bs)
+    ref = torch.autograd.grad(y64, leaves64, dy64)
+    leaves = [t.detach().float().to(DEV).requires_grad_(True) for t in leaves64]
+    x = leaves[0]
+    p = [leaves[1:4], leaves[4:7], leaves[7:10]]
+    y = ops.resblock(x, *p)
+    mine = torch.autograd.grad(y, leaves, dy64.float().to(DEV))
+
+    def rel(a, b):
+        a, b = a.detach().double().cpu(), b.detach().double()
+        return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+    names = ['x', 'v1', 'g1', 'b1', 'v2', 'g2', 'b2', 'vs', 'gs', 'bs']
+    errs = {'y': rel(y, y64)} | {f'd{n}': rel(m, r) for n, m, r in zip(names, mine, ref)}
+    print(f'C {C} T {T} B {B}: ' + ' '.join(f'{k} {v:.1e}' for k, v in errs.items()))
+    assert errs['y'] < 1e-5, errs
+    assert all(v < 1e-4 for v in errs.values()), errs
+
+
+def test_fused_resblock_matches_unfused_block():
+    """The SEANet block with the fused kernel vs the same block on the three separate conv kernels
+    (ENCX_RESBLOCK=0): forward and every grad within fp32 rounding of each other."""
+    import os
+    from encx.modules.seanet import SEANetResnetBlock
+    torch.manual_seed(3)
+    blk = SEANetResnetBlock(32, norm='weight_norm', causal=True, true_skip=False).to(DEV)
+    x0 = (0.5 * torch.randn(2, 32, 4800)).to(DEV)
+    dy = torch.randn(2, 32, 4800).to(DEV)
+    outs = []
+    for fused in ('1', '0'):
+        os.environ['ENCX_RESBLOCK'] = fused
+        try:
+            x = x0.clone().requires_grad_(True)
+            y = blk(x)
+            gs = torch.autograd.grad(y, [x] + list(blk.parameters()), dy)
+            outs.append([y.detach()] + [g.detach() for g in gs])
+        finally:
+            os.environ.pop('ENCX_RESBLOCK', None)
+    for a, b in zip(*outs):
+        assert float((a - b).abs().max()) <= 2e-5 * float(b.abs().max()) + 1e-7, (float((a - b).abs().max()), float(b.abs().max()))

@@ -190,3 +190,28 @@ def test_weight_norm_batch_matches_per_layer():
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
     assert float((d0 - d1).abs().max()) <= 1e-5 * float(d0.abs().max())
+
+
+@pytest.mark.parametrize('segmented', [False, True])
+def test_two_graph_keys_back_to_back_match_eager(segmented):
+    """Two graph keys (bandwidths 6 and 3 kbps: n_q 8 and 4) alternating step by step, so every
+    replay of one key follows a replay of the other in the shared graph pool: the generator and
+    discriminator flat grads and parameters after EVERY step equal the eager trainer's bit for
+    bit; segmented=True captures the data-parallel segment list (one graph per segment) at world 1."""
+    xs = batches(8)
+    runs = []
+    for graphs in (False, True):
+        tr = make_trainer(graphs=graphs)
+        tr.segmented = segmented
+        per_step = []
+        for i, x in enumerate(xs):
+            tr.model.target_bandwidths = [6.0 if i % 2 == 0 else 3.0]
+            tr.step(x)
+            torch.cuda.synchronize()
+            per_step.append([t.clone() for t in (tr.opt.flat_grad, tr.opt.flat, tr.opt_d.flat_grad, tr.opt_d.flat)])
+        runs.append(per_step)
+        if graphs:
+            assert sum(isinstance(v, tuple) for v in tr._graphs.values()) == 2
+    for i, (a, b) in enumerate(zip(*runs)):
+        for k, (ta, tb) in enumerate(zip(a, b)):
+            assert torch.equal(ta, tb), (i, k, float((ta - tb).abs().max()))
