@@ -18,6 +18,7 @@
 //            work items into slabs, summed in a fixed order (deterministic).
 #include "common.h"
 #include "gemm.h"
+#include "fft.h"
 #include "prof.h"
 
 namespace {
@@ -3551,6 +3552,12 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
 /* Spectrogram of DiscriminatorSTFT (msstftd.py:62-64, 97-99): x [B][C][T] -> z [B][2C][Fr][nb]
  * (channels re_0..re_{C-1}, im_0..im_{C-1}), Fr = (T - n)/hop + 1, nb = n/2 + 1, scaled by
  * 1/sqrt(sum w^2) (normalized=True). tables: the mel-table layout of n (encx_mel_tables_init). */
+// ENCX_FFT=0: the spectrogram as the framed DFT GEMM (round 3) instead of the real FFT (fft.h)
+static bool disc_fft(int64_t n) {
+    static const bool on = [] { const char* v = getenv("ENCX_FFT"); return !v || atoi(v) != 0; }();
+    return on && encx_fft::fft_ok(n);
+}
+
 int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B, int64_t C, int64_t T,
                        int64_t n_fft, int64_t hop, encx_stream_t stream) {
     ENCX_REQUIRE(x && tables && z && T >= n_fft && hop > 0);
@@ -3558,8 +3565,13 @@ int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B,
     const int Fr = (int)((T - n_fft) / hop + 1), nb = (int)(n_fft / 2 + 1);
     const float inv = (float)(1.0 / sqrt(3.0 * (double)n_fft / 8.0));  // sum of periodic hann^2 = 3n/8
     const int M = (int)(B * C * Fr), N = 2 * nb, K = (int)n_fft;
-    encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * (B * C * T + (int64_t)M * N), "spec_fwd");
+    const bool fft = disc_fft(n_fft);
+    encx_prof_scope ps(st, fft ? 2.5 * M * K * log2((double)K) : 2.0 * M * N * K, 4.0 * (B * C * T + (int64_t)M * N), "spec_fwd");
     ps.tag(" n%ld", (long)n_fft);
+    if (fft) {  // real FFT of each hann-windowed frame (fft.h), written in the (t, f) channel layout
+        encx_fft::FftArgs a{x, tables, N, z, (int)T, Fr, (int)hop, 0, M, 1, (int)C, inv};
+        return encx_fft::r2c(a, (int)n_fft, st);
+    }
     return gemm_launch(LdSpecD{x, tables, (int)T, Fr, (int)hop, N, make_fastdiv((uint32_t)Fr)}, EpSpecD{z, (int)C, Fr, nb, inv}, M, N, K, st);
 }
 
@@ -3577,9 +3589,17 @@ int encx_disc_spec_bwd(const float* dz, const float* tables, float* dx, float* w
     const float inv = (float)(1.0 / sqrt(3.0 * (double)n_fft / 8.0));
     const int M = (int)(B * C * Fr), N = (int)n_fft, K = 2 * nb;
     {
-        encx_prof_scope ps(st, 2.0 * M * N * K, 4.0 * ((int64_t)M * K + (int64_t)M * N), "spec_bwd");
+        const bool fft = disc_fft(n_fft);
+        encx_prof_scope ps(st, fft ? 2.5 * M * N * log2((double)N) : 2.0 * M * N * K,
+                           4.0 * ((int64_t)M * K + (int64_t)M * N), "spec_bwd");
         ps.tag(" n%ld", (long)n_fft);
-        int rc = gemm_launch(LdSpecDB{dz, tables, (int)C, Fr, nb, K, inv}, EpFrames{ws, N}, M, N, K, st);
+        int rc;
+        if (fft) {  // the transpose of the windowed real DFT per frame (fft.h c2r)
+            encx_fft::FftArgs a{dz, tables, K, ws, (int)T, Fr, (int)hop, 0, M, 1, (int)C, inv};
+            rc = encx_fft::c2r(a, (int)n_fft, st);
+        } else {
+            rc = gemm_launch(LdSpecDB{dz, tables, (int)C, Fr, nb, K, inv}, EpFrames{ws, N}, M, N, K, st);
+        }
         if (rc) return rc;
     }
     const int64_t tot = B * C * T;

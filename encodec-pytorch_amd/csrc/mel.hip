@@ -11,6 +11,7 @@
 #include "common.h"
 #include "prof.h"
 #include "gemm.h"
+#include "fft.h"
 
 namespace {
 
@@ -203,6 +204,23 @@ __global__ void overlap_add(const float* dframe, float* grad, int Bn, int T, int
     grad[i] += s;
 }
 
+// ENCX_FFT=0: the spectrogram as the framed DFT GEMM (round 3) instead of the real FFT (fft.h)
+static bool use_fft(int64_t n) {
+    static const bool on = [] { const char* v = getenv("ENCX_FFT"); return !v || atoi(v) != 0; }();
+    return on && encx_fft::fft_ok(n);
+}
+// spec [rows][2nb] (re | im) of the reflect-padded, hann-windowed frames of wav
+static int spec_rows(const float* wav, const float* bt, float* spec, int64_t B, int64_t T, int n, int h, int p,
+                     int F, hipStream_t st) {
+    const int nb2 = 2 * (n / 2 + 1);
+    if (use_fft(n)) {
+        encx_fft::FftArgs a{wav, bt, nb2, spec, (int)T, F, h, p, (int)(B * F), 0, 1, 1.f};
+        return encx_fft::r2c(a, n, st);
+    }
+    return gemm_launch(LdSpec{wav, bt, (int)T, F, h, p, nb2, make_fastdiv((uint32_t)F)}, EpStore{spec, nb2},
+                       (int)(B * F), nb2, n, st);
+}
+
 struct Geo {
     int n, h, p, nb, F, rows;
     int64_t spec, lmx, mely, dframe;  // workspace offsets (floats)
@@ -257,8 +275,7 @@ int encx_mel_logmel(const float* x, const float* tables, float* ws, float* out, 
     const float* bt = tables;
     const float* mt = tables + (int64_t)g.n * 2 * g.nb;
     const int nb2 = 2 * g.nb;
-    int rc = gemm_launch(LdSpec{x, bt, (int)T, g.F, g.h, g.p, nb2, make_fastdiv((uint32_t)g.F)}, EpStore{ws + g.spec, nb2}, g.rows,
-                         nb2, g.n, st);
+    int rc = spec_rows(x, bt, ws + g.spec, B, T, g.n, g.h, g.p, g.F, st);
     if (rc) return rc;
     return gemm_launch(LdMel{ws + g.spec, mt, g.nb, nm}, EpLogT{out, nm, g.F}, g.rows, nm, g.nb, st);
 }
@@ -268,7 +285,9 @@ int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws
                   encx_stream_t stream) {
     ENCX_REQUIRE(x && y && tables && ws && loss && B > 0 && n_fft >= 4 && (n_fft % 4) == 0);
     const double rows_ = (double)geo(B, T, n_fft, n_mels).rows, nb_ = (double)(n_fft / 2 + 1);
-    encx_prof_scope ps((hipStream_t)stream, 2.0 * rows_ * (2 * nb_ * n_fft * 2 + nb_ * n_mels * 2) + (grad ? 2.0 * rows_ * (nb_ * n_mels + 2 * nb_ * n_fft) : 0.0),
+    // algorithmic flops: the transforms at 5 n log2 n per real frame with the FFT (2 n (n + 2) as the DFT GEMM)
+    const double lg = log2((double)n_fft), dft = use_fft(n_fft) ? 2.5 * n_fft * lg : 2.0 * nb_ * n_fft * 2;
+    encx_prof_scope ps((hipStream_t)stream, rows_ * (2 * dft + 2.0 * nb_ * n_mels * 2) + (grad ? rows_ * (2.0 * nb_ * n_mels + dft) : 0.0),
                        4.0 * B * T * (grad ? 3 : 2), "mel_loss");
     hipStream_t st = (hipStream_t)stream;
     const int nm = (int)n_mels;
@@ -285,12 +304,12 @@ int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws
     const int nb2 = 2 * g.nb;
     int rc;
     // target: logmel(x)
-    rc = gemm_launch(LdSpec{x, bt, (int)T, g.F, g.h, g.p, nb2, make_fastdiv((uint32_t)g.F)}, EpStore{spec, nb2}, g.rows, nb2, g.n, st);
+    rc = spec_rows(x, bt, spec, B, T, g.n, g.h, g.p, g.F, st);
     if (rc) return rc;
     rc = gemm_launch(LdMel{spec, mt, g.nb, nm}, EpLog{lmx, nm}, g.rows, nm, g.nb, st);
     if (rc) return rc;
     // output: mel(y)
-    rc = gemm_launch(LdSpec{y, bt, (int)T, g.F, g.h, g.p, nb2, make_fastdiv((uint32_t)g.F)}, EpStore{spec, nb2}, g.rows, nb2, g.n, st);
+    rc = spec_rows(y, bt, spec, B, T, g.n, g.h, g.p, g.F, st);
     if (rc) return rc;
     rc = gemm_launch(LdMel{spec, mt, g.nb, nm}, EpStore{mely, nm}, g.rows, nm, g.nb, st);
     if (rc) return rc;
@@ -305,7 +324,12 @@ int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws
     if (!grad) return 0;
     rc = gemm_launch(LdDP{mely, mb, g.nb, nm}, EpG{spec, g.nb}, g.rows, g.nb, nm, st);
     if (rc) return rc;
-    rc = gemm_launch(LdDF{spec, bt, nb2}, EpStore{dframe, g.n}, g.rows, g.n, nb2, st);
+    if (use_fft(g.n)) {  // dframe = w * Re sum_k G_k e^{+i theta}: the real inverse transform
+        encx_fft::FftArgs fa{spec, bt, nb2, dframe, (int)T, g.F, g.h, g.p, g.rows, 0, 1, 1.f};
+        rc = encx_fft::c2r(fa, g.n, st);
+    } else {
+        rc = gemm_launch(LdDF{spec, bt, nb2}, EpStore{dframe, g.n}, g.rows, g.n, nb2, st);
+    }
     if (rc) return rc;
     hipLaunchKernelGGL(overlap_add, dim3(cdiv(B * T, 256)), dim3(256), 0, st, dframe, grad, (int)B,
                        (int)T, g.n, g.h, g.p, g.F);

@@ -47,7 +47,9 @@ ENCX_DEV uint64_t shfl_xor64(uint64_t v, int o) {
 // into Bs[d][code] (row stride 129: conflict-free transposed writes), so a workgroup does one
 // load phase, one barrier and 64 MFMA k-steps. 38 x 8 = 304 workgroups at N = 2400.
 constexpr int AR_ROWS = 64, AR_CODES = 128, AR_BS = AR_CODES + 1;
-constexpr int AR_PER = 8;  // staging loads in flight per thread
+constexpr int AR_PER = 8;    // staging loads in flight per thread (scalar code path)
+constexpr int AR_XPER = 32;  // frame-element loads in flight per thread
+constexpr int AR_EPER = 16;  // code quads in flight per thread
 
 __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed, uint64_t* keys,
                                                       int N, int D, int Kc) {
@@ -61,8 +63,9 @@ __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed
     const int n0 = blockIdx.x * AR_ROWS, k0 = blockIdx.y * AR_CODES;
     const int h = lane >> 5, l32 = lane & 31;
     const int wm0 = (wave >> 1) * 32, wn0 = (wave & 1) * 64;
-    // staging: AR_PER loads in flight per thread from clamped addresses, values selected after
-    // the load (a branch around each load serialises the latency: one round trip per element)
+    // staging: AR_XPER (frames) / AR_EPER (code quads) loads in flight per thread from clamped
+    // addresses, values selected after the load (a branch around each load serialises the
+    // latency: one round trip per element); at D = 128 each operand is ONE round of loads
     {
         const int r = tid & (AR_ROWS - 1), dq = tid / AR_ROWS, n = n0 + r;  // frame fixed per thread
         const bool okn = n < N;
@@ -70,21 +73,44 @@ __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed
         const int bb = nc / x.Tf, tt = nc - bb * x.Tf;
         const float* xp = x.p + bb * x.sB + tt * x.sT;
         constexpr int DSTEP = NT / AR_ROWS;
-        for (int d0 = 0; d0 < D; d0 += DSTEP * AR_PER) {
-            float v[AR_PER];
+        for (int d0 = 0; d0 < D; d0 += DSTEP * AR_XPER) {
+            float v[AR_XPER];
 #pragma unroll
-            for (int q = 0; q < AR_PER; ++q) {
+            for (int q = 0; q < AR_XPER; ++q) {
                 const int d = d0 + dq + DSTEP * q;
                 const float t = xp[(int64_t)(d < D ? d : D - 1) * x.sD];
                 v[q] = (okn && d < D) ? t : 0.f;
             }
 #pragma unroll
-            for (int q = 0; q < AR_PER; ++q) {
+            for (int q = 0; q < AR_XPER; ++q) {
                 const int d = d0 + dq + DSTEP * q;
                 if (d < D) As[d * AR_ROWS + r] = v[q];
             }
         }
     }
+    if ((D & 3) == 0) {  // codes as 16-byte quads along d, transposed into Bs[d][code]
+        const int D4 = D >> 2;
+        for (int i0 = 0; i0 < AR_CODES * D4; i0 += NT * AR_EPER) {
+            f32x4 v[AR_EPER];
+#pragma unroll
+            for (int q = 0; q < AR_EPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int c = i / D4, d4 = i - c * D4, k = k0 + c;
+                const bool ok = i < AR_CODES * D4 && k < Kc;
+                const f32x4 t = ld4u(embed + (ok ? (int64_t)k * D + 4 * d4 : 0));
+                v[q] = ok ? t : (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int q = 0; q < AR_EPER; ++q) {
+                const int i = i0 + q * NT + tid;
+                const int c = i / D4, d4 = i - c * D4;
+                if (i < AR_CODES * D4) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) Bs[(4 * d4 + e) * AR_BS + c] = v[q][e];
+                }
+            }
+        }
+    } else
     for (int i0 = 0; i0 < AR_CODES * D; i0 += NT * AR_PER) {
         float v[AR_PER];
 #pragma unroll

@@ -419,3 +419,31 @@ def test_fused_resblock_matches_unfused_block():
             os.environ.pop('ENCX_RESBLOCK', None)
     for a, b in zip(*outs):
         assert float((a - b).abs().max()) <= 2e-5 * float(b.abs().max()) + 1e-7, (float((a - b).abs().max()), float(b.abs().max()))
+
+
+@pytest.mark.parametrize('n', [32, 64, 128, 256, 512, 1024, 2048])
+def test_spectrogram_fft_vs_torch_fp64(n):
+    """The real-FFT spectrogram (csrc/fft.h, the discriminator's Spectrogram: hann window,
+    center=False, normalized, msstftd.py:62-64, 97-99) and its transpose, at every power-of-2
+    size the mel loss and the discriminator use, against torch.stft / autograd in fp64: relative
+    to each tensor's largest magnitude."""
+    from encx import ops
+    B, C, Tn = 2, 2, 6000
+    x64 = torch.from_numpy(synth_wave((B, C, Tn), n)).double().requires_grad_(True)
+    w = torch.hann_window(n, dtype=torch.float64)
+    st = torch.stft(x64.reshape(B * C, Tn), n_fft=n, hop_length=n // 4, window=w, center=False,
+                    return_complex=True) / w.pow(2).sum().sqrt()  # [BC][nb][Fr]
+    ref = torch.cat([st.real, st.imag], 0).reshape(2, B, C, n // 2 + 1, -1).permute(1, 0, 2, 4, 3)
+    ref = ref.reshape(B, 2 * C, -1, n // 2 + 1)  # [b][re c | im c][fr][k]
+    xg = x64.detach().float().to(DEV).requires_grad_(True)
+    z = ops.DiscSpecFn.apply(xg, n, n // 4, 24000)
+    dz = torch.randn(ref.shape, generator=torch.Generator().manual_seed(n), dtype=torch.float64)
+    gx, = torch.autograd.grad(z, [xg], dz.float().to(DEV))
+    gref, = torch.autograd.grad(ref, [x64], dz)
+
+    def rel(a, b):
+        a, b = a.detach().double().cpu(), b.detach().double()
+        return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+    ez, eg = rel(z, ref), rel(gx, gref)
+    print(f'n {n}: spectrogram {ez:.1e}, its transpose {eg:.1e}')
+    assert ez < 2e-6 and eg < 2e-6, (ez, eg)
