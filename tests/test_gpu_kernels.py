@@ -398,15 +398,16 @@ def test_fused_resblock_vs_torch_fp64(C, T, B):
     assert all(v < 1e-4 for v in errs.values()), errs
 
 
-def test_fused_resblock_matches_unfused_block():
-    """The SEANet block with the fused kernel vs the same block on the three separate conv kernels
+@pytest.mark.parametrize('C', [32, 64])
+def test_fused_resblock_matches_unfused_block(C):
+    """The SEANet block with the fused kernels vs the same block on the three separate conv kernels
     (ENCX_RESBLOCK=0): forward and every grad within fp32 rounding of each other."""
     import os
     from encx.modules.seanet import SEANetResnetBlock
     torch.manual_seed(3)
-    blk = SEANetResnetBlock(32, norm='weight_norm', causal=True, true_skip=False).to(DEV)
-    x0 = (0.5 * torch.randn(2, 32, 4800)).to(DEV)
-    dy = torch.randn(2, 32, 4800).to(DEV)
+    blk = SEANetResnetBlock(C, norm='weight_norm', causal=True, true_skip=False).to(DEV)
+    x0 = (0.5 * torch.randn(2, C, 4800)).to(DEV)
+    dy = torch.randn(2, C, 4800).to(DEV)
     outs = []
     for fused in ('1', '0'):
         os.environ['ENCX_RESBLOCK'] = fused
