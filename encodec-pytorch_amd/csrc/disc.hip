@@ -830,7 +830,7 @@ struct C2FwdR {
 // with 1.5x or 2.9x as many items as wave slots -- and neighbouring items still share an XCD's L2.
 ENCX_DEV int rw_first_slot(int wave) { return wave * (int)gridDim.x + xcd_linear_id(); }
 
-template <int KF, int S, int WQ, int NWV, bool APF>
+template <int KF, int S, int WQ, int NWV, bool APF, bool GP = false>
 __global__ __launch_bounds__(NWV * 64) void c2_fwd_rw_kernel(C2FwdR a) {
     constexpr int NE = 4 * WQ, KT = 3;  // window elements per lane; kernel rows (host-checked)
     extern __shared__ float smem[];
@@ -892,6 +892,9 @@ __global__ __launch_bounds__(NWV * 64) void c2_fwd_rw_kernel(C2FwdR a) {
         };
         load(wb[0], 0, 0);
         load_a(ab[0], 0, 0);
+        // GP: each tap's weight read one tap ahead (across steps too), pinned by a scheduling
+        // barrier so the tap's MFMAs never wait on the LDS read that feeds them
+        float gnx = GP ? wcol(0, 0)[0] : 0.f;
         for (int c = 0; c < CP; ++c) {
 #pragma unroll
             for (int kt = 0; kt < KT; ++kt) {
@@ -911,9 +914,17 @@ __global__ __launch_bounds__(NWV * 64) void c2_fwd_rw_kernel(C2FwdR a) {
                     }
                 }
                 const float* wk = wcol(c, kt);
+                const float* wkn = wcol(nc, nk);
 #pragma unroll
                 for (int kf = 0; kf < KF; ++kf) {
-                    const float av = APF ? ab[kt][APF ? kf : 0] : wk[kf * 32];
+                    float av;
+                    if (GP) {
+                        av = gnx;
+                        gnx = kf + 1 < KF ? wk[(kf + 1) * 32] : wkn[0];
+                        __builtin_amdgcn_sched_barrier(0);
+                    } else {
+                        av = APF ? ab[kt][APF ? kf : 0] : wk[kf * 32];
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int r = S * j + kf;
@@ -1411,10 +1422,12 @@ struct C2DgR {
     int U4;     // quads per polyphase row
     int tiles;  // ceil(B * T2 * U4 / 32)
 };
-template <int J, int S, int RT, int WQ, bool YM, int NWV, int TM, bool APF, bool SB = true>
+template <int J, int S, int RT, int WQ, bool YM, int NWV, int TM, bool APF, bool SB = true, bool GP = false>
 __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
     // RT row tiles of 32 (M = Ci*S = 32 RT); a work item is (column tile, TM row tiles); APF:
-    // the weight columns of step s + 1 are read from LDS during step s (else just in time)
+    // the weight columns of step s + 1 are read from LDS during step s (else just in time); GP:
+    // each tap's weight column is read one tap ahead (across steps too), pinned there by a
+    // scheduling barrier, so the MFMAs of tap q never wait on the LDS read that feeds them
     constexpr int NE = 4 * WQ, KT = 3, M = 32 * RT, RG = RT / TM;
     const C2Dg& a = R.d;
     extern __shared__ float smem[];
@@ -1477,6 +1490,9 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){0};
         load(0, 0, 0);
+        float gnx[TM];  // GP: the next tap's weight column
+#pragma unroll
+        for (int i = 0; i < TM; ++i) gnx[i] = GP ? acol(0, 0)[i * 32] : 0.f;
         for (int c0 = 0; c0 < CP; c0 += 2) {
 #pragma unroll
             for (int u = 0; u < 2 * KT; ++u) {
@@ -1508,11 +1524,22 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
                     }
                 }
                 const float* ak = acol(c, kt);
+                const float* akn = acol(nc, nu % KT);
 #pragma unroll
                 for (int q = 0; q < J; ++q) {
                     float av[TM];
+                    if (GP) {
+                        const float* src = q + 1 < J ? ak + (q + 1) * M : akn;
 #pragma unroll
-                    for (int i = 0; i < TM; ++i) av[i] = APF ? ab[k][APF ? q * TM + i : 0] : ak[q * M + i * 32];
+                        for (int i = 0; i < TM; ++i) {
+                            av[i] = gnx[i];
+                            gnx[i] = src[i * 32];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < TM; ++i) av[i] = APF ? ab[k][APF ? q * TM + i : 0] : ak[q * M + i * 32];
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int r = j - q + J - 1;  // window element of column u0 + j, tap q
@@ -2979,7 +3006,7 @@ static bool dgr_ok(const C2Geo& g) {
     const int J = (g.KF + g.sf - 1) / g.sf;
     return (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float) <= 150 * 1024;
 }
-template <int NWV, int TM, bool APF, bool SB = true>
+template <int NWV, int TM, bool APF, bool SB = true, bool GP = false>
 static int run_dgrad_rw_n(const C2Dg& d, int wgs, hipStream_t st) {
     const C2Geo& g = d.g;
     C2DgR R{d, 0, 0};
@@ -2992,11 +3019,11 @@ static int run_dgrad_rw_n(const C2Dg& d, int wgs, hipStream_t st) {
     const int grid = (int)min((int64_t)wgs, cdiv((int64_t)R.tiles * rg, NWV));
     const bool ym = d.yact != nullptr;
     if (g.KF == 9) {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, TM, APF, SB>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, TM, APF, SB>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, TM, APF, SB, GP>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, TM, APF, SB, GP>), dim3(grid), dim3(NWV * 64), lds, st, R);
     } else {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV, 1, APF, SB>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV, 1, APF, SB>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV, 1, APF, SB, GP>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV, 1, APF, SB, GP>), dim3(grid), dim3(NWV * 64), lds, st, R);
     }
     ENCX_CHECK_LAUNCH();
     return 0;
@@ -3004,10 +3031,12 @@ static int run_dgrad_rw_n(const C2Dg& d, int wgs, hipStream_t st) {
 // variant: 0 = 8 waves, both row tiles per item, weights just in time; 1 = 8 waves, one row tile
 // per item, weights prefetched; 2 = 12 waves, one row tile, prefetched; 3 = 8 waves, one row tile,
 // just in time; 4 = variant 0 without the scheduling barrier (the window loads sink to the end
-// of the step: the round-3 kernel, for A/B)
+// of the step: the round-3 kernel, for A/B); 5 = variant 0 with the weight columns read one tap
+// ahead (GP)
 static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st, int variant = 0) {
     if (!dgr_ok(d.g)) return ENCX_EINVAL;
     switch (variant) {
+        case 5: return run_dgrad_rw_n<8, 2, false, true, true>(d, wgs, st);
         case 4: return run_dgrad_rw_n<8, 2, false, false>(d, wgs, st);
         case 1: return run_dgrad_rw_n<8, 1, true>(d, wgs, st);
         case 2: return run_dgrad_rw_n<12, 1, true>(d, wgs, st);
@@ -3025,7 +3054,7 @@ static bool fwr_ok(const C2Geo& g) {
     if (!((g.KF == 9 && (g.sf == 2 || g.sf == 1)) || (g.KF == 3 && g.sf == 1))) return false;
     return (size_t)g.Ci * g.KT * g.KF * 32 * sizeof(float) <= 128 * 1024;
 }
-template <int NWV, bool APF>
+template <int NWV, bool APF, bool GP = false>
 static int run_fwd_rw_n(const C2Fwd& f, int wgs, hipStream_t st) {
     const C2Geo& g = f.g;
     C2FwdR a{g, f.x, f.wf, f.bias, f.y, f.act, (int)cdiv(g.Fo, 4), 0};
@@ -3033,18 +3062,20 @@ static int run_fwd_rw_n(const C2Fwd& f, int wgs, hipStream_t st) {
     const size_t lds = ((size_t)g.Ci * g.KT * g.KF * 32 + 32) * sizeof(float);
     const int grid = (int)min((int64_t)wgs, cdiv(a.tiles, NWV));
     if (g.KF == 9 && g.sf == 2)
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 2, 4, NWV, APF>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 2, 4, NWV, APF, GP>), dim3(grid), dim3(NWV * 64), lds, st, a);
     else if (g.KF == 9)
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 1, 3, NWV, APF>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 1, 3, NWV, APF, GP>), dim3(grid), dim3(NWV * 64), lds, st, a);
     else
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<3, 1, 2, NWV, APF>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<3, 1, 2, NWV, APF, GP>), dim3(grid), dim3(NWV * 64), lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
 // wgs: workgroups (one per CU holds the layer's weights); variant: 0 = 8 waves, weights just in
-// time from LDS; 1 = 8 waves, weights prefetched a step ahead
+// time from LDS; 1 = 8 waves, weights prefetched a step ahead; 2 = 8 waves, weights read one tap
+// ahead (GP)
 static int run_fwd_rw(const C2Fwd& f, int wgs, hipStream_t st, int variant = 0) {
     if (!fwr_ok(f.g)) return ENCX_EINVAL;
+    if (variant == 2) return run_fwd_rw_n<8, false, true>(f, wgs, st);
     return variant == 1 ? run_fwd_rw_n<8, true>(f, wgs, st) : run_fwd_rw_n<8, false>(f, wgs, st);
 }
 template <int BN, int KFC, int MQ, int CKM, int OCC = 1>
@@ -3340,9 +3371,11 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
     // register-window form (c2_fwd_rw_kernel); ENCX_FWR = workgroups (0: off)
     static const int fw_wgs = [] { const char* v = getenv("ENCX_FWR"); return v ? atoi(v) : 256; }();
+    // ENCX_FWR_VARIANT: run_fwd_rw's kernel variant (A/B; default 0)
+    static const int fw_var = [] { const char* v = getenv("ENCX_FWR_VARIANT"); return v ? atoi(v) : 0; }();
     if (fw_wgs > 0 && fwr_ok(g) &&
         ((Ci * KT < 16 && g_c2_select != 2) || rw_pays(cdiv(B * T2 * cdiv(Fo, 4), 32), B * T2 * Fo, 87.0 / 66.0)) &&
-        run_fwd_rw(a, fw_wgs, st) == 0)
+        run_fwd_rw(a, fw_wgs, st, fw_var) == 0)
         return 0;
     if (Co == 1 && KT == 3 && KF == 3 && (sf == 1 || sf == 2)) {
         dim3 grid((unsigned)cdiv(T2 * Fo, 64), (unsigned)B);

@@ -91,7 +91,7 @@ ENCX_DEV float bload(rsrc_t r, int voff, int soff) {
 // ------------------------------------------------------------------------------------ forward
 // Wave (strip s = wv & 3, group g = wv >> 2): positions 16 s .. 16 s + 15 of the tile, h columns
 // g * HD / CG .., y columns g * C / CG ..
-template <int C>
+template <int C, bool PF>
 __global__ __launch_bounds__(Rb<C>::NT) void rb_fwd_kernel(RbArgs a) {
     constexpr int HD = C / 2, CG = Rb<C>::CG, NT = Rb<C>::NT, N1 = HD / 16 / CG, N2 = C / 16 / CG;
     extern __shared__ float sm[];
@@ -133,21 +133,32 @@ __global__ __launch_bounds__(Rb<C>::NT) void rb_fwd_kernel(RbArgs a) {
         for (int u = 0; u < PR; ++u) pf[u] = bload(rx, vo, u * NW * T * 4);
         if (tid < 2 * C) pfh = bload(rx, (hc * T + reflect_clamp(t0 - 2 + hp, T)) * 4, 0);
     };
-    if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
+    if (PF && (int)blockIdx.x < ntiles) fetch(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int b = tile / a.NT, t0 = (tile - b * a.NT) * TT;
         __syncthreads();  // the previous tile's LDS reads are done
+        if (PF) {
 #pragma unroll
-        for (int u = 0; u < PR; ++u) {
-            xs[(wv + NW * u) * XF + lane] = pf[u];
-            es[(wv + NW * u) * XF + lane] = elu(pf[u]);
-        }
-        if (tid < 2 * C) {
-            xs[hc * XF + hp] = pfh;
-            es[hc * XF + hp] = elu(pfh);
+            for (int u = 0; u < PR; ++u) {
+                xs[(wv + NW * u) * XF + lane] = pf[u];
+                es[(wv + NW * u) * XF + lane] = elu(pf[u]);
+            }
+            if (tid < 2 * C) {
+                xs[hc * XF + hp] = pfh;
+                es[hc * XF + hp] = elu(pfh);
+            }
+        } else {  // staged just in time
+            const float* xb = a.x + (int64_t)b * C * T;
+#pragma unroll 4
+            for (int i = tid; i < C * HALO; i += NT) {
+                const int c = i / HALO, p = i - c * HALO;
+                const float v = xb[(int64_t)c * T + reflect_clamp(t0 - 2 + p, T)];  // past T: unused
+                xs[c * XF + p] = v;
+                es[c * XF + p] = elu(v);
+            }
         }
         __syncthreads();
-        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
+        if (PF && tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
         // h^T[m][j] = b1[j] + sum_{c,k} ELU(x)[c][t - 2 + k] W1[c][k][j]   (rows = positions)
         f32x4v acc1[N1];
 #pragma unroll
@@ -202,7 +213,7 @@ __global__ __launch_bounds__(Rb<C>::NT) void rb_fwd_kernel(RbArgs a) {
 // Wave (strip, group) as in the forward: dh columns g * HD / CG .., dx columns g * C / CG ..
 // The right-halo dh (positions TT, TT + 1, read by the k3 transpose of the last positions) on
 // the vector ALU: TPO threads per (j, p), C / TPO terms each, summed by lane shuffles.
-template <int C>
+template <int C, bool PF>
 __global__ __launch_bounds__(Rb<C>::NT) void rb_dgrad_kernel(RbArgs a) {
     constexpr int HD = C / 2, CG = Rb<C>::CG, NT = Rb<C>::NT, NH = HD / 16 / CG, NX = C / 16 / CG;
     constexpr int TPO = NT / (2 * HD), U = C / TPO;
@@ -263,22 +274,42 @@ __global__ __launch_bounds__(Rb<C>::NT) void rb_dgrad_kernel(RbArgs a) {
         const int th = t0 + hp;
         hh = a.h[((int64_t)b * HD + hj) * T + (th < T ? th : T - 1)];
     };
-    if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
+    if (PF && (int)blockIdx.x < ntiles) fetch(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int b = tile / a.NT, t0 = (tile - b * a.NT) * TT;
         __syncthreads();
+        if (PF) {
 #pragma unroll
-        for (int u = 0; u < PR; ++u) dys[(wv + NW * u) * XF + lane] = pf[u];
-        if (tid < 2 * C) dys[hc * XF + hpp] = pfh;
+            for (int u = 0; u < PR; ++u) dys[(wv + NW * u) * XF + lane] = pf[u];
+            if (tid < 2 * C) dys[hc * XF + hpp] = pfh;
+        } else {  // staged just in time
+            const float* dyb = a.dy + (int64_t)b * C * T;
+#pragma unroll 4
+            for (int i = tid; i < C * HALO; i += NT) {
+                const int c = i / HALO, p = i - c * HALO, t = t0 + p;
+                const float v = dyb[(int64_t)c * T + (t < T ? t : T - 1)];
+                dys[c * XF + p] = t < T ? v : 0.f;
+            }
+        }
         __syncthreads();
-        f32x4v hcur[NH], xcur[NX];
-#pragma unroll
-        for (int n = 0; n < NH; ++n) hcur[n] = hv[n];
-#pragma unroll
-        for (int n = 0; n < NX; ++n) xcur[n] = xv[n];
-        const float hhcur = hh;
-        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
         const int tq = t0 + m0 + 4 * lk;
+        f32x4v hcur[NH], xcur[NX];
+        float hhcur;
+        if (PF) {
+#pragma unroll
+            for (int n = 0; n < NH; ++n) hcur[n] = hv[n];
+#pragma unroll
+            for (int n = 0; n < NX; ++n) xcur[n] = xv[n];
+            hhcur = hh;
+            if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
+        } else {
+#pragma unroll
+            for (int n = 0; n < NH; ++n) hcur[n] = ld4(a.h + ((int64_t)b * HD + (g * NH + n) * 16 + lc) * T, tq, T);
+#pragma unroll
+            for (int n = 0; n < NX; ++n) xcur[n] = ld4(a.x + ((int64_t)b * C + (g * NX + n) * 16 + lc) * T, tq, T);
+            const int th = t0 + hp;
+            hhcur = a.h[((int64_t)b * HD + hj) * T + (th < T ? th : T - 1)];
+        }
         // ---- dh^T[p][j] = ELU'(h) * sum_o dy[o][p] W2[j][o] for p < TT ...
         {
             f32x4v acc[NH];
@@ -382,7 +413,7 @@ ENCX_DEV void wgemm(const float* ap, const WTile* t, f32x16* acc) {
 // (dWs, dW2); w2 / w3: A = dh x ELU(x) rows {0-31, 32-63} at taps {0, 0, 1} / {1, 2, 2} (dW1).
 // C = 32 -- w0: A = dy x {x, ELU(h)}; w1..w3: A = dh x ELU(x) at tap w - 1 (16-row operands
 // read twice, the duplicate rows / columns of the tile dropped at the store).
-template <int C>
+template <int C, bool PF>
 __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
     constexpr int HD = C / 2, NTL = C == 64 ? 3 : 2;
     extern __shared__ float sm[];
@@ -435,9 +466,10 @@ __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
     // x (reflect) as rows wv + 4 u at positions lane; x's last two halo columns by threads < 2 C
     constexpr int PD = C / 4, PH = HD / 4;
     float pd[PD], pdh[PH], ph[PH], px[PD], pxh = 0.f;
-    float bacc[PD + PH];  // this lane's partial bias sums: dy rows wv + 4 u, then dh rows
+    float bacc[PD + PH];  // PF: this lane's partial bias sums: dy rows wv + 4 u, then dh rows
 #pragma unroll
     for (int u = 0; u < PD + PH; ++u) bacc[u] = 0.f;
+    float bsum = 0.f;     // else: tid < C: sum of dy[o = tid]; C <= tid < C + HD: sum of dh[j = tid - C]
     const int hc = tid >> 1, hp = TT + (tid & 1);
     auto fetch = [&](int tile) {
         const int b = tile / a.NT, t0 = (tile - b * a.NT) * TT, t = t0 + lane;
@@ -460,30 +492,65 @@ __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
         }
         if (tid < 2 * C) pxh = bload(rx, (hc * T + reflect_clamp(t0 - 2 + hp, T)) * 4, 0);
     };
-    if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
+    if (PF && (int)blockIdx.x < ntiles) fetch(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         __syncthreads();
+        if (PF) {
 #pragma unroll
-        for (int u = 0; u < PD; ++u) {
-            dys[(wv + 4 * u) * XW + lane] = pd[u];
-            xs[(wv + 4 * u) * XW + lane] = px[u];
-            exs[(wv + 4 * u) * XW + lane] = elu(px[u]);
-            bacc[u] += pd[u];
-        }
+            for (int u = 0; u < PD; ++u) {
+                dys[(wv + 4 * u) * XW + lane] = pd[u];
+                xs[(wv + 4 * u) * XW + lane] = px[u];
+                exs[(wv + 4 * u) * XW + lane] = elu(px[u]);
+                bacc[u] += pd[u];
+            }
 #pragma unroll
-        for (int u = 0; u < PH; ++u) {
-            dhs[(wv + 4 * u) * XW + lane] = pdh[u];
-            hes[(wv + 4 * u) * XW + lane] = elu(ph[u]);
-            bacc[PD + u] += pdh[u];
-        }
-        if (tid < 2 * C) {
-            xs[hc * XW + hp] = pxh;
-            exs[hc * XW + hp] = elu(pxh);
+            for (int u = 0; u < PH; ++u) {
+                dhs[(wv + 4 * u) * XW + lane] = pdh[u];
+                hes[(wv + 4 * u) * XW + lane] = elu(ph[u]);
+                bacc[PD + u] += pdh[u];
+            }
+            if (tid < 2 * C) {
+                xs[hc * XW + hp] = pxh;
+                exs[hc * XW + hp] = elu(pxh);
+            }
+        } else {  // staged just in time
+            const int b = tile / a.NT, t0 = (tile - b * a.NT) * TT;
+            const float* dyb = a.dy + (int64_t)b * C * T;
+            const float* dhb = a.dh + (int64_t)b * HD * T;
+            const float* hb = a.h + (int64_t)b * HD * T;
+            const float* xb = a.x + (int64_t)b * C * T;
+#pragma unroll 4
+            for (int i = tid; i < C * TT; i += 256) {
+                const int c = i / TT, q = i - c * TT, t = t0 + q;
+                const float v = dyb[(int64_t)c * T + (t < T ? t : T - 1)];
+                dys[c * XW + q] = t < T ? v : 0.f;
+            }
+#pragma unroll 4
+            for (int i = tid; i < HD * TT; i += 256) {
+                const int j = i / TT, q = i - j * TT, t = t0 + q, tc = t < T ? t : T - 1;
+                const float d = dhb[(int64_t)j * T + tc], hv = hb[(int64_t)j * T + tc];
+                dhs[j * XW + q] = t < T ? d : 0.f;
+                hes[j * XW + q] = elu(hv);
+            }
+#pragma unroll 4
+            for (int i = tid; i < C * HALO; i += 256) {
+                const int c = i / HALO, p = i - c * HALO;
+                const float v = xb[(int64_t)c * T + reflect_clamp(t0 - 2 + p, T)];
+                xs[c * XW + p] = v;
+                exs[c * XW + p] = elu(v);
+            }
         }
         __syncthreads();
-        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
+        if (PF && tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
         if (C == 64 || ntl == NTL) wgemm<NTL>(ap, tl, acc);
         else wgemm<1>(ap, tl, acc);
+        if (!PF) {  // bias sums from the staged tile: thread o < C sums dy[o], C <= tid < C + HD dh[tid - C]
+            if (tid < C) {
+                for (int q = 0; q < TT; ++q) bsum += dys[tid * XW + q];
+            } else if (tid < C + HD) {
+                for (int q = 0; q < TT; ++q) bsum += dhs[(tid - C) * XW + q];
+            }
+        }
     }
     // ---- this workgroup's partial weight grads -> slab [dWs C x C][dW2 C x HD][dW1 HD x C x 3][db C][db1 HD]
     // (natural layouts: dWs[o][c], dW2[o][j], dW1[j][c][k])
@@ -503,10 +570,14 @@ __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
             }
         }
     }
+    if (PF) {
 #pragma unroll
-    for (int u = 0; u < PD + PH; ++u) {  // db rows wv + 4 u, then db1 rows wv + 4 u
-        const float v = wave_sum(bacc[u]);
-        if (lane == 0) sl[C * C + C * HD + HD * 3 * C + (u < PD ? wv + 4 * u : C + wv + 4 * (u - PD))] = v;
+        for (int u = 0; u < PD + PH; ++u) {  // db rows wv + 4 u, then db1 rows wv + 4 u
+            const float v = wave_sum(bacc[u]);
+            if (lane == 0) sl[C * C + C * HD + HD * 3 * C + (u < PD ? wv + 4 * u : C + wv + 4 * (u - PD))] = v;
+        }
+    } else if (tid < C + HD) {
+        sl[C * C + C * HD + HD * 3 * C + tid] = bsum;
     }
 }
 
@@ -566,25 +637,41 @@ int rb_grid(K kernel, int threads, size_t lds, int64_t tiles) {
 }
 bool rb_ok(int64_t C, int64_t T) { return (C == 32 || C == 64) && T >= 3; }
 
-template <int C>
-int rb_wgrad_grid(int64_t tiles) {
-    static int g = 0;  // cached (the workspace size must not move between the size query and the launch)
-    if (!g) g = rb_grid(rb_wgrad_kernel<C>, 256, rb_wgrad_lds(C), (int64_t)1 << 40);
-    return (int)(tiles < g ? tiles : g);
+// ENCX_RB_PREFETCH=1: each next tile staged in registers (buffer loads) while the current one
+// computes; default: staged just in time
+bool rb_prefetch() {
+    static const int v = [] { const char* e = getenv("ENCX_RB_PREFETCH"); return e ? atoi(e) : 0; }();
+    return v != 0;
 }
 
 template <int C>
+int rb_wgrad_grid(int64_t tiles) {
+    static int g = 0;  // cached (the workspace size must not move between the size query and the launch)
+    if (!g) g = rb_prefetch() ? rb_grid(rb_wgrad_kernel<C, true>, 256, rb_wgrad_lds(C), (int64_t)1 << 40)
+                              : rb_grid(rb_wgrad_kernel<C, false>, 256, rb_wgrad_lds(C), (int64_t)1 << 40);
+    return (int)(tiles < g ? tiles : g);
+}
+
+template <int C, bool PF>
 void launch_bwd(const RbArgs& a, float* dws, float* dw2, float* dw1, float* db2, float* dbs, float* db1, int acc_w,
                 int acc_b, hipStream_t st) {
     const int64_t tiles = (int64_t)a.B * a.NT;
     static int gd = 0;
-    if (!gd) gd = rb_grid(rb_dgrad_kernel<C>, Rb<C>::NT, rb_dgrad_lds(C), (int64_t)1 << 40);
-    hipLaunchKernelGGL(rb_dgrad_kernel<C>, dim3((unsigned)(tiles < gd ? tiles : gd)), dim3(Rb<C>::NT),
+    if (!gd) gd = rb_grid(rb_dgrad_kernel<C, PF>, Rb<C>::NT, rb_dgrad_lds(C), (int64_t)1 << 40);
+    hipLaunchKernelGGL((rb_dgrad_kernel<C, PF>), dim3((unsigned)(tiles < gd ? tiles : gd)), dim3(Rb<C>::NT),
                        rb_dgrad_lds(C), st, a);
     const int gw = rb_wgrad_grid<C>(tiles);
-    hipLaunchKernelGGL(rb_wgrad_kernel<C>, dim3(gw), dim3(256), rb_wgrad_lds(C), st, a);
+    hipLaunchKernelGGL((rb_wgrad_kernel<C, PF>), dim3(gw), dim3(256), rb_wgrad_lds(C), st, a);
     hipLaunchKernelGGL(rb_wgrad_reduce<C>, dim3((unsigned)cdiv(Rb<C>::SLAB, 64)), dim3(256), 0, st, a.slab, gw, dws,
                        dw2, dw1, db2, dbs, db1, acc_w, acc_b);
+}
+
+template <int C, bool PF>
+void launch_fwd(const RbArgs& a, int64_t tiles, hipStream_t st) {
+    static int g = 0;
+    if (!g) g = rb_grid(rb_fwd_kernel<C, PF>, Rb<C>::NT, rb_fwd_lds(C), (int64_t)1 << 40);
+    hipLaunchKernelGGL((rb_fwd_kernel<C, PF>), dim3((unsigned)(tiles < g ? tiles : g)), dim3(Rb<C>::NT), rb_fwd_lds(C),
+                       st, a);
 }
 
 }  // namespace
@@ -602,15 +689,11 @@ int encx_resblock_fwd(const float* x, const float* w1, const float* b1, const fl
     RbArgs a{x, w1, b1, w2, b2, ws, bs, h, y, nullptr, nullptr, nullptr, nullptr, (int)B, (int)T, (int)cdiv(T, TT)};
     const int64_t tiles = B * a.NT;
     if (C == 32) {
-        static int g = 0;
-        if (!g) g = rb_grid(rb_fwd_kernel<32>, Rb<32>::NT, rb_fwd_lds(32), (int64_t)1 << 40);
-        hipLaunchKernelGGL(rb_fwd_kernel<32>, dim3((unsigned)(tiles < g ? tiles : g)), dim3(Rb<32>::NT),
-                           rb_fwd_lds(32), st, a);
+        if (rb_prefetch()) launch_fwd<32, true>(a, tiles, st);
+        else launch_fwd<32, false>(a, tiles, st);
     } else {
-        static int g = 0;
-        if (!g) g = rb_grid(rb_fwd_kernel<64>, Rb<64>::NT, rb_fwd_lds(64), (int64_t)1 << 40);
-        hipLaunchKernelGGL(rb_fwd_kernel<64>, dim3((unsigned)(tiles < g ? tiles : g)), dim3(Rb<64>::NT),
-                           rb_fwd_lds(64), st, a);
+        if (rb_prefetch()) launch_fwd<64, true>(a, tiles, st);
+        else launch_fwd<64, false>(a, tiles, st);
     }
     ENCX_CHECK_LAUNCH();
     return 0;
@@ -638,8 +721,14 @@ int encx_resblock_bwd(const float* dy, const float* x, const float* h, const flo
     float* slab = wsp + (size_t)B * HD * T;
     RbArgs a{x, w1, nullptr, w2, nullptr, ws, nullptr, const_cast<float*>(h), nullptr, dy, dx, dh, slab, (int)B, (int)T,
              (int)cdiv(T, TT)};
-    if (C == 32) launch_bwd<32>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
-    else launch_bwd<64>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
+    const bool pf = rb_prefetch();
+    if (C == 32) {
+        if (pf) launch_bwd<32, true>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
+        else launch_bwd<32, false>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
+    } else {
+        if (pf) launch_bwd<64, true>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
+        else launch_bwd<64, false>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
+    }
     ENCX_CHECK_LAUNCH();
     return 0;
 }
