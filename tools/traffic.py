@@ -19,8 +19,10 @@ import json
 import re
 
 # kernels launched by the conv / convtr / conv2d ABI entry points (csrc/conv1d.hip, disc.hip)
+# (csrc/resblock.hip's fused residual-block kernels are conv ABI calls too: encx_resblock_*)
 FAMILY = re.compile(r'conv_fwd_kernel|pw_kernel|pw_wgrad_kernel|conv_poly_kernel|conv_wgrad|wgrad_reduce|conv_fwd_reduce|'
-                    r'conv_poly_reduce|conv_fold_edges|LdConvFlat|LdPolyFlat|c2_')
+                    r'conv_poly_reduce|conv_fold_edges|LdConvFlat|LdPolyFlat|c2_|rb_fwd_kernel|rb_bwd_kernel|'
+                    r'rb_dgrad_kernel|rb_wgrad_kernel|rb_wgrad_reduce')
 
 
 def per_dispatch(d, counter):
