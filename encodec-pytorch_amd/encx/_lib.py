@@ -60,6 +60,26 @@ def parse_header(path=HEADER):
     return out
 
 
+def check_build_id(lib):
+    """Refuse a library built from other sources than the ones beside it (buildid.py). An A/B
+    build picked with ENCX_LIB is an experiment: a mismatch there only warns."""
+    import sys
+    sys.path.insert(0, os.path.dirname(_HERE))
+    try:
+        from buildid import build_id
+    finally:
+        sys.path.pop(0)
+    want, have = build_id(), lib.encx_build_id().decode()
+    if want == have:
+        return
+    msg = (f'encx: {LIB_PATH} was built from other sources (build id {have}, sources {want}); '
+           'rebuild with `make -C encodec-pytorch_amd`')
+    if 'ENCX_LIB' in os.environ:
+        print('warning: ' + msg, file=sys.stderr)
+        return
+    raise RuntimeError(msg)
+
+
 class _Lib:
     def __init__(self):
         self._lib = None
@@ -76,6 +96,7 @@ class _Lib:
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            check_build_id(lib)
             self._lib = lib
         return self._lib
 

@@ -36,6 +36,9 @@ typedef struct ihipStream_t* encx_stream_t; /* == hipStream_t */
 
 /* ---------------------------------------------------------------- library */
 int encx_version(void);
+/* Hash of the sources this library was built from (encodec-pytorch_amd/buildid.py); the
+ * Python binding refuses a library whose hash differs from the sources beside it. */
+const char* encx_build_id(void);
 const char* encx_strerror(int code);
 /* Select the device; cheap, idempotent. */
 int encx_init(int device);

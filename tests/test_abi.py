@@ -28,6 +28,26 @@ def test_library_exports_every_header_symbol():
     assert len(sigs) >= 40
 
 
+def test_library_build_id_matches_sources():
+    """The library carries the hash of the sources it was built from; a stale library is
+    refused at load (encx._lib.check_build_id)."""
+    from encx import _lib as L
+    from buildid import build_id
+    lib = _lib()
+    assert lib.encx_build_id().decode() == build_id()
+
+    class Stale:
+        def encx_build_id(self):
+            return b'0' * 32
+    env = os.environ.pop('ENCX_LIB', None)
+    try:
+        with pytest.raises(RuntimeError, match='built from other sources'):
+            L.check_build_id(Stale())
+    finally:
+        if env is not None:
+            os.environ['ENCX_LIB'] = env
+
+
 def test_host_only_queries():
     lib = _lib()
     assert lib.encx_version() == 1
