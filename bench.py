@@ -11,7 +11,8 @@ l_t / l_f / l_g / l_feat through the Balancer, commit loss, Adam, then the discr
 resident in HBM before the timed region. Rank 0 prints one JSON line.
 
 Steps replay HIP graphs at N = 1 (encx.train.Trainer(graphs=True): the step captured once
-after one eager step); at N > 1 the steps run eagerly (Trainer.step); --no-graphs steps eagerly.
+after one eager step); at N > 1 the steps run eagerly (Trainer.step; ENCX_DP_GRAPHS=1 replays one
+graph per segment between the collectives, opt-in: DESIGN.md §6); --no-graphs steps eagerly.
 The warmup covers the eager step and the capture. The roofline / whole-step books come from a
 second, untimed, profiled pass of K eager steps (identical kernels).
 """

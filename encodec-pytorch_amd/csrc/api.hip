@@ -1,6 +1,7 @@
 // Library entry points: version, error strings, device selection, launch profiling.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -25,7 +26,41 @@ struct ProfState {
 };
 ProfState g_prof;
 std::atomic<bool> g_prof_on{false};
+
+// kernel-selection options (common.h EncxOpt): name, default; initial value from ENCX_<name>
+struct OptDef {
+    const char* name;
+    int64_t def;
+};
+constexpr OptDef kOpts[OPT_COUNT] = {
+    {"FFT", 1}, {"PW", 1}, {"PW_WG_TMAX", 12000}, {"LSTM_FUSE", 0}, {"RB_PREFETCH", 0}, {"FWR", 256},
+    {"FWR_VARIANT", 0}, {"DGR", 256}, {"DGR_VARIANT", 0}, {"WGR", 2048}, {"WGR_WGS", 256},
+};
+std::atomic<int64_t> g_opt[OPT_COUNT];
+std::once_flag g_opt_once;
+void opt_init() {
+    std::call_once(g_opt_once, [] {
+        for (int i = 0; i < OPT_COUNT; ++i) {
+            char env[64];
+            snprintf(env, sizeof(env), "ENCX_%s", kOpts[i].name);
+            const char* v = getenv(env);
+            g_opt[i].store(v ? atoll(v) : kOpts[i].def);
+        }
+    });
+}
+int opt_find(const char* name) {
+    if (!name) return -1;
+    if (!strncmp(name, "ENCX_", 5)) name += 5;
+    for (int i = 0; i < OPT_COUNT; ++i)
+        if (!strcmp(name, kOpts[i].name)) return i;
+    return -1;
+}
 }  // namespace
+
+int64_t encx_opt(EncxOpt id) {
+    opt_init();
+    return g_opt[id].load(std::memory_order_relaxed);
+}
 
 encx_prof_scope::encx_prof_scope(hipStream_t s, double f, double b, const char* kind, bool timed)
     : st(s), slot(-1) {
@@ -62,6 +97,26 @@ const char* encx_strerror(int code) {
     if (code == ENCX_OK) return "ok";
     if (code == ENCX_EINVAL) return "encx: invalid argument (shape, stride or null pointer)";
     return hipGetErrorString((hipError_t)code);
+}
+
+int encx_option_count(void) { return OPT_COUNT; }
+
+const char* encx_option_name(int i) { return i >= 0 && i < OPT_COUNT ? kOpts[i].name : nullptr; }
+
+int encx_get_option(const char* name, int64_t* value) {
+    const int i = opt_find(name);
+    if (i < 0 || !value) return ENCX_EINVAL;
+    *value = encx_opt((EncxOpt)i);
+    return 0;
+}
+
+int encx_set_option(const char* name, int64_t value, int64_t* previous) {
+    const int i = opt_find(name);
+    if (i < 0) return ENCX_EINVAL;
+    opt_init();
+    const int64_t prev = g_opt[i].exchange(value);
+    if (previous) *previous = prev;
+    return 0;
 }
 
 int encx_init(int device) {

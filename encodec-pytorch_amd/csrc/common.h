@@ -165,3 +165,23 @@ ENCX_DEV TileId xcd_tile() {
 }
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Kernel-selection options (api.hip): each starts from its ENCX_<NAME> environment variable (or
+// its default) and is read on every call, so a test or an A/B run can flip it in-process through
+// encx_set_option. Set them before sizing workspaces: a workspace query and the launch that uses
+// it must see the same options.
+enum EncxOpt {
+    OPT_FFT,           // spectrograms by real FFT (0: framed-DFT GEMM)
+    OPT_PW,            // pointwise GEMM kernels for the short, wide 1x1 convs
+    OPT_PW_WG_TMAX,    // longest T served by the 1x1 weight-grad GEMM
+    OPT_LSTM_FUSE,     // LSTM backward: elementwise step fused into the next GEMM launch
+    OPT_RB_PREFETCH,   // fused residual block: next tile staged in registers
+    OPT_FWR,           // register-window Conv2d forward: workgroups (0: off)
+    OPT_FWR_VARIANT,   // register-window Conv2d forward kernel variant
+    OPT_DGR,           // register-window Conv2d bwd-data: workgroups (0: off)
+    OPT_DGR_VARIANT,   // register-window Conv2d bwd-data kernel variant
+    OPT_WGR,           // register-window Conv2d weight grad: waves (0: off)
+    OPT_WGR_WGS,       // its 8-wave workgroup form: workgroups (0: one-wave form)
+    OPT_COUNT
+};
+int64_t encx_opt(EncxOpt id);

@@ -1222,8 +1222,7 @@ static int pw_launch(const PwArgs& a, int B, int epi, hipStream_t st) {
 // us; the long, HBM-bound ones (T >= 3000) stay on conv_fwd_kernel, whose epilogue streams
 // the residual better (64x64 at T 12000: 108 us there, 145 here)
 static bool pw_ok(int K, int s, int d, int pl, int pr, int e, int Tin, int Tout, int Cin, int Cout) {
-    static const int on = [] { const char* v = getenv("ENCX_PW"); return v ? atoi(v) : 1; }();
-    return on && K == 1 && s == 1 && d == 1 && pl == 0 && pr == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 &&
+    return encx_opt(OPT_PW) != 0 && K == 1 && s == 1 && d == 1 && pl == 0 && pr == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 &&
            Tout <= 1024 && Cin % 4 == 0 && Cout % 4 == 0;
 }
 
@@ -1357,9 +1356,8 @@ static size_t pw_wgrad_ws_bytes(int64_t B, int64_t M, int64_t N, int64_t T) {
 // the layers pw_wgrad serves: 1x1, T <= 12000 (A/B: 3000 -> 12000 +0.2 %), at least 64 x 64
 static bool pw_wgrad_ok(int64_t K, int64_t s, int64_t d, int64_t pl, int64_t e, int64_t Tin, int64_t Tout, int64_t Cin,
                         int64_t Cout) {
-    static const int on = [] { const char* v = getenv("ENCX_PW"); return v ? atoi(v) : 1; }();
-    static const int tmax = [] { const char* v = getenv("ENCX_PW_WG_TMAX"); return v ? atoi(v) : 12000; }();
-    return on && K == 1 && s == 1 && d == 1 && pl == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 && Tout <= tmax &&
+    const int64_t tmax = encx_opt(OPT_PW_WG_TMAX);
+    return encx_opt(OPT_PW) != 0 && K == 1 && s == 1 && d == 1 && pl == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 && Tout <= tmax &&
            Cin >= 64 && Cout >= 64 && Cin % 4 == 0 && Cout % 4 == 0;
 }
 static void pw_wgrad_run(const float* dy, const float* x, float* dw, float* db, float* ws, int64_t B, int64_t M,
@@ -1505,8 +1503,7 @@ static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K)
         p.tiles = (int)(cdiv(N, p.BN) * cdiv(A, p.BM));
     }
     p.items = (int)(B * cdiv(Tl, p.BT));
-    // ~1024 workgroups in flight (ENCX_WG_TARGET overrides, for tuning runs)
-    static const int64_t target = getenv("ENCX_WG_TARGET") ? atoll(getenv("ENCX_WG_TARGET")) : 1024;
+    constexpr int64_t target = 1024;  // ~1024 workgroups in flight
     int64_t want = cdiv(target, p.tiles);
     int64_t cap = (64ll << 20) / (4 * A * N);           // <= 64 MB of partials
     int64_t minper = cdiv(p.items, (int64_t)p.items >= 8 ? 8 : 1);

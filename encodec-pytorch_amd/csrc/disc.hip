@@ -3369,10 +3369,8 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + B * Co * T2 * Fo), "c2_fwd");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
-    // register-window form (c2_fwd_rw_kernel); ENCX_FWR = workgroups (0: off)
-    static const int fw_wgs = [] { const char* v = getenv("ENCX_FWR"); return v ? atoi(v) : 256; }();
-    // ENCX_FWR_VARIANT: run_fwd_rw's kernel variant (A/B; default 0)
-    static const int fw_var = [] { const char* v = getenv("ENCX_FWR_VARIANT"); return v ? atoi(v) : 0; }();
+    // register-window form (c2_fwd_rw_kernel); option FWR = workgroups (0: off), FWR_VARIANT its variant
+    const int fw_wgs = (int)encx_opt(OPT_FWR), fw_var = (int)encx_opt(OPT_FWR_VARIANT);
     if (fw_wgs > 0 && fwr_ok(g) &&
         ((Ci * KT < 16 && g_c2_select != 2) || rw_pays(cdiv(B * T2 * cdiv(Fo, 4), 32), B * T2 * Fo, 87.0 / 66.0)) &&
         run_fwd_rw(a, fw_wgs, st, fw_var) == 0)
@@ -3439,10 +3437,8 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
         ENCX_CHECK_LAUNCH();
         return 0;
     }
-    // register-window form (c2_dgrad_rw_kernel); ENCX_DGR = workgroups (0: off)
-    static const int dg_wgs = [] { const char* v = getenv("ENCX_DGR"); return v ? atoi(v) : 256; }();
-    // ENCX_DGR_VARIANT: run_dgrad_rw's kernel variant (A/B; default 0)
-    static const int dg_var = [] { const char* v = getenv("ENCX_DGR_VARIANT"); return v ? atoi(v) : 0; }();
+    // register-window form (c2_dgrad_rw_kernel); option DGR = workgroups (0: off), DGR_VARIANT its variant
+    const int dg_wgs = (int)encx_opt(OPT_DGR), dg_var = (int)encx_opt(OPT_DGR_VARIANT);
     if (dg_wgs > 0 && dgr_ok(g) && rw_pays(cdiv(B * T2 * cdiv(a.U, 4), 32), B * T2 * a.U, 92.0 / 78.0) &&
         run_dgrad_rw(a, dg_wgs, st, dg_var) == 0)
         return 0;
@@ -3513,9 +3509,9 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
         ENCX_CHECK_LAUNCH();
         return 0;
     }
-    static const int rw_waves = [] { const char* v = getenv("ENCX_WGR"); return v ? min(atoi(v), 4096) : 2048; }();
-    // 8-wave workgroups summing their partials in LDS (one per CU); ENCX_WGR_WGS=0: one-wave form
-    static const int rw_wgs = [] { const char* v = getenv("ENCX_WGR_WGS"); return v ? min(atoi(v), 1024) : 256; }();
+    const int rw_waves = (int)min(encx_opt(OPT_WGR), (int64_t)4096);
+    // 8-wave workgroups summing their partials in LDS (one per CU); option WGR_WGS = 0: one-wave form
+    const int rw_wgs = (int)min(encx_opt(OPT_WGR_WGS), (int64_t)1024);
     if (rw_waves > 0 && rw_wgs > 0 && wgr_ok(g) && g_c2_select != 2) {
         const WgPlanR q = plan_wgr(g, 0, rw_wgs);
         if (run_wgrad_rw(g, dy, yact, x, ws, q, st, true) == 0) {
@@ -3585,10 +3581,9 @@ int encx_conv2d_bwd_weight(const float* dy, const float* yact, const float* x, f
 /* Spectrogram of DiscriminatorSTFT (msstftd.py:62-64, 97-99): x [B][C][T] -> z [B][2C][Fr][nb]
  * (channels re_0..re_{C-1}, im_0..im_{C-1}), Fr = (T - n)/hop + 1, nb = n/2 + 1, scaled by
  * 1/sqrt(sum w^2) (normalized=True). tables: the mel-table layout of n (encx_mel_tables_init). */
-// ENCX_FFT=0: the spectrogram as the framed DFT GEMM (round 3) instead of the real FFT (fft.h)
+// option FFT = 0: the spectrogram as the framed DFT GEMM (round 3) instead of the real FFT (fft.h)
 static bool disc_fft(int64_t n) {
-    static const bool on = [] { const char* v = getenv("ENCX_FFT"); return !v || atoi(v) != 0; }();
-    return on && encx_fft::fft_ok(n);
+    return encx_opt(OPT_FFT) != 0 && encx_fft::fft_ok(n);
 }
 
 int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B, int64_t C, int64_t T,

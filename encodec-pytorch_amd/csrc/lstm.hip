@@ -534,7 +534,7 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
     // 21.7 us per fused launch against 9.0 + 4.9 us for G(k) and E(k + 1) (profiles/r03): each
     // workgroup's agent-scope release (L2 write-back) and the last arriver's acquire cost more
     // than the launch they save.
-    static const bool fuse = [] { const char* v = getenv("ENCX_LSTM_FUSE"); return v && atoi(v) != 0; }();
+    const bool fuse = encx_opt(OPT_LSTM_FUSE) != 0;
     BwdArgs a{DA, wcatT, P, (int)B, (int)T, (int)H, (int)L, 0, gper, dout, dcn, Cst, Gs, dx, acc_x,
               fuse ? cnt : nullptr};
     if (fuse) {

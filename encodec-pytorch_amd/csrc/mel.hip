@@ -204,10 +204,9 @@ __global__ void overlap_add(const float* dframe, float* grad, int Bn, int T, int
     grad[i] += s;
 }
 
-// ENCX_FFT=0: the spectrogram as the framed DFT GEMM (round 3) instead of the real FFT (fft.h)
+// option FFT = 0: the spectrogram as the framed DFT GEMM (round 3) instead of the real FFT (fft.h)
 static bool use_fft(int64_t n) {
-    static const bool on = [] { const char* v = getenv("ENCX_FFT"); return !v || atoi(v) != 0; }();
-    return on && encx_fft::fft_ok(n);
+    return encx_opt(OPT_FFT) != 0 && encx_fft::fft_ok(n);
 }
 // spec [rows][2nb] (re | im) of the reflect-padded, hann-windowed frames of wav
 static int spec_rows(const float* wav, const float* bt, float* spec, int64_t B, int64_t T, int n, int h, int p,

@@ -637,19 +637,22 @@ int rb_grid(K kernel, int threads, size_t lds, int64_t tiles) {
 }
 bool rb_ok(int64_t C, int64_t T) { return (C == 32 || C == 64) && T >= 3; }
 
-// ENCX_RB_PREFETCH=1: each next tile staged in registers (buffer loads) while the current one
+// option RB_PREFETCH = 1: each next tile staged in registers (buffer loads) while the current one
 // computes; default: staged just in time
-bool rb_prefetch() {
-    static const int v = [] { const char* e = getenv("ENCX_RB_PREFETCH"); return e ? atoi(e) : 0; }();
-    return v != 0;
-}
+bool rb_prefetch() { return encx_opt(OPT_RB_PREFETCH) != 0; }
 
-template <int C>
+// cached per variant; the workspace is sized for the larger of the two, so flipping the option
+// between the size query and the launch stays in bounds
+template <int C, bool PF>
 int rb_wgrad_grid(int64_t tiles) {
-    static int g = 0;  // cached (the workspace size must not move between the size query and the launch)
-    if (!g) g = rb_prefetch() ? rb_grid(rb_wgrad_kernel<C, true>, 256, rb_wgrad_lds(C), (int64_t)1 << 40)
-                              : rb_grid(rb_wgrad_kernel<C, false>, 256, rb_wgrad_lds(C), (int64_t)1 << 40);
+    static int g = 0;
+    if (!g) g = rb_grid(rb_wgrad_kernel<C, PF>, 256, rb_wgrad_lds(C), (int64_t)1 << 40);
     return (int)(tiles < g ? tiles : g);
+}
+template <int C>
+int rb_wgrad_grid_max(int64_t tiles) {
+    const int a = rb_wgrad_grid<C, false>(tiles), b = rb_wgrad_grid<C, true>(tiles);
+    return a > b ? a : b;
 }
 
 template <int C, bool PF>
@@ -660,7 +663,7 @@ void launch_bwd(const RbArgs& a, float* dws, float* dw2, float* dw1, float* db2,
     if (!gd) gd = rb_grid(rb_dgrad_kernel<C, PF>, Rb<C>::NT, rb_dgrad_lds(C), (int64_t)1 << 40);
     hipLaunchKernelGGL((rb_dgrad_kernel<C, PF>), dim3((unsigned)(tiles < gd ? tiles : gd)), dim3(Rb<C>::NT),
                        rb_dgrad_lds(C), st, a);
-    const int gw = rb_wgrad_grid<C>(tiles);
+    const int gw = rb_wgrad_grid<C, PF>(tiles);
     hipLaunchKernelGGL((rb_wgrad_kernel<C, PF>), dim3(gw), dim3(256), rb_wgrad_lds(C), st, a);
     hipLaunchKernelGGL(rb_wgrad_reduce<C>, dim3((unsigned)cdiv(Rb<C>::SLAB, 64)), dim3(256), 0, st, a.slab, gw, dws,
                        dw2, dw1, db2, dbs, db1, acc_w, acc_b);
@@ -703,8 +706,8 @@ int encx_resblock_fwd(const float* x, const float* w1, const float* b1, const fl
 size_t encx_resblock_bwd_workspace(int64_t B, int64_t C, int64_t T) {
     if (!rb_ok(C, T) || B <= 0) return 0;
     const int64_t tiles = B * cdiv(T, TT);
-    const size_t slab = C == 32 ? (size_t)rb_wgrad_grid<32>(tiles) * Rb<32>::SLAB
-                                : (size_t)rb_wgrad_grid<64>(tiles) * Rb<64>::SLAB;
+    const size_t slab = C == 32 ? (size_t)rb_wgrad_grid_max<32>(tiles) * Rb<32>::SLAB
+                                : (size_t)rb_wgrad_grid_max<64>(tiles) * Rb<64>::SLAB;
     return ((size_t)B * (C / 2) * T + slab) * sizeof(float);
 }
 

@@ -119,6 +119,43 @@ def call(name, *args):
     check(getattr(lib, name)(*args), name)
 
 
+def get_option(name):
+    v = ctypes.c_int64()
+    call('encx_get_option', name.encode(), ctypes.byref(v))
+    return v.value
+
+
+def set_option(name, value):
+    """Set a kernel-selection option (encx.h encx_set_option); returns the previous value."""
+    prev = ctypes.c_int64()
+    call('encx_set_option', name.encode(), int(value), ctypes.byref(prev))
+    return prev.value
+
+
+def options():
+    """{name: current value} of every kernel-selection option."""
+    names = [lib.encx_option_name(i).decode() for i in range(lib.encx_option_count())]
+    return {n: get_option(n) for n in names}
+
+
+class option:
+    """`with option(DGR_VARIANT=5, ...):` -- set options for a block, restore them after."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+        self.prev = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.prev[k] = set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.prev.items():
+            set_option(k, v)
+        return False
+
+
 def ptr(t):
     """Device pointer of a contiguous fp32/int64 CUDA tensor (None -> NULL)."""
     if t is None:

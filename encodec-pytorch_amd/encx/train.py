@@ -32,6 +32,10 @@ from .ops import DiscGradMode, WnBatch, defer_codebook_sync
 from .optim import FlatAdam
 from .scheduler import WarmupCosineLrScheduler
 
+def _noop():
+    pass
+
+
 DEFAULT_WEIGHTS = {'l_t': 0.1, 'l_f': 1, 'l_g': 3, 'l_feat': 3}  # config/config.yaml:55-60
 
 
@@ -120,12 +124,11 @@ class Trainer:
         if train_d:
             self.opt_d.prepare()
         key = (bw, train_d, tuple(x.shape))
-        # At world > 1 the step is cut into segments around the collectives, one graph each
-        # (ENCX_DP_GRAPHS=0: eager there). The round-3 replay drift does not reproduce: replays
-        # are bit-identical to the eager step at world 2 with the round-3 code and at HEAD, with
-        # and without device syncs, HIP packet capture or the older Conv2d kernels, and at world
-        # 1 for every segmentation (profiles/r04/graph_drift, tests/test_gpu_dp.py).
-        if self.graphs and (not distrib.is_distributed() or os.environ.get('ENCX_DP_GRAPHS', '1') != '0') \
+        # At world > 1 the step would be cut into segments around the collectives, one graph
+        # each. That is opt-in (ENCX_DP_GRAPHS=1): round 3 recorded replays drifting from the
+        # eager step at world 2 (profiles/r03/dp_graph_replay_diag.txt) with no cause proven,
+        # and no multi-GPU RCCL run has compared replays with eager steps.
+        if self.graphs and (not distrib.is_distributed() or os.environ.get('ENCX_DP_GRAPHS', '0') == '1') \
                 and self._graph_ok(key):
             out = self._graph_step(key, x)
         else:
@@ -272,11 +275,11 @@ class Trainer:
             return [(lambda: [s() for s in segs], None)], c
         if not dist:  # world 1, segmented on request: the same segments, no collectives
             return [(seg_gen, None), (seg_losses, None), (seg_dec, None),
-                    (seg_enc if split else (lambda: None), None), (seg_disc, None), (seg_opt, None)], c
+                    (seg_enc if split else _noop, None), (seg_disc, None), (seg_opt, None)], c
         return [(seg_gen, coll_gen if self.model.quantizer.sync_codebooks else None),
                 (seg_losses, self.balancer.reduce_stats),
                 (seg_dec, coll_dec if split else None),
-                (seg_enc if split else (lambda: None), coll_enc),
+                (seg_enc if split else _noop, coll_enc),
                 (seg_disc, coll_disc),
                 (seg_opt, None)], c
 
@@ -308,14 +311,15 @@ class Trainer:
         if ent == 'warm':  # second occurrence: capture, which also runs this step
             ent = self._graphs[key] = self._capture(key, x)
         else:
-            graphs, colls, xs, out, codes = ent
+            graphs, colls, xs, out, codes, cap_c = ent
             xs.copy_(x)
             for i, (g, coll) in enumerate(zip(graphs, colls)):
-                g.replay()
+                if g is not None:
+                    g.replay()
                 if coll is not None:
                     coll()
                 if self._seg_hook is not None:
-                    self._seg_hook(i, self._cap_c)
+                    self._seg_hook(i, cap_c)
         out = ent[3]
         # this key's graphs rewrite its own codes tensor (held by the entry, so its pool block is
         # never handed to another key); after another key ran, last_codes must point back at it
@@ -331,15 +335,16 @@ class Trainer:
         torch.cuda.synchronize()
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
-        self._cap_c = c
         graphs, colls, pending = [], [], []
         for seg, coll in segs:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._pool):
-                seg()
+            g = None
+            if seg is not _noop:  # an empty segment (no split backward) is not captured
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._pool):
+                    seg()
+                pending.append(g)
             graphs.append(g)
             colls.append(coll)
-            pending.append(g)
             if coll is not None:
                 # capture only records: run every segment captured since the last collective for
                 # real (in order: a segment without a collective of its own still feeds the next),
@@ -352,7 +357,7 @@ class Trainer:
             pg.replay()
         if self._seg_hook is not None:
             self._seg_hook(len(segs) - 1, c)
-        return graphs, colls, xs, c['out'], self.model.last_codes
+        return graphs, colls, xs, c['out'], self.model.last_codes, c
 
     # ------------------------------------------------------------------ checkpoints
     def state_dicts(self):

@@ -40,6 +40,14 @@ int encx_version(void);
  * Python binding refuses a library whose hash differs from the sources beside it. */
 const char* encx_build_id(void);
 const char* encx_strerror(int code);
+/* Kernel-selection options (A/B switches and variants of the hot kernels). Each starts from its
+ * environment variable ENCX_<name> or its default, and every launch reads the current value, so
+ * tests flip them in-process. Process-wide. Set them before querying workspaces: a workspace size
+ * and the launch using it must see the same options. Names with or without the ENCX_ prefix. */
+int encx_option_count(void);
+const char* encx_option_name(int i);  /* NULL past the last */
+int encx_get_option(const char* name, int64_t* value);
+int encx_set_option(const char* name, int64_t value, int64_t* previous /* may be NULL */);
 /* Select the device; cheap, idempotent. */
 int encx_init(int device);
 /* Kernel timing for bench.py's roofline: while enabled, every launch of the named kernel

@@ -48,6 +48,21 @@ def test_library_build_id_matches_sources():
             os.environ['ENCX_LIB'] = env
 
 
+def test_kernel_options_settable_in_process():
+    """encx_set_option / encx_get_option: every kernel-selection option is readable, settable
+    (with or without the ENCX_ prefix) and restorable; unknown names are refused."""
+    from encx import _lib as L
+    opts = L.options()
+    assert {'FFT', 'RB_PREFETCH', 'FWR_VARIANT', 'DGR_VARIANT', 'LSTM_FUSE', 'PW'} <= set(opts)
+    assert opts['FFT'] == int(os.environ.get('ENCX_FFT', 1))
+    with L.option(DGR_VARIANT=5, RB_PREFETCH=1):
+        assert L.get_option('DGR_VARIANT') == 5 and L.get_option('ENCX_RB_PREFETCH') == 1
+    assert L.options() == opts
+    lib = _lib()
+    assert lib.encx_set_option(b'NO_SUCH_OPTION', 1, None) == 9001
+    assert lib.encx_option_name(lib.encx_option_count()) is None
+
+
 def test_host_only_queries():
     lib = _lib()
     assert lib.encx_version() == 1

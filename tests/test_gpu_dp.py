@@ -98,10 +98,15 @@ def _run_case(name, x):
     tr = Trainer(m, disc, lr=3e-4, disc_lr=3e-4, scheduler=False, weights=weights,
                  balancer_kwargs={'rescale_grads': rescale}, graphs=graphs)
     losses = []
-    for i in range(steps):
-        o = tr.step(x.to(DEV) * (1.0 + 0.1 * i))
-        losses.append(torch.stack([o[k].reshape(()) for k in sorted(o)]).cpu())
-    torch.cuda.synchronize()
+    # graphs at world > 1 are opt-in (ENCX_DP_GRAPHS=1, encx/train.py)
+    os.environ['ENCX_DP_GRAPHS'] = '1' if graphs else '0'
+    try:
+        for i in range(steps):
+            o = tr.step(x.to(DEV) * (1.0 + 0.1 * i))
+            losses.append(torch.stack([o[k].reshape(()) for k in sorted(o)]).cpu())
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop('ENCX_DP_GRAPHS', None)
     captured = any(isinstance(v, tuple) for v in tr._graphs.values())
     assert captured == (graphs and steps >= 2), (name, captured)
     out = {'gen_grad': tr.opt.flat_grad.cpu(), 'gen_param': tr.opt.flat.cpu(), 'losses': torch.stack(losses),

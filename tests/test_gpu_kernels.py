@@ -300,13 +300,15 @@ def test_normalize_and_scale():
 
 
 # --------------------------------------------------------------------------- LSTM
-@pytest.mark.parametrize('B,H,Tn,L', [(3, 32, 7, 1), (17, 64, 20, 2), (5, 48, 9, 3), (32, 512, 75, 2)])
-def test_lstm_vs_oracle(B, H, Tn, L):
+@pytest.mark.parametrize('B,H,Tn,L,fuse', [(3, 32, 7, 1, 0), (17, 64, 20, 2, 0), (5, 48, 9, 3, 0), (32, 512, 75, 2, 0),
+                                            (17, 64, 20, 2, 1), (32, 512, 75, 2, 1)])
+def test_lstm_vs_oracle(B, H, Tn, L, fuse):
     """encx LSTM (csrc/lstm.hip, all layers as one diagonal wavefront) forward + backward
     against the oracle's step-by-step restatement of SLSTM (modules/lstm.py:22-28) run in fp64
     on the CPU, for 1, 2 and 3 layers: every output and grad within 4x the error of the same
-    restatement run in plain fp32."""
+    restatement run in plain fp32. fuse: the opt-in fused backward step (option LSTM_FUSE)."""
     from encx import ops
+    from encx._lib import option
     gen = torch.Generator().manual_seed(B * 1000 + H)
     k = 1.0 / np.sqrt(H)
     names = ['weight_ih', 'weight_hh', 'bias_ih', 'bias_hh']
@@ -322,9 +324,10 @@ def test_lstm_vs_oracle(B, H, Tn, L):
     y64 = O.slstm(x64, p64, 'm', L)
     (y64 * r64).sum().backward()
     x = x64.detach().float().to(DEV).requires_grad_(True)
-    y = ops.lstm(x, wts, skip=True)
-    (y * r64.float().to(DEV)).sum().backward()
-    torch.cuda.synchronize()
+    with option(LSTM_FUSE=fuse):
+        y = ops.lstm(x, wts, skip=True)
+        (y * r64.float().to(DEV)).sum().backward()
+        torch.cuda.synchronize()
 
     def rel_close(a, b, what, tol=2e-4):
         b = b.detach()
@@ -354,14 +357,17 @@ def test_lstm_vs_oracle(B, H, Tn, L):
 
 
 # --------------------------------------------------------------------------- fused residual block
+@pytest.mark.parametrize('prefetch', [0, 1], ids=['jit', 'prefetch'])
 @pytest.mark.parametrize('C,T,B', [(32, 2048, 3), (32, 24000, 2), (64, 12000, 2), (64, 3001, 3), (32, 2113, 1)])
-def test_fused_resblock_vs_torch_fp64(C, T, B):
+def test_fused_resblock_vs_torch_fp64(C, T, B, prefetch):
     """ops.ResBlockFn (csrc/resblock.hip: SEANetResnetBlock, modules/seanet.py:46-63, as one
     kernel per direction) against torch's fp64 restatement of the block: ELU -> reflect-padded
     causal k3 conv (C -> C/2) -> ELU -> 1x1 conv (C/2 -> C), plus the 1x1 shortcut, all weight
     normed. Output, input grad and every weight / bias grad under a seeded output grad, relative to
-    each tensor's largest magnitude; incl. T not a multiple of the 64-position tile."""
+    each tensor's largest magnitude; incl. T not a multiple of the 64-position tile. For both
+    tile-staging variants (option RB_PREFETCH)."""
     from encx import ops
+    from encx._lib import option
     g = torch.Generator().manual_seed(C * 7 + T)
     HD = C // 2
 
@@ -385,8 +391,9 @@ def test_fused_resblock_vs_torch_fp64(C, T, B):
     leaves = [t.detach().float().to(DEV).requires_grad_(True) for t in leaves64]
     x = leaves[0]
     p = [leaves[1:4], leaves[4:7], leaves[7:10]]
-    y = ops.resblock(x, *p)
-    mine = torch.autograd.grad(y, leaves, dy64.float().to(DEV))
+    with option(RB_PREFETCH=prefetch):
+        y = ops.resblock(x, *p)
+        mine = torch.autograd.grad(y, leaves, dy64.float().to(DEV))
 
     def rel(a, b):
         a, b = a.detach().double().cpu(), b.detach().double()
@@ -422,13 +429,15 @@ def test_fused_resblock_matches_unfused_block(C):
         assert float((a - b).abs().max()) <= 2e-5 * float(b.abs().max()) + 1e-7, (float((a - b).abs().max()), float(b.abs().max()))
 
 
+@pytest.mark.parametrize('fft', [1, 0], ids=['fft', 'dft_gemm'])
 @pytest.mark.parametrize('n', [32, 64, 128, 256, 512, 1024, 2048])
-def test_spectrogram_fft_vs_torch_fp64(n):
+def test_spectrogram_fft_vs_torch_fp64(n, fft):
     """The real-FFT spectrogram (csrc/fft.h, the discriminator's Spectrogram: hann window,
     center=False, normalized, msstftd.py:62-64, 97-99) and its transpose, at every power-of-2
     size the mel loss and the discriminator use, against torch.stft / autograd in fp64: relative
-    to each tensor's largest magnitude."""
+    to each tensor's largest magnitude. fft = 0: the framed-DFT GEMM path (option FFT)."""
     from encx import ops
+    from encx._lib import option
     B, C, Tn = 2, 2, 6000
     x64 = torch.from_numpy(synth_wave((B, C, Tn), n)).double().requires_grad_(True)
     w = torch.hann_window(n, dtype=torch.float64)
@@ -437,9 +446,10 @@ def test_spectrogram_fft_vs_torch_fp64(n):
     ref = torch.cat([st.real, st.imag], 0).reshape(2, B, C, n // 2 + 1, -1).permute(1, 0, 2, 4, 3)
     ref = ref.reshape(B, 2 * C, -1, n // 2 + 1)  # [b][re c | im c][fr][k]
     xg = x64.detach().float().to(DEV).requires_grad_(True)
-    z = ops.DiscSpecFn.apply(xg, n, n // 4, 24000)
     dz = torch.randn(ref.shape, generator=torch.Generator().manual_seed(n), dtype=torch.float64)
-    gx, = torch.autograd.grad(z, [xg], dz.float().to(DEV))
+    with option(FFT=fft):
+        z = ops.DiscSpecFn.apply(xg, n, n // 4, 24000)
+        gx, = torch.autograd.grad(z, [xg], dz.float().to(DEV))
     gref, = torch.autograd.grad(ref, [x64], dz)
 
     def rel(a, b):
