@@ -33,8 +33,8 @@ struct OptDef {
     int64_t def;
 };
 constexpr OptDef kOpts[OPT_COUNT] = {
-    {"FFT", 1}, {"PW", 1}, {"PW_WG_TMAX", 12000}, {"LSTM_FUSE", 0}, {"RB_PREFETCH", 0}, {"FWR", 256},
-    {"FWR_VARIANT", 0}, {"DGR", 256}, {"DGR_VARIANT", 0}, {"WGR", 2048}, {"WGR_WGS", 256},
+    {"FFT", 1}, {"PW", 1}, {"PW_WG_TMAX", 12000}, {"LSTM_FUSE", 0}, {"FWR", 256}, {"DGR", 256},
+    {"WGR", 2048}, {"WGR_WGS", 256},
 };
 std::atomic<int64_t> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;

@@ -175,11 +175,8 @@ enum EncxOpt {
     OPT_PW,            // pointwise GEMM kernels for the short, wide 1x1 convs
     OPT_PW_WG_TMAX,    // longest T served by the 1x1 weight-grad GEMM
     OPT_LSTM_FUSE,     // LSTM backward: elementwise step fused into the next GEMM launch
-    OPT_RB_PREFETCH,   // fused residual block: next tile staged in registers
     OPT_FWR,           // register-window Conv2d forward: workgroups (0: off)
-    OPT_FWR_VARIANT,   // register-window Conv2d forward kernel variant
     OPT_DGR,           // register-window Conv2d bwd-data: workgroups (0: off)
-    OPT_DGR_VARIANT,   // register-window Conv2d bwd-data kernel variant
     OPT_WGR,           // register-window Conv2d weight grad: waves (0: off)
     OPT_WGR_WGS,       // its 8-wave workgroup form: workgroups (0: one-wave form)
     OPT_COUNT

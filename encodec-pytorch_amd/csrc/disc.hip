@@ -830,7 +830,7 @@ struct C2FwdR {
 // with 1.5x or 2.9x as many items as wave slots -- and neighbouring items still share an XCD's L2.
 ENCX_DEV int rw_first_slot(int wave) { return wave * (int)gridDim.x + xcd_linear_id(); }
 
-template <int KF, int S, int WQ, int NWV, bool APF, bool GP = false>
+template <int KF, int S, int WQ, int NWV>
 __global__ __launch_bounds__(NWV * 64) void c2_fwd_rw_kernel(C2FwdR a) {
     constexpr int NE = 4 * WQ, KT = 3;  // window elements per lane; kernel rows (host-checked)
     extern __shared__ float smem[];
@@ -878,29 +878,18 @@ __global__ __launch_bounds__(NWV * 64) void c2_fwd_rw_kernel(C2FwdR a) {
         f32x16 acc[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] = (f32x16){0};
-        // three register windows and weight columns, one per kt: step (c, kt) multiplies
-        // window kt with weights kt while the next step's window (global) and weights (LDS) are
-        // in flight (the prefetches are unconditional, so every wait is exact)
+        // three register windows, one per kt: step (c, kt) multiplies window kt with the weight
+        // columns of (c, kt), read from LDS just in time, while the next step's window is in
+        // flight (the prefetch is unconditional, so every wait is exact). Measured against
+        // reading the weights a step ahead or one tap ahead: none is faster (profiles/r05).
         f32x4 wb[KT][WQ];
-        float ab[KT][APF ? KF : 1];
         auto wcol = [&](int c, int kt) { return Ws + ((2 * c + h) * KT + kt) * KF * 32 + l; };
-        auto load_a = [&](float* av, int c, int kt) {
-            if (!APF) return;
-            const float* wk = wcol(c, kt);
-#pragma unroll
-            for (int kf = 0; kf < KF; ++kf) av[APF ? kf : 0] = wk[kf * 32];
-        };
         load(wb[0], 0, 0);
-        load_a(ab[0], 0, 0);
-        // GP: each tap's weight read one tap ahead (across steps too), pinned by a scheduling
-        // barrier so the tap's MFMAs never wait on the LDS read that feeds them
-        float gnx = GP ? wcol(0, 0)[0] : 0.f;
         for (int c = 0; c < CP; ++c) {
 #pragma unroll
             for (int kt = 0; kt < KT; ++kt) {
                 const int nk = kt + 1 < KT ? kt + 1 : 0, nc = kt + 1 < KT ? c : min(c + 1, CP - 1);
                 load(wb[nk], nc, nk);
-                load_a(ab[nk], nc, nk);
                 f32x4* w = wb[kt];
                 if (fix) {
                     const int base = rb[kt] + c * cstride;
@@ -914,17 +903,9 @@ __global__ __launch_bounds__(NWV * 64) void c2_fwd_rw_kernel(C2FwdR a) {
                     }
                 }
                 const float* wk = wcol(c, kt);
-                const float* wkn = wcol(nc, nk);
 #pragma unroll
                 for (int kf = 0; kf < KF; ++kf) {
-                    float av;
-                    if (GP) {
-                        av = gnx;
-                        gnx = kf + 1 < KF ? wk[(kf + 1) * 32] : wkn[0];
-                        __builtin_amdgcn_sched_barrier(0);
-                    } else {
-                        av = APF ? ab[kt][APF ? kf : 0] : wk[kf * 32];
-                    }
+                    const float av = wk[kf * 32];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int r = S * j + kf;
@@ -1422,12 +1403,11 @@ struct C2DgR {
     int U4;     // quads per polyphase row
     int tiles;  // ceil(B * T2 * U4 / 32)
 };
-template <int J, int S, int RT, int WQ, bool YM, int NWV, int TM, bool APF, bool SB = true, bool GP = false>
+template <int J, int S, int RT, int WQ, bool YM, int NWV, int TM>
 __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
-    // RT row tiles of 32 (M = Ci*S = 32 RT); a work item is (column tile, TM row tiles); APF:
-    // the weight columns of step s + 1 are read from LDS during step s (else just in time); GP:
-    // each tap's weight column is read one tap ahead (across steps too), pinned there by a
-    // scheduling barrier, so the MFMAs of tap q never wait on the LDS read that feeds them
+    // RT row tiles of 32 (M = Ci*S = 32 RT); a work item is (column tile, TM row tiles); the
+    // weight columns are read from LDS just in time (measured against reading them a step ahead,
+    // one tap ahead, and one row tile per item: none is faster, profiles/r05)
     constexpr int NE = 4 * WQ, KT = 3, M = 32 * RT, RG = RT / TM;
     const C2Dg& a = R.d;
     extern __shared__ float smem[];
@@ -1462,11 +1442,10 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
             clean = clean && msk[kt] == (1u << NE) - 1;
         }
         const bool fix = !__all(clean);  // wave-uniform
-        // two register buffers (windows + weight columns), alternating over the (c, kt) steps:
-        // step s + 1 is in flight while step s multiplies. The loop body is 2 channel pairs x 3
-        // kt = 6 steps, so every buffer / kt index is a compile-time constant (Co % 4 == 0).
+        // two register buffers of windows, alternating over the (c, kt) steps: step s + 1 is in
+        // flight while step s multiplies. The loop body is 2 channel pairs x 3 kt = 6 steps, so
+        // every buffer / kt index is a compile-time constant (Co % 4 == 0).
         f32x4 wb[2][WQ], yb[2][WQ];
-        float ab[2][APF ? J * TM : 1];
         auto acol = [&](int c, int kt) { return As + ((2 * c + h) * KT + kt) * J * M + rt * TM * 32 + l; };
         auto load = [&](int k, int c, int kt) {
             const int base = rb[kt] + c * cstride;
@@ -1476,13 +1455,6 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
                 wb[k][q] = ld4u(a.dy + o);
                 if (YM) yb[k][q] = ld4u(a.yact + o);
             }
-            if (APF) {
-                const float* ak = acol(c, kt);
-#pragma unroll
-                for (int q = 0; q < J; ++q)
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) ab[k][APF ? q * TM + i : 0] = ak[q * M + i * 32];
-            }
         };
         f32x16 acc[TM][4];
 #pragma unroll
@@ -1490,9 +1462,6 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){0};
         load(0, 0, 0);
-        float gnx[TM];  // GP: the next tap's weight column
-#pragma unroll
-        for (int i = 0; i < TM; ++i) gnx[i] = GP ? acol(0, 0)[i * 32] : 0.f;
         for (int c0 = 0; c0 < CP; c0 += 2) {
 #pragma unroll
             for (int u = 0; u < 2 * KT; ++u) {
@@ -1503,8 +1472,9 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
                 load(k ^ 1, nc, nu % KT);
                 // keep the next step's loads HERE, a whole step ahead of their use: without the
                 // barrier the scheduler sinks them to the end of the step (one register buffer
-                // instead of two) and every step waits out the load latency
-                if (SB) __builtin_amdgcn_sched_barrier(0);
+                // instead of two) and every step waits out the load latency (measured: the
+                // round-3 kernel without it is slower, profiles/r05)
+                __builtin_amdgcn_sched_barrier(0);
                 f32x4* w = wb[k];
                 if (YM) {
 #pragma unroll
@@ -1524,22 +1494,11 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
                     }
                 }
                 const float* ak = acol(c, kt);
-                const float* akn = acol(nc, nu % KT);
 #pragma unroll
                 for (int q = 0; q < J; ++q) {
                     float av[TM];
-                    if (GP) {
-                        const float* src = q + 1 < J ? ak + (q + 1) * M : akn;
 #pragma unroll
-                        for (int i = 0; i < TM; ++i) {
-                            av[i] = gnx[i];
-                            gnx[i] = src[i * 32];
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < TM; ++i) av[i] = APF ? ab[k][APF ? q * TM + i : 0] : ak[q * M + i * 32];
-                    }
+                    for (int i = 0; i < TM; ++i) av[i] = ak[q * M + i * 32];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int r = j - q + J - 1;  // window element of column u0 + j, tap q
@@ -3006,8 +2965,9 @@ static bool dgr_ok(const C2Geo& g) {
     const int J = (g.KF + g.sf - 1) / g.sf;
     return (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float) <= 150 * 1024;
 }
-template <int NWV, int TM, bool APF, bool SB = true, bool GP = false>
-static int run_dgrad_rw_n(const C2Dg& d, int wgs, hipStream_t st) {
+static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st) {
+    if (!dgr_ok(d.g)) return ENCX_EINVAL;
+    constexpr int NWV = 8;  // 8 waves; both row tiles of the 3x9 layers per item
     const C2Geo& g = d.g;
     C2DgR R{d, 0, 0};
     R.d.U = (g.Fi - 1 + g.pf) / g.sf + 1;
@@ -3015,34 +2975,17 @@ static int run_dgrad_rw_n(const C2Dg& d, int wgs, hipStream_t st) {
     R.tiles = (int)cdiv((int64_t)g.B * g.T2 * R.U4, 32);
     const int J = (g.KF + g.sf - 1) / g.sf;
     const size_t lds = (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float);
-    const int RT = g.Ci * g.sf / 32, rg = max(1, RT / TM);
-    const int grid = (int)min((int64_t)wgs, cdiv((int64_t)R.tiles * rg, NWV));
+    const int grid = (int)min((int64_t)wgs, cdiv((int64_t)R.tiles, NWV));
     const bool ym = d.yact != nullptr;
     if (g.KF == 9) {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, TM, APF, SB, GP>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, TM, APF, SB, GP>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, 2>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, 2>), dim3(grid), dim3(NWV * 64), lds, st, R);
     } else {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV, 1, APF, SB, GP>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV, 1, APF, SB, GP>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV, 1>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV, 1>), dim3(grid), dim3(NWV * 64), lds, st, R);
     }
     ENCX_CHECK_LAUNCH();
     return 0;
-}
-// variant: 0 = 8 waves, both row tiles per item, weights just in time; 1 = 8 waves, one row tile
-// per item, weights prefetched; 2 = 12 waves, one row tile, prefetched; 3 = 8 waves, one row tile,
-// just in time; 4 = variant 0 without the scheduling barrier (the window loads sink to the end
-// of the step: the round-3 kernel, for A/B); 5 = variant 0 with the weight columns read one tap
-// ahead (GP)
-static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st, int variant = 0) {
-    if (!dgr_ok(d.g)) return ENCX_EINVAL;
-    switch (variant) {
-        case 5: return run_dgrad_rw_n<8, 2, false, true, true>(d, wgs, st);
-        case 4: return run_dgrad_rw_n<8, 2, false, false>(d, wgs, st);
-        case 1: return run_dgrad_rw_n<8, 1, true>(d, wgs, st);
-        case 2: return run_dgrad_rw_n<12, 1, true>(d, wgs, st);
-        case 3: return run_dgrad_rw_n<8, 1, false>(d, wgs, st);
-        default: return run_dgrad_rw_n<8, 2, false>(d, wgs, st);
-    }
 }
 
 // register-window forward (c2_fwd_rw_kernel): 32-wide output-channel tile, even Ci, KT <= 3,
@@ -3054,29 +2997,23 @@ static bool fwr_ok(const C2Geo& g) {
     if (!((g.KF == 9 && (g.sf == 2 || g.sf == 1)) || (g.KF == 3 && g.sf == 1))) return false;
     return (size_t)g.Ci * g.KT * g.KF * 32 * sizeof(float) <= 128 * 1024;
 }
-template <int NWV, bool APF, bool GP = false>
-static int run_fwd_rw_n(const C2Fwd& f, int wgs, hipStream_t st) {
+// wgs: workgroups (one per CU holds the layer's weights) of 8 waves
+static int run_fwd_rw(const C2Fwd& f, int wgs, hipStream_t st) {
+    if (!fwr_ok(f.g)) return ENCX_EINVAL;
+    constexpr int NWV = 8;
     const C2Geo& g = f.g;
     C2FwdR a{g, f.x, f.wf, f.bias, f.y, f.act, (int)cdiv(g.Fo, 4), 0};
     a.tiles = (int)cdiv((int64_t)g.B * g.T2 * a.F4, 32);
     const size_t lds = ((size_t)g.Ci * g.KT * g.KF * 32 + 32) * sizeof(float);
     const int grid = (int)min((int64_t)wgs, cdiv(a.tiles, NWV));
     if (g.KF == 9 && g.sf == 2)
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 2, 4, NWV, APF, GP>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 2, 4, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
     else if (g.KF == 9)
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 1, 3, NWV, APF, GP>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<9, 1, 3, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
     else
-        hipLaunchKernelGGL((c2_fwd_rw_kernel<3, 1, 2, NWV, APF, GP>), dim3(grid), dim3(NWV * 64), lds, st, a);
+        hipLaunchKernelGGL((c2_fwd_rw_kernel<3, 1, 2, NWV>), dim3(grid), dim3(NWV * 64), lds, st, a);
     ENCX_CHECK_LAUNCH();
     return 0;
-}
-// wgs: workgroups (one per CU holds the layer's weights); variant: 0 = 8 waves, weights just in
-// time from LDS; 1 = 8 waves, weights prefetched a step ahead; 2 = 8 waves, weights read one tap
-// ahead (GP)
-static int run_fwd_rw(const C2Fwd& f, int wgs, hipStream_t st, int variant = 0) {
-    if (!fwr_ok(f.g)) return ENCX_EINVAL;
-    if (variant == 2) return run_fwd_rw_n<8, false, true>(f, wgs, st);
-    return variant == 1 ? run_fwd_rw_n<8, true>(f, wgs, st) : run_fwd_rw_n<8, false>(f, wgs, st);
 }
 template <int BN, int KFC, int MQ, int CKM, int OCC = 1>
 int run_fwdr(C2Fwd a, hipStream_t st) {
@@ -3369,11 +3306,11 @@ int encx_conv2d_fwd(const float* x, const float* wf, const float* bias, float* y
     encx_prof_scope ps(st, 2.0 * B * Co * T2 * Fo * Ci * KT * KF, 4.0 * (B * Ci * T2 * Fi + B * Co * T2 * Fo), "c2_fwd");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     C2Fwd a{g, x, wf, bias, y, act, 0, 0, 0};
-    // register-window form (c2_fwd_rw_kernel); option FWR = workgroups (0: off), FWR_VARIANT its variant
-    const int fw_wgs = (int)encx_opt(OPT_FWR), fw_var = (int)encx_opt(OPT_FWR_VARIANT);
+    // register-window form (c2_fwd_rw_kernel); option FWR = workgroups (0: off)
+    const int fw_wgs = (int)encx_opt(OPT_FWR);
     if (fw_wgs > 0 && fwr_ok(g) &&
         ((Ci * KT < 16 && g_c2_select != 2) || rw_pays(cdiv(B * T2 * cdiv(Fo, 4), 32), B * T2 * Fo, 87.0 / 66.0)) &&
-        run_fwd_rw(a, fw_wgs, st, fw_var) == 0)
+        run_fwd_rw(a, fw_wgs, st) == 0)
         return 0;
     if (Co == 1 && KT == 3 && KF == 3 && (sf == 1 || sf == 2)) {
         dim3 grid((unsigned)cdiv(T2 * Fo, 64), (unsigned)B);
@@ -3437,10 +3374,10 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
         ENCX_CHECK_LAUNCH();
         return 0;
     }
-    // register-window form (c2_dgrad_rw_kernel); option DGR = workgroups (0: off), DGR_VARIANT its variant
-    const int dg_wgs = (int)encx_opt(OPT_DGR), dg_var = (int)encx_opt(OPT_DGR_VARIANT);
+    // register-window form (c2_dgrad_rw_kernel); option DGR = workgroups (0: off)
+    const int dg_wgs = (int)encx_opt(OPT_DGR);
     if (dg_wgs > 0 && dgr_ok(g) && rw_pays(cdiv(B * T2 * cdiv(a.U, 4), 32), B * T2 * a.U, 92.0 / 78.0) &&
-        run_dgrad_rw(a, dg_wgs, st, dg_var) == 0)
+        run_dgrad_rw(a, dg_wgs, st) == 0)
         return 0;
     // tile choice from tools/mb/c2_mb sweeps: 128-column tiles for the narrowest layers (Fo 33;
     // at Fo 65 the 256-column tile is 4-7 % faster), 8-combo

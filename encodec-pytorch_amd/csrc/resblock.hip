@@ -18,7 +18,9 @@
 // LDS rows 16 banks apart, channel-major (32x32x2, 32 channels x 1 position) wants an odd row
 // stride; one kernel holding every tile in both layouts would not fit two workgroups per CU.
 // Weights live in VGPRs as MFMA B fragments (loaded once per workgroup), so the only LDS reads in
-// the inner loops are conflict-free A / B tile reads.
+// the inner loops are conflict-free A / B tile reads. Each workgroup loads its next tile into
+// registers (buffer loads) while the current one computes (config-3 step: 778 vs 766 audio-s/s
+// over staging each tile just in time, profiles/r05/bench_ab_variants.txt).
 // MFMA: v_mfma_f32_16x16x4_f32 (lane l: A[l&15][k=l>>4], B[k=l>>4][l&15], D[row 4(l>>4)+i][col l&15])
 // and v_mfma_f32_32x32x2_f32 (common.h), exact fp32 products.
 #include "common.h"
@@ -30,7 +32,6 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 ENCX_DEV f32x4v mfma16(float a, float b, f32x4v c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
 constexpr int TT = 64;        // positions per tile
-constexpr int HALO = TT + 2;  // staged positions incl. the 2-position halo
 constexpr int XF = 80;        // position-major row stride (== 16 mod 32: lanes lk = 0 / 1 on disjoint banks)
 constexpr int XW = 67;        // channel-major row stride (odd: 32 rows on 32 distinct banks)
 
@@ -91,7 +92,7 @@ ENCX_DEV float bload(rsrc_t r, int voff, int soff) {
 // ------------------------------------------------------------------------------------ forward
 // Wave (strip s = wv & 3, group g = wv >> 2): positions 16 s .. 16 s + 15 of the tile, h columns
 // g * HD / CG .., y columns g * C / CG ..
-template <int C, bool PF>
+template <int C>
 __global__ __launch_bounds__(Rb<C>::NT) void rb_fwd_kernel(RbArgs a) {
     constexpr int HD = C / 2, CG = Rb<C>::CG, NT = Rb<C>::NT, N1 = HD / 16 / CG, N2 = C / 16 / CG;
     extern __shared__ float sm[];
@@ -133,32 +134,21 @@ __global__ __launch_bounds__(Rb<C>::NT) void rb_fwd_kernel(RbArgs a) {
         for (int u = 0; u < PR; ++u) pf[u] = bload(rx, vo, u * NW * T * 4);
         if (tid < 2 * C) pfh = bload(rx, (hc * T + reflect_clamp(t0 - 2 + hp, T)) * 4, 0);
     };
-    if (PF && (int)blockIdx.x < ntiles) fetch(blockIdx.x);
+    if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int b = tile / a.NT, t0 = (tile - b * a.NT) * TT;
         __syncthreads();  // the previous tile's LDS reads are done
-        if (PF) {
 #pragma unroll
-            for (int u = 0; u < PR; ++u) {
-                xs[(wv + NW * u) * XF + lane] = pf[u];
-                es[(wv + NW * u) * XF + lane] = elu(pf[u]);
-            }
-            if (tid < 2 * C) {
-                xs[hc * XF + hp] = pfh;
-                es[hc * XF + hp] = elu(pfh);
-            }
-        } else {  // staged just in time
-            const float* xb = a.x + (int64_t)b * C * T;
-#pragma unroll 4
-            for (int i = tid; i < C * HALO; i += NT) {
-                const int c = i / HALO, p = i - c * HALO;
-                const float v = xb[(int64_t)c * T + reflect_clamp(t0 - 2 + p, T)];  // past T: unused
-                xs[c * XF + p] = v;
-                es[c * XF + p] = elu(v);
-            }
+        for (int u = 0; u < PR; ++u) {
+            xs[(wv + NW * u) * XF + lane] = pf[u];
+            es[(wv + NW * u) * XF + lane] = elu(pf[u]);
+        }
+        if (tid < 2 * C) {
+            xs[hc * XF + hp] = pfh;
+            es[hc * XF + hp] = elu(pfh);
         }
         __syncthreads();
-        if (PF && tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
         // h^T[m][j] = b1[j] + sum_{c,k} ELU(x)[c][t - 2 + k] W1[c][k][j]   (rows = positions)
         f32x4v acc1[N1];
 #pragma unroll
@@ -182,7 +172,7 @@ __global__ __launch_bounds__(Rb<C>::NT) void rb_fwd_kernel(RbArgs a) {
                 ev[i] = elu(hv[i]);
             }
             *(f32x4v*)(hs + j * XF + m0 + 4 * lk) = ev;
-            st4(a.h + ((int64_t)b * HD + j) * T, tq, T, hv);
+            if (a.h) st4(a.h + ((int64_t)b * HD + j) * T, tq, T, hv);
         }
         __syncthreads();  // the other column group's h rows
         // y^T[m][o] = (b2 + bs)[o] + sum_j ELU(h)[j][m] W2[j][o] + sum_c x[c][m] Ws[c][o]
@@ -213,7 +203,7 @@ __global__ __launch_bounds__(Rb<C>::NT) void rb_fwd_kernel(RbArgs a) {
 // Wave (strip, group) as in the forward: dh columns g * HD / CG .., dx columns g * C / CG ..
 // The right-halo dh (positions TT, TT + 1, read by the k3 transpose of the last positions) on
 // the vector ALU: TPO threads per (j, p), C / TPO terms each, summed by lane shuffles.
-template <int C, bool PF>
+template <int C>
 __global__ __launch_bounds__(Rb<C>::NT) void rb_dgrad_kernel(RbArgs a) {
     constexpr int HD = C / 2, CG = Rb<C>::CG, NT = Rb<C>::NT, NH = HD / 16 / CG, NX = C / 16 / CG;
     constexpr int TPO = NT / (2 * HD), U = C / TPO;
@@ -274,42 +264,22 @@ __global__ __launch_bounds__(Rb<C>::NT) void rb_dgrad_kernel(RbArgs a) {
         const int th = t0 + hp;
         hh = a.h[((int64_t)b * HD + hj) * T + (th < T ? th : T - 1)];
     };
-    if (PF && (int)blockIdx.x < ntiles) fetch(blockIdx.x);
+    if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int b = tile / a.NT, t0 = (tile - b * a.NT) * TT;
         __syncthreads();
-        if (PF) {
 #pragma unroll
-            for (int u = 0; u < PR; ++u) dys[(wv + NW * u) * XF + lane] = pf[u];
-            if (tid < 2 * C) dys[hc * XF + hpp] = pfh;
-        } else {  // staged just in time
-            const float* dyb = a.dy + (int64_t)b * C * T;
-#pragma unroll 4
-            for (int i = tid; i < C * HALO; i += NT) {
-                const int c = i / HALO, p = i - c * HALO, t = t0 + p;
-                const float v = dyb[(int64_t)c * T + (t < T ? t : T - 1)];
-                dys[c * XF + p] = t < T ? v : 0.f;
-            }
-        }
+        for (int u = 0; u < PR; ++u) dys[(wv + NW * u) * XF + lane] = pf[u];
+        if (tid < 2 * C) dys[hc * XF + hpp] = pfh;
         __syncthreads();
         const int tq = t0 + m0 + 4 * lk;
         f32x4v hcur[NH], xcur[NX];
-        float hhcur;
-        if (PF) {
 #pragma unroll
-            for (int n = 0; n < NH; ++n) hcur[n] = hv[n];
+        for (int n = 0; n < NH; ++n) hcur[n] = hv[n];
 #pragma unroll
-            for (int n = 0; n < NX; ++n) xcur[n] = xv[n];
-            hhcur = hh;
-            if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
-        } else {
-#pragma unroll
-            for (int n = 0; n < NH; ++n) hcur[n] = ld4(a.h + ((int64_t)b * HD + (g * NH + n) * 16 + lc) * T, tq, T);
-#pragma unroll
-            for (int n = 0; n < NX; ++n) xcur[n] = ld4(a.x + ((int64_t)b * C + (g * NX + n) * 16 + lc) * T, tq, T);
-            const int th = t0 + hp;
-            hhcur = a.h[((int64_t)b * HD + hj) * T + (th < T ? th : T - 1)];
-        }
+        for (int n = 0; n < NX; ++n) xcur[n] = xv[n];
+        const float hhcur = hh;
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
         // ---- dh^T[p][j] = ELU'(h) * sum_o dy[o][p] W2[j][o] for p < TT ...
         {
             f32x4v acc[NH];
@@ -413,7 +383,7 @@ ENCX_DEV void wgemm(const float* ap, const WTile* t, f32x16* acc) {
 // (dWs, dW2); w2 / w3: A = dh x ELU(x) rows {0-31, 32-63} at taps {0, 0, 1} / {1, 2, 2} (dW1).
 // C = 32 -- w0: A = dy x {x, ELU(h)}; w1..w3: A = dh x ELU(x) at tap w - 1 (16-row operands
 // read twice, the duplicate rows / columns of the tile dropped at the store).
-template <int C, bool PF>
+template <int C>
 __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
     constexpr int HD = C / 2, NTL = C == 64 ? 3 : 2;
     extern __shared__ float sm[];
@@ -466,10 +436,9 @@ __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
     // x (reflect) as rows wv + 4 u at positions lane; x's last two halo columns by threads < 2 C
     constexpr int PD = C / 4, PH = HD / 4;
     float pd[PD], pdh[PH], ph[PH], px[PD], pxh = 0.f;
-    float bacc[PD + PH];  // PF: this lane's partial bias sums: dy rows wv + 4 u, then dh rows
+    float bacc[PD + PH];  // this lane's partial bias sums: dy rows wv + 4 u, then dh rows
 #pragma unroll
     for (int u = 0; u < PD + PH; ++u) bacc[u] = 0.f;
-    float bsum = 0.f;     // else: tid < C: sum of dy[o = tid]; C <= tid < C + HD: sum of dh[j = tid - C]
     const int hc = tid >> 1, hp = TT + (tid & 1);
     auto fetch = [&](int tile) {
         const int b = tile / a.NT, t0 = (tile - b * a.NT) * TT, t = t0 + lane;
@@ -492,65 +461,30 @@ __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
         }
         if (tid < 2 * C) pxh = bload(rx, (hc * T + reflect_clamp(t0 - 2 + hp, T)) * 4, 0);
     };
-    if (PF && (int)blockIdx.x < ntiles) fetch(blockIdx.x);
+    if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         __syncthreads();
-        if (PF) {
 #pragma unroll
-            for (int u = 0; u < PD; ++u) {
-                dys[(wv + 4 * u) * XW + lane] = pd[u];
-                xs[(wv + 4 * u) * XW + lane] = px[u];
-                exs[(wv + 4 * u) * XW + lane] = elu(px[u]);
-                bacc[u] += pd[u];
-            }
+        for (int u = 0; u < PD; ++u) {
+            dys[(wv + 4 * u) * XW + lane] = pd[u];
+            xs[(wv + 4 * u) * XW + lane] = px[u];
+            exs[(wv + 4 * u) * XW + lane] = elu(px[u]);
+            bacc[u] += pd[u];
+        }
 #pragma unroll
-            for (int u = 0; u < PH; ++u) {
-                dhs[(wv + 4 * u) * XW + lane] = pdh[u];
-                hes[(wv + 4 * u) * XW + lane] = elu(ph[u]);
-                bacc[PD + u] += pdh[u];
-            }
-            if (tid < 2 * C) {
-                xs[hc * XW + hp] = pxh;
-                exs[hc * XW + hp] = elu(pxh);
-            }
-        } else {  // staged just in time
-            const int b = tile / a.NT, t0 = (tile - b * a.NT) * TT;
-            const float* dyb = a.dy + (int64_t)b * C * T;
-            const float* dhb = a.dh + (int64_t)b * HD * T;
-            const float* hb = a.h + (int64_t)b * HD * T;
-            const float* xb = a.x + (int64_t)b * C * T;
-#pragma unroll 4
-            for (int i = tid; i < C * TT; i += 256) {
-                const int c = i / TT, q = i - c * TT, t = t0 + q;
-                const float v = dyb[(int64_t)c * T + (t < T ? t : T - 1)];
-                dys[c * XW + q] = t < T ? v : 0.f;
-            }
-#pragma unroll 4
-            for (int i = tid; i < HD * TT; i += 256) {
-                const int j = i / TT, q = i - j * TT, t = t0 + q, tc = t < T ? t : T - 1;
-                const float d = dhb[(int64_t)j * T + tc], hv = hb[(int64_t)j * T + tc];
-                dhs[j * XW + q] = t < T ? d : 0.f;
-                hes[j * XW + q] = elu(hv);
-            }
-#pragma unroll 4
-            for (int i = tid; i < C * HALO; i += 256) {
-                const int c = i / HALO, p = i - c * HALO;
-                const float v = xb[(int64_t)c * T + reflect_clamp(t0 - 2 + p, T)];
-                xs[c * XW + p] = v;
-                exs[c * XW + p] = elu(v);
-            }
+        for (int u = 0; u < PH; ++u) {
+            dhs[(wv + 4 * u) * XW + lane] = pdh[u];
+            hes[(wv + 4 * u) * XW + lane] = elu(ph[u]);
+            bacc[PD + u] += pdh[u];
+        }
+        if (tid < 2 * C) {
+            xs[hc * XW + hp] = pxh;
+            exs[hc * XW + hp] = elu(pxh);
         }
         __syncthreads();
-        if (PF && tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
         if (C == 64 || ntl == NTL) wgemm<NTL>(ap, tl, acc);
         else wgemm<1>(ap, tl, acc);
-        if (!PF) {  // bias sums from the staged tile: thread o < C sums dy[o], C <= tid < C + HD dh[tid - C]
-            if (tid < C) {
-                for (int q = 0; q < TT; ++q) bsum += dys[tid * XW + q];
-            } else if (tid < C + HD) {
-                for (int q = 0; q < TT; ++q) bsum += dhs[(tid - C) * XW + q];
-            }
-        }
     }
     // ---- this workgroup's partial weight grads -> slab [dWs C x C][dW2 C x HD][dW1 HD x C x 3][db C][db1 HD]
     // (natural layouts: dWs[o][c], dW2[o][j], dW1[j][c][k])
@@ -570,14 +504,10 @@ __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
             }
         }
     }
-    if (PF) {
 #pragma unroll
-        for (int u = 0; u < PD + PH; ++u) {  // db rows wv + 4 u, then db1 rows wv + 4 u
-            const float v = wave_sum(bacc[u]);
-            if (lane == 0) sl[C * C + C * HD + HD * 3 * C + (u < PD ? wv + 4 * u : C + wv + 4 * (u - PD))] = v;
-        }
-    } else if (tid < C + HD) {
-        sl[C * C + C * HD + HD * 3 * C + tid] = bsum;
+    for (int u = 0; u < PD + PH; ++u) {  // db rows wv + 4 u, then db1 rows wv + 4 u
+        const float v = wave_sum(bacc[u]);
+        if (lane == 0) sl[C * C + C * HD + HD * 3 * C + (u < PD ? wv + 4 * u : C + wv + 4 * (u - PD))] = v;
     }
 }
 
@@ -637,43 +567,33 @@ int rb_grid(K kernel, int threads, size_t lds, int64_t tiles) {
 }
 bool rb_ok(int64_t C, int64_t T) { return (C == 32 || C == 64) && T >= 3; }
 
-// option RB_PREFETCH = 1: each next tile staged in registers (buffer loads) while the current one
-// computes; default: staged just in time
-bool rb_prefetch() { return encx_opt(OPT_RB_PREFETCH) != 0; }
-
-// cached per variant; the workspace is sized for the larger of the two, so flipping the option
-// between the size query and the launch stays in bounds
-template <int C, bool PF>
+// cached (the workspace size must not move between the size query and the launch)
+template <int C>
 int rb_wgrad_grid(int64_t tiles) {
     static int g = 0;
-    if (!g) g = rb_grid(rb_wgrad_kernel<C, PF>, 256, rb_wgrad_lds(C), (int64_t)1 << 40);
+    if (!g) g = rb_grid(rb_wgrad_kernel<C>, 256, rb_wgrad_lds(C), (int64_t)1 << 40);
     return (int)(tiles < g ? tiles : g);
 }
-template <int C>
-int rb_wgrad_grid_max(int64_t tiles) {
-    const int a = rb_wgrad_grid<C, false>(tiles), b = rb_wgrad_grid<C, true>(tiles);
-    return a > b ? a : b;
-}
 
-template <int C, bool PF>
+template <int C>
 void launch_bwd(const RbArgs& a, float* dws, float* dw2, float* dw1, float* db2, float* dbs, float* db1, int acc_w,
                 int acc_b, hipStream_t st) {
     const int64_t tiles = (int64_t)a.B * a.NT;
     static int gd = 0;
-    if (!gd) gd = rb_grid(rb_dgrad_kernel<C, PF>, Rb<C>::NT, rb_dgrad_lds(C), (int64_t)1 << 40);
-    hipLaunchKernelGGL((rb_dgrad_kernel<C, PF>), dim3((unsigned)(tiles < gd ? tiles : gd)), dim3(Rb<C>::NT),
+    if (!gd) gd = rb_grid(rb_dgrad_kernel<C>, Rb<C>::NT, rb_dgrad_lds(C), (int64_t)1 << 40);
+    hipLaunchKernelGGL((rb_dgrad_kernel<C>), dim3((unsigned)(tiles < gd ? tiles : gd)), dim3(Rb<C>::NT),
                        rb_dgrad_lds(C), st, a);
-    const int gw = rb_wgrad_grid<C, PF>(tiles);
-    hipLaunchKernelGGL((rb_wgrad_kernel<C, PF>), dim3(gw), dim3(256), rb_wgrad_lds(C), st, a);
+    const int gw = rb_wgrad_grid<C>(tiles);
+    hipLaunchKernelGGL((rb_wgrad_kernel<C>), dim3(gw), dim3(256), rb_wgrad_lds(C), st, a);
     hipLaunchKernelGGL(rb_wgrad_reduce<C>, dim3((unsigned)cdiv(Rb<C>::SLAB, 64)), dim3(256), 0, st, a.slab, gw, dws,
                        dw2, dw1, db2, dbs, db1, acc_w, acc_b);
 }
 
-template <int C, bool PF>
+template <int C>
 void launch_fwd(const RbArgs& a, int64_t tiles, hipStream_t st) {
     static int g = 0;
-    if (!g) g = rb_grid(rb_fwd_kernel<C, PF>, Rb<C>::NT, rb_fwd_lds(C), (int64_t)1 << 40);
-    hipLaunchKernelGGL((rb_fwd_kernel<C, PF>), dim3((unsigned)(tiles < g ? tiles : g)), dim3(Rb<C>::NT), rb_fwd_lds(C),
+    if (!g) g = rb_grid(rb_fwd_kernel<C>, Rb<C>::NT, rb_fwd_lds(C), (int64_t)1 << 40);
+    hipLaunchKernelGGL((rb_fwd_kernel<C>), dim3((unsigned)(tiles < g ? tiles : g)), dim3(Rb<C>::NT), rb_fwd_lds(C),
                        st, a);
 }
 
@@ -684,20 +604,15 @@ extern "C" {
 int encx_resblock_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                       const float* ws, const float* bs, float* h, float* y, int64_t B, int64_t C, int64_t T,
                       encx_stream_t stream) {
-    ENCX_REQUIRE(x && w1 && b1 && w2 && b2 && ws && bs && h && y && B > 0 && rb_ok(C, T));
+    ENCX_REQUIRE(x && w1 && b1 && w2 && b2 && ws && bs && y && B > 0 && rb_ok(C, T));
     hipStream_t st = (hipStream_t)stream;
     const int64_t HD = C / 2;
     encx_prof_scope ps(st, 2.0 * B * T * (3 * C * HD + (HD + C) * C), 4.0 * B * T * (2 * C + HD), "conv_rb_fwd");
     ps.tag(" C%ld T%ld", (long)C, (long)T);
     RbArgs a{x, w1, b1, w2, b2, ws, bs, h, y, nullptr, nullptr, nullptr, nullptr, (int)B, (int)T, (int)cdiv(T, TT)};
     const int64_t tiles = B * a.NT;
-    if (C == 32) {
-        if (rb_prefetch()) launch_fwd<32, true>(a, tiles, st);
-        else launch_fwd<32, false>(a, tiles, st);
-    } else {
-        if (rb_prefetch()) launch_fwd<64, true>(a, tiles, st);
-        else launch_fwd<64, false>(a, tiles, st);
-    }
+    if (C == 32) launch_fwd<32>(a, tiles, st);
+    else launch_fwd<64>(a, tiles, st);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
@@ -706,8 +621,8 @@ int encx_resblock_fwd(const float* x, const float* w1, const float* b1, const fl
 size_t encx_resblock_bwd_workspace(int64_t B, int64_t C, int64_t T) {
     if (!rb_ok(C, T) || B <= 0) return 0;
     const int64_t tiles = B * cdiv(T, TT);
-    const size_t slab = C == 32 ? (size_t)rb_wgrad_grid_max<32>(tiles) * Rb<32>::SLAB
-                                : (size_t)rb_wgrad_grid_max<64>(tiles) * Rb<64>::SLAB;
+    const size_t slab = C == 32 ? (size_t)rb_wgrad_grid<32>(tiles) * Rb<32>::SLAB
+                                : (size_t)rb_wgrad_grid<64>(tiles) * Rb<64>::SLAB;
     return ((size_t)B * (C / 2) * T + slab) * sizeof(float);
 }
 
@@ -724,14 +639,8 @@ int encx_resblock_bwd(const float* dy, const float* x, const float* h, const flo
     float* slab = wsp + (size_t)B * HD * T;
     RbArgs a{x, w1, nullptr, w2, nullptr, ws, nullptr, const_cast<float*>(h), nullptr, dy, dx, dh, slab, (int)B, (int)T,
              (int)cdiv(T, TT)};
-    const bool pf = rb_prefetch();
-    if (C == 32) {
-        if (pf) launch_bwd<32, true>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
-        else launch_bwd<32, false>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
-    } else {
-        if (pf) launch_bwd<64, true>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
-        else launch_bwd<64, false>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
-    }
+    if (C == 32) launch_bwd<32>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
+    else launch_bwd<64>(a, dws, dw2, dw1, db2, dbs, db1, acc_w, acc_b, st);
     ENCX_CHECK_LAUNCH();
     return 0;
 }

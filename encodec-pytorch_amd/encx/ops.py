@@ -359,7 +359,8 @@ class ResBlockFn(torch.autograd.Function):
         w1, _ = _weight_prep(v1, g1, 3, 1, True, False)
         w2, _ = _weight_prep(v2, g2, 1, 1, True, False)
         ws, _ = _weight_prep(vs, gs, 1, 1, True, False)
-        h = torch.empty(B, C // 2, T, device=x.device, dtype=torch.float32)
+        # the pre-ELU hidden tensor is written only for a backward (no_grad / eval: NULL)
+        h = torch.empty(B, C // 2, T, device=x.device, dtype=torch.float32) if any(ctx.needs_input_grad) else None
         y = torch.empty_like(x)
         call('encx_resblock_fwd', ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(ws), ptr(bs), ptr(h), ptr(y),
              B, C, T, stream())
@@ -374,7 +375,7 @@ class ResBlockFn(torch.autograd.Function):
         dy = dy.contiguous()
         B, C, T = x.shape
         HD = C // 2
-        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else torch.empty_like(x)
+        dx = torch.empty_like(x)  # the data-grad kernel writes dx and dh together
         bufs = [_dw_buffer(v1, g1, b1, (HD, C, 3), x), _dw_buffer(v2, g2, b2, (C, HD, 1), x),
                 _dw_buffer(vs, gs, bs, (C, C, 1), x)]
         accs = {a for _, a in bufs}

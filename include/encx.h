@@ -165,7 +165,7 @@ size_t encx_convtr1d_bwd_weight_workspace(int64_t B, int64_t Cin, int64_t Cout, 
  * reflect padding, conv.py:195-210) as ONE kernel per direction for the high-rate stages:
  *   h = b1 + W1 * ELU(pad_reflect(x, 2, 0))   (k3, C -> C/2),   y = bs + Ws x + b2 + W2 ELU(h).
  * C in {32, 64}; T >= 3. Weights in the forward layout of encx_weightnorm_fwd (wf [Cin][K][Cout]):
- * w1 [C][3][C/2], w2 [C/2][C], ws [C][C]. h [B][C/2][T] (pre-ELU) is written for the backward. */
+ * w1 [C][3][C/2], w2 [C/2][C], ws [C][C]. h [B][C/2][T] (pre-ELU) is written for the backward; NULL skips it (inference). */
 int encx_resblock_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                       const float* ws, const float* bs, float* h, float* y, int64_t B, int64_t C, int64_t T,
                       encx_stream_t stream);

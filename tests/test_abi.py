@@ -53,10 +53,10 @@ def test_kernel_options_settable_in_process():
     (with or without the ENCX_ prefix) and restorable; unknown names are refused."""
     from encx import _lib as L
     opts = L.options()
-    assert {'FFT', 'RB_PREFETCH', 'FWR_VARIANT', 'DGR_VARIANT', 'LSTM_FUSE', 'PW'} <= set(opts)
+    assert {'FFT', 'LSTM_FUSE', 'PW', 'FWR', 'DGR', 'WGR'} <= set(opts)
     assert opts['FFT'] == int(os.environ.get('ENCX_FFT', 1))
-    with L.option(DGR_VARIANT=5, RB_PREFETCH=1):
-        assert L.get_option('DGR_VARIANT') == 5 and L.get_option('ENCX_RB_PREFETCH') == 1
+    with L.option(DGR=7, LSTM_FUSE=1):
+        assert L.get_option('DGR') == 7 and L.get_option('ENCX_LSTM_FUSE') == 1
     assert L.options() == opts
     lib = _lib()
     assert lib.encx_set_option(b'NO_SUCH_OPTION', 1, None) == 9001

@@ -357,17 +357,14 @@ def test_lstm_vs_oracle(B, H, Tn, L, fuse):
 
 
 # --------------------------------------------------------------------------- fused residual block
-@pytest.mark.parametrize('prefetch', [0, 1], ids=['jit', 'prefetch'])
 @pytest.mark.parametrize('C,T,B', [(32, 2048, 3), (32, 24000, 2), (64, 12000, 2), (64, 3001, 3), (32, 2113, 1)])
-def test_fused_resblock_vs_torch_fp64(C, T, B, prefetch):
+def test_fused_resblock_vs_torch_fp64(C, T, B):
     """ops.ResBlockFn (csrc/resblock.hip: SEANetResnetBlock, modules/seanet.py:46-63, as one
     kernel per direction) against torch's fp64 restatement of the block: ELU -> reflect-padded
     causal k3 conv (C -> C/2) -> ELU -> 1x1 conv (C/2 -> C), plus the 1x1 shortcut, all weight
     normed. Output, input grad and every weight / bias grad under a seeded output grad, relative to
-    each tensor's largest magnitude; incl. T not a multiple of the 64-position tile. For both
-    tile-staging variants (option RB_PREFETCH)."""
+    each tensor's largest magnitude; incl. T not a multiple of the 64-position tile."""
     from encx import ops
-    from encx._lib import option
     g = torch.Generator().manual_seed(C * 7 + T)
     HD = C // 2
 
@@ -391,9 +388,8 @@ def test_fused_resblock_vs_torch_fp64(C, T, B, prefetch):
     leaves = [t.detach().float().to(DEV).requires_grad_(True) for t in leaves64]
     x = leaves[0]
     p = [leaves[1:4], leaves[4:7], leaves[7:10]]
-    with option(RB_PREFETCH=prefetch):
-        y = ops.resblock(x, *p)
-        mine = torch.autograd.grad(y, leaves, dy64.float().to(DEV))
+    y = ops.resblock(x, *p)
+    mine = torch.autograd.grad(y, leaves, dy64.float().to(DEV))
 
     def rel(a, b):
         a, b = a.detach().double().cpu(), b.detach().double()
