@@ -206,6 +206,21 @@ def test_slope_mask_audit_flags_only_real_sign_errors():
     logs[torch.float64][3] = (z64, bad.view_as(m))
     with pytest.raises(AssertionError):
         check_masks(logs[torch.float64], logs[torch.float32], 'one flipped slope')
+    # the per-element rule: a flip at an element with little rounding error of its own is caught
+    # even where |z64| is below 4x the map's LARGEST error (the map-wide rule let those pass)
+    logs[torch.float64][3] = (z64, m)
+    for k, ((za64, mk), (za32, _)) in enumerate(zip(logs[torch.float64], logs[torch.float32])):
+        za, err = za64.double().reshape(-1).abs(), (za32.double() - za64.double()).reshape(-1).abs()
+        cand = (za < 4 * float(err.max())) & (za > 4.5 * err.clamp_min(float(err[za > 0].median())))
+        if bool(cand.any()):
+            break
+    assert bool(cand.any())
+    j = int(torch.nonzero(cand)[0])
+    bad = mk.clone().reshape(-1)
+    bad[j] = ~bad[j]
+    logs[torch.float64][k] = (za64, bad.view_as(mk))
+    with pytest.raises(AssertionError, match='rounding'):
+        check_masks(logs[torch.float64], logs[torch.float32], 'one flip within the map-wide bound')
 
 
 # --------------------------------------------------------------------------- G6 balancer
