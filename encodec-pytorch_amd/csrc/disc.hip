@@ -1144,6 +1144,81 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
 // (t, u), reduction (co, kt) pairs x JC taps; the staged B image is dy * LeakyReLU'(y), both
 // read as aligned quads (dy columns [base, base + RLp), base = the window start rounded down to
 // a multiple of 4) and masked in the commit.
+// c2_dgradr_kernel's epilogue, its terms fixed at compile time (MODE bits as rw_dg_epi): no
+// branches around the loads, and the output never aliases the maps read, so the 8 row pairs of a
+// (row tile, column tile) are loaded together, then combined and stored.
+template <int TM, int TN, int MODE>
+ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0, int nl, int nend, int U, int M,
+                      int S, int lane, float fc) {
+    constexpr bool F = MODE & 1, XM = MODE & 2, XL = MODE & 4, A = MODE & 8, LX = F || XL;
+    const C2Geo& g = a.g;
+    const float* __restrict__ xs = XL ? a.xact : a.ffx;
+    const float* __restrict__ rs = a.ffr;
+    float* __restrict__ dx = a.dx;
+    auto combine = [&](float u, float x, float r, float d) {
+        if (F) {
+            const float e = x - r;
+            u += e > 0.f ? fc : (e < 0.f ? -fc : 0.f);
+        }
+        if (XM) u *= lrelu_grad(x);
+        return A ? d + u : u;
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = nl + j * 32;
+            if (n >= nend) continue;
+            const int tr = n / U, u = n - tr * U;
+            if (S == 2) {
+                // rows m, m + 1 (registers r, r + 1) are phases 0 / 1 of the same ci: the two
+                // adjacent f of this column, one 8-byte access
+                const int f = 2 * u - g.pf;
+                if (f >= 0 && f + 1 < g.Fi && m0 + i * 32 + 32 <= M) {
+                    int64_t o[8];
+                    f32x2u X[8], R[8], D[8];
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) {
+                        const int m = m0 + i * 32 + mfma_row(2 * p, lane);
+                        o[p] = (((int64_t)b * g.Ci + (m >> 1)) * g.T2 + tr) * g.Fi + f;
+                        if (LX) X[p] = *(const f32x2u*)(xs + o[p]);
+                        if (F) R[p] = *(const f32x2u*)(rs + o[p]);
+                        if (A) D[p] = *(const f32x2u*)(dx + o[p]);
+                    }
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) {
+                        f32x2u s2;
+#pragma unroll
+                        for (int e = 0; e < 2; ++e)
+                            s2[e] = combine(acc[i][j][2 * p + e], LX ? X[p][e] : 0.f, F ? R[p][e] : 0.f,
+                                            A ? D[p][e] : 0.f);
+                        *(f32x2u*)(dx + o[p]) = s2;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m0 + i * 32 + mfma_row(r, lane);
+                        const int fe = f + (r & 1);
+                        if (m >= M || fe < 0 || fe >= g.Fi) continue;
+                        const int64_t q = (((int64_t)b * g.Ci + (m >> 1)) * g.T2 + tr) * g.Fi + fe;
+                        dx[q] = combine(acc[i][j][r], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f);
+                    }
+                }
+                continue;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + i * 32 + mfma_row(r, lane);
+                if (m >= M) continue;
+                const int ci = m / S, rr = m - ci * S;
+                const int f = u * S + rr - g.pf;
+                if (f < 0 || f >= g.Fi) continue;
+                const int64_t q = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
+                dx[q] = combine(acc[i][j][r], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f);
+            }
+        }
+}
+
 template <int TM, int BN, int JC, int MQ, int CKM, int OCC = 1, int DB = 0, bool YM = true>
 __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
     constexpr int BM = 32 * TM, TN = BN / 128, MW = (JC * CKM * BM / 4 + NT - 1) / NT;
@@ -1330,61 +1405,17 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
             compute(Xs, As);
         }
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wn0 + j * 32 + l32;
-            if (n >= nend) continue;
-            const int tr = n / U, u = n - tr * U;
-            if (S == 2) {
-                // rows m, m + 1 (registers r, r + 1) are phases 0 / 1 of the same ci: the two
-                // adjacent f of this column, stored (and masked) as one 8-byte access
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                    const int m = m0 + i * 32 + mfma_row(r, lane);
-                    if (m >= M) continue;
-                    const int f = 2 * u - g.pf;
-                    const int64_t o = (((int64_t)b * g.Ci + (m >> 1)) * g.T2 + tr) * g.Fi + f;
-                    float v0 = acc[i][j][r], v1 = acc[i][j][r + 1];
-                    if (f >= 0 && f + 1 < g.Fi) {
-                        f32x2u xa;
-                        if (a.ffr) {
-                            const f32x2u x2 = *(const f32x2u*)(a.ffx + o), r2 = *(const f32x2u*)(a.ffr + o);
-                            const float d0 = x2[0] - r2[0], d1 = x2[1] - r2[1];
-                            v0 += d0 > 0.f ? fc : (d0 < 0.f ? -fc : 0.f);
-                            v1 += d1 > 0.f ? fc : (d1 < 0.f ? -fc : 0.f);
-                            xa = x2;
-                        }
-                        if (a.xact) {
-                            if (!(a.ffr && a.ffx == a.xact)) xa = *(const f32x2u*)(a.xact + o);
-                            v0 *= lrelu_grad(xa[0]);
-                            v1 *= lrelu_grad(xa[1]);
-                        }
-                        if (a.accumulate) {
-                            const f32x2u t = *(const f32x2u*)(a.dx + o);
-                            v0 += t[0];
-                            v1 += t[1];
-                        }
-                        *(f32x2u*)(a.dx + o) = (f32x2u){v0, v1};
-                    } else {
-                        if (f >= 0 && f < g.Fi) a.dx[o] = dg_out(a, fc, o, v0);
-                        if (f + 1 >= 0 && f + 1 < g.Fi) a.dx[o + 1] = dg_out(a, fc, o + 1, v1);
-                    }
-                }
-                continue;
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + i * 32 + mfma_row(r, lane);
-                if (m >= M) continue;
-                const int ci = m / S, rr = m - ci * S;
-                const int f = u * S + rr - g.pf;
-                if (f < 0 || f >= g.Fi) continue;
-                const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
-                a.dx[o] = dg_out(a, fc, o, acc[i][j][r]);
-            }
-        }
+    // epilogue (dgr_epi): the feature-matching term, LeakyReLU'(x), accumulate
+    const bool ldx = a.xact && !(a.ffr && a.ffx == a.xact);
+    const int mode = (a.ffr ? 1 : 0) | (a.xact ? 2 : 0) | (ldx ? 4 : 0) | (a.accumulate ? 8 : 0);
+    switch (mode) {
+#define ENCX_EPI(m) \
+    case m: dgr_epi<TM, TN, m>(a, acc, b, m0, n0 + wn0 + l32, nend, U, M, S, lane, fc); break;
+        ENCX_EPI(0) ENCX_EPI(1) ENCX_EPI(3) ENCX_EPI(6) ENCX_EPI(7)
+        ENCX_EPI(8) ENCX_EPI(9) ENCX_EPI(11) ENCX_EPI(14) ENCX_EPI(15)
+#undef ENCX_EPI
+        default: break;
+    }
 }
 
 
@@ -1403,6 +1434,116 @@ struct C2DgR {
     int U4;     // quads per polyphase row
     int tiles;  // ceil(B * T2 * U4 / 32)
 };
+// c2_dgrad_rw_kernel's epilogue for one item, the combination of its terms fixed at compile time
+// (MODE bits: 1 feature term, 2 LeakyReLU'(x), 4 x read from xact (else from ffx), 8 accumulate),
+// so the per-quad code has no branches around its loads: with them, every load sat in its own
+// basic block behind a wait, one memory round trip per quad. The output never aliases the maps
+// read here, so the loads of EP rows are issued together, then combined and stored.
+template <int S, int TM, int MODE>
+ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int lane, int b, int t, int u0, float fc) {
+    constexpr bool F = MODE & 1, XM = MODE & 2, XL = MODE & 4, A = MODE & 8, LX = F || XL;
+    constexpr int EP = 2;  // S == 2: ci rows (2 phases x 2 quads each) per batch; S == 1: 2 EP rows
+    const C2Geo& g = a.g;
+    const float* __restrict__ xs = XL ? a.xact : a.ffx;
+    const float* __restrict__ rs = a.ffr;
+    float* __restrict__ dx = a.dx;
+    auto combine = [&](float u, float x, float r, float d) {
+        if (F) {
+            const float e = x - r;
+            u += e > 0.f ? fc : (e < 0.f ? -fc : 0.f);
+        }
+        if (XM) u *= lrelu_grad(x);
+        return A ? d + u : u;
+    };
+    if (S == 2) {  // registers r, r + 1 are phases 0 / 1 of one ci: with the 4 columns, 8 consecutive f
+        const int f = 2 * u0 - g.pf;
+        const bool inb = f >= 0 && f + 8 <= g.Fi;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r0 = 0; r0 < 16; r0 += 2 * EP) {
+                int64_t o[EP];
+#pragma unroll
+                for (int p = 0; p < EP; ++p) {
+                    const int ci = ((rt * TM + i) * 32 + mfma_row(r0 + 2 * p, lane)) >> 1;
+                    o[p] = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
+                }
+                auto val = [&](int p, int e8) { return acc[i][e8 >> 1][r0 + 2 * p + (e8 & 1)]; };
+                if (inb) {
+                    f32x4 X[EP][2], R[EP][2], D[EP][2];
+#pragma unroll
+                    for (int p = 0; p < EP; ++p)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            if (LX) X[p][h] = ld4u(xs + o[p] + 4 * h);
+                            if (F) R[p][h] = ld4u(rs + o[p] + 4 * h);
+                            if (A) D[p][h] = ld4u(dx + o[p] + 4 * h);
+                        }
+#pragma unroll
+                    for (int p = 0; p < EP; ++p)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            f32x4 s4;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                s4[e] = combine(val(p, 4 * h + e), LX ? X[p][h][e] : 0.f, F ? R[p][h][e] : 0.f,
+                                                A ? D[p][h][e] : 0.f);
+                            *(f32x4u*)(dx + o[p] + 4 * h) = s4;
+                        }
+                } else {
+#pragma unroll
+                    for (int p = 0; p < EP; ++p)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            if (f + e >= 0 && f + e < g.Fi) {
+                                const int64_t q = o[p] + e;
+                                dx[q] = combine(val(p, e), LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f);
+                            }
+                }
+            }
+    } else {
+        const int f = u0 - g.pf;
+        const bool inb = f >= 0 && f + 4 <= g.Fi;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r0 = 0; r0 < 16; r0 += 2 * EP) {
+                int64_t o[2 * EP];
+#pragma unroll
+                for (int p = 0; p < 2 * EP; ++p) {
+                    const int ci = (rt * TM + i) * 32 + mfma_row(r0 + p, lane);
+                    o[p] = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
+                }
+                if (inb) {
+                    f32x4 X[2 * EP], R[2 * EP], D[2 * EP];
+#pragma unroll
+                    for (int p = 0; p < 2 * EP; ++p) {
+                        if (LX) X[p] = ld4u(xs + o[p]);
+                        if (F) R[p] = ld4u(rs + o[p]);
+                        if (A) D[p] = ld4u(dx + o[p]);
+                    }
+#pragma unroll
+                    for (int p = 0; p < 2 * EP; ++p) {
+                        f32x4 s4;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            s4[e] = combine(acc[i][e][r0 + p], LX ? X[p][e] : 0.f, F ? R[p][e] : 0.f, A ? D[p][e] : 0.f);
+                        *(f32x4u*)(dx + o[p]) = s4;
+                    }
+                } else {
+#pragma unroll
+                    for (int p = 0; p < 2 * EP; ++p)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (f + e >= 0 && f + e < g.Fi) {
+                                const int64_t q = o[p] + e;
+                                dx[q] = combine(acc[i][e][r0 + p], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f);
+                            }
+                }
+            }
+    }
+}
+
 template <int J, int S, int RT, int WQ, bool YM, int NWV, int TM>
 __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
     // RT row tiles of 32 (M = Ci*S = 32 RT); a work item is (column tile, TM row tiles); the
@@ -1508,85 +1649,17 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
                 }
             }
         }
-        // ---- epilogue
+        // ---- epilogue (rw_dg_epi): the feature-matching term, LeakyReLU'(x), accumulate
         if (tile * 32 + l >= quads) continue;
-        if (S == 2) {
-            // registers r, r + 1 are phases 0 / 1 of one ci: with the 4 columns, 8 consecutive f
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                    const int ci = ((rt * TM + i) * 32 + mfma_row(r, lane)) >> 1;
-                    const int f = 2 * u0 - g.pf;
-                    const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
-                    float v[8];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        v[2 * j] = acc[i][j][r];
-                        v[2 * j + 1] = acc[i][j][r + 1];
-                    }
-                    if (f >= 0 && f + 8 <= g.Fi) {
-#pragma unroll
-                        for (int hq = 0; hq < 2; ++hq) {
-                            f32x4 x4, r4, d4;
-                            if (a.ffr) {
-                                x4 = ld4u(a.ffx + o + 4 * hq);
-                                r4 = ld4u(a.ffr + o + 4 * hq);
-                            }
-                            if (a.xact && !(a.ffr && a.ffx == a.xact)) x4 = ld4u(a.xact + o + 4 * hq);
-                            if (a.accumulate) d4 = ld4u(a.dx + o + 4 * hq);
-                            f32x4 s4;
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) {
-                                float u = v[4 * hq + e];
-                                if (a.ffr) {
-                                    const float d = x4[e] - r4[e];
-                                    u += d > 0.f ? fc : (d < 0.f ? -fc : 0.f);
-                                }
-                                if (a.xact) u *= lrelu_grad(x4[e]);
-                                s4[e] = a.accumulate ? d4[e] + u : u;
-                            }
-                            *(f32x4u*)(a.dx + o + 4 * hq) = s4;
-                        }
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 8; ++e)
-                            if (f + e >= 0 && f + e < g.Fi) a.dx[o + e] = dg_out(a, fc, o + e, v[e]);
-                    }
-                }
-        } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int ci = (rt * TM + i) * 32 + mfma_row(r, lane);
-                    const int f = u0 - g.pf;
-                    const int64_t o = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
-                    if (f >= 0 && f + 4 <= g.Fi) {
-                        f32x4 x4, r4, d4, s4;
-                        if (a.ffr) {
-                            x4 = ld4u(a.ffx + o);
-                            r4 = ld4u(a.ffr + o);
-                        }
-                        if (a.xact && !(a.ffr && a.ffx == a.xact)) x4 = ld4u(a.xact + o);
-                        if (a.accumulate) d4 = ld4u(a.dx + o);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            float u = acc[i][e][r];
-                            if (a.ffr) {
-                                const float d = x4[e] - r4[e];
-                                u += d > 0.f ? fc : (d < 0.f ? -fc : 0.f);
-                            }
-                            if (a.xact) u *= lrelu_grad(x4[e]);
-                            s4[e] = a.accumulate ? d4[e] + u : u;
-                        }
-                        *(f32x4u*)(a.dx + o) = s4;
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (f + e >= 0 && f + e < g.Fi) a.dx[o + e] = dg_out(a, fc, o + e, acc[i][e][r]);
-                    }
-                }
+        const bool ldx = a.xact && !(a.ffr && a.ffx == a.xact);  // x from xact (else from ffx)
+        const int mode = (a.ffr ? 1 : 0) | (a.xact ? 2 : 0) | (ldx ? 4 : 0) | (a.accumulate ? 8 : 0);
+        switch (mode) {
+#define ENCX_EPI(m) \
+    case m: rw_dg_epi<S, TM, m>(a, acc, rt, lane, b, t, u0, fc); break;
+            ENCX_EPI(0) ENCX_EPI(1) ENCX_EPI(3) ENCX_EPI(6) ENCX_EPI(7)
+            ENCX_EPI(8) ENCX_EPI(9) ENCX_EPI(11) ENCX_EPI(14) ENCX_EPI(15)
+#undef ENCX_EPI
+            default: break;  // (xact without its own load needs ffr: modes 2, 10 do not occur)
         }
     }
 }
