@@ -195,20 +195,18 @@ def main():
         lib.encx_prof_enable(0)
         achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         # traffic: HBM bytes per conv-family ABI call from the committed rocprofv3 PMC passes
-        # (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic.py); null when no pass exists for the config
-        traffic = traffic_cons = None
+        # (FETCH_SIZE x2 + WRITE_SIZE, calibrated: tools/traffic.py); null when no pass exists
+        traffic = None
         tpath = next((p for p in (os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', r,
-                                               f'traffic_{args.config}.json') for r in ('r04', 'r03', 'r02'))
+                                               f'traffic_{args.config}.json') for r in ('r05', 'r04', 'r03', 'r02'))
                       if os.path.exists(p)), '')
         if os.path.exists(tpath) and launches:
             with open(tpath) as fh:
                 tj = json.load(fh)
             traffic = round(tj['hbm_bytes_per_step'] / (launches / args.steps))
-            if 'hbm_bytes_per_step_conservative' in tj:  # FETCH_SIZE x2 on every kernel
-                traffic_cons = round(tj['hbm_bytes_per_step_conservative'] / (launches / args.steps))
         roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': MI355X_FP32_PEAK_TFLOPS,
                 'unit': 'TFLOP/s', 'frac': round(achieved / MI355X_FP32_PEAK_TFLOPS, 4), 'traffic': traffic,
-                'traffic_conservative': traffic_cons, 'traffic_source': os.path.relpath(tpath) if tpath else None,
+                'traffic_source': os.path.relpath(tpath) if tpath else None,
                 'algorithmic_bytes_per_launch': round(by / launches) if launches else None,
                 'kernel': 'encx conv/convtr/conv2d fwd + bwd-data + bwd-weight (implicit-GEMM f32 MFMA)',
                 'launches': launches, 'kernel_ms_per_step': round(ms / args.steps, 3),

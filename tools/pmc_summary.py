@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc CSVs per kernel (last timed step of a bench run):
 python tools/pmc_summary.py gpurun_out/pmc1 [gpurun_out/pmc2 ...]
-FETCH_SIZE is doubled only for the kernels whose reads are dwordx4 loads (tools/traffic.py WIDE,
-the width MI355X_MICROARCH.md calibrates); the `x2` column says which rows got it."""
+FETCH_SIZE is doubled for every kernel: on gfx950 it reports half the bytes read for 16-B aligned,
+16-B unaligned, 8-B and 4-B loads alike (tools/mb/fetch_calib.hip, profiles/r05/fetch_calibration.md)."""
 import collections
 import csv
 import os
@@ -9,10 +9,7 @@ import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from traffic import WIDE  # noqa: E402
 
-# non-conv kernels that also read with dwordx4 loads (gemm.h loaders, LSTM, RVQ, mel, Adam)
-WIDE_OTHER = re.compile(r'gemm_kernel|lstm_|rvq_argmin_mfma|adam_kernel|mel_loss_kernel')
 
 
 def load(d):
@@ -42,8 +39,8 @@ def main():
                     per[k][c] += x
     rows = sorted(per.items(), key=lambda kv: -kv[1]["_ns"])[:int(os.environ.get("PMC_TOP", "28"))]
     print('| kernel | calls | us/call | mfma busy | wait any | wait inst | lds conf | vgpr | lds B | fetch MB/call | '
-          'write MB/call | HBM GB/s | x2 |')
-    print('|---|---|---|---|---|---|---|---|---|---|---|---|---|')
+          'write MB/call | HBM GB/s |')
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     for k, v in rows:
         n = cnt[k]
         wc = v.get('SQ_WAVE_CYCLES', 0) or 1
@@ -51,14 +48,13 @@ def main():
         mb = v.get('SQ_VALU_MFMA_BUSY_CYCLES', 0)
         gui = v.get('GRBM_GUI_ACTIVE', 0)
         busy = mb / (gui / 8 * 256 * 4) if gui else float('nan')
-        wide = bool(WIDE.search(k) or WIDE_OTHER.search(k))
-        fetch = v.get('FETCH_SIZE', 0) / n / 1024 * (2 if wide else 1)  # KB -> MB; x2 gfx950 half-count
+        fetch = v.get('FETCH_SIZE', 0) / n / 1024 * 2  # KB -> MB; x2: gfx950 counts half (calibrated)
         write = v.get('WRITE_SIZE', 0) / n / 1024
         gbs = (fetch + write) / max(v['_ns'] / n / 1e3, 1e-9) * 1e3  # MB per us = TB/s -> GB/s
         print(f"| `{k}` | {n} | {v['_ns'] / n / 1e3:.1f} | {busy:.2f} | {v.get('SQ_WAIT_ANY', 0) / wc:.2f} | "
               f"{v.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | "
               f"{v.get('SQ_LDS_BANK_CONFLICT', 0) / max(1, v.get('SQ_LDS_IDX_ACTIVE', 0)):.2f} | {v['_vgpr']:.0f} | "
-              f"{v['_lds']:.0f} | {fetch:.1f} | {write:.1f} | {gbs:.0f} | {'x2' if wide else '-'} |")
+              f"{v['_lds']:.0f} | {fetch:.1f} | {write:.1f} | {gbs:.0f} |")
 
 
 if __name__ == '__main__':

@@ -5,13 +5,11 @@
 
 --fetch / --write: output dirs of `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs (one
 counter block per pass) of `bench.py --steps S --warmup W --no-roofline`; --steps = S + W (every
-train step the profiled process ran). Corrections as in MI355X_MICROARCH.md "HBM": counters are in
-KiB; FETCH_SIZE is doubled ONLY for the kernels whose reads are 16-byte-per-lane (dwordx4) loads,
-the access width the guide calibrates (gfx950 tallies their 128-B requests at 64 B); the kernels
-that read with 4-byte loads (the fixed-order slab reductions, the one-channel post conv, the
-first-layer forward) are left uncorrected, as the guide leaves other widths uncalibrated. Both
-lists are written into the output. The result is per train step and per conv-family ABI call
-(bench.py reads it into roofline.traffic)."""
+train step the profiled process ran). Corrections, calibrated on this GPU (tools/mb/fetch_calib.hip,
+profiles/r05/fetch_calibration.md: 512 MiB read once with 16-B aligned, 16-B unaligned, 8-B and 4-B
+loads, and written with 16-B and 4-B stores): counters are in KiB; FETCH_SIZE reports half the bytes
+read for EVERY load width (so x2 on every kernel), WRITE_SIZE the bytes written exactly. The result
+is per train step and per conv-family ABI call (bench.py reads it into roofline.traffic)."""
 import argparse
 import collections
 import csv
@@ -37,24 +35,16 @@ def per_dispatch(d, counter):
     return out, names
 
 
-# conv-family kernels whose operand reads are dwordx4 (ld4u / f32x4) loads
-WIDE = re.compile(r'conv_fwd_kernel|conv_poly_kernel|conv_wgrad_kernel|pw_kernel|pw_wgrad_kernel|'
-                  r'LdConvFlat|LdPolyFlat|c2_fwd_rw|c2_dgrad_rw|c2_wgrad_rw|c2_fwdr|c2_dgradr|c2_wgrad3|'
-                  r'c2_dgrad_narrow')
-
-
-def family_kib(d, counter, split=False):
+def family_kib(d, counter):
+    """-> (KiB over the conv-family dispatches, dispatch count, kernel names)."""
     vals, names = per_dispatch(d, counter)
-    tot, wide, n = 0.0, 0.0, 0
-    kinds = {'wide': set(), 'narrow': set()}
+    tot, n, kinds = 0.0, 0, set()
     for k, v in vals.items():
         if FAMILY.search(names[k]):
             tot += v
             n += 1
-            w = bool(WIDE.search(names[k]))
-            wide += v if w else 0.0
-            kinds['wide' if w else 'narrow'].add(re.sub(r'[<(].*', '', names[k].replace('(anonymous namespace)::', '')).replace('void ', ''))
-    return (tot, wide, n, kinds) if split else (tot, n)
+            kinds.add(re.sub(r'[<(].*', '', names[k].replace('(anonymous namespace)::', '')).replace('void ', ''))
+    return tot, n, kinds
 
 
 def main():
@@ -67,23 +57,20 @@ def main():
                     help='conv-family ABI calls per step (bench roofline "launches" / steps)')
     ap.add_argument('--out', required=True)
     args = ap.parse_args()
-    f_kib, f_wide, nf, kinds = family_kib(args.fetch, 'FETCH_SIZE', split=True)
-    w_kib, nw = family_kib(args.write, 'WRITE_SIZE')
-    fetch = (f_kib + f_wide) * 1024 / args.steps  # x2 on the wide-load kernels only
+    f_kib, nf, kinds = family_kib(args.fetch, 'FETCH_SIZE')
+    w_kib, nw, _ = family_kib(args.write, 'WRITE_SIZE')
+    fetch = 2 * f_kib * 1024 / args.steps  # calibrated: x2 for every load width (gfx950)
     write = w_kib * 1024 / args.steps
     res = {'config': args.config, 'fetch_bytes_per_step': fetch, 'write_bytes_per_step': write,
            'hbm_bytes_per_step': fetch + write, 'kernel_dispatches_per_step': nf / args.steps,
            'fetch_bytes_per_step_uncorrected': f_kib * 1024 / args.steps,
-           # every conv-family kernel's FETCH_SIZE doubled (the upper bound if the narrow-load
-           # kernels' requests are tallied at half size too; their width is uncalibrated)
-           'hbm_bytes_per_step_conservative': 2 * f_kib * 1024 / args.steps + write,
-           'correction': 'FETCH_SIZE x2 on the dwordx4-load kernels only (gfx950), KiB -> bytes',
-           'fetch_x2_kernels': sorted(kinds['wide']), 'fetch_uncorrected_kernels': sorted(kinds['narrow']),
+           'correction': 'FETCH_SIZE x2 on every kernel (calibrated for 16-B aligned / unaligned, 8-B and '
+                         '4-B loads: profiles/r05/fetch_calibration.md), WRITE_SIZE x1; KiB -> bytes',
+           'kernels': sorted(kinds),
            'steps_profiled': args.steps}
     if args.calls_per_step:
         res['abi_calls_per_step'] = args.calls_per_step
         res['hbm_bytes_per_call'] = (fetch + write) / args.calls_per_step
-        res['hbm_bytes_per_call_conservative'] = res['hbm_bytes_per_step_conservative'] / args.calls_per_step
     json.dump(res, open(args.out, 'w'), indent=1)
     print(json.dumps(res))
 
