@@ -34,7 +34,7 @@ struct OptDef {
 };
 constexpr OptDef kOpts[OPT_COUNT] = {
     {"FFT", 1}, {"PW", 1}, {"PW_WG_TMAX", 12000}, {"LSTM_FUSE", 0}, {"FWR", 256}, {"DGR", 256},
-    {"WGR", 2048}, {"WGR_WGS", 256},
+    {"WGR", 2048}, {"WGR_WGS", 256}, {"FEAT_CODE", 1}, {"CONV_CK", 64}, {"CONV_SPLIT", 1024}, {"CONV_WG_SPLIT", 1024},
 };
 std::atomic<int64_t> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;

@@ -179,6 +179,10 @@ enum EncxOpt {
     OPT_DGR,           // register-window Conv2d bwd-data: workgroups (0: off)
     OPT_WGR,           // register-window Conv2d weight grad: waves (0: off)
     OPT_WGR_WGS,       // its 8-wave workgroup form: workgroups (0: one-wave form)
+    OPT_FEAT_CODE,     // Conv2d bwd-data feature term from the pair's 1-byte code (else both maps)
+    OPT_CONV_CK,       // conv1d fwd / bwd-data: reduction elements (channels x taps) per LDS chunk
+    OPT_CONV_SPLIT,    // conv1d fwd / bwd-data: split-K until this many workgroups
+    OPT_CONV_WG_SPLIT, // conv1d weight grad: split the positions until this many workgroups
     OPT_COUNT
 };
 int64_t encx_opt(EncxOpt id);

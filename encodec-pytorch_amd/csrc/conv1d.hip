@@ -973,7 +973,7 @@ static int even_up(int v) { return (v + 1) & ~1; }
 // channels per LDS stage: ~64 reduction elements, even, and preferably dividing C exactly
 // (a ragged last chunk is zero-padded MFMA work)
 static int pick_ck(int C, int taps) {
-    int cap = 64 / taps;
+    int cap = (int)encx_opt(OPT_CONV_CK) / taps;  // default 64 reduction elements
     if (cap < 2) cap = 2;
     cap = even_up(cap);
     if (cap >= C) return even_up(C);
@@ -996,8 +996,9 @@ static int tile_bn(Tile t) { return (t == T128x32) ? 32 : (t == T64x64 || t == T
 static void plan_split(int64_t blocks, int C, int CK, int* KS, int* cps) {
     int nch = (C + CK - 1) / CK;
     int ks = 1;
-    if (blocks < 1024 && nch >= 4) {
-        ks = (int)cdiv(1024, blocks);
+    const int64_t target = encx_opt(OPT_CONV_SPLIT);  // workgroups to aim for (default 1024)
+    if (blocks < target && nch >= 4) {
+        ks = (int)cdiv(target, blocks);
         if (ks > nch / 2) ks = nch / 2;
         if (ks > 16) ks = 16;
         if (ks < 1) ks = 1;
@@ -1503,7 +1504,7 @@ static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K)
         p.tiles = (int)(cdiv(N, p.BN) * cdiv(A, p.BM));
     }
     p.items = (int)(B * cdiv(Tl, p.BT));
-    constexpr int64_t target = 1024;  // ~1024 workgroups in flight
+    const int64_t target = encx_opt(OPT_CONV_WG_SPLIT);  // ~1024 workgroups in flight
     int64_t want = cdiv(target, p.tiles);
     int64_t cap = (64ll << 20) / (4 * A * N);           // <= 64 MB of partials
     int64_t minper = cdiv(p.items, (int64_t)p.items >= 8 ? 8 : 1);

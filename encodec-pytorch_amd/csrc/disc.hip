@@ -956,7 +956,13 @@ struct C2Dg {
     const float* fden;  // mean |fr| of the pair
     const float* fg;    // upstream grad of the loss (null: 1)
     float fscale;
+    // optional per-element code of the pair (encx_feat_loss_code): bit 0 ffx > ffr, bit 1
+    // ffx < ffr, bit 2 ffx > 0. The register-window and tiled epilogues read it (1 byte) instead
+    // of ffx / ffr (8 bytes) when the mask comes from ffx or is absent
+    const uint8_t* fcode;
 };
+ENCX_DEV float code_term(uint32_t c, float fc) { return (c & 1u) ? fc : ((c & 2u) ? -fc : 0.f); }
+ENCX_DEV float code_mask(uint32_t c) { return (c & 4u) ? 1.f : 0.2f; }
 
 ENCX_DEV float feat_coef(const C2Dg& a) {
     return a.ffr ? (a.fg ? a.fg[0] : 1.f) * a.fscale / a.fden[0] : 0.f;
@@ -1150,17 +1156,21 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
 template <int TM, int TN, int MODE>
 ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0, int nl, int nend, int U, int M,
                       int S, int lane, float fc) {
-    constexpr bool F = MODE & 1, XM = MODE & 2, XL = MODE & 4, A = MODE & 8, LX = F || XL;
+    constexpr bool C = MODE & 16, F = (MODE & 1) && !C, XM = (MODE & 2) && !C, XL = MODE & 4, A = MODE & 8,
+                   LX = F || XL, CX = C && (MODE & 2);
     const C2Geo& g = a.g;
     const float* __restrict__ xs = XL ? a.xact : a.ffx;
     const float* __restrict__ rs = a.ffr;
+    const uint8_t* __restrict__ cs = a.fcode;
     float* __restrict__ dx = a.dx;
-    auto combine = [&](float u, float x, float r, float d) {
+    auto combine = [&](float u, float x, float r, float d, uint32_t c) {
         if (F) {
             const float e = x - r;
             u += e > 0.f ? fc : (e < 0.f ? -fc : 0.f);
         }
         if (XM) u *= lrelu_grad(x);
+        if (C) u += code_term(c, fc);
+        if (CX) u *= code_mask(c);
         return A ? d + u : u;
     };
 #pragma unroll
@@ -1177,6 +1187,7 @@ ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0,
                 if (f >= 0 && f + 1 < g.Fi && m0 + i * 32 + 32 <= M) {
                     int64_t o[8];
                     f32x2u X[8], R[8], D[8];
+                    uint32_t Cc[8][2];
 #pragma unroll
                     for (int p = 0; p < 8; ++p) {
                         const int m = m0 + i * 32 + mfma_row(2 * p, lane);
@@ -1184,6 +1195,10 @@ ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0,
                         if (LX) X[p] = *(const f32x2u*)(xs + o[p]);
                         if (F) R[p] = *(const f32x2u*)(rs + o[p]);
                         if (A) D[p] = *(const f32x2u*)(dx + o[p]);
+                        if (C) {
+                            Cc[p][0] = cs[o[p]];
+                            Cc[p][1] = cs[o[p] + 1];
+                        }
                     }
 #pragma unroll
                     for (int p = 0; p < 8; ++p) {
@@ -1191,7 +1206,7 @@ ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0,
 #pragma unroll
                         for (int e = 0; e < 2; ++e)
                             s2[e] = combine(acc[i][j][2 * p + e], LX ? X[p][e] : 0.f, F ? R[p][e] : 0.f,
-                                            A ? D[p][e] : 0.f);
+                                            A ? D[p][e] : 0.f, C ? Cc[p][e] : 0u);
                         *(f32x2u*)(dx + o[p]) = s2;
                     }
                 } else {
@@ -1201,7 +1216,8 @@ ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0,
                         const int fe = f + (r & 1);
                         if (m >= M || fe < 0 || fe >= g.Fi) continue;
                         const int64_t q = (((int64_t)b * g.Ci + (m >> 1)) * g.T2 + tr) * g.Fi + fe;
-                        dx[q] = combine(acc[i][j][r], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f);
+                        dx[q] = combine(acc[i][j][r], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f,
+                                        C ? (uint32_t)cs[q] : 0u);
                     }
                 }
                 continue;
@@ -1214,7 +1230,8 @@ ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0,
                 const int f = u * S + rr - g.pf;
                 if (f < 0 || f >= g.Fi) continue;
                 const int64_t q = (((int64_t)b * g.Ci + ci) * g.T2 + tr) * g.Fi + f;
-                dx[q] = combine(acc[i][j][r], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f);
+                dx[q] = combine(acc[i][j][r], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f,
+                                C ? (uint32_t)cs[q] : 0u);
             }
         }
 }
@@ -1407,12 +1424,14 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
     }
     // epilogue (dgr_epi): the feature-matching term, LeakyReLU'(x), accumulate
     const bool ldx = a.xact && !(a.ffr && a.ffx == a.xact);
-    const int mode = (a.ffr ? 1 : 0) | (a.xact ? 2 : 0) | (ldx ? 4 : 0) | (a.accumulate ? 8 : 0);
+    const int mode = (a.ffr ? 1 : 0) | (a.xact ? 2 : 0) | (ldx ? 4 : 0) | (a.accumulate ? 8 : 0) |
+                     (a.fcode && a.ffr && !ldx ? 16 : 0);
     switch (mode) {
 #define ENCX_EPI(m) \
     case m: dgr_epi<TM, TN, m>(a, acc, b, m0, n0 + wn0 + l32, nend, U, M, S, lane, fc); break;
         ENCX_EPI(0) ENCX_EPI(1) ENCX_EPI(3) ENCX_EPI(6) ENCX_EPI(7)
         ENCX_EPI(8) ENCX_EPI(9) ENCX_EPI(11) ENCX_EPI(14) ENCX_EPI(15)
+        ENCX_EPI(17) ENCX_EPI(19) ENCX_EPI(25) ENCX_EPI(27)
 #undef ENCX_EPI
         default: break;
     }
@@ -1441,18 +1460,23 @@ struct C2DgR {
 // read here, so the loads of EP rows are issued together, then combined and stored.
 template <int S, int TM, int MODE>
 ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int lane, int b, int t, int u0, float fc) {
-    constexpr bool F = MODE & 1, XM = MODE & 2, XL = MODE & 4, A = MODE & 8, LX = F || XL;
+    // MODE 16: the feature term (and LeakyReLU'(ffx)) from the 1-byte pair code
+    constexpr bool C = MODE & 16, F = (MODE & 1) && !C, XM = (MODE & 2) && !C, XL = MODE & 4, A = MODE & 8,
+                   LX = F || XL, CX = C && (MODE & 2);
     constexpr int EP = 2;  // S == 2: ci rows (2 phases x 2 quads each) per batch; S == 1: 2 EP rows
     const C2Geo& g = a.g;
     const float* __restrict__ xs = XL ? a.xact : a.ffx;
     const float* __restrict__ rs = a.ffr;
+    const uint8_t* __restrict__ cs = a.fcode;
     float* __restrict__ dx = a.dx;
-    auto combine = [&](float u, float x, float r, float d) {
+    auto combine = [&](float u, float x, float r, float d, uint32_t c) {
         if (F) {
             const float e = x - r;
             u += e > 0.f ? fc : (e < 0.f ? -fc : 0.f);
         }
         if (XM) u *= lrelu_grad(x);
+        if (C) u += code_term(c, fc);
+        if (CX) u *= code_mask(c);
         return A ? d + u : u;
     };
     if (S == 2) {  // registers r, r + 1 are phases 0 / 1 of one ci: with the 4 columns, 8 consecutive f
@@ -1471,14 +1495,20 @@ ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int l
                 auto val = [&](int p, int e8) { return acc[i][e8 >> 1][r0 + 2 * p + (e8 & 1)]; };
                 if (inb) {
                     f32x4 X[EP][2], R[EP][2], D[EP][2];
+                    uint32_t Cc[EP][8];
 #pragma unroll
-                    for (int p = 0; p < EP; ++p)
+                    for (int p = 0; p < EP; ++p) {
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
                             if (LX) X[p][h] = ld4u(xs + o[p] + 4 * h);
                             if (F) R[p][h] = ld4u(rs + o[p] + 4 * h);
                             if (A) D[p][h] = ld4u(dx + o[p] + 4 * h);
                         }
+                        if (C) {
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) Cc[p][e] = cs[o[p] + e];
+                        }
+                    }
 #pragma unroll
                     for (int p = 0; p < EP; ++p)
 #pragma unroll
@@ -1487,7 +1517,7 @@ ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int l
 #pragma unroll
                             for (int e = 0; e < 4; ++e)
                                 s4[e] = combine(val(p, 4 * h + e), LX ? X[p][h][e] : 0.f, F ? R[p][h][e] : 0.f,
-                                                A ? D[p][h][e] : 0.f);
+                                                A ? D[p][h][e] : 0.f, C ? Cc[p][4 * h + e] : 0u);
                             *(f32x4u*)(dx + o[p] + 4 * h) = s4;
                         }
                 } else {
@@ -1497,7 +1527,8 @@ ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int l
                         for (int e = 0; e < 8; ++e)
                             if (f + e >= 0 && f + e < g.Fi) {
                                 const int64_t q = o[p] + e;
-                                dx[q] = combine(val(p, e), LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f);
+                                dx[q] = combine(val(p, e), LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f,
+                                                C ? (uint32_t)cs[q] : 0u);
                             }
                 }
             }
@@ -1516,18 +1547,24 @@ ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int l
                 }
                 if (inb) {
                     f32x4 X[2 * EP], R[2 * EP], D[2 * EP];
+                    uint32_t Cc[2 * EP][4];
 #pragma unroll
                     for (int p = 0; p < 2 * EP; ++p) {
                         if (LX) X[p] = ld4u(xs + o[p]);
                         if (F) R[p] = ld4u(rs + o[p]);
                         if (A) D[p] = ld4u(dx + o[p]);
+                        if (C) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) Cc[p][e] = cs[o[p] + e];
+                        }
                     }
 #pragma unroll
                     for (int p = 0; p < 2 * EP; ++p) {
                         f32x4 s4;
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
-                            s4[e] = combine(acc[i][e][r0 + p], LX ? X[p][e] : 0.f, F ? R[p][e] : 0.f, A ? D[p][e] : 0.f);
+                            s4[e] = combine(acc[i][e][r0 + p], LX ? X[p][e] : 0.f, F ? R[p][e] : 0.f, A ? D[p][e] : 0.f,
+                                            C ? Cc[p][e] : 0u);
                         *(f32x4u*)(dx + o[p]) = s4;
                     }
                 } else {
@@ -1537,7 +1574,8 @@ ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int l
                         for (int e = 0; e < 4; ++e)
                             if (f + e >= 0 && f + e < g.Fi) {
                                 const int64_t q = o[p] + e;
-                                dx[q] = combine(acc[i][e][r0 + p], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f);
+                                dx[q] = combine(acc[i][e][r0 + p], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f,
+                                                C ? (uint32_t)cs[q] : 0u);
                             }
                 }
             }
@@ -1652,12 +1690,14 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
         // ---- epilogue (rw_dg_epi): the feature-matching term, LeakyReLU'(x), accumulate
         if (tile * 32 + l >= quads) continue;
         const bool ldx = a.xact && !(a.ffr && a.ffx == a.xact);  // x from xact (else from ffx)
-        const int mode = (a.ffr ? 1 : 0) | (a.xact ? 2 : 0) | (ldx ? 4 : 0) | (a.accumulate ? 8 : 0);
+        const int mode = (a.ffr ? 1 : 0) | (a.xact ? 2 : 0) | (ldx ? 4 : 0) | (a.accumulate ? 8 : 0) |
+                         (a.fcode && a.ffr && !ldx ? 16 : 0);
         switch (mode) {
 #define ENCX_EPI(m) \
     case m: rw_dg_epi<S, TM, m>(a, acc, rt, lane, b, t, u0, fc); break;
             ENCX_EPI(0) ENCX_EPI(1) ENCX_EPI(3) ENCX_EPI(6) ENCX_EPI(7)
             ENCX_EPI(8) ENCX_EPI(9) ENCX_EPI(11) ENCX_EPI(14) ENCX_EPI(15)
+            ENCX_EPI(17) ENCX_EPI(19) ENCX_EPI(25) ENCX_EPI(27)
 #undef ENCX_EPI
             default: break;  // (xact without its own load needs ffr: modes 2, 10 do not occur)
         }
@@ -2705,7 +2745,9 @@ __global__ __launch_bounds__(256) void hinge_kernel(const float* x, int64_t n, f
 }
 // parts[b] = (sum |fr - ff|, sum |fr|) over a grid-stride slice: float4 loads, 4 in flight per
 // operand and thread (n % 4 == 0, 16-byte aligned maps: torch allocations of 32-channel maps)
-__global__ __launch_bounds__(256) void feat_kernel(const float* fr, const float* ff, int64_t n, float* parts) {
+template <bool CODE>
+__global__ __launch_bounds__(256) void feat_kernel(const float* fr, const float* ff, int64_t n, float* parts,
+                                                   uint32_t* code) {
     __shared__ float red[16];
     const f32x4* r4 = (const f32x4*)fr;
     const f32x4* f4 = (const f32x4*)ff;
@@ -2723,11 +2765,15 @@ __global__ __launch_bounds__(256) void feat_kernel(const float* fr, const float*
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (i0 + u * stride < n4) {
+                uint32_t cw = 0;  // CODE: 4 bytes, one per element (code_term / code_mask)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
+                    const float d = fv[u][c] - rv[u][c];
                     s1 += fabsf(rv[u][c] - fv[u][c]);
                     s2 += fabsf(rv[u][c]);
+                    cw |= ((d > 0.f ? 1u : (d < 0.f ? 2u : 0u)) | (fv[u][c] > 0.f ? 4u : 0u)) << (8 * c);
                 }
+                if (CODE) code[i0 + u * stride] = cw;
             }
         }
     }
@@ -3411,15 +3457,16 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
                          int accumulate, int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
                          int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf,
                          encx_stream_t stream) {
-    return encx_conv2d_bwd_data_feat(dy, yact, wp, xact, dx, accumulate, nullptr, nullptr, nullptr, nullptr, 0.0, B,
+    return encx_conv2d_bwd_data_feat(dy, yact, wp, xact, dx, accumulate, nullptr, nullptr, nullptr, nullptr, 0.0,
+                                     nullptr, B,
                                      Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf, stream);
 }
 
 int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
                               int accumulate, const float* feat_real, const float* feat_fake, const float* feat_denom,
-                              const float* feat_g, double feat_scale, int64_t B, int64_t Ci, int64_t T2, int64_t Fi,
-                              int64_t Co, int64_t Fo, int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt,
-                              int64_t pf, encx_stream_t stream) {
+                              const float* feat_g, double feat_scale, const uint8_t* feat_code, int64_t B, int64_t Ci,
+                              int64_t T2, int64_t Fi, int64_t Co, int64_t Fo, int64_t KT, int64_t KF, int64_t sf,
+                              int64_t dt, int64_t pt, int64_t pf, encx_stream_t stream) {
     ENCX_REQUIRE(dy && wp && dx);
     ENCX_REQUIRE(!feat_real || (feat_fake && feat_denom));
     C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
@@ -3429,7 +3476,7 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
                        4.0 * (B * Ci * T2 * Fi * (feat_real ? 3 : 1) + 2 * B * Co * T2 * Fo), "c2_dgrad");
     ps.tag(" %ldx%ld %ldx%ld s%ld T%ld F%ld", (long)Ci, (long)Co, (long)KT, (long)KF, (long)sf, (long)T2, (long)Fo);
     C2Dg a{g, dy, yact, wp, xact, dx, 0, 0, 0, 0, 0, accumulate, feat_real, feat_fake, feat_denom, feat_g,
-           (float)feat_scale};
+           (float)feat_scale, feat_real && encx_opt(OPT_FEAT_CODE) ? feat_code : nullptr};
     constexpr int BN = 128;
     a.J = (int)cdiv(KF, sf);
     a.U = (int)((Fi - 1 + pf) / sf + 1);
@@ -3671,7 +3718,23 @@ int encx_feat_loss(const float* fr, const float* ff, int64_t n, double scale, fl
     encx_prof_scope ps((hipStream_t)stream, 4.0 * n, 8.0 * n, "feat", false);
     hipStream_t st = (hipStream_t)stream;
     const int nb = (int)min((int64_t)LP, cdiv(n, 1024));
-    hipLaunchKernelGGL(feat_kernel, dim3(nb), dim3(256), 0, st, fr, ff, n, ws);
+    hipLaunchKernelGGL(feat_kernel<false>, dim3(nb), dim3(256), 0, st, fr, ff, n, ws, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(loss_finish, dim3(1), dim3(256), 0, st, ws, nb, 2, (double)n, (float)scale, out, denom,
+                       accumulate);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+/* encx_feat_loss + the pair's per-element code (code[i] = [ff > fr] | 2 [ff < fr] | 4 [ff > 0], one
+ * byte per element, 4-byte aligned), which encx_conv2d_bwd_data_feat reads instead of the two maps. */
+int encx_feat_loss_code(const float* fr, const float* ff, int64_t n, double scale, float* out, float* denom,
+                        int accumulate, float* ws, uint8_t* code, encx_stream_t stream) {
+    ENCX_REQUIRE(fr && ff && out && ws && code && n > 0 && n % 4 == 0 && ((uintptr_t)fr & 15) == 0 &&
+                 ((uintptr_t)ff & 15) == 0 && ((uintptr_t)code & 3) == 0);
+    encx_prof_scope ps((hipStream_t)stream, 4.0 * n, 9.0 * n, "feat", false);
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = (int)min((int64_t)LP, cdiv(n, 1024));
+    hipLaunchKernelGGL(feat_kernel<true>, dim3(nb), dim3(256), 0, st, fr, ff, n, ws, (uint32_t*)code);
     hipLaunchKernelGGL(loss_finish, dim3(1), dim3(256), 0, st, ws, nb, 2, (double)n, (float)scale, out, denom,
                        accumulate);
     ENCX_CHECK_LAUNCH();

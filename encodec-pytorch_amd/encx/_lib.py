@@ -93,6 +93,8 @@ class _Lib:
                                    'or `make -C encodec-pytorch_amd`')
             lib = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in self.sigs.items():
+                if 'ENCX_LIB' in os.environ and not hasattr(lib, name):
+                    continue  # an A/B build of an older revision: entry points added since are absent
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
@@ -139,7 +141,7 @@ def options():
 
 
 class option:
-    """`with option(DGR_VARIANT=5, ...):` -- set options for a block, restore them after."""
+    """`with option(DGR=256, ...):` -- set options for a block, restore them after."""
 
     def __init__(self, **kv):
         self.kv = kv

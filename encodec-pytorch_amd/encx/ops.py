@@ -955,9 +955,9 @@ class Conv2dFn(torch.autograd.Function):
             if feat is None:
                 call('encx_conv2d_bwd_data', ptr(dy), ptr(yact), ptr(wp), ptr(xact), ptr(dx), 0, *dims, st)
             else:  # + FeatFn's grad of this input map, in the epilogue
-                fr, den, fg, fscale = feat
+                fr, den, fg, fscale, code = feat
                 call('encx_conv2d_bwd_data_feat', ptr(dy), ptr(yact), ptr(wp), ptr(xact), ptr(dx), 0, ptr(fr),
-                     ptr(x), ptr(den), ptr(fg), float(fscale), *dims, st)
+                     ptr(x), ptr(den), ptr(fg), float(fscale), ptr(code), *dims, st)
         elif feat is not None:
             raise RuntimeError('encx: a feature-matching grad was handed to a Conv2d whose input grad '
                                'is not computed')
@@ -1100,17 +1100,26 @@ class FeatFn(torch.autograd.Function):
         ws = _ws(lib.encx_disc_loss_workspace(), out)
         frs = [f.contiguous() for f in frs]
         ffs = [f.contiguous() for f in ffs]
-        for i, (fr, ff) in enumerate(zip(frs, ffs)):
-            _check(ff)
-            call('encx_feat_loss', ptr(fr), ptr(ff), ff.numel(), float(scale), ptr(out), ptr(denom[i:i + 1]),
-                 1, ptr(ws), stream())
-        ctx.save_for_backward(denom, *frs, *ffs)
-        ctx.scale, ctx.n = scale, n_pairs
         # park a map's grad only when the Conv2d reading it produces another map of this loss:
         # that Conv2d is then on every traversal from this loss and is sure to collect it
         slots = [getattr(f, '_encx_feat_slot', None) for f in maps[n_pairs:]]
         live = {id(sl) for sl in slots if sl is not None}
         ctx.slots = [sl if sl is not None and id(sl.consumer_out) in live else None for sl in slots]
+        # a parked pair also gets its 1-byte-per-element code (sign(ff - fr), ff > 0), which the
+        # reading Conv2d's bwd-data epilogue reads instead of both maps (encx_feat_loss_code)
+        ctx.codes = [None] * n_pairs
+        for i, (fr, ff) in enumerate(zip(frs, ffs)):
+            _check(ff)
+            if ctx.slots[i] is not None and ctx.needs_input_grad[2 + n_pairs + i]:
+                code = torch.empty(ff.numel(), device=ff.device, dtype=torch.uint8)
+                call('encx_feat_loss_code', ptr(fr), ptr(ff), ff.numel(), float(scale), ptr(out),
+                     ptr(denom[i:i + 1]), 1, ptr(ws), ptr(code), stream())
+                ctx.codes[i] = code
+            else:
+                call('encx_feat_loss', ptr(fr), ptr(ff), ff.numel(), float(scale), ptr(out), ptr(denom[i:i + 1]),
+                     1, ptr(ws), stream())
+        ctx.save_for_backward(denom, *frs, *ffs)
+        ctx.scale, ctx.n = scale, n_pairs
         for sl, parked in zip(slots, ctx.slots):
             if sl is not None and parked is None:
                 sl.autograd_feat = True  # a second gradient path into the map: its reader must not premask
@@ -1125,7 +1134,7 @@ class FeatFn(torch.autograd.Function):
         grads = [None] * (2 * n)
         for i, (fr, ff) in enumerate(zip(frs, ffs)):
             if ctx.needs_input_grad[2 + n + i] and ctx.slots[i] is not None:
-                ctx.slots[i].pending = (fr, denom[i:i + 1], g, ctx.scale)  # the reading Conv2d adds it
+                ctx.slots[i].pending = (fr, denom[i:i + 1], g, ctx.scale, ctx.codes[i])  # the reading Conv2d adds it
             elif ctx.needs_input_grad[2 + n + i]:
                 d = torch.empty_like(ff)
                 call('encx_feat_loss_bwd', ptr(fr), ptr(ff), ff.numel(), float(ctx.scale), ptr(denom[i:i + 1]),

@@ -373,9 +373,10 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
  * term is added before the xact mask: dx (+)= (d/dx + feature term) * LeakyReLU'(xact). */
 int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
                               int accumulate, const float* feat_real, const float* feat_fake,
-                              const float* feat_denom, const float* feat_g, double feat_scale, int64_t B,
-                              int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo, int64_t KT, int64_t KF,
-                              int64_t sf, int64_t dt, int64_t pt, int64_t pf, encx_stream_t stream);
+                              const float* feat_denom, const float* feat_g, double feat_scale,
+                              const uint8_t* feat_code /* may be NULL */, int64_t B, int64_t Ci, int64_t T2,
+                              int64_t Fi, int64_t Co, int64_t Fo, int64_t KT, int64_t KF, int64_t sf, int64_t dt,
+                              int64_t pt, int64_t pf, encx_stream_t stream);
 size_t encx_conv2d_bwd_weight_workspace(int64_t B, int64_t Ci, int64_t T2, int64_t Fi, int64_t Co, int64_t Fo,
                                         int64_t KT, int64_t KF, int64_t sf, int64_t dt, int64_t pt, int64_t pf);
 /* dw [Co][Ci][KT][KF] and db [Co] (either may be NULL), written or added (acc_w / acc_b). */
@@ -406,6 +407,11 @@ int encx_hinge_loss_bwd(const float* x, int64_t n, double s, double scale, const
 /* out[0] (+)= scale * mean|fr - ff| / mean|fr|; denom[0] = sum|fr| for the backward */
 int encx_feat_loss(const float* fr, const float* ff, int64_t n, double scale, float* out, float* denom,
                    int accumulate, float* ws, encx_stream_t stream);
+/* encx_feat_loss that also writes the pair's per-element code (1 byte each: bit 0 ff > fr, bit 1
+ * ff < fr, bit 2 ff > 0; `code` 4-byte aligned). encx_conv2d_bwd_data_feat given the code
+ * (feat_code) reads it in place of feat_real / feat_fake where its kernel supports it. */
+int encx_feat_loss_code(const float* fr, const float* ff, int64_t n, double scale, float* out, float* denom,
+                        int accumulate, float* ws, uint8_t* code, encx_stream_t stream);
 int encx_feat_loss_bwd(const float* fr, const float* ff, int64_t n, double scale, const float* denom,
                        const float* g0, float* dff, encx_stream_t stream);
 

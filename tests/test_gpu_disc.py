@@ -345,3 +345,50 @@ def test_conv2d_full_size_vs_torch_fp64(family):
         assert not bad, bad
     finally:
         lib.encx_conv2d_select(prev)
+
+
+@pytest.mark.parametrize('family', [1, 2], ids=['regwin', 'tiled'])
+@pytest.mark.parametrize('li,T2,Fi', [(1, 43, 1025), (2, 90, 257), (3, 184, 129), (4, 90, 65)])
+def test_feat_code_epilogue_bit_identical(li, T2, Fi, family):
+    """encx_conv2d_bwd_data_feat with the pair's 1-byte code (encx_feat_loss_code: sign(ff - fr),
+    ff > 0) against the same call reading both float maps: dx bit for bit, with the LeakyReLU'
+    mask from the fake map (premask) and without, accumulating and not, at config-3 layer sizes
+    (B 32) for each kernel family; and the loss and denominator of encx_feat_loss_code equal
+    encx_feat_loss's."""
+    from encx import ops
+    from encx._lib import lib, call, ptr, stream
+    Ci, Co, k, s, d, pad = LAYERS[li]
+    KT, KF, sf, dt, pt, pf, Fo = ops.conv2d_geometry(Fi, k, s, d, pad)
+    B = 32
+    g = torch.Generator(device=DEV).manual_seed(li * 7 + T2)
+    dy = torch.randn(B, Co, T2, Fo, generator=g, device=DEV)
+    y = torch.randn(B, Co, T2, Fo, generator=g, device=DEV)
+    ff = torch.randn(B, Ci, T2, Fi, generator=g, device=DEV)
+    fr = ff + 0.3 * torch.randn(B, Ci, T2, Fi, generator=g, device=DEV)
+    fr.view(-1)[::97] = ff.view(-1)[::97]  # ties: sign 0
+    wf = 0.1 * torch.randn(Co * Ci * KT * KF, generator=g, device=DEV)
+    wp = ops._wpoly(wf, Co, Ci, KT, KF, sf, dy)
+    den = torch.rand(1, generator=g, device=DEV) + 0.5
+    fg = torch.rand(1, generator=g, device=DEV) + 0.5
+    n = ff.numel()
+    code = torch.empty(n, device=DEV, dtype=torch.uint8)
+    outs, dens = torch.zeros(2, device=DEV), torch.zeros(2, device=DEV)
+    ws = torch.empty(lib.encx_disc_loss_workspace() // 4, device=DEV)
+    call('encx_feat_loss', ptr(fr), ptr(ff), n, 3.0, ptr(outs[0:1]), ptr(dens[0:1]), 0, ptr(ws), stream())
+    call('encx_feat_loss_code', ptr(fr), ptr(ff), n, 3.0, ptr(outs[1:2]), ptr(dens[1:2]), 0, ptr(ws), ptr(code),
+         stream())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(dens[0], dens[1])
+    dims = (B, Ci, T2, Fi, Co, Fo, KT, KF, sf, dt, pt, pf)
+    prev = lib.encx_conv2d_select(family)
+    try:
+        for xact in (None, ff):
+            for acc in (0, 1):
+                res = []
+                for c in (None, code):
+                    dx = torch.full_like(ff, 0.5)
+                    call('encx_conv2d_bwd_data_feat', ptr(dy), ptr(y), ptr(wp), ptr(xact), ptr(dx), acc, ptr(fr),
+                         ptr(ff), ptr(den), ptr(fg), 3.0, ptr(c), *dims, stream())
+                    res.append(dx)
+                assert torch.equal(res[0], res[1]), (xact is not None, acc, float((res[0] - res[1]).abs().max()))
+    finally:
+        lib.encx_conv2d_select(prev)
