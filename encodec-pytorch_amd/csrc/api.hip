@@ -27,15 +27,24 @@ struct ProfState {
 ProfState g_prof;
 std::atomic<bool> g_prof_on{false};
 
-// kernel-selection options (common.h EncxOpt): name, default; initial value from ENCX_<name>
+// kernel-selection options (common.h EncxOpt): id, name, default; initial value from ENCX_<name>
 struct OptDef {
+    EncxOpt id;
     const char* name;
     int64_t def;
 };
 constexpr OptDef kOpts[OPT_COUNT] = {
-    {"FFT", 1}, {"PW", 1}, {"PW_WG_TMAX", 12000}, {"LSTM_FUSE", 0}, {"FWR", 256}, {"DGR", 256},
-    {"WGR", 2048}, {"WGR_WGS", 256}, {"FEAT_CODE", 1}, {"CONV_CK", 64}, {"CONV_SPLIT", 1024}, {"CONV_WG_SPLIT", 1024},
+    {OPT_FFT, "FFT", 1}, {OPT_PW, "PW", 1}, {OPT_PW_WG_TMAX, "PW_WG_TMAX", 12000}, {OPT_LSTM_FUSE, "LSTM_FUSE", 0},
+    {OPT_FWR, "FWR", 256}, {OPT_DGR, "DGR", 256}, {OPT_WGR, "WGR", 2048},
+    {OPT_WGR_WGS, "WGR_WGS", 256}, {OPT_FEAT_CODE, "FEAT_CODE", 1}, {OPT_CONV_CK, "CONV_CK", 64},
+    {OPT_CONV_SPLIT, "CONV_SPLIT", 1024}, {OPT_CONV_WG_SPLIT, "CONV_WG_SPLIT", 1024},
 };
+constexpr bool opts_in_order() {
+    for (int i = 0; i < OPT_COUNT; ++i)
+        if (kOpts[i].id != i) return false;
+    return true;
+}
+static_assert(opts_in_order(), "kOpts must list every EncxOpt in enum order");
 std::atomic<int64_t> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
 void opt_init() {

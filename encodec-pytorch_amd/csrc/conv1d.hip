@@ -21,6 +21,7 @@
 // Plus VALU kernels for the 1-channel ends of the stack (Cout = 1 forward, tiny wgrads).
 #include <stdlib.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -992,25 +993,36 @@ static Tile pick_tile(int64_t M, int64_t N) {
 static int tile_bm(Tile t) { return (t == T32x128) ? 32 : (t == T64x64 || t == T64x128) ? 64 : 128; }
 static int tile_bn(Tile t) { return (t == T128x32) ? 32 : (t == T64x64 || t == T128x64) ? 64 : 128; }
 
-// split the channel reduction when the plain grid would underfill the 256 CUs
-static void plan_split(int64_t blocks, int C, int CK, int* KS, int* cps) {
-    int nch = (C + CK - 1) / CK;
+// Split the channel reduction (split-K into partial slabs + a fixed-order reduce that applies the
+// epilogue) when the plain grid would underfill the chip. The slabs cost KS x the output in
+// writes and reads, so (round 5, tools/conv_sweep.py on every config-3 layer):
+//  * split only below CONV_SPLIT / 2 workgroups (default 512: two per CU) -- or below CONV_SPLIT
+//    (1024) when the direct epilogue reads operands (act'(x), residual, accumulate: its loads
+//    wait out a round trip per sub-tile at the end of every workgroup, which the streaming
+//    reduce does not);
+//  * keep >= 192 reduction elements (channels x taps) per split and <= 1536 workgroups;
+//  * split evenly: KS divides the channel chunks (an uneven last split idles the others).
+// Measured against the round-4 rule (split up to 1024 workgroups): 8.76 -> 8.3-8.5 ms per step.
+static void plan_split(int64_t blocks, int C, int CK, int red, bool heavy_epi, int* KS, int* cps) {
+    const int nch = (C + CK - 1) / CK;
+    const int64_t target = encx_opt(OPT_CONV_SPLIT);
     int ks = 1;
-    const int64_t target = encx_opt(OPT_CONV_SPLIT);  // workgroups to aim for (default 1024)
-    if (blocks < target && nch >= 4) {
-        ks = (int)cdiv(target, blocks);
-        if (ks > nch / 2) ks = nch / 2;
-        if (ks > 16) ks = 16;
-        if (ks < 1) ks = 1;
+    if (blocks < (heavy_epi ? target : target / 2) && nch >= 4) {
+        int64_t cap = red / 192;
+        if (cap > (3 * target / 2) / blocks) cap = (3 * target / 2) / blocks;
+        if (cap > nch / 2) cap = nch / 2;
+        if (cap > 16) cap = 16;
+        for (ks = (int)(cap < 1 ? 1 : cap); ks > 1 && nch % ks; --ks) {
+        }
     }
-    int per = (int)cdiv(nch, ks);
+    const int per = (int)cdiv(nch, ks);
     *cps = per * CK;
     *KS = (int)cdiv(C, *cps);
 }
 
 struct FwdPlan { Tile t; int CK, Up, KS, cps; bool small; };
 static FwdPlan plan_fwd(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K, int64_t s,
-                        int64_t d) {
+                        int64_t d, bool heavy_epi) {
     FwdPlan p;
     p.small = Cout <= 4;
     const int ck = pick_ck((int)Cin, (int)K);
@@ -1022,12 +1034,12 @@ static FwdPlan plan_fwd(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int6
     int64_t blocks = cdiv(Tout, BN) * cdiv(Cout, tile_bm(p.t)) * B;
     p.KS = 1;
     p.cps = (int)Cin;
-    if (!p.small) plan_split(blocks, (int)Cin, ck, &p.KS, &p.cps);
+    if (!p.small) plan_split(blocks, (int)Cin, ck, (int)(Cin * K), heavy_epi, &p.KS, &p.cps);
     return p;
 }
 
 struct PolyPlan { Tile t; int CK, Ub, KS, cps; };
-static PolyPlan plan_poly(int64_t B, int64_t Ci, int64_t M, int64_t ncols, int64_t J) {
+static PolyPlan plan_poly(int64_t B, int64_t Ci, int64_t M, int64_t ncols, int64_t J, bool heavy_epi) {
     PolyPlan p;
     const int ck = pick_ck((int)Ci, (int)J);
     p.CK = ck;
@@ -1036,7 +1048,7 @@ static PolyPlan plan_poly(int64_t B, int64_t Ci, int64_t M, int64_t ncols, int64
     p.Ub = BN + (int)J - 1;
     if ((p.Ub & 31) == 0) p.Ub += 1;
     int64_t blocks = cdiv(ncols, BN) * cdiv(M, tile_bm(p.t)) * B;
-    plan_split(blocks, (int)Ci, ck, &p.KS, &p.cps);
+    plan_split(blocks, (int)Ci, ck, (int)(Ci * J), heavy_epi, &p.KS, &p.cps);
     return p;
 }
 
@@ -1397,7 +1409,7 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
         }
         return 0;
     }
-    FwdPlan p = plan_fwd(a.B, a.Cin, a.Cout, a.Tout, a.K, a.s, a.d);
+    FwdPlan p = plan_fwd(a.B, a.Cin, a.Cout, a.Tout, a.K, a.s, a.d, a.res || a.xact || a.accumulate);
     if (p.small) {
         int ck = 64 / a.K;
         if (ck < 1) ck = 1;
@@ -1434,8 +1446,13 @@ size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K
         const int slabs = fwd_flat_slabs(B, Cin, Cout, Tout, K);
         return slabs > 1 ? (size_t)slabs * B * Cout * Tout * sizeof(float) : 0;
     }
-    FwdPlan p = plan_fwd(B, Cin, Cout, Tout, K, s, d);
-    return (p.small || p.KS == 1) ? 0 : (size_t)p.KS * B * Cout * Tout * sizeof(float);
+    // (the epilogue's operands are not known here: the larger of the two plans)
+    size_t ws = 0;
+    for (const bool heavy : {false, true}) {
+        const FwdPlan p = plan_fwd(B, Cin, Cout, Tout, K, s, d, heavy);
+        if (!p.small && p.KS > 1) ws = std::max(ws, (size_t)p.KS * B * Cout * Tout * sizeof(float));
+    }
+    return ws;
 }
 
 int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
@@ -1456,7 +1473,8 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
         }
         return 0;
     }
-    PolyPlan p = plan_poly(a.B, a.Ci, (int64_t)a.Co * a.s, ncols, a.J);
+    PolyPlan p = plan_poly(a.B, a.Ci, (int64_t)a.Co * a.s, ncols, a.J,
+                           a.mode != 0 && (a.act != ENCX_ACT_NONE || a.accumulate));
     a.CK = p.CK; a.Ub = p.Ub; a.KS = p.KS; a.cps = p.cps; a.Q = ncols * a.s; a.part = ws;
     ENCX_REQUIRE(a.KS == 1 || ws);
     switch (p.t) {
@@ -1480,8 +1498,12 @@ size_t poly_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int6
         const int slabs = gemm_slabs(Kred, gemm_splits((int)(Co * s), (int)(B * ncols), Kred));
         return slabs > 1 ? (size_t)slabs * B * Co * ncols * s * sizeof(float) : 0;
     }
-    PolyPlan p = plan_poly(B, Ci, Co * s, ncols, J);
-    return p.KS == 1 ? 0 : (size_t)p.KS * B * Co * ncols * s * sizeof(float);
+    size_t ws = 0;
+    for (const bool heavy : {false, true}) {
+        const PolyPlan p = plan_poly(B, Ci, Co * s, ncols, J, heavy);
+        if (p.KS > 1) ws = std::max(ws, (size_t)p.KS * B * Co * ncols * s * sizeof(float));
+    }
+    return ws;
 }
 
 // wgrad planning shared by the launcher and the workspace query
@@ -1506,7 +1528,9 @@ static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K)
     p.items = (int)(B * cdiv(Tl, p.BT));
     const int64_t target = encx_opt(OPT_CONV_WG_SPLIT);  // ~1024 workgroups in flight
     int64_t want = cdiv(target, p.tiles);
-    int64_t cap = (64ll << 20) / (4 * A * N);           // <= 64 MB of partials
+    // <= 32 MB of partials: the slabs are written and read back once each (64 MB cost the big
+    // weights 10 % over 32 MB, round 5 sweep; the small ones never reach the cap)
+    int64_t cap = (32ll << 20) / (4 * A * N);
     int64_t minper = cdiv(p.items, (int64_t)p.items >= 8 ? 8 : 1);
     (void)minper;
     if (cap < 1) cap = 1;

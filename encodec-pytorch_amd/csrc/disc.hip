@@ -849,57 +849,76 @@ __global__ __launch_bounds__(NWV * 64) void c2_fwd_rw_kernel(C2FwdR a) {
     const int plane = g.T2 * g.Fi, xlast = g.B * g.Ci * plane - 4;
     const int CP = g.Ci >> 1;  // channel pairs
     const int cstride = 2 * plane;
-    for (int tile = rw_first_slot(wave); tile < a.tiles; tile += gridDim.x * NWV) {
+    // one item's geometry: window element e of step (c, kt) is x[b][2c + h][row(kt)][col0 + e]
+    struct Geo {
+        int t, b, f0;
+        int rb[KT];
+        uint32_t msk[KT];
+        bool fix;  // wave-uniform: some lane's window leaves the input
+    };
+    auto geo = [&](int tile) {
+        Geo q;
         const int qd = min(tile * 32 + l, quads - 1);
         const int fq = qd % a.F4, bt = qd / a.F4;
-        const int t = bt % g.T2, b = bt / g.T2;
-        const int f0 = 4 * fq, col0 = S * f0 - g.pf;
-        // window element e of step (c, kt) is x[b][2c + h][row(kt)][col0 + e]
+        q.t = bt % g.T2;
+        q.b = bt / g.T2;
+        q.f0 = 4 * fq;
+        const int col0 = S * q.f0 - g.pf;
         uint32_t cmask = 0;
 #pragma unroll
         for (int e = 0; e < NE; ++e) cmask |= (col0 + e >= 0 && col0 + e < g.Fi) ? (1u << e) : 0u;
-        int rb[KT];
-        uint32_t msk[KT];
         bool clean = true;  // every element of every window of this lane is in the input
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
-            const int row = t + kt * g.dt - g.pt;
+            const int row = q.t + kt * g.dt - g.pt;
             const bool ok = row >= 0 && row < g.T2;
-            rb[kt] = (b * g.Ci + h) * plane + (ok ? row : 0) * g.Fi + col0;
-            msk[kt] = ok ? cmask : 0u;
-            clean = clean && msk[kt] == (1u << NE) - 1;
+            q.rb[kt] = (q.b * g.Ci + h) * plane + (ok ? row : 0) * g.Fi + col0;
+            q.msk[kt] = ok ? cmask : 0u;
+            clean = clean && q.msk[kt] == (1u << NE) - 1;
         }
-        const bool fix = !__all(clean);  // wave-uniform
-        auto load = [&](f32x4* w, int c, int kt) {
-            const int base = rb[kt] + c * cstride;
+        q.fix = !__all(clean);
+        return q;
+    };
+    auto load = [&](f32x4* w, const Geo& q, int c, int kt) {
+        const int base = q.rb[kt] + c * cstride;
 #pragma unroll
-            for (int q = 0; q < WQ; ++q) w[q] = ld4u(a.x + min(max(base + 4 * q, 0), xlast));
-        };
+        for (int w4 = 0; w4 < WQ; ++w4) w[w4] = ld4u(a.x + min(max(base + 4 * w4, 0), xlast));
+    };
+    // three register windows, one per kt: step (c, kt) multiplies window kt with the weight
+    // columns of (c, kt), read from LDS just in time, while the next step's window is in flight
+    // (the prefetch is unconditional, so every wait is exact). The last step of an item loads the
+    // NEXT item's first window, so it is in flight during this item's epilogue stores and the
+    // next item does not start by waiting out a memory round trip behind them (vmcnt counts the
+    // stores too). Measured against reading the weights a step ahead or one tap ahead: none is
+    // faster (profiles/r05).
+    f32x4 wb[KT][WQ];
+    auto wcol = [&](int c, int kt) { return Ws + ((2 * c + h) * KT + kt) * KF * 32 + l; };
+    const int stride = gridDim.x * NWV;
+    int tile = rw_first_slot(wave);
+    if (tile < a.tiles) load(wb[0], geo(tile), 0, 0);
+    for (; tile < a.tiles; tile += stride) {
+        const Geo cur = geo(tile);  // (recomputed: cheaper than holding the next item's in registers)
+        const int t = cur.t, b = cur.b, f0 = cur.f0;
         f32x16 acc[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] = (f32x16){0};
-        // three register windows, one per kt: step (c, kt) multiplies window kt with the weight
-        // columns of (c, kt), read from LDS just in time, while the next step's window is in
-        // flight (the prefetch is unconditional, so every wait is exact). Measured against
-        // reading the weights a step ahead or one tap ahead: none is faster (profiles/r05).
-        f32x4 wb[KT][WQ];
-        auto wcol = [&](int c, int kt) { return Ws + ((2 * c + h) * KT + kt) * KF * 32 + l; };
-        load(wb[0], 0, 0);
         for (int c = 0; c < CP; ++c) {
 #pragma unroll
             for (int kt = 0; kt < KT; ++kt) {
-                const int nk = kt + 1 < KT ? kt + 1 : 0, nc = kt + 1 < KT ? c : min(c + 1, CP - 1);
-                load(wb[nk], nc, nk);
+                const int nk = kt + 1 < KT ? kt + 1 : 0;
+                if (kt + 1 < KT) load(wb[nk], cur, c, nk);
+                else if (c + 1 < CP) load(wb[0], cur, c + 1, 0);
+                else load(wb[0], geo(tile + stride < a.tiles ? tile + stride : tile), 0, 0);  // (past the last: own)
                 f32x4* w = wb[kt];
-                if (fix) {
-                    const int base = rb[kt] + c * cstride;
+                if (cur.fix) {
+                    const int base = cur.rb[kt] + c * cstride;
 #pragma unroll
                     for (int q = 0; q < WQ; ++q) {
                         const int o = base + 4 * q;
                         if (__any(o < 0 || o > xlast)) w[q] = quad_abs(w[q], o, xlast);  // tensor ends
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
-                            if (!((msk[kt] >> (4 * q + e)) & 1u)) w[q][e] = 0.f;
+                            if (!((cur.msk[kt] >> (4 * q + e)) & 1u)) w[q][e] = 0.f;
                     }
                 }
                 const float* wk = wcol(c, kt);
@@ -1451,7 +1470,7 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
 struct C2DgR {
     C2Dg d;
     int U4;     // quads per polyphase row
-    int tiles;  // ceil(B * T2 * U4 / 32)
+    int tiles;  // column tiles (32 quads each): ceil(B * T2 * U4 / 32)
 };
 // c2_dgrad_rw_kernel's epilogue for one item, the combination of its terms fixed at compile time
 // (MODE bits: 1 feature term, 2 LeakyReLU'(x), 4 x read from xact (else from ffx), 8 accumulate),
@@ -1600,55 +1619,74 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
     const int plane = g.T2 * g.Fo, ylast = g.B * g.Co * plane - 4;
     const int CP = g.Co >> 1, cstride = 2 * plane;
     const float fc = feat_coef(a);
-    for (int item = rw_first_slot(wave); item < R.tiles * RG; item += gridDim.x * NWV) {
-        const int tile = item / RG, rt = item - tile * RG;  // rows rt*TM*32 .. + TM*32
-        const int qd = min(tile * 32 + l, quads - 1);
+    // one item's geometry: window element e of step (c, kt) is dy[b][2c + h][row(kt)][e0 + e]
+    struct Geo {
+        int rt, tile, t, b, u0;
+        int rb[KT];
+        uint32_t msk[KT];
+        bool fix;  // wave-uniform: some lane's window leaves the map
+    };
+    auto geo = [&](int item) {
+        Geo q;
+        q.rt = item % RG;
+        q.tile = item / RG;  // rows rt*TM*32 .. + TM*32
+        const int qd = min(q.tile * 32 + l, quads - 1);
         const int uq = qd % R.U4, bt = qd / R.U4;
-        const int t = bt % g.T2, b = bt / g.T2;
-        const int u0 = 4 * uq, e0 = u0 - (J - 1);  // dy column of window element 0
+        q.t = bt % g.T2;
+        q.b = bt / g.T2;
+        q.u0 = 4 * uq;
+        const int e0 = q.u0 - (J - 1);  // dy column of window element 0
         uint32_t cmask = 0;
 #pragma unroll
         for (int e = 0; e < NE; ++e) cmask |= (e0 + e >= 0 && e0 + e < g.Fo) ? (1u << e) : 0u;
-        int rb[KT];
-        uint32_t msk[KT];
         bool clean = true;
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
-            const int row = t + g.pt - kt * g.dt;
+            const int row = q.t + g.pt - kt * g.dt;
             const bool ok = row >= 0 && row < g.T2;
-            rb[kt] = (b * g.Co + h) * plane + (ok ? row : 0) * g.Fo + e0;
-            msk[kt] = ok ? cmask : 0u;
-            clean = clean && msk[kt] == (1u << NE) - 1;
+            q.rb[kt] = (q.b * g.Co + h) * plane + (ok ? row : 0) * g.Fo + e0;
+            q.msk[kt] = ok ? cmask : 0u;
+            clean = clean && q.msk[kt] == (1u << NE) - 1;
         }
-        const bool fix = !__all(clean);  // wave-uniform
-        // two register buffers of windows, alternating over the (c, kt) steps: step s + 1 is in
-        // flight while step s multiplies. The loop body is 2 channel pairs x 3 kt = 6 steps, so
-        // every buffer / kt index is a compile-time constant (Co % 4 == 0).
-        f32x4 wb[2][WQ], yb[2][WQ];
-        auto acol = [&](int c, int kt) { return As + ((2 * c + h) * KT + kt) * J * M + rt * TM * 32 + l; };
-        auto load = [&](int k, int c, int kt) {
-            const int base = rb[kt] + c * cstride;
+        q.fix = !__all(clean);
+        return q;
+    };
+    // two register buffers of windows, alternating over the (c, kt) steps: step s + 1 is in
+    // flight while step s multiplies. The loop body is 2 channel pairs x 3 kt = 6 steps, so
+    // every buffer / kt index is a compile-time constant (Co % 4 == 0). The last step of an item
+    // loads the NEXT item's first window, so it is in flight during this item's epilogue and the
+    // next item does not start by waiting out a round trip behind the epilogue's stores.
+    f32x4 wb[2][WQ], yb[2][WQ];
+    auto load = [&](int k, const Geo& q, int c, int kt) {
+        const int base = q.rb[kt] + c * cstride;
 #pragma unroll
-            for (int q = 0; q < WQ; ++q) {
-                const int o = min(max(base + 4 * q, 0), ylast);
-                wb[k][q] = ld4u(a.dy + o);
-                if (YM) yb[k][q] = ld4u(a.yact + o);
-            }
-        };
+        for (int w4 = 0; w4 < WQ; ++w4) {
+            const int o = min(max(base + 4 * w4, 0), ylast);
+            wb[k][w4] = ld4u(a.dy + o);
+            if (YM) yb[k][w4] = ld4u(a.yact + o);
+        }
+    };
+    const int stride = gridDim.x * NWV, nitems = R.tiles * RG;
+    int item = rw_first_slot(wave);
+    if (item < nitems) load(0, geo(item), 0, 0);
+    for (; item < nitems; item += stride) {
+        const Geo cur = geo(item);  // (recomputed: cheaper than holding the next item's in registers)
+        const int rt = cur.rt, tile = cur.tile, t = cur.t, b = cur.b, u0 = cur.u0;
+        auto acol = [&](int c, int kt) { return As + ((2 * c + h) * KT + kt) * J * M + rt * TM * 32 + l; };
         f32x16 acc[TM][4];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = (f32x16){0};
-        load(0, 0, 0);
         for (int c0 = 0; c0 < CP; c0 += 2) {
 #pragma unroll
             for (int u = 0; u < 2 * KT; ++u) {
                 const int kt = u % KT, c = c0 + u / KT, k = u & 1;
-                // the next step (past the end: the last one again, never used)
+                // the next step: within the item, or the next item's first (past the last item
+                // its own first again, never used)
                 const int nu = u + 1 < 2 * KT ? u + 1 : 0;
-                const int nc = u + 1 < 2 * KT ? c0 + nu / KT : min(c0 + 2, CP - 1);
-                load(k ^ 1, nc, nu % KT);
+                if (u + 1 < 2 * KT || c0 + 2 < CP) load(k ^ 1, cur, u + 1 < 2 * KT ? c0 + nu / KT : c0 + 2, nu % KT);
+                else load(k ^ 1, geo(item + stride < nitems ? item + stride : item), 0, 0);
                 // keep the next step's loads HERE, a whole step ahead of their use: without the
                 // barrier the scheduler sinks them to the end of the step (one register buffer
                 // instead of two) and every step waits out the load latency (measured: the
@@ -1661,15 +1699,15 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e) w[q][e] *= lrelu_grad(yb[k][q][e]);
                 }
-                if (fix) {
-                    const int base = rb[kt] + c * cstride;
+                if (cur.fix) {
+                    const int base = cur.rb[kt] + c * cstride;
 #pragma unroll
                     for (int q = 0; q < WQ; ++q) {
                         const int o = base + 4 * q;
                         if (__any(o < 0 || o > ylast)) w[q] = quad_abs(w[q], o, ylast);  // tensor ends
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
-                            if (!((msk[kt] >> (4 * q + e)) & 1u)) w[q][e] = 0.f;
+                            if (!((cur.msk[kt] >> (4 * q + e)) & 1u)) w[q][e] = 0.f;
                     }
                 }
                 const float* ak = acol(c, kt);
@@ -1688,13 +1726,13 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
             }
         }
         // ---- epilogue (rw_dg_epi): the feature-matching term, LeakyReLU'(x), accumulate
-        if (tile * 32 + l >= quads) continue;
+        const bool live = tile * 32 + l < quads;
         const bool ldx = a.xact && !(a.ffr && a.ffx == a.xact);  // x from xact (else from ffx)
         const int mode = (a.ffr ? 1 : 0) | (a.xact ? 2 : 0) | (ldx ? 4 : 0) | (a.accumulate ? 8 : 0) |
                          (a.fcode && a.ffr && !ldx ? 16 : 0);
         switch (mode) {
 #define ENCX_EPI(m) \
-    case m: rw_dg_epi<S, TM, m>(a, acc, rt, lane, b, t, u0, fc); break;
+    case m: if (live) rw_dg_epi<S, TM, m>(a, acc, rt, lane, b, t, u0, fc); break;
             ENCX_EPI(0) ENCX_EPI(1) ENCX_EPI(3) ENCX_EPI(6) ENCX_EPI(7)
             ENCX_EPI(8) ENCX_EPI(9) ENCX_EPI(11) ENCX_EPI(14) ENCX_EPI(15)
             ENCX_EPI(17) ENCX_EPI(19) ENCX_EPI(25) ENCX_EPI(27)
@@ -3084,25 +3122,34 @@ static bool dgr_ok(const C2Geo& g) {
     const int J = (g.KF + g.sf - 1) / g.sf;
     return (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float) <= 150 * 1024;
 }
-static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st) {
-    if (!dgr_ok(d.g)) return ENCX_EINVAL;
-    constexpr int NWV = 8;  // 8 waves; both row tiles of the 3x9 layers per item
-    const C2Geo& g = d.g;
-    C2DgR R{d, 0, 0};
-    R.d.U = (g.Fi - 1 + g.pf) / g.sf + 1;
-    R.U4 = (int)cdiv(R.d.U, 4);
-    R.tiles = (int)cdiv((int64_t)g.B * g.T2 * R.U4, 32);
-    const int J = (g.KF + g.sf - 1) / g.sf;
-    const size_t lds = (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float);
-    const int grid = (int)min((int64_t)wgs, cdiv((int64_t)R.tiles, NWV));
-    const bool ym = d.yact != nullptr;
-    if (g.KF == 9) {
-        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, 2>), dim3(grid), dim3(NWV * 64), lds, st, R);
-        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, 2>), dim3(grid), dim3(NWV * 64), lds, st, R);
+template <int TM>
+static void launch_dgrad_rw(const C2DgR& R, int grid, size_t lds, hipStream_t st) {
+    constexpr int NWV = 8;
+    const bool ym = R.d.yact != nullptr;
+    if (R.d.g.KF == 9) {
+        if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, true, NWV, TM>), dim3(grid), dim3(NWV * 64), lds, st, R);
+        else hipLaunchKernelGGL((c2_dgrad_rw_kernel<5, 2, 2, 2, false, NWV, TM>), dim3(grid), dim3(NWV * 64), lds, st, R);
     } else {
         if (ym) hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, true, NWV, 1>), dim3(grid), dim3(NWV * 64), lds, st, R);
         else hipLaunchKernelGGL((c2_dgrad_rw_kernel<3, 1, 1, 2, false, NWV, 1>), dim3(grid), dim3(NWV * 64), lds, st, R);
     }
+}
+// 8 waves per workgroup, items of both row tiles of the 3x9 layers (TM = 2). Measured and
+// dropped (round 5): a half-full last round of items handed to a second launch as one-row-tile
+// items (TM = 1, twice the items at half the work): 799.0 vs 802.0 audio-s/s.
+static int run_dgrad_rw(const C2Dg& d, int wgs, hipStream_t st) {
+    if (!dgr_ok(d.g)) return ENCX_EINVAL;
+    constexpr int NWV = 8;
+    const C2Geo& g = d.g;
+    C2DgR R{d, 0, 0};
+    R.d.U = (g.Fi - 1 + g.pf) / g.sf + 1;
+    R.U4 = (int)cdiv(R.d.U, 4);
+    const int tiles = (int)cdiv((int64_t)g.B * g.T2 * R.U4, 32);
+    const int J = (g.KF + g.sf - 1) / g.sf;
+    const size_t lds = (size_t)g.Co * 3 * J * g.Ci * g.sf * sizeof(float);
+    const int grid = (int)min((int64_t)wgs, cdiv((int64_t)tiles, NWV));
+    R.tiles = tiles;
+    launch_dgrad_rw<2>(R, grid, lds, st);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
