@@ -136,6 +136,164 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_wave(const float* xt, const 
     }
 }
 
+// ------------------------------------------------------------------------- persistent forward
+// ONE launch runs the whole recurrence (option LSTM_PERSIST). Workgroup (l, bg, ug) owns the PU
+// hidden units u0 = PU ug .. u0 + PU - 1 (4 PU = 32 gate columns, two 16-column MFMA tiles) of
+// layer l for the 16 batch rows 16 bg .., and keeps its slice of wcat_l ([32][2H], 64 KB at
+// H = 512) in registers for all T frames: the per-frame weight loads and launch boundaries of
+// lstm_fwd_wave are gone. Frame t of layer l needs x_l(t) = h_{l-1}(t) and h_l(t-1) of its rows,
+// i.e. the outputs of the NUG workgroups of (l-1, bg) and (l, bg). The hand-off is the counter
+// form of the write-through protocol (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md
+// visibility table, first row): h is stored sc1, every storing wave drains (s_waitcnt vmcnt(0)),
+// a workgroup barrier, then ONE lane adds 1 to cnt[l][bg]; a consumer's wave 0 polls that word
+// with relaxed agent-scope (sc1) loads until it reaches NUG (t + 1), the workgroup joins a
+// barrier, and EVERY load of h is an sc1 buffer load (no L1 copy can be stale, no acquire). Layer
+// 0 never waits on layer 1, so the layers run as a wavefront with no global step. Every spin is
+// bounded: a timeout counts in the error word (encx_lstm_sync_errors) and the launch drains.
+// All L NBG NUG workgroups must be resident together: the host uses this form only when they are
+// at most one per CU. The arithmetic (k-group order, LDS sum order, gate math) is that of
+// lstm_fwd_wave, so both forms give the same bits.
+constexpr int PU = 8;           // hidden units per persistent workgroup
+constexpr int SYNC_LINE = 32;   // ints per counter: one 128-byte line each
+constexpr int SYNC_LINES = 512;
+// hand-off counters [SYNC_LINES][SYNC_LINE] (zeroed per launch), then the error word's line
+__device__ int g_lstm_sync[(SYNC_LINES + 1) * SYNC_LINE];
+
+// wave-wide bounded poll: cnt >= target (relaxed agent loads, sc1); false after ~1 s
+ENCX_DEV bool poll_ge(const int* cnt, int target, int* err) {
+    for (int i = 0; i < (1 << 20); ++i) {
+        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+}
+ENCX_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const float* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
+}
+constexpr int SC1 = 16;  // buffer op cache-policy bit: write-through store / L1-bypassing load
+ENCX_DEV float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+    // (the whole vector is bit-cast: clang 20 miscompiles a bit_cast of one element, v[i], into a
+    // read of element 0)
+    const f32x4v v = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, SC1));
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// grid L * NBG * NUG (NUG = H / PU), FW waves; G = 2H / (16 FW) k-groups per wave (H % 128 == 0, so
+// groups g < G / 2 of every wave are in the input half of K and the others in the recurrent half)
+template <int G>
+__global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const float* wcat, const float* bsum,
+                                                         float* Y, float* Cst, float* Gs, int B, int T, int H,
+                                                         int NBG, int* sync) {
+    const int NUG = H / PU;
+    const int id = blockIdx.x, ug = id % NUG, bg = (id / NUG) % NBG, l = id / (NUG * NBG);
+    __shared__ float red[FW][16][33];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 15, kk = lane >> 4;
+    const int u0 = ug * PU, K = 2 * H;
+    const int64_t BTH = (int64_t)B * T * H;
+    // the resident weight slice: wr[g][c] = wcat_l[j][16 gi + 4 kk ..], gate column n = 16 c + col
+    // (gate n / PU, unit u0 + n % PU)
+    float4 wr[G][2];
+    {
+        const float* W = wcat + (int64_t)l * 4 * H * K;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int n = 16 * c + col, j = (n / PU) * H + u0 + n % PU;
+                wr[g][c] = ld4(W + (int64_t)j * K + (wave + FW * g) * 16 + 4 * kk);
+            }
+    }
+    // every load of a sequence goes through these descriptors with sc1 (the host checks that the
+    // byte offsets fit 32 bits)
+    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(l == 0 ? xt : Y + (l - 1) * BTH, (uint32_t)(BTH * 4));
+    const __amdgpu_buffer_rsrc_t ry = buf_rsrc(Y + l * BTH, (uint32_t)(BTH * 4));
+    const int arow = min(bg * 16 + col, B - 1);  // rows >= B compute garbage that is never stored
+    // the gate phase: thread p < 16 PU owns (row 16 bg + p / PU, unit u0 + p % PU) for all frames
+    const int pr = tid / PU, pu = u0 + tid % PU, pb = bg * 16 + pr;
+    const bool pact = tid < 16 * PU && pb < B;
+    float bias[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bias[g] = pact ? bsum[(int64_t)l * 4 * H + g * H + pu] : 0.f;
+    float* Cl = Cst + l * BTH;
+    int* const cnt_self = sync + (l * NBG + bg) * SYNC_LINE;
+    const int* const cnt_in = sync + ((l > 0 ? l - 1 : 0) * NBG + bg) * SYNC_LINE;
+    int* const err = sync + SYNC_LINES * SYNC_LINE;
+    bool live = true;  // wave 0: no poll has timed out
+    float c = 0.f;
+    for (int t = 0; t < T; ++t) {
+        f32x4v acc[2] = {(f32x4v){0.f, 0.f, 0.f, 0.f}, (f32x4v){0.f, 0.f, 0.f, 0.f}};
+        // ---- input part x_l(t): layer 0 reads xt (written before this launch), layer l > 0
+        // waits for h_{l-1}(t) of all NUG workgroups of (l-1, bg)
+        if (l > 0) {
+            if (wave == 0 && live) live = poll_ge(cnt_in, NUG * (t + 1), err);
+            __syncthreads();
+        }
+        {  // k-groups g < G / 2 of every wave lie in the input half (H % 128 == 0)
+            float4 a[G / 2];
+            const uint32_t rb = (uint32_t)(((int64_t)arow * T + t) * H + 4 * kk) * 4u;
+#pragma unroll
+            for (int g = 0; g < G / 2; ++g) a[g] = ld4_sc1(rx, rb + (uint32_t)(wave + FW * g) * 64u);
+            __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
+#pragma unroll
+            for (int g = 0; g < G / 2; ++g)
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma16(at4(a[g], s), at4(wr[g][cc], s), acc[cc]);
+        }
+        // ---- recurrent part h_l(t-1) (zero at t = 0): k-groups g >= G / 2
+        if (t > 0) {
+            if (wave == 0 && live) live = poll_ge(cnt_self, NUG * t, err);
+            __syncthreads();
+            float4 a[G / 2];
+            const uint32_t rb = (uint32_t)(((int64_t)arow * T + t - 1) * H + 4 * kk - H) * 4u;
+#pragma unroll
+            for (int g = 0; g < G / 2; ++g) a[g] = ld4_sc1(ry, rb + (uint32_t)(wave + FW * (g + G / 2)) * 64u);
+            __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
+#pragma unroll
+            for (int g = 0; g < G / 2; ++g)
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int cc = 0; cc < 2; ++cc)
+                        acc[cc] = mfma16(at4(a[g], s), at4(wr[g + G / 2][cc], s), acc[cc]);
+        }
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[wave][kk * 4 + q][16 * cc + col] = acc[cc][q];
+        __syncthreads();
+        if (pact) {
+            float pre[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = g * PU + (pu - u0);
+                float s = red[0][pr][n];
+#pragma unroll
+                for (int w = 1; w < FW; ++w) s += red[w][pr][n];
+                pre[g] = s + bias[g];
+            }
+            const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanhf(pre[2]), og = sigm(pre[3]);
+            c = fg * c + ig * gg;
+            const int64_t po = ((int64_t)pb * T + t) * H + pu;
+            Cl[po] = c;
+            // h: handed off inside this launch, so written through (sc1)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, og * tanhf(c)), ry,
+                                                  (int)((uint32_t)po * 4u), 0, SC1);
+            float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)pb * T + t) * 4 * H;
+            gs[pu] = ig;
+            gs[H + pu] = fg;
+            gs[2 * H + pu] = gg;
+            gs[3 * H + pu] = og;
+        }
+        // publish: every storing wave drained, a barrier, one lane's arrival
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(cnt_self, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ------------------------------------------------------------------------- backward step
 // E(k), grid (cdiv(B*H, 256), L + [dx]): role l < L: layer l at frame t = T-1-k+(L-1-l):
 //   dh = (top layer: dout[b][u][t]; else sum_s P_{l+1}[s][b][u])      -- grad of h_l(t) from above
@@ -465,6 +623,36 @@ static int bwd_splits(int64_t H) {
     while (groups % ns) --ns;
     return ns;
 }
+// ---- the persistent forms: residency and the hand-off words
+static int device_cus() {
+    static int cus[64];
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 0;
+    if (!cus[d] && hipDeviceGetAttribute(&cus[d], hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) cus[d] = 0;
+    return cus[d];
+}
+static int* sync_words() {
+    static int* addr[64];
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return nullptr;
+    if (!addr[d] && hipGetSymbolAddress((void**)&addr[d], HIP_SYMBOL(g_lstm_sync)) != hipSuccess) addr[d] = nullptr;
+    return addr[d];
+}
+// workgroups of the persistent forward, or 0 when the shape or the device does not admit it (the
+// workgroups must be resident together: at most one per CU; the sequences' byte offsets 32-bit)
+static int fwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
+    if (encx_opt(OPT_LSTM_PERSIST) == 0 || H % 128 || H > 512 || B * T * H * 4 >= ((int64_t)1 << 31)) return 0;
+    const int64_t nbg = cdiv(B, 16), nwg = L * nbg * (H / PU);
+    if (L * nbg > SYNC_LINES || nwg > device_cus() || !sync_words()) return 0;
+    return (int)nwg;
+}
+template <int G>
+static void fwd_pers_launch(int nwg, hipStream_t st, const float* xt, const float* wcat, const float* bsum, float* Y,
+                            float* C, float* Gs, int B, int T, int H, int nbg, int* sync) {
+    hipLaunchKernelGGL((lstm_fwd_pers<G>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C, Gs, B, T,
+                       H, nbg, sync);
+}
+
 static bool lstm_shape_ok(int64_t B, int64_t T, int64_t H, int64_t L) {
     return B > 0 && B <= 64 && T > 0 && H >= 16 && (H % 16) == 0 && H <= 1024 && L >= 1 && L <= 16 &&
            B * T * 4 * H < ((int64_t)1 << 31);
@@ -498,14 +686,41 @@ int encx_lstm_fwd(const float* x, const float* wcat, const float* bsum, float* x
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)cdiv(T, 32), (unsigned)cdiv(H, 32), (unsigned)B),
                        dim3(32, 8), 0, st, x, xt, (int)H, (int)T);
     const int RT = (int)cdiv(B, 16), G = (int)cdiv(H / 8, FW);
-    const dim3 grid((unsigned)(H / UNITS), (unsigned)L);
-    for (int k = 0; k < (int)(T + L - 1); ++k)
-        fwd_step(G, RT, grid, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, k);
+    if (const int nwg = fwd_pers_grid(B, T, H, L)) {
+        int* sync = sync_words();
+        const int nbg = (int)cdiv(B, 16);
+        const hipError_t e = hipMemsetAsync(sync, 0, (size_t)L * nbg * SYNC_LINE * sizeof(int), st);
+        if (e != hipSuccess) return (int)e;
+        ps.tag(" persist");
+        switch (G) {  // H / 64
+            case 2: fwd_pers_launch<2>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
+            case 4: fwd_pers_launch<4>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
+            case 6: fwd_pers_launch<6>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
+            default: fwd_pers_launch<8>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
+        }
+    } else {
+        const dim3 grid((unsigned)(H / UNITS), (unsigned)L);
+        for (int k = 0; k < (int)(T + L - 1); ++k)
+            fwd_step(G, RT, grid, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, k);
+    }
     const int64_t n = B * H * T;
     hipLaunchKernelGGL(lstm_out_skip, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, Y + (L - 1) * B * T * H, x,
                        out, (int)B, (int)T, (int)H, skip);
     ENCX_CHECK_LAUNCH();
     return 0;
+}
+
+int encx_lstm_sync_errors(int64_t* count) {
+    ENCX_REQUIRE(count);
+    int* w = sync_words();
+    ENCX_REQUIRE(w);
+    hipError_t e = hipDeviceSynchronize();
+    int v = 0;
+    if (e == hipSuccess) e = hipMemcpy(&v, w + SYNC_LINES * SYNC_LINE, sizeof(int), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemset(w + SYNC_LINES * SYNC_LINE, 0, sizeof(int));
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    *count = v;
+    return (int)e;
 }
 
 size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t L) {

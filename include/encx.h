@@ -339,6 +339,11 @@ size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t L);
 int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const float* Gs, float* DA, float* dx,
                   int acc_x, float* ws, int64_t B, int64_t T, int64_t H, int64_t L, encx_stream_t stream);
 size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H);
+/* The persistent forward / backward (option LSTM_PERSIST) run the recurrence in ONE launch whose
+ * workgroups hand frames to each other through counters with bounded spins. Returns (in *count)
+ * and clears the number of spins that timed out on the current device since the last call (0 on
+ * a healthy run; nonzero means a launch's results are garbage). Synchronises the device. */
+int encx_lstm_sync_errors(int64_t* count);
 /* Weight grads of layer `layer` from DA: dw_ih, dw_hh [4H][H] and the bias grad (to both db_ih
  * and db_hh; either may be NULL), written (acc = 0) or added (acc = 1). */
 int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float* dw_ih, float* dw_hh,

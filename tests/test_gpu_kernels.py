@@ -300,15 +300,19 @@ def test_normalize_and_scale():
 
 
 # --------------------------------------------------------------------------- LSTM
-@pytest.mark.parametrize('B,H,Tn,L,fuse', [(3, 32, 7, 1, 0), (17, 64, 20, 2, 0), (5, 48, 9, 3, 0), (32, 512, 75, 2, 0),
-                                            (17, 64, 20, 2, 1), (32, 512, 75, 2, 1)])
-def test_lstm_vs_oracle(B, H, Tn, L, fuse):
-    """encx LSTM (csrc/lstm.hip, all layers as one diagonal wavefront) forward + backward
-    against the oracle's step-by-step restatement of SLSTM (modules/lstm.py:22-28) run in fp64
-    on the CPU, for 1, 2 and 3 layers: every output and grad within 4x the error of the same
-    restatement run in plain fp32. fuse: the opt-in fused backward step (option LSTM_FUSE)."""
+@pytest.mark.parametrize('B,H,Tn,L,fuse,persist', [
+    (3, 32, 7, 1, 0, 1), (17, 64, 20, 2, 0, 1), (5, 48, 9, 3, 0, 1), (32, 512, 75, 2, 0, 1), (32, 512, 75, 2, 0, 0),
+    (17, 64, 20, 2, 1, 0), (32, 512, 75, 2, 1, 0), (17, 128, 20, 2, 0, 1), (5, 256, 9, 3, 0, 1), (40, 384, 11, 1, 0, 1)])
+def test_lstm_vs_oracle(B, H, Tn, L, fuse, persist):
+    """encx LSTM (csrc/lstm.hip) forward + backward against the oracle's step-by-step
+    restatement of SLSTM (modules/lstm.py:22-28) run in fp64 on the CPU, for 1, 2 and 3 layers:
+    every output and grad within 4x the error of the same restatement run in plain fp32.
+    persist: the one-launch recurrences (option LSTM_PERSIST; used where H % 128 == 0, H <= 512
+    and the workgroups fit the CUs, else the launch-per-step wavefront); fuse: the opt-in fused
+    backward step of the wavefront (option LSTM_FUSE)."""
+    import ctypes
     from encx import ops
-    from encx._lib import option
+    from encx._lib import option, call
     gen = torch.Generator().manual_seed(B * 1000 + H)
     k = 1.0 / np.sqrt(H)
     names = ['weight_ih', 'weight_hh', 'bias_ih', 'bias_hh']
@@ -324,10 +328,13 @@ def test_lstm_vs_oracle(B, H, Tn, L, fuse):
     y64 = O.slstm(x64, p64, 'm', L)
     (y64 * r64).sum().backward()
     x = x64.detach().float().to(DEV).requires_grad_(True)
-    with option(LSTM_FUSE=fuse):
+    with option(LSTM_FUSE=fuse, LSTM_PERSIST=persist):
         y = ops.lstm(x, wts, skip=True)
         (y * r64.float().to(DEV)).sum().backward()
         torch.cuda.synchronize()
+    nerr = ctypes.c_int64()
+    call('encx_lstm_sync_errors', ctypes.byref(nerr))
+    assert nerr.value == 0, f'{nerr.value} hand-off spins timed out'
 
     def rel_close(a, b, what, tol=2e-4):
         b = b.detach()
@@ -354,6 +361,43 @@ def test_lstm_vs_oracle(B, H, Tn, L, fuse):
     rel_close(x.grad, x64.grad, 'dx')
     for i, (n, w) in enumerate(p64.items()):
         rel_close(wts[i].grad, w.grad, n, tol=5e-4)
+
+
+@pytest.mark.parametrize('B,H,Tn,L', [(17, 256, 20, 2), (32, 512, 75, 2), (3, 128, 5, 3)])
+def test_lstm_persistent_bit_identical(B, H, Tn, L):
+    """The one-launch forward and backward (option LSTM_PERSIST) produce the same bits as the
+    launch-per-step wavefront: h, c, the gates, the gate grads DA and dx (same k-group order, same
+    LDS sum order, same gate arithmetic), with no hand-off spin timing out."""
+    import ctypes
+    from encx._lib import call, ptr, option, lib
+    gen = torch.Generator().manual_seed(7 * B + H)
+    k = H ** -0.5
+    f = lambda *s: ((torch.rand(*s, generator=gen) * 2 - 1) * k).to(DEV)
+    e = lambda n: torch.empty(n, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    wcat, wcatT, bsum = e(L * 8 * H * H), e(L * 8 * H * H), e(L * 4 * H)
+    for l in range(L):
+        call('encx_lstm_pack', *(ptr(f(*s)) for s in [(4 * H, H), (4 * H, H), (4 * H,), (4 * H,)]),
+             ptr(wcat), ptr(wcatT), ptr(bsum), H, l, st)
+    x = torch.randn(B, H, Tn, generator=gen).to(DEV)
+    dout = torch.randn(B, H, Tn, generator=gen).to(DEV)
+    res = []
+    for persist in (0, 1):
+        xt, Y, Cs, Gs = e(B * Tn * H), e(L * B * Tn * H), e(L * B * Tn * H), e(L * B * Tn * 4 * H)
+        out, DA, dx = torch.empty_like(x), e(L * B * Tn * 4 * H), torch.empty_like(x)
+        ws = torch.empty(lib.encx_lstm_bwd_workspace(B, Tn, H, L), dtype=torch.uint8, device=DEV)
+        with option(LSTM_PERSIST=persist):
+            call('encx_lstm_fwd', ptr(x), ptr(wcat), ptr(bsum), ptr(xt), ptr(Y), ptr(Cs), ptr(Gs), ptr(out), 1,
+                 B, Tn, H, L, st)
+            call('encx_lstm_bwd', ptr(dout), ptr(wcatT), ptr(Cs), ptr(Gs), ptr(DA), ptr(dx), 0, ptr(ws),
+                 B, Tn, H, L, st)
+        torch.cuda.synchronize()
+        res.append((out, Y, Cs, Gs, DA, dx))
+    nerr = ctypes.c_int64()
+    call('encx_lstm_sync_errors', ctypes.byref(nerr))
+    assert nerr.value == 0
+    for name, a, b in zip(['out', 'h', 'c', 'gates', 'DA', 'dx'], *res):
+        assert torch.equal(a, b), (name, float((a - b).abs().max()))
 
 
 # --------------------------------------------------------------------------- fused residual block
