@@ -442,6 +442,174 @@ __global__ __launch_bounds__(BW * 64) void lstm_bwd_gemm(const float* DA, const 
                        ux * 16 + (q & 15));
 }
 
+// ------------------------------------------------------------------------- persistent backward
+// ONE launch runs the backward recurrence of all layers (option LSTM_PERSIST). Workgroup
+// (l, bg, ct) owns the 16 columns n = 16 ct .. of P_l = DA_l . wcat_l (K = 4H) for the 16 batch
+// rows of bg, with its slice of wcatT_l ([16][4H], 128 KB at H = 512) resident in registers:
+//   ct >= H/16 (recurrent tile, units u = 16 (ct - H/16) ..): frame t takes the recurrent grad of
+//     h_l(t) from DA_l(t+1), adds the grad from above (dout for the top layer, else the input-grad
+//     tile of layer l+1 for the same units and frame, handed over by workgroup (l+1, bg, ct - H/16)),
+//     runs the cell backward of its 16 x 16 points (dc kept in registers across frames) and
+//     publishes DA_l(t) of its units;
+//   ct < H/16 (input tile): frame t contracts DA_l(t) into the input grad of layer l (dx for l = 0,
+//     else handed to the recurrent tile of layer l-1).
+// The hand-offs are those of lstm_fwd_pers (write-through stores, drain, barrier, one arrival;
+// sc1 loads after a bounded poll). The contraction keeps the exact split structure of
+// lstm_bwd_gemm + lstm_bwd_elem (4 splits of the 4H/16 k-groups, each 4 interleaved chains summed
+// in chain order, the splits summed in ascending order), so both forms give the same bits: wave w
+// runs chains (s, c) = (w / 2, 2 (w % 2) + h), h = 0, 1, of G k-groups each (H % 128 == 0, G = H/64).
+// grid L * NBG * 2H/16, FW waves. XP [L-1][B][T][H]: the input-grad tiles between layers.
+template <int G>
+__global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, const float* wcatT, const float* Cst,
+                                                         const float* Gs, float* DA, float* dx, int acc_x,
+                                                         float* XP, int B, int T, int H, int L, int NBG,
+                                                         int* sync) {
+    const int NRT = H / 16, NCT = 2 * NRT;
+    const int id = blockIdx.x, ct = id % NCT, bg = (id / NCT) % NBG, l = id / (NCT * NBG);
+    const bool recw = ct >= NRT;
+    const int ut = recw ? ct - NRT : ct;
+    __shared__ float red[16][16][17];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 15, kk = lane >> 4;
+    const int K = 4 * H, gper = 4 * G;
+    const int64_t BTH = (int64_t)B * T * H;
+    float4 wr[2][G];
+    {
+        const float* Wt = wcatT + (int64_t)l * 2 * H * K + (int64_t)(ct * 16 + col) * K;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                wr[h][g] = ld4(Wt + ((wave >> 1) * gper + 2 * (wave & 1) + h + 4 * g) * 16 + 4 * kk);
+    }
+    const __amdgpu_buffer_rsrc_t rda = buf_rsrc(DA + l * 4 * BTH, (uint32_t)(BTH * 16));
+    const __amdgpu_buffer_rsrc_t rxp = buf_rsrc(XP, (uint32_t)((L > 1 ? L - 1 : 1) * BTH * 4));
+    const int arow = min(bg * 16 + col, B - 1);
+    // point phase: thread p < 256 owns (row 16 bg + p / 16, unit 16 ut + p % 16)
+    const int pr = tid >> 4, pu = ut * 16 + (tid & 15), pb = bg * 16 + pr;
+    const bool pact = tid < 256 && pb < B;
+    const int pbc = min(pb, B - 1);
+    const float* Cl = Cst + l * BTH;
+    const float* Gl = Gs + l * 4 * BTH;
+    int* const cnt_da = sync + (l * NBG + bg) * SYNC_LINE;  // DA_l rows of bg: NRT arrivals per frame
+    int* const xf_out = sync + (L * NBG + ((l > 0 ? l - 1 : 0) * NBG + bg) * NRT + ut) * SYNC_LINE;
+    const int* const xf_in = sync + (L * NBG + (l * NBG + bg) * NRT + ut) * SYNC_LINE;
+    int* const err = sync + SYNC_LINES * SYNC_LINE;
+    const bool top = l == L - 1;
+    bool live = true;
+    float dcn = 0.f;
+    for (int i = 0; i < T; ++i) {
+        const int t = T - 1 - i;
+        // the point phase's own operands (forward state, dout): loaded behind the DA loads, so no
+        // poll or MFMA waits for them
+        float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, c = 0.f, cpl = 0.f, dtop = 0.f;
+        const int64_t o = ((int64_t)pbc * T + t) * H + pu;
+        auto load_point = [&]() {
+            if (recw && tid < 256) {
+                const float* gs = Gl + ((int64_t)pbc * T + t) * 4 * H;
+                ig = gs[pu];
+                fg = gs[H + pu];
+                gg = gs[2 * H + pu];
+                og = gs[3 * H + pu];
+                c = Cl[o];
+                cpl = Cl[t > 0 ? o - H : o];
+                if (top) dtop = dout[((int64_t)pbc * H + pu) * T + t];
+            }
+        };
+        // ---- the contraction over DA_l(tf): tf = t + 1 for the recurrent tile, t for the input tile
+        const int tf = recw ? t + 1 : t;
+        float tile = 0.f;
+        if (tf < T) {
+            if (wave == 0 && live) live = poll_ge(cnt_da, NRT * (T - tf), err);
+            __syncthreads();
+            float4 a[2][G];
+            const uint32_t rb = (uint32_t)(((int64_t)arow * T + tf) * K + 4 * kk) * 4u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    a[h][g] = ld4_sc1(rda, rb + (uint32_t)((wave >> 1) * gper + 2 * (wave & 1) + h + 4 * g) * 64u);
+            load_point();
+            __builtin_amdgcn_sched_barrier(0);
+            f32x4v acc[2] = {(f32x4v){0.f, 0.f, 0.f, 0.f}, (f32x4v){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) acc[h] = mfma16(at4(a[h][g], q), at4(wr[h][g], q), acc[h]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) red[2 * wave + h][kk * 4 + q][col] = acc[h][q];
+            __syncthreads();
+            if (tid < 256) {
+                const int r = tid >> 4, cc = tid & 15;
+                float tot = 0.f;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    float v = red[4 * s][r][cc];
+#pragma unroll
+                    for (int w = 1; w < 4; ++w) v += red[4 * s + w][r][cc];
+                    tot += v;
+                }
+                tile = tot;
+            }
+        } else {
+            load_point();
+        }
+        bool publish = false;
+        int* pub = cnt_da;
+        if (!recw) {
+            // ---- input tile: dx (layer 0) or the grad from above of layer l-1
+            if (l == 0) {
+                if (dx && pact) {
+                    const int64_t ox = ((int64_t)pb * H + pu) * T + t;
+                    dx[ox] = acc_x ? dx[ox] + tile : tile;
+                }
+            } else {
+                if (pact)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, tile), rxp,
+                                                          (int)((uint32_t)((l - 1) * BTH + o) * 4u), 0, SC1);
+                publish = true;
+                pub = xf_out;
+            }
+        } else {
+            // ---- recurrent tile: the cell backward of frame t
+            float above = dtop;
+            if (!top) {
+                if (wave == 0 && live) live = poll_ge(xf_in, i + 1, err);
+                __syncthreads();
+                if (tid < 256)
+                    above = __builtin_bit_cast(
+                        float, __builtin_amdgcn_raw_buffer_load_b32(rxp, (int)((uint32_t)(l * BTH + o) * 4u), 0, SC1));
+            }
+            const bool rec = t < T - 1;
+            const float dh = above + (rec ? tile : 0.f);
+            const float cp = t > 0 ? cpl : 0.f, tc = tanhf(c);
+            const float dc = dh * og * (1.f - tc * tc) + (rec ? dcn : 0.f);
+            if (pact) {
+                const uint32_t ob = (uint32_t)(((int64_t)pb * T + t) * 4 * H + pu) * 4u;
+                const uint32_t hb = (uint32_t)H * 4u;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dc * gg * ig * (1.f - ig)), rda,
+                                                      (int)ob, 0, SC1);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dc * cp * fg * (1.f - fg)), rda,
+                                                      (int)(ob + hb), 0, SC1);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dc * ig * (1.f - gg * gg)), rda,
+                                                      (int)(ob + 2 * hb), 0, SC1);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dh * tc * og * (1.f - og)), rda,
+                                                      (int)(ob + 3 * hb), 0, SC1);
+            }
+            dcn = dc * fg;
+            publish = true;
+        }
+        // publish: every storing wave drained, a barrier (also ends this frame's reads of red), one
+        // lane's arrival
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (publish && tid == 0) __hip_atomic_fetch_add(pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ------------------------------------------------------------------------- layout kernels
 // wcat[j] = [w_ih[j] | w_hh[j]] ([4H][2H]), wcatT its transpose ([2H][4H]), bsum = b_ih + b_hh
 __global__ void lstm_pack_kernel(const float* wih, const float* whh, const float* bih, const float* bhh,
@@ -646,6 +814,13 @@ static int fwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
     if (L * nbg > SYNC_LINES || nwg > device_cus() || !sync_words()) return 0;
     return (int)nwg;
 }
+// workgroups of the persistent backward, or 0 (as fwd_pers_grid; plus the hand-off lines)
+static int bwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
+    if (encx_opt(OPT_LSTM_PERSIST) == 0 || H % 128 || H > 512 || B * T * H * 16 >= ((int64_t)1 << 31)) return 0;
+    const int64_t nbg = cdiv(B, 16), nwg = L * nbg * (2 * H / 16);
+    if (L * nbg + (L - 1) * nbg * (H / 16) > SYNC_LINES || nwg > device_cus() || !sync_words()) return 0;
+    return (int)nwg;
+}
 template <int G>
 static void fwd_pers_launch(int nwg, hipStream_t st, const float* xt, const float* wcat, const float* bsum, float* Y,
                             float* C, float* Gs, int B, int T, int H, int nbg, int* sync) {
@@ -724,9 +899,11 @@ int encx_lstm_sync_errors(int64_t* count) {
 }
 
 size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t L) {
-    (void)T;
-    // dcn [L][B][H], P [L][ns][B][2H], the fused step's arrival counters [(L + 1) * H/16] (int)
-    return ((size_t)L * B * H + (size_t)L * bwd_splits(H) * B * 2 * H + (size_t)(L + 1) * (H / 16)) * sizeof(float);
+    // step form: dcn [L][B][H], P [L][ns][B][2H], the fused step's arrival counters [(L + 1) * H/16]
+    // (int); persistent form: XP [L-1][B][T][H]
+    const size_t step = (size_t)L * B * H + (size_t)L * bwd_splits(H) * B * 2 * H + (size_t)(L + 1) * (H / 16);
+    const size_t pers = (size_t)(L > 1 ? L - 1 : 1) * B * T * H;
+    return (step > pers ? step : pers) * sizeof(float);
 }
 
 int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const float* Gs, float* DA, float* dx,
@@ -744,6 +921,26 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
     const int BH = (int)(B * H);
     const dim3 egrid((unsigned)cdiv(BH, 256), (unsigned)(L + (dx ? 1 : 0)));
     const dim3 ggrid((unsigned)(2 * H / 16), (unsigned)ns, (unsigned)L);
+    if (const int nwg = bwd_pers_grid(B, T, H, L)) {
+        int* sync = sync_words();
+        const int nbg = (int)cdiv(B, 16);
+        const size_t lines = (size_t)L * nbg + (size_t)(L - 1) * nbg * (H / 16);
+        const hipError_t e = hipMemsetAsync(sync, 0, lines * SYNC_LINE * sizeof(int), st);
+        if (e != hipSuccess) return (int)e;
+        ps.tag(" persist");
+#define BWD_PERS(G_)                                                                                            \
+    hipLaunchKernelGGL((lstm_bwd_pers<G_>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, dout, wcatT, Cst, Gs, DA, dx, \
+                       acc_x, ws, (int)B, (int)T, (int)H, (int)L, nbg, sync)
+        switch (H / 64) {
+            case 2: BWD_PERS(2); break;
+            case 4: BWD_PERS(4); break;
+            case 6: BWD_PERS(6); break;
+            default: BWD_PERS(8); break;
+        }
+#undef BWD_PERS
+        ENCX_CHECK_LAUNCH();
+        return 0;
+    }
     const int steps = (int)(T + L);
     // E(k + 1) fused into G(k): opt-in (ENCX_LSTM_FUSE=1). Measured slower in the config-3 step:
     // 21.7 us per fused launch against 9.0 + 4.9 us for G(k) and E(k + 1) (profiles/r03): each
