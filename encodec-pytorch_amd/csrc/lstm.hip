@@ -34,6 +34,18 @@ ENCX_DEV f32x4v mfma16(float a, float b, f32x4v c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 ENCX_DEV float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// The cell forward of one (b, u) point from its gate pre-activations: gates i, f, g, o, the cell c
+// (from the previous frame's cp) and h. Shared by the step and the persistent forms, contraction
+// limited to single expressions so that both compile to the same arithmetic.
+ENCX_DEV void cell_fwd(const float pre[4], float cp, float g4[4], float* c, float* h) {
+#pragma clang fp contract(on)
+    g4[0] = sigm(pre[0]);
+    g4[1] = sigm(pre[1]);
+    g4[2] = tanhf(pre[2]);
+    g4[3] = sigm(pre[3]);
+    *c = g4[1] * cp + g4[0] * g4[2];
+    *h = g4[3] * tanhf(*c);
+}
 
 constexpr int UNITS = 4;  // hidden units per forward workgroup (16 gate columns)
 constexpr int FW = 8;     // waves per forward workgroup (K split)
@@ -124,15 +136,13 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_wave(const float* xt, const 
             for (int w = 1; w < FW; ++w) s += red[w][pb][cc];
             pre[g] = s + bias[g];
         }
-        const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanhf(pre[2]), og = sigm(pre[3]);
-        const float c = fg * cpv + ig * gg;
+        float g4[4], c, h;
+        cell_fwd(pre, cpv, g4, &c, &h);
         Cl[po] = c;
-        Yl[po] = og * tanhf(c);
+        Yl[po] = h;
         float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)pb * T + t) * 4 * H;
-        gs[pu] = ig;
-        gs[H + pu] = fg;
-        gs[2 * H + pu] = gg;
-        gs[3 * H + pu] = og;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gs[q * H + pu] = g4[q];
     }
 }
 
@@ -274,18 +284,16 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
                 for (int w = 1; w < FW; ++w) s += red[w][pr][n];
                 pre[g] = s + bias[g];
             }
-            const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanhf(pre[2]), og = sigm(pre[3]);
-            c = fg * c + ig * gg;
+            float g4[4], h;
+            cell_fwd(pre, c, g4, &c, &h);
             const int64_t po = ((int64_t)pb * T + t) * H + pu;
             Cl[po] = c;
             // h: handed off inside this launch, so written through (sc1)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, og * tanhf(c)), ry,
-                                                  (int)((uint32_t)po * 4u), 0, SC1);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, h), ry, (int)((uint32_t)po * 4u), 0,
+                                                  SC1);
             float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)pb * T + t) * 4 * H;
-            gs[pu] = ig;
-            gs[H + pu] = fg;
-            gs[2 * H + pu] = gg;
-            gs[3 * H + pu] = og;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gs[q * H + pu] = g4[q];
         }
         // publish: every storing wave drained, a barrier, one lane's arrival
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -301,6 +309,22 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
 //   dc = dh o (1 - tanh^2 c) + dcn;  da_{i,f,g,o} -> DA_l[b][t];  dcn <- dc f
 // role L: dx[b][u][t0] (+)= sum_s P_0[s][b][u] for the frame t0 layer 0 finished in step k-1.
 // Partial sums over the split index s are added in ascending s (deterministic).
+// The cell backward of one (b, u) point: gate pre-activation grads da[4] and the cell grad carried
+// to frame t-1 (dc f), from dh, the carried dcn (rec: t < T-1) and the forward state. Shared by the
+// step and the persistent forms, with contraction limited to single expressions so that both
+// compile to the same arithmetic.
+ENCX_DEV void cell_bwd(float dh, float dcn, bool rec, float ig, float fg, float gg, float og, float c, float cp,
+                       float da[4], float* dcn_out) {
+#pragma clang fp contract(on)
+    const float tc = tanhf(c);
+    const float dc = dh * og * (1.f - tc * tc) + (rec ? dcn : 0.f);
+    da[0] = dc * gg * ig * (1.f - ig);
+    da[1] = dc * cp * fg * (1.f - fg);
+    da[2] = dc * ig * (1.f - gg * gg);
+    da[3] = dh * tc * og * (1.f - og);
+    *dcn_out = dc * fg;
+}
+
 // one (b, u) point of E(k) in `role` (the body of lstm_bwd_elem; the fused step's tail)
 ENCX_DEV void bwd_elem_point(const float* dout, const float* P, int ns, float* dcn, const float* Cst,
                              const float* Gs, float* DA, float* dx, int acc_x, int B, int T, int H, int L, int k,
@@ -328,16 +352,15 @@ ENCX_DEV void bwd_elem_point(const float* dout, const float* P, int ns, float* d
     const float* Cl = Cst + (int64_t)l * BTH;
     const float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)b * T + t) * 4 * H;
     const float ig = gs[u], fg = gs[H + u], gg = gs[2 * H + u], og = gs[3 * H + u];
-    const float c = Cl[o], cpl = Cl[t > 0 ? o - H : o], cp = t > 0 ? cpl : 0.f, tc = tanhf(c);
+    const float c = Cl[o], cpl = Cl[t > 0 ? o - H : o], cp = t > 0 ? cpl : 0.f;
     float* dcl = dcn + (int64_t)l * B * H;
-    const float dcv = dcl[p];
-    const float dc = dh * og * (1.f - tc * tc) + (rec ? dcv : 0.f);
+    float g4[4];
+    cell_bwd(dh, dcl[p], rec, ig, fg, gg, og, c, cp, g4, &dcl[p]);
     float* da = DA + (int64_t)l * 4 * BTH + ((int64_t)b * T + t) * 4 * H;
-    da[u] = dc * gg * ig * (1.f - ig);
-    da[H + u] = dc * cp * fg * (1.f - fg);
-    da[2 * H + u] = dc * ig * (1.f - gg * gg);
-    da[3 * H + u] = dh * tc * og * (1.f - og);
-    dcl[p] = dc * fg;
+    da[u] = g4[0];
+    da[H + u] = g4[1];
+    da[2 * H + u] = g4[2];
+    da[3 * H + u] = g4[3];
 }
 
 __global__ __launch_bounds__(256) void lstm_bwd_elem(const float* dout, const float* P, int ns, float* dcn,
@@ -585,21 +608,15 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
             }
             const bool rec = t < T - 1;
             const float dh = above + (rec ? tile : 0.f);
-            const float cp = t > 0 ? cpl : 0.f, tc = tanhf(c);
-            const float dc = dh * og * (1.f - tc * tc) + (rec ? dcn : 0.f);
+            float g4[4];
+            cell_bwd(dh, dcn, rec, ig, fg, gg, og, c, t > 0 ? cpl : 0.f, g4, &dcn);
             if (pact) {
                 const uint32_t ob = (uint32_t)(((int64_t)pb * T + t) * 4 * H + pu) * 4u;
-                const uint32_t hb = (uint32_t)H * 4u;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dc * gg * ig * (1.f - ig)), rda,
-                                                      (int)ob, 0, SC1);
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dc * cp * fg * (1.f - fg)), rda,
-                                                      (int)(ob + hb), 0, SC1);
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dc * ig * (1.f - gg * gg)), rda,
-                                                      (int)(ob + 2 * hb), 0, SC1);
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dh * tc * og * (1.f - og)), rda,
-                                                      (int)(ob + 3 * hb), 0, SC1);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g4[q]), rda,
+                                                          (int)(ob + (uint32_t)(q * H) * 4u), 0, SC1);
             }
-            dcn = dc * fg;
             publish = true;
         }
         // publish: every storing wave drained, a barrier (also ends this frame's reads of red), one
