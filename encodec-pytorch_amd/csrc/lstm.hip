@@ -169,6 +169,22 @@ constexpr int SYNC_LINES = 512;
 // hand-off counters [SYNC_LINES][SYNC_LINE] (zeroed per launch), then the error word's line
 __device__ int g_lstm_sync[(SYNC_LINES + 1) * SYNC_LINE];
 
+// Development tracing (build with -DENCX_LSTM_TRACE; encx_lstm_trace reads it): thread 0 of every
+// persistent workgroup stamps the steady clock at up to 8 points of every frame,
+// g_lstm_trace[kernel (0 fwd, 1 bwd)][workgroup < 256][frame < 128][point].
+#ifdef ENCX_LSTM_TRACE
+__device__ long long g_lstm_trace[2 * 256 * 128 * 8];
+#define LSTM_TRACE(kern, i, k)                                                               \
+    do {                                                                                     \
+        if (tid == 0 && blockIdx.x < 256 && (i) < 128)                                       \
+            g_lstm_trace[(((kern) * 256 + blockIdx.x) * 128 + (i)) * 8 + (k)] = wall_clock64(); \
+    } while (0)
+#else
+#define LSTM_TRACE(kern, i, k) \
+    do {                       \
+    } while (0)
+#endif
+
 // wave-wide bounded poll: cnt >= target (relaxed agent loads, sc1); false after ~1 s
 ENCX_DEV bool poll_ge(const int* cnt, int target, int* err) {
     for (int i = 0; i < (1 << 20); ++i) {
@@ -232,6 +248,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
     bool live = true;  // wave 0: no poll has timed out
     float c = 0.f;
     for (int t = 0; t < T; ++t) {
+        LSTM_TRACE(0, t, 0);
         f32x4v acc[2] = {(f32x4v){0.f, 0.f, 0.f, 0.f}, (f32x4v){0.f, 0.f, 0.f, 0.f}};
         // ---- input part x_l(t): layer 0 reads xt (written before this launch), layer l > 0
         // waits for h_{l-1}(t) of all NUG workgroups of (l-1, bg)
@@ -239,6 +256,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
             if (wave == 0 && live) live = poll_ge(cnt_in, NUG * (t + 1), err);
             __syncthreads();
         }
+        LSTM_TRACE(0, t, 1);
         {  // k-groups g < G / 2 of every wave lie in the input half (H % 128 == 0)
             float4 a[G / 2];
             const uint32_t rb = (uint32_t)(((int64_t)arow * T + t) * H + 4 * kk) * 4u;
@@ -254,8 +272,10 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
         }
         // ---- recurrent part h_l(t-1) (zero at t = 0): k-groups g >= G / 2
         if (t > 0) {
+            LSTM_TRACE(0, t, 2);
             if (wave == 0 && live) live = poll_ge(cnt_self, NUG * t, err);
             __syncthreads();
+            LSTM_TRACE(0, t, 3);
             float4 a[G / 2];
             const uint32_t rb = (uint32_t)(((int64_t)arow * T + t - 1) * H + 4 * kk - H) * 4u;
 #pragma unroll
@@ -274,6 +294,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
 #pragma unroll
             for (int q = 0; q < 4; ++q) red[wave][kk * 4 + q][16 * cc + col] = acc[cc][q];
         __syncthreads();
+        LSTM_TRACE(0, t, 4);
         if (pact) {
             float pre[4];
 #pragma unroll
@@ -296,8 +317,10 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
             for (int q = 0; q < 4; ++q) gs[q * H + pu] = g4[q];
         }
         // publish: every storing wave drained, a barrier, one lane's arrival
+        LSTM_TRACE(0, t, 5);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        LSTM_TRACE(0, t, 6);
         if (tid == 0) __hip_atomic_fetch_add(cnt_self, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -522,6 +545,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
     float dcn = 0.f;
     for (int i = 0; i < T; ++i) {
         const int t = T - 1 - i;
+        LSTM_TRACE(1, i, 0);
         // the point phase's own operands (forward state, dout): loaded behind the DA loads, so no
         // poll or MFMA waits for them
         float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, c = 0.f, cpl = 0.f, dtop = 0.f;
@@ -544,6 +568,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
         if (tf < T) {
             if (wave == 0 && live) live = poll_ge(cnt_da, NRT * (T - tf), err);
             __syncthreads();
+            LSTM_TRACE(1, i, 1);
             float4 a[2][G];
             const uint32_t rb = (uint32_t)(((int64_t)arow * T + tf) * K + 4 * kk) * 4u;
 #pragma unroll
@@ -565,6 +590,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
 #pragma unroll
                 for (int q = 0; q < 4; ++q) red[2 * wave + h][kk * 4 + q][col] = acc[h][q];
             __syncthreads();
+            LSTM_TRACE(1, i, 2);
             if (tid < 256) {
                 const int r = tid >> 4, cc = tid & 15;
                 float tot = 0.f;
@@ -602,6 +628,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
             if (!top) {
                 if (wave == 0 && live) live = poll_ge(xf_in, i + 1, err);
                 __syncthreads();
+                LSTM_TRACE(1, i, 3);
                 if (tid < 256)
                     above = __builtin_bit_cast(
                         float, __builtin_amdgcn_raw_buffer_load_b32(rxp, (int)((uint32_t)(l * BTH + o) * 4u), 0, SC1));
@@ -621,8 +648,10 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
         }
         // publish: every storing wave drained, a barrier (also ends this frame's reads of red), one
         // lane's arrival
+        LSTM_TRACE(1, i, 4);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        LSTM_TRACE(1, i, 5);
         if (publish && tid == 0) __hip_atomic_fetch_add(pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -900,6 +929,19 @@ int encx_lstm_fwd(const float* x, const float* wcat, const float* bsum, float* x
                        out, (int)B, (int)T, (int)H, skip);
     ENCX_CHECK_LAUNCH();
     return 0;
+}
+
+int encx_lstm_trace(int64_t* out, int64_t n) {
+#ifdef ENCX_LSTM_TRACE
+    ENCX_REQUIRE(out && n >= 0 && n <= 2 * 256 * 128 * 8);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_trace), (size_t)n * sizeof(int64_t));
+    return (int)e;
+#else
+    (void)out;
+    (void)n;
+    return ENCX_EINVAL;
+#endif
 }
 
 int encx_lstm_sync_errors(int64_t* count) {

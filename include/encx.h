@@ -344,6 +344,10 @@ size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H);
  * and clears the number of spins that timed out on the current device since the last call (0 on
  * a healthy run; nonzero means a launch's results are garbage). Synchronises the device. */
 int encx_lstm_sync_errors(int64_t* count);
+/* Development: the persistent kernels' per-frame clock stamps (steady clock, 100 MHz) as
+ * [kernel 0 fwd / 1 bwd][workgroup < 256][frame < 128][8 points] int64, first n of them; EINVAL
+ * unless the library was built with -DENCX_LSTM_TRACE (tools/lstm_trace.py). Synchronises. */
+int encx_lstm_trace(int64_t* out, int64_t n);
 /* Weight grads of layer `layer` from DA: dw_ih, dw_hh [4H][H] and the bias grad (to both db_ih
  * and db_hh; either may be NULL), written (acc = 0) or added (acc = 1). */
 int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float* dw_ih, float* dw_hh,
