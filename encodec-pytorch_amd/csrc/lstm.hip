@@ -162,7 +162,12 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_wave(const float* xt, const 
 // bounded: a timeout counts in the error word (encx_lstm_sync_errors) and the launch drains.
 // All L NBG NUG workgroups must be resident together: the host uses this form only when they are
 // at most one per CU. The arithmetic (k-group order, LDS sum order, gate math) is that of
-// lstm_fwd_wave, so both forms give the same bits.
+// lstm_fwd_wave, so both forms give the same bits. Measured (tools/lstm_trace.py, profiles/r05/
+// lstm): a frame takes 4.9 us (input part 1.5, recurrent loads + MFMA 1.6, gates 0.7, hand-off
+// 0.8). Starting frame t+1's input part during frame t's gate phase (the two storing waves
+// signalling through an LDS count) was slower, 389 -> 440 us per forward (frame 7.0 us: the early
+// MFMAs delay the gate phase), and plain loads of the handed-off frames instead of sc1 loads
+// gained nothing in either direction.
 constexpr int PU = 8;           // hidden units per persistent workgroup
 constexpr int SYNC_LINE = 32;   // ints per counter: one 128-byte line each
 constexpr int SYNC_LINES = 512;
@@ -198,30 +203,22 @@ ENCX_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const float* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
 }
 constexpr int SC1 = 16;  // buffer op cache-policy bit: write-through store / L1-bypassing load
-// 16-byte buffer load with cache policy AUX (SC1, or 0: a plain load, L1 and L2 allocating)
-template <int AUX>
-ENCX_DEV float4 ld4_buf(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+ENCX_DEV float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
     // (the whole vector is bit-cast: clang 20 miscompiles a bit_cast of one element, v[i], into a
     // read of element 0)
-    const f32x4v v = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, AUX));
+    const f32x4v v = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, SC1));
     return make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // grid L * NBG * NUG (NUG = H / PU), FW waves; G = 2H / (16 FW) k-groups per wave (H % 128 == 0, so
-// groups g < G / 2 of every wave are in the input half of K and the others in the recurrent half).
-// AUX: the cache policy of the loads of handed-off h (SC1; 0 = plain, see encx_lstm_fwd).
-// Frame order per workgroup: the input part of frame t+1 runs while frame t's gates are computed
-// and published (waves 2.. start it at once; waves 0 and 1, which own the gate phase, after they
-// have stored and drained; the second of them to drain signals the frame, through an LDS count),
-// so only the recurrent part, the gates and the hand-off are on the recurrence's critical path.
-template <int G, int AUX>
+// groups g < G / 2 of every wave are in the input half of K and the others in the recurrent half)
+template <int G>
 __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const float* wcat, const float* bsum,
                                                          float* Y, float* Cst, float* Gs, int B, int T, int H,
                                                          int NBG, int* sync) {
     const int NUG = H / PU;
     const int id = blockIdx.x, ug = id % NUG, bg = (id / NUG) % NBG, l = id / (NUG * NBG);
     __shared__ float red[FW][16][33];
-    __shared__ int s_arrive;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 15, kk = lane >> 4;
     const int u0 = ug * PU, K = 2 * H;
     const int64_t BTH = (int64_t)B * T * H;
@@ -238,8 +235,8 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
                 wr[g][c] = ld4(W + (int64_t)j * K + (wave + FW * g) * 16 + 4 * kk);
             }
     }
-    // every load of a sequence goes through these descriptors (the host checks that the byte
-    // offsets fit 32 bits)
+    // every load of a sequence goes through these descriptors with sc1 (the host checks that the
+    // byte offsets fit 32 bits)
     const __amdgpu_buffer_rsrc_t rx = buf_rsrc(l == 0 ? xt : Y + (l - 1) * BTH, (uint32_t)(BTH * 4));
     const __amdgpu_buffer_rsrc_t ry = buf_rsrc(Y + l * BTH, (uint32_t)(BTH * 4));
     const int arow = min(bg * 16 + col, B - 1);  // rows >= B compute garbage that is never stored
@@ -253,38 +250,41 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
     int* const cnt_self = sync + (l * NBG + bg) * SYNC_LINE;
     const int* const cnt_in = sync + ((l > 0 ? l - 1 : 0) * NBG + bg) * SYNC_LINE;
     int* const err = sync + SYNC_LINES * SYNC_LINE;
-    if (tid == 0) s_arrive = 0;
-    bool live = true;  // this wave: no poll has timed out
-    // ---- input part x_l(t) (k-groups g < G / 2) into acc: layer 0 reads xt (written before this
-    // launch); for l > 0 the wave itself first waits for h_{l-1}(t) of all NUG workgroups of (l-1, bg)
-    auto input_part = [&](int t, f32x4v* acc) {
-        if (l > 0 && live) live = poll_ge(cnt_in, NUG * (t + 1), err);
-        float4 a[G / 2];
-        const uint32_t rb = (uint32_t)(((int64_t)arow * T + t) * H + 4 * kk) * 4u;
-#pragma unroll
-        for (int g = 0; g < G / 2; ++g) a[g] = ld4_buf<AUX>(rx, rb + (uint32_t)(wave + FW * g) * 64u);
-        __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
-#pragma unroll
-        for (int g = 0; g < G / 2; ++g)
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma16(at4(a[g], s), at4(wr[g][cc], s), acc[cc]);
-    };
-    f32x4v acc[2] = {(f32x4v){0.f, 0.f, 0.f, 0.f}, (f32x4v){0.f, 0.f, 0.f, 0.f}};
-    input_part(0, acc);
+    bool live = true;  // wave 0: no poll has timed out
     float c = 0.f;
     for (int t = 0; t < T; ++t) {
         LSTM_TRACE(0, t, 0);
+        f32x4v acc[2] = {(f32x4v){0.f, 0.f, 0.f, 0.f}, (f32x4v){0.f, 0.f, 0.f, 0.f}};
+        // ---- input part x_l(t): layer 0 reads xt (written before this launch), layer l > 0
+        // waits for h_{l-1}(t) of all NUG workgroups of (l-1, bg)
+        if (l > 0) {
+            if (wave == 0 && live) live = poll_ge(cnt_in, NUG * (t + 1), err);
+            __syncthreads();
+        }
+        LSTM_TRACE(0, t, 1);
+        {  // k-groups g < G / 2 of every wave lie in the input half (H % 128 == 0)
+            float4 a[G / 2];
+            const uint32_t rb = (uint32_t)(((int64_t)arow * T + t) * H + 4 * kk) * 4u;
+#pragma unroll
+            for (int g = 0; g < G / 2; ++g) a[g] = ld4_sc1(rx, rb + (uint32_t)(wave + FW * g) * 64u);
+            __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
+#pragma unroll
+            for (int g = 0; g < G / 2; ++g)
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma16(at4(a[g], s), at4(wr[g][cc], s), acc[cc]);
+        }
         // ---- recurrent part h_l(t-1) (zero at t = 0): k-groups g >= G / 2
         if (t > 0) {
+            LSTM_TRACE(0, t, 2);
             if (wave == 0 && live) live = poll_ge(cnt_self, NUG * t, err);
             __syncthreads();
-            LSTM_TRACE(0, t, 1);
+            LSTM_TRACE(0, t, 3);
             float4 a[G / 2];
             const uint32_t rb = (uint32_t)(((int64_t)arow * T + t - 1) * H + 4 * kk - H) * 4u;
 #pragma unroll
-            for (int g = 0; g < G / 2; ++g) a[g] = ld4_buf<AUX>(ry, rb + (uint32_t)(wave + FW * (g + G / 2)) * 64u);
+            for (int g = 0; g < G / 2; ++g) a[g] = ld4_sc1(ry, rb + (uint32_t)(wave + FW * (g + G / 2)) * 64u);
             __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
 #pragma unroll
             for (int g = 0; g < G / 2; ++g)
@@ -299,41 +299,34 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
 #pragma unroll
             for (int q = 0; q < 4; ++q) red[wave][kk * 4 + q][16 * cc + col] = acc[cc][q];
         __syncthreads();
-        LSTM_TRACE(0, t, 2);
+        LSTM_TRACE(0, t, 4);
+        if (pact) {
+            float pre[4];
 #pragma unroll
-        for (int cc = 0; cc < 2; ++cc) acc[cc] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-        if (wave < 2) {  // the gate phase (16 PU = 128 threads), then the frame's publication
-            if (pact) {
-                float pre[4];
+            for (int g = 0; g < 4; ++g) {
+                const int n = g * PU + (pu - u0);
+                float s = red[0][pr][n];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int n = g * PU + (pu - u0);
-                    float s = red[0][pr][n];
-#pragma unroll
-                    for (int w = 1; w < FW; ++w) s += red[w][pr][n];
-                    pre[g] = s + bias[g];
-                }
-                float g4[4], h;
-                cell_fwd(pre, c, g4, &c, &h);
-                const int64_t po = ((int64_t)pb * T + t) * H + pu;
-                Cl[po] = c;
-                // h: handed off inside this launch, so written through (sc1)
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, h), ry, (int)((uint32_t)po * 4u),
-                                                      0, SC1);
-                float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)pb * T + t) * 4 * H;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) gs[q * H + pu] = g4[q];
+                for (int w = 1; w < FW; ++w) s += red[w][pr][n];
+                pre[g] = s + bias[g];
             }
-            LSTM_TRACE(0, t, 3);
-            // publish: each storing wave drains, then counts itself in LDS; the second signals
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0 && atomicAdd(&s_arrive, 1) == 1) {
-                s_arrive = 0;  // next frame's arrivals come after the next workgroup barrier
-                __hip_atomic_fetch_add(cnt_self, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            LSTM_TRACE(0, t, 4);
+            float g4[4], h;
+            cell_fwd(pre, c, g4, &c, &h);
+            const int64_t po = ((int64_t)pb * T + t) * H + pu;
+            Cl[po] = c;
+            // h: handed off inside this launch, so written through (sc1)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, h), ry, (int)((uint32_t)po * 4u), 0,
+                                                  SC1);
+            float* gs = Gs + (int64_t)l * 4 * BTH + ((int64_t)pb * T + t) * 4 * H;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gs[q * H + pu] = g4[q];
         }
-        if (t + 1 < T) input_part(t + 1, acc);
+        // publish: every storing wave drained, a barrier, one lane's arrival
+        LSTM_TRACE(0, t, 5);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        LSTM_TRACE(0, t, 6);
+        if (tid == 0) __hip_atomic_fetch_add(cnt_self, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -516,9 +509,8 @@ __global__ __launch_bounds__(BW * 64) void lstm_bwd_gemm(const float* DA, const 
 // lstm_bwd_gemm + lstm_bwd_elem (4 splits of the 4H/16 k-groups, each 4 interleaved chains summed
 // in chain order, the splits summed in ascending order), so both forms give the same bits: wave w
 // runs chains (s, c) = (w / 2, 2 (w % 2) + h), h = 0, 1, of G k-groups each (H % 128 == 0, G = H/64).
-// grid L * NBG * 2H/16, FW waves. XP [L-1][B][T][H]: the input-grad tiles between layers. AUX: the
-// cache policy of the loads of handed-off DA and XP (SC1; 0 = plain, see encx_lstm_fwd).
-template <int G, int AUX>
+// grid L * NBG * 2H/16, FW waves. XP [L-1][B][T][H]: the input-grad tiles between layers.
+template <int G>
 __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, const float* wcatT, const float* Cst,
                                                          const float* Gs, float* DA, float* dx, int acc_x,
                                                          float* XP, int B, int T, int H, int L, int NBG,
@@ -588,7 +580,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
             for (int h = 0; h < 2; ++h)
 #pragma unroll
                 for (int g = 0; g < G; ++g)
-                    a[h][g] = ld4_buf<AUX>(rda, rb + (uint32_t)((wave >> 1) * gper + 2 * (wave & 1) + h + 4 * g) * 64u);
+                    a[h][g] = ld4_sc1(rda, rb + (uint32_t)((wave >> 1) * gper + 2 * (wave & 1) + h + 4 * g) * 64u);
             load_point();
             __builtin_amdgcn_sched_barrier(0);
             f32x4v acc[2] = {(f32x4v){0.f, 0.f, 0.f, 0.f}, (f32x4v){0.f, 0.f, 0.f, 0.f}};
@@ -644,7 +636,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
                 LSTM_TRACE(1, i, 3);
                 if (tid < 256)
                     above = __builtin_bit_cast(
-                        float, __builtin_amdgcn_raw_buffer_load_b32(rxp, (int)((uint32_t)(l * BTH + o) * 4u), 0, AUX));
+                        float, __builtin_amdgcn_raw_buffer_load_b32(rxp, (int)((uint32_t)(l * BTH + o) * 4u), 0, SC1));
             }
             const bool rec = t < T - 1;
             const float dh = above + (rec ? tile : 0.f);
@@ -865,11 +857,6 @@ static int* sync_words() {
     if (!addr[d] && hipGetSymbolAddress((void**)&addr[d], HIP_SYMBOL(g_lstm_sync)) != hipSuccess) addr[d] = nullptr;
     return addr[d];
 }
-// LSTM_PERSIST = 2: the handed-off sequences are read with plain (L1 / L2 allocating) loads instead
-// of sc1 loads. Every such line is written exactly once per launch, write-through, before any
-// workgroup reads it (the counters order every read after the write), and no cache holds it from
-// an earlier launch: the kernel boundary writes back and invalidates the caches.
-static bool pers_plain_loads() { return encx_opt(OPT_LSTM_PERSIST) == 2; }
 // workgroups of the persistent forward, or 0 when the shape or the device does not admit it (the
 // workgroups must be resident together: at most one per CU; the sequences' byte offsets 32-bit)
 static int fwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
@@ -888,23 +875,8 @@ static int bwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
 template <int G>
 static void fwd_pers_launch(int nwg, hipStream_t st, const float* xt, const float* wcat, const float* bsum, float* Y,
                             float* C, float* Gs, int B, int T, int H, int nbg, int* sync) {
-    if (pers_plain_loads())
-        hipLaunchKernelGGL((lstm_fwd_pers<G, 0>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C, Gs,
-                           B, T, H, nbg, sync);
-    else
-        hipLaunchKernelGGL((lstm_fwd_pers<G, SC1>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C,
-                           Gs, B, T, H, nbg, sync);
-}
-template <int G>
-static void bwd_pers_launch(int nwg, hipStream_t st, const float* dout, const float* wcatT, const float* Cst,
-                            const float* Gs, float* DA, float* dx, int acc_x, float* XP, int B, int T, int H, int L,
-                            int nbg, int* sync) {
-    if (pers_plain_loads())
-        hipLaunchKernelGGL((lstm_bwd_pers<G, 0>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, dout, wcatT, Cst, Gs, DA,
-                           dx, acc_x, XP, B, T, H, L, nbg, sync);
-    else
-        hipLaunchKernelGGL((lstm_bwd_pers<G, SC1>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, dout, wcatT, Cst, Gs,
-                           DA, dx, acc_x, XP, B, T, H, L, nbg, sync);
+    hipLaunchKernelGGL((lstm_fwd_pers<G>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C, Gs, B, T,
+                       H, nbg, sync);
 }
 
 static bool lstm_shape_ok(int64_t B, int64_t T, int64_t H, int64_t L) {
@@ -1020,13 +992,16 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
         const hipError_t e = hipMemsetAsync(sync, 0, lines * SYNC_LINE * sizeof(int), st);
         if (e != hipSuccess) return (int)e;
         ps.tag(" persist");
-        const int Bi = (int)B, Ti = (int)T, Hi = (int)H, Li = (int)L;
+#define BWD_PERS(G_)                                                                                            \
+    hipLaunchKernelGGL((lstm_bwd_pers<G_>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, dout, wcatT, Cst, Gs, DA, dx, \
+                       acc_x, ws, (int)B, (int)T, (int)H, (int)L, nbg, sync)
         switch (H / 64) {
-            case 2: bwd_pers_launch<2>(nwg, st, dout, wcatT, Cst, Gs, DA, dx, acc_x, ws, Bi, Ti, Hi, Li, nbg, sync); break;
-            case 4: bwd_pers_launch<4>(nwg, st, dout, wcatT, Cst, Gs, DA, dx, acc_x, ws, Bi, Ti, Hi, Li, nbg, sync); break;
-            case 6: bwd_pers_launch<6>(nwg, st, dout, wcatT, Cst, Gs, DA, dx, acc_x, ws, Bi, Ti, Hi, Li, nbg, sync); break;
-            default: bwd_pers_launch<8>(nwg, st, dout, wcatT, Cst, Gs, DA, dx, acc_x, ws, Bi, Ti, Hi, Li, nbg, sync); break;
+            case 2: BWD_PERS(2); break;
+            case 4: BWD_PERS(4); break;
+            case 6: BWD_PERS(6); break;
+            default: BWD_PERS(8); break;
         }
+#undef BWD_PERS
         ENCX_CHECK_LAUNCH();
         return 0;
     }

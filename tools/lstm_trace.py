@@ -46,17 +46,18 @@ def main():
     nug = H // 8
     nwg = L * nbg * nug
     fw = tr[0, :nwg, :T]
+    names = ['wait x', 'x MFMA', 'poll h', 'h load+MFMA+LDS', 'gates+stores', 'drain+barrier', 'to next frame']
     print(f'forward: {nwg} workgroups, frame cadence (median over workgroups of start(t+1) - start(t)): '
           f'{np.median(np.diff(fw[:, :, 0], axis=1)):.2f} us; whole recurrence '
-          f'{fw[:, T - 1, 4].max() - fw[:, 0, 0].min():.1f} us')
+          f'{fw[:, T - 1, 6].max() - fw[:, 0, 0].min():.1f} us')
     for l in range(L):
-        s = fw[l * nbg * nug:(l + 1) * nbg * nug]
-        seg = lambda a, b: np.median(s[:, 1:, b] - s[:, 1:, a])
-        print(f'  layer {l}: poll h {seg(0, 1):.2f}, h load+MFMA+LDS {seg(1, 2):.2f}, gates+stores {seg(2, 3):.2f}, '
-              f'drain+signal {seg(3, 4):.2f}, to next frame (input part) {np.median(s[:, 1:, 0] - s[:, :-1, 4]):.2f}')
-        pub = s[:, :, 4].max(axis=0)
-        got = s[:, 1:, 1]
-        print(f'    h hand-off: last producer signal -> consumer poll done: median '
+        sel = fw[l * nbg * nug:(l + 1) * nbg * nug, 1:]
+        d = np.diff(np.concatenate([sel, np.roll(sel[:, :, :1], -1, axis=1)], axis=2), axis=2)[:, :-1]
+        print(f'  layer {l}: ' + ', '.join(f'{nm} {np.median(d[:, :, i]):.2f}' for i, nm in enumerate(names)))
+        # hand-off: poll h done (point 3) of frame t vs the last publish (point 6) of frame t-1 of the layer
+        pub = sel[:, :, 6].max(axis=0)
+        got = sel[:, 1:, 3]
+        print(f'    h hand-off: last producer publish -> consumer poll done: median '
               f'{np.median(got - pub[None, :-1]):.2f} us, max {np.max(got - pub[None, :-1]):.2f}')
     # ---- backward: workgroup (l, bg, ct), NCT = 2H / 16
     nct = 2 * H // 16
