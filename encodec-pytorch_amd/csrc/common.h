@@ -12,6 +12,7 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
 ENCX_DEV f32x4 ld4u(const float* p) { return *(const f32x4u*)p; }  // 4-byte aligned quad load
 

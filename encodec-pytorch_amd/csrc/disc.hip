@@ -1763,11 +1763,14 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
     const float* dyb = a.dy + (int64_t)b * g.Co * plane;
     const float* yab = YM ? a.yact + (int64_t)b * g.Co * plane : dyb;
     const int items = DN_CC * NRW * RC;
-    float acc[CI][DN_FPT];
+    // accumulators as (ci, ci + 1) pairs: one packed FMA (v_pk_fma_f32, the weight pair from
+    // SGPRs) per two channels
+    static_assert(CI % 2 == 0, "channel pairs");
+    f32x2 acc[CI / 2][DN_FPT];
 #pragma unroll
-    for (int c = 0; c < CI; ++c)
+    for (int c = 0; c < CI / 2; ++c)
 #pragma unroll
-        for (int e = 0; e < DN_FPT; ++e) acc[c][e] = 0.f;
+        for (int e = 0; e < DN_FPT; ++e) acc[c][e] = (f32x2){0.f, 0.f};
     // VQ: the tile is staged as quads along f (ld4u; lanes outside [0, Fo) or outside the
     // tensor masked), one index split per 4 elements instead of per element
     constexpr int RQ = RC / 4, QP = 4;
@@ -1855,10 +1858,13 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
 #pragma unroll
                 for (int kf = 0; kf < KF; ++kf)
 #pragma unroll
-                    for (int c = 0; c < CI; ++c) {
-                        const float w = wr[kf * CI + c];
+                    for (int c = 0; c < CI / 2; ++c) {
+                        const f32x2 w = {wr[kf * CI + 2 * c], wr[kf * CI + 2 * c + 1]};
 #pragma unroll
-                        for (int e = 0; e < DN_FPT; ++e) acc[c][e] = fmaf(w, win[e + KF - 1 - kf], acc[c][e]);
+                        for (int e = 0; e < DN_FPT; ++e) {
+                            const float xv = win[e + KF - 1 - kf];
+                            acc[c][e] = __builtin_elementwise_fma(w, (f32x2){xv, xv}, acc[c][e]);
+                        }
                     }
             }
         }
@@ -1872,7 +1878,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
             const int f = f0 + 4 * tx + e;
             if (f >= g.Fi) continue;
             const int64_t o = (((int64_t)b * CI + c) * g.T2 + t) * g.Fi + f;
-            float v = acc[c][e];
+            float v = acc[c / 2][e][c % 2];
             if (a.ffr) v += feat_term(a, feat_coef(a), o);
             if (a.xact) v *= lrelu_grad(a.xact[o]);
             a.dx[o] = a.accumulate ? a.dx[o] + v : v;
