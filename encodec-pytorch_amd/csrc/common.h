@@ -185,7 +185,6 @@ enum EncxOpt {
     OPT_CONV_CK,       // conv1d fwd / bwd-data: reduction elements (channels x taps) per LDS chunk
     OPT_CONV_SPLIT,    // conv1d fwd / bwd-data: split-K until this many workgroups
     OPT_CONV_WG_SPLIT, // conv1d weight grad: split the positions until this many workgroups
-    OPT_CONV_PF,       // conv1d: register-prefetched LDS staging where the chunk fits the slots
     OPT_COUNT
 };
 int64_t encx_opt(EncxOpt id);

@@ -52,6 +52,7 @@ struct FwdArgs {
     int Up;   // LDS words per (ci, phase) row
     int KS;   // channel splits
     int cps;  // channels per split (multiple of CK)
+    FastDiv fs;  // division by s (set by launch_fwd): the phase split of every staged element
 };
 
 // y = [acc ? y : 0] + act'(xact) * (v + bias) + res
@@ -68,12 +69,7 @@ ENCX_DEV void fwd_store(const FwdArgs& a, int64_t o, int co, float v) {
 // layers. EPI_RES: + residual; EPI_XACT: * act'(xact); EPI_ACC: + y; EPI_PART: split-K
 // partial store (no bias, no operands).
 enum { EPI_RES = 1, EPI_XACT = 2, EPI_ACC = 4, EPI_PART = 8 };
-// PF: register-prefetched staging. The next chunk's X window and weights are loaded into
-// registers (PF_XQ + PF_WQ float4 per thread; the host admits a plan only if its items fit) while
-// the MFMAs run on the current chunk, then written to LDS between two barriers: the global-load
-// round trip of every chunk but the first is hidden behind MFMA work.
-constexpr int PF_XQ = 2 * SPER, PF_WQ = 3 * SPER;
-template <int BM, int BN, int WM, int WN, int EPI, bool PF = false>
+template <int BM, int BN, int WM, int WN, int EPI>
 __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     extern __shared__ float smem[];
@@ -108,113 +104,6 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
     const int BM4 = BM / 4, nw = K * CK * BM4;
     // item (cl, vi) of thread tid advances by NT items per step: no per-item division
     const int dcl = NT / nv, dvi = NT - dcl * nv, cl_init = tid / nv, vi_init = tid - cl_init * nv;
-    if constexpr (PF) {
-        f32x4 xr[PF_XQ], wr[PF_WQ];
-        // slot m holds item tid + NT m of the chunk's X window (cl, vi) and of its weights
-        auto load = [&](int c0) {
-            int cl_n = cl_init, vi_n = vi_init;
-#pragma unroll
-            for (int m = 0; m < PF_XQ; ++m) {
-                const int c = c0 + cl_n, p = ab + 4 * vi_n;
-                const bool ok = cl_n < CK && c < cend;
-                f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
-                if (a.vec) {
-                    const int pc = p < 0 ? 0 : (p > a.Tin - 4 ? a.Tin - 4 : p);
-                    const f32x4 t = *(const f32x4*)(xb + (int64_t)(ok ? c : cbeg) * a.Tin + pc);
-                    if (ok && p >= 0 && p + 3 < a.Tin) v = t;
-                }
-                if (ok && !(a.vec && p >= 0 && p + 3 < a.Tin)) {
-                    const float* xrow = xb + (int64_t)c * a.Tin;
-                    for (int e = 0; e < 4; ++e) {
-                        const int mm = pad_src(p + e + a.pl, a.pl, a.Tin, a.e, a.mode);
-                        v[e] = mm >= 0 ? xrow[mm] : 0.f;
-                    }
-                }
-                xr[m] = v;
-                vi_n += dvi;
-                cl_n += dcl;
-                if (vi_n >= nv) {
-                    vi_n -= nv;
-                    ++cl_n;
-                }
-            }
-            const int wrows = (min(cend, c0 + CK) - c0) * K;
-#pragma unroll
-            for (int m = 0; m < PF_WQ; ++m) {
-                const int it = m * NT + tid;
-                const int r = it / BM4, c4 = it - r * BM4, co = co0 + 4 * c4;
-                const bool ok = r < wrows;
-                const float* wrow = a.wf + ((int64_t)c0 * K + (ok ? r : 0)) * a.Cout;
-                f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
-                if (a.vec) {
-                    const int coc = co + 3 < a.Cout ? co : a.Cout - 4;
-                    const f32x4 t = *(const f32x4*)(wrow + coc);
-                    if (ok && co + 3 < a.Cout) v = t;
-                } else if (ok) {
-                    for (int e = 0; e < 4; ++e) v[e] = co + e < a.Cout ? wrow[co + e] : 0.f;
-                }
-                wr[m] = v;
-            }
-        };
-        auto store = [&]() {
-            int cl_n = cl_init, vi_n = vi_init;
-#pragma unroll
-            for (int m = 0; m < PF_XQ; ++m) {
-                if (cl_n < CK) {
-                    float* xs = Xs + cl_n * span;
-                    const int q0 = 4 * vi_n - woff;
-                    if (S == 1 && q0 >= 0 && q0 + 3 < span) {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) xs[q0 + e] = act_apply(a.act, xr[m][e]);
-                    } else {
-                        for (int e = 0; e < 4; ++e) {
-                            const int qq = q0 + e;
-                            if (qq >= 0 && qq < span) {
-                                const int u = qq / S, ph = qq - u * S;
-                                xs[ph * Up + u] = act_apply(a.act, xr[m][e]);
-                            }
-                        }
-                    }
-                }
-                vi_n += dvi;
-                cl_n += dcl;
-                if (vi_n >= nv) {
-                    vi_n -= nv;
-                    ++cl_n;
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < PF_WQ; ++m) {
-                const int it = m * NT + tid;
-                if (it < nw) *(f32x4*)(Ws + 4 * it) = wr[m];
-            }
-        };
-        load(cbeg);
-        for (int c0 = cbeg; c0 < cend; c0 += CK) {
-            __syncthreads();  // the previous chunk's MFMAs are done with Xs / Ws
-            store();
-            __syncthreads();
-            if (c0 + CK < cend) load(c0 + CK);
-            const int h = lane >> 5, l32 = lane & 31;
-            for (int k = 0; k < K; ++k) {
-                const int kd = k * a.d, ph = kd % S, off = kd / S;
-                const float* wk = Ws + (h * K + k) * BM + wm0 + l32;
-                const float* xk = Xs + (h * S + ph) * Up + wn0 + l32 + off;
-#pragma unroll 4
-                for (int cp = 0; cp < CK; cp += 2) {
-                    float av[TM], bv[TN];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) av[i] = wk[cp * K * BM + i * 32];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) bv[j] = xk[cp * S * Up + j * 32];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
-                }
-            }
-        }
-    } else
     for (int c0 = cbeg; c0 < cend; c0 += CK) {
         __syncthreads();
         // SPER items per thread in flight: interior items load as float4 from a clamped address
@@ -271,7 +160,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(FwdArgs a) {
                     for (int e = 0; e < 4; ++e) {
                         const int qq = q0 + e;
                         if (qq >= 0 && qq < span) {
-                            const int u = qq / S, ph = qq - u * S;
+                            const int u = (int)fdiv((uint32_t)qq, a.fs), ph = qq - u * S;
                             xs[ph * Up + u] = act_apply(a.act, v[q][e]);
                         }
                     }
@@ -1170,17 +1059,11 @@ void launch_fwd(FwdArgs a, hipStream_t st) {
     dim3 grid(cdiv(a.Tout, BN), cdiv(a.Cout, BM), a.B * a.KS);
     size_t lds = (size_t)(((a.CK * a.s * a.Up + 3) & ~3) + a.K * a.CK * BM + BM) * sizeof(float);
     a.vec = (a.Tin % 4 == 0) && (a.Cout % 4 == 0) && ((uintptr_t)a.x % 16 == 0) && ((uintptr_t)a.wf % 16 == 0);
+    a.fs = make_fastdiv((uint32_t)a.s);
     const int epi = a.KS > 1 ? EPI_PART
                              : ((a.res ? EPI_RES : 0) | (a.xact ? EPI_XACT : 0) | (a.accumulate ? EPI_ACC : 0));
-    // register prefetch when the chunk's items fit the slots (the window of a chunk spans at most
-    // (s Up + 6) / 4 float4 items per channel, whatever its alignment)
-    const bool pf = encx_opt(OPT_CONV_PF) != 0 && a.CK * ((a.s * a.Up + 6) / 4) <= PF_XQ * NT &&
-                    a.K * a.CK * BM / 4 <= PF_WQ * NT;
-#define ENCX_FWD_EPI(E)                                                                                 \
-    case E:                                                                                             \
-        if (pf) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, E, true>), grid, dim3(NT), lds, st, a); \
-        else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, E>), grid, dim3(NT), lds, st, a);        \
-        break
+#define ENCX_FWD_EPI(E) \
+    case E: hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, E>), grid, dim3(NT), lds, st, a); break
     switch (epi) {
         ENCX_FWD_EPI(0); ENCX_FWD_EPI(1); ENCX_FWD_EPI(2); ENCX_FWD_EPI(3); ENCX_FWD_EPI(4);
         ENCX_FWD_EPI(5); ENCX_FWD_EPI(6); ENCX_FWD_EPI(7); ENCX_FWD_EPI(8);

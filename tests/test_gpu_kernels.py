@@ -133,33 +133,6 @@ def test_conv_model_shapes_vs_oracle(li):
     near(b0.grad, p['m.' + pre + '.bias'].grad, 1e-4, 1e-5, tag + ' db')
 
 
-@pytest.mark.parametrize('li', range(len(MODEL_LAYERS)))
-def test_conv_prefetch_bit_identical(li):
-    """Register-prefetched LDS staging (option CONV_PF) changes when the operands are loaded, not
-    the arithmetic: forward output and every grad are bitwise those of the plain staging."""
-    from encx import ops
-    from encx._lib import option
-    kind, cin, cout, K, s, pre_elu, Tin = MODEL_LAYERS[li]
-    Tin = max(Tin, 32) * 4  # longer rows: several chunks and column tiles per workgroup grid
-    v0, g0, b0 = _case_params(700 + li, kind, cin, cout, K)
-    x0 = synth_wave((3, cin, Tin), 990 + li, amp=1.0)
-    act = 'elu' if pre_elu else None
-    res = []
-    for pf in (0, 1):
-        with option(CONV_PF=pf):
-            x = G(x0).requires_grad_(True)
-            v, g, b = (t.detach().clone().requires_grad_(True) for t in (v0, g0, b0))
-            if kind == 'conv':
-                y = ops.conv1d(x, v, g, b, K, s, 1, True, 'reflect', act)
-            else:
-                y = ops.convtr1d(x, v, g, b, K, s, True, 1.0, act)
-            y.backward(G(synth_wave(tuple(y.shape), 1990 + li, amp=1.0)))
-            torch.cuda.synchronize()
-            res.append([t.detach().clone() for t in (y, x.grad, v.grad, g.grad, b.grad)])
-    for name, a, b in zip(['y', 'dx', 'dv', 'dg', 'db'], *res):
-        assert torch.equal(a, b), (kind, cin, cout, K, s, name, float((a - b).abs().max()))
-
-
 # --------------------------------------------------------------------------- RVQ
 class _CB:
     def __init__(self, d):
