@@ -31,7 +31,10 @@
 namespace {
 
 constexpr int NT = 256;  // threads per workgroup (4 waves)
-constexpr int SPER = 4;  // staging items (float4) in flight per thread
+#ifndef ENCX_SPER
+#define ENCX_SPER 4
+#endif
+constexpr int SPER = ENCX_SPER;  // staging items (float4) in flight per thread
 constexpr int FLAT_T = 128;  // layers with T_out <= this run as one (b, t)-flattened GEMM
 
 // LDS staging: position lanes per channel lane for a window of `len` positions (QP | NT)
