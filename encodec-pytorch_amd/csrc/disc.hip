@@ -2440,6 +2440,7 @@ struct C2WgR {
     int per_split;  // items per wave
     int ktg;        // kt groups (tasks per split per ci block): KT for KF = 9, 1 for KF = 3
     int cib;        // 32-channel ci blocks
+    int SW, NCS;    // item order: strips of SW chunks (SW | NC, NCS = NC / SW), t within a strip
 };
 template <int KTW, int WQ>
 struct RwStage {  // one item's operands, loaded a whole item ahead of their MFMAs
@@ -2480,7 +2481,11 @@ __global__ __launch_bounds__(NW * 64, NW == 1 ? 2 : 1) void c2_wgrad_rw_kernel(C
     // row's ends read the neighbouring row (in bounds) and compute() zeroes them; only a quad
     // past the END of the tensor is read from a clamped address and shifted.
     auto load = [&](RwStage<KTW, WQ>& st, int it) {
-        const int c = it % a.NC, bt = it / a.NC, t = bt % g.T2, b = bt / g.T2;
+        // items run (b, strip, t, chunk in strip), the chunk fastest: the kt-group workgroups of a
+        // task (same ci block and split, same XCD) read the same dy / y quads at the same time and
+        // x rows one or two steps of t apart, a reuse distance of a strip's bytes, not a row's
+        const int cs = it % a.SW, r1 = it / a.SW, t = r1 % g.T2, r2 = r1 / g.T2;
+        const int c = (r2 % a.NCS) * a.SW + cs, b = r2 / a.NCS;
         const int f0 = c * 8, p = f0 + 4 * h;
         const int oa = (b * g.Co + (co_ok ? l : 0)) * plane_y + t * g.Fo + p;
         const int oac = min(oa, ylast);
@@ -3312,7 +3317,7 @@ int run_wgrad3(const C2Geo& g, const float* dy, const float* yact, const float* 
 // register-window weight grad (c2_wgrad_rw_kernel): 3x9 stride-2 and 3x3 stride-1 layers with
 // 32-channel blocks of input channels and <= 32 output channels
 struct WgPlanR {
-    int NC, items, ktg, cib, splits, per_split;
+    int NC, items, ktg, cib, splits, per_split, SW, NCS;
 };
 static bool wgr_ok(const C2Geo& g) {
     if (g.Co > 32 || g.Ci < 16 || g.KT != 3 || g.Fo < 4 || g.Fi < 4) return false;
@@ -3326,6 +3331,15 @@ static WgPlanR plan_wgr(const C2Geo& g, int waves = 2048, int wgs = 0) {
     WgPlanR p;
     p.NC = (int)cdiv(g.Fo, 8);
     p.items = g.B * g.T2 * p.NC;
+    // strip width: NC itself up to 17 chunks, else its largest divisor <= 16 (65 -> 13, 33 -> 11)
+    p.SW = p.NC;
+    if (p.NC > 17)
+        for (int w = 16; w >= 1; --w)
+            if (p.NC % w == 0) {
+                p.SW = w;
+                break;
+            }
+    p.NCS = p.NC / p.SW;
     p.ktg = g.KF == 9 ? g.KT : 1;
     p.cib = (int)cdiv(g.Ci, 32);
     const int per = p.ktg * p.cib;
@@ -3341,7 +3355,7 @@ static int64_t wgr_slab(const C2Geo& g, const WgPlanR& p) {  // task-major slab 
 static int run_wgrad_rw(const C2Geo& g, const float* dy, const float* yact, const float* x, float* ws,
                         const WgPlanR& p, hipStream_t st, bool wg8 = false) {
     if (!wgr_ok(g)) return ENCX_EINVAL;
-    C2WgR a{g, dy, yact, x, ws, p.NC, p.items, p.per_split, p.ktg, p.cib};
+    C2WgR a{g, dy, yact, x, ws, p.NC, p.items, p.per_split, p.ktg, p.cib, p.SW, p.NCS};
     const dim3 grid((unsigned)(p.splits * p.ktg * p.cib));
     if (wg8) {
         const size_t lds = (4 * 32 * 32 * 9 + 8 * 32) * sizeof(float);
