@@ -36,6 +36,7 @@ struct OptDef {
 constexpr OptDef kOpts[OPT_COUNT] = {
     {OPT_FFT, "FFT", 1}, {OPT_PW, "PW", 1}, {OPT_PW_WG_TMAX, "PW_WG_TMAX", 12000}, {OPT_LSTM_FUSE, "LSTM_FUSE", 0},
     {OPT_LSTM_PERSIST, "LSTM_PERSIST", 1},
+    {OPT_LSTM_WG_SPLITS, "LSTM_WG_SPLITS", 32},
     {OPT_FWR, "FWR", 256}, {OPT_DGR, "DGR", 256}, {OPT_WGR, "WGR", 2048},
     {OPT_WGR_WGS, "WGR_WGS", 256}, {OPT_FEAT_CODE, "FEAT_CODE", 1}, {OPT_CONV_CK, "CONV_CK", 64},
     {OPT_CONV_SPLIT, "CONV_SPLIT", 1024}, {OPT_CONV_WG_SPLIT, "CONV_WG_SPLIT", 1024},

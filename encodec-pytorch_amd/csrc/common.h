@@ -177,6 +177,7 @@ enum EncxOpt {
     OPT_PW_WG_TMAX,    // longest T served by the 1x1 weight-grad GEMM
     OPT_LSTM_FUSE,     // LSTM backward: elementwise step fused into the next GEMM launch
     OPT_LSTM_PERSIST,  // LSTM: one persistent launch per recurrence (0: a launch per wavefront step)
+    OPT_LSTM_WG_SPLITS, // LSTM weight grad: at most this many k-splits (partial slabs) of the GEMM
     OPT_FWR,           // register-window Conv2d forward: workgroups (0: off)
     OPT_DGR,           // register-window Conv2d bwd-data: workgroups (0: off)
     OPT_WGR,           // register-window Conv2d weight grad: waves (0: off)

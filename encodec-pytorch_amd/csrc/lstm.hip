@@ -1036,7 +1036,7 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
 
 size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H) {
     const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
-    const int S = gemm_slabs(M, gemm_splits_128(N4, Nw, M));
+    const int S = gemm_slabs(M, gemm_splits_128(N4, Nw, M, 256, (int)encx_opt(OPT_LSTM_WG_SPLITS)));
     return (size_t)S * N4 * Nw * sizeof(float);
 }
 
@@ -1051,7 +1051,7 @@ int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float
     const int64_t BTH = B * T * H;
     const float* in = layer == 0 ? xt : Y + (layer - 1) * BTH;
     const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
-    const int sp = gemm_splits_128(N4, Nw, M);
+    const int sp = gemm_splits_128(N4, Nw, M, 256, (int)encx_opt(OPT_LSTM_WG_SPLITS));
     const int S = gemm_slabs(M, sp);
     int rc = gemm_launch_128(LdWcat{DA + layer * 4 * BTH, in, Y + layer * BTH, (int)H, (int)T, make_fastdiv((uint32_t)T)}, EpSlabs{ws, N4, Nw},
                          N4, Nw, M, st, sp);

@@ -1,8 +1,8 @@
 """LSTM recurrence timing (csrc/lstm.hip) at the config-3 size (B 32, H 512, T 75, L 2) under
 kernel-selection option settings, each captured in a HIP graph and replayed (the form the training
 step runs it in). Usage (GPU box): python tools/lstm_bench.py "LSTM_PERSIST=0" "LSTM_PERSIST=1" ...
-Prints us per forward and per backward for every setting, and checks that every setting gives the
-same forward outputs and input grads as the first (bitwise, and the max difference)."""
+Prints us per forward, backward and weight-grad pass (all layers) for every setting, and compares
+every output and grad with the first setting's (bitwise, and the max difference)."""
 import os
 import sys
 
@@ -41,6 +41,15 @@ def main():
         call('encx_lstm_bwd', ptr(dout), ptr(wcatT), ptr(Cs), ptr(Gs), ptr(DA), ptr(dx), 0, ptr(ws), B, T, H, L,
              torch.cuda.current_stream().cuda_stream)
 
+    dws = [[torch.empty(4 * H, H, device=dev), torch.empty(4 * H, H, device=dev), torch.empty(4 * H, device=dev),
+            torch.empty(4 * H, device=dev)] for _ in range(L)]
+
+    def wgrad():
+        wsw = torch.empty(lib.encx_lstm_bwd_weight_workspace(B, T, H), dtype=torch.uint8, device=dev)
+        for l in range(L):
+            call('encx_lstm_bwd_weight', ptr(DA), ptr(xt), ptr(Y), *(ptr(t) for t in dws[l]), 0, ptr(wsw), B, T, H, L,
+                 l, torch.cuda.current_stream().cuda_stream)
+
     def timed(fn, reps=20):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -68,15 +77,17 @@ def main():
         tb = timed(bwd)
         fwd()
         bwd()
+        tw = timed(wgrad)
+        wgrad()
         torch.cuda.synchronize()
         n = ctypes.c_int64()
         call('encx_lstm_sync_errors', ctypes.byref(n))
-        got = [t.clone() for t in (out, Y, Cs, Gs, DA, dx)]
+        got = [t.clone() for t in (out, Y, Cs, Gs, DA, dx, *[w for d in dws for w in d])]
         if ref is None:
             ref = got
         diff = max(float((a - b).abs().max()) for a, b in zip(got, ref))
         same = all(torch.equal(a, b) for a, b in zip(got, ref))
-        print(f'{sset}: fwd {tf:.1f} us, bwd {tb:.1f} us; vs first setting: bitwise {same}, max diff {diff:.3g}; '
+        print(f'{sset}: fwd {tf:.1f} us, bwd {tb:.1f} us, weight grads {tw:.1f} us; vs first setting: bitwise {same}, max diff {diff:.3g}; '
               f'sync errors {n.value}', flush=True)
         for kk, v in prev.items():
             set_option(kk, v)
