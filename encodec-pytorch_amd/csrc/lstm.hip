@@ -756,6 +756,24 @@ struct EpSlabs {  // split-K partial slabs [z][M][N]
         ws[((int64_t)blockIdx.z * M + m) * N + n] = v;
     }
 };
+// unsplit weight grad: the GEMM's element straight into dw_ih (n < H), dw_hh (n < 2H) and the bias
+// grads (n == 2H, to both); += when acc (the same bits as one slab through lstm_slab_reduce)
+struct EpDWcat {
+    float* dwi;
+    float* dwh;
+    float* db1;
+    float* db2;
+    int H, acc;
+    ENCX_DEV void operator()(int m, int n, float v) const {
+        if (n < 2 * H) {
+            float* p = n < H ? dwi + (int64_t)m * H + n : dwh + (int64_t)m * H + (n - H);
+            *p = acc ? *p + v : v;
+        } else {
+            if (db1) db1[m] = acc ? db1[m] + v : v;
+            if (db2) db2[m] = acc ? db2[m] + v : v;
+        }
+    }
+};
 // sum split slabs [S][4H][2H+1] in ascending slab order into dw_ih (n < H), dw_hh (n < 2H) and
 // the bias grad (n == 2H, written to both b_ih and b_hh grads); += when acc
 __global__ __launch_bounds__(256) void lstm_slab_reduce(const float* ws, int S, int H, float* dwi, float* dwh,
@@ -1053,8 +1071,9 @@ int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float
     const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
     const int sp = gemm_splits_128(N4, Nw, M, 256, (int)encx_opt(OPT_LSTM_WG_SPLITS));
     const int S = gemm_slabs(M, sp);
-    int rc = gemm_launch_128(LdWcat{DA + layer * 4 * BTH, in, Y + layer * BTH, (int)H, (int)T, make_fastdiv((uint32_t)T)}, EpSlabs{ws, N4, Nw},
-                         N4, Nw, M, st, sp);
+    const LdWcat ld{DA + layer * 4 * BTH, in, Y + layer * BTH, (int)H, (int)T, make_fastdiv((uint32_t)T)};
+    if (S == 1) return gemm_launch_128(ld, EpDWcat{dw_ih, dw_hh, db_ih, db_hh, (int)H, acc}, N4, Nw, M, st, 1);
+    int rc = gemm_launch_128(ld, EpSlabs{ws, N4, Nw}, N4, Nw, M, st, sp);
     if (rc) return rc;
     hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 64)), dim3(256), 0, st, ws, S,
                        (int)H, dw_ih, dw_hh, db_ih, db_hh, acc);
