@@ -551,8 +551,8 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
     for (int i = 0; i < T; ++i) {
         const int t = T - 1 - i;
         LSTM_TRACE(1, i, 0);
-        // the point phase's own operands (forward state, dout): loaded behind the DA loads, so no
-        // poll or MFMA waits for them
+        // the point phase's own operands (forward state, dout): loaded after the poll (a poll's
+        // wait would otherwise wait for them), ahead of the DA loads
         float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, c = 0.f, cpl = 0.f, dtop = 0.f;
         const int64_t o = ((int64_t)pbc * T + t) * H + pu;
         auto load_point = [&]() {
@@ -574,14 +574,16 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
             if (wave == 0 && live) live = poll_ge(cnt_da, NRT * (T - tf), err);
             __syncthreads();
             LSTM_TRACE(1, i, 1);
+            load_point();  // (older than the DA loads: the MFMAs' in-order waits are not pushed back)
             float4 a[2][G];
             const uint32_t rb = (uint32_t)(((int64_t)arow * T + tf) * K + 4 * kk) * 4u;
+            // issued in the order the MFMAs consume them (k-group g of both chains), so the chains
+            // start as the first loads land instead of after half of them
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int g = 0; g < G; ++g)
 #pragma unroll
-                for (int g = 0; g < G; ++g)
+                for (int h = 0; h < 2; ++h)
                     a[h][g] = ld4_sc1(rda, rb + (uint32_t)((wave >> 1) * gper + 2 * (wave & 1) + h + 4 * g) * 64u);
-            load_point();
             __builtin_amdgcn_sched_barrier(0);
             f32x4v acc[2] = {(f32x4v){0.f, 0.f, 0.f, 0.f}, (f32x4v){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
