@@ -34,7 +34,7 @@ struct OptDef {
     int64_t def;
 };
 constexpr OptDef kOpts[OPT_COUNT] = {
-    {OPT_FFT, "FFT", 1}, {OPT_PW, "PW", 1}, {OPT_PW_WG_TMAX, "PW_WG_TMAX", 12000}, {OPT_LSTM_FUSE, "LSTM_FUSE", 0},
+    {OPT_FFT, "FFT", 1}, {OPT_PW, "PW", 1}, {OPT_PW_TMAX, "PW_TMAX", 1024}, {OPT_PW_WG_TMAX, "PW_WG_TMAX", 12000}, {OPT_LSTM_FUSE, "LSTM_FUSE", 0},
     {OPT_LSTM_PERSIST, "LSTM_PERSIST", 1},
     {OPT_LSTM_WG_SPLITS, "LSTM_WG_SPLITS", 32},
     {OPT_FWR, "FWR", 256}, {OPT_DGR, "DGR", 256}, {OPT_WGR, "WGR", 2048},

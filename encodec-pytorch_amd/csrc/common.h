@@ -174,6 +174,7 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 enum EncxOpt {
     OPT_FFT,           // spectrograms by real FFT (0: framed-DFT GEMM)
     OPT_PW,            // pointwise GEMM kernels for the short, wide 1x1 convs
+    OPT_PW_TMAX,       // longest T served by the 1x1 forward / bwd-data GEMM
     OPT_PW_WG_TMAX,    // longest T served by the 1x1 weight-grad GEMM
     OPT_LSTM_FUSE,     // LSTM backward: elementwise step fused into the next GEMM launch
     OPT_LSTM_PERSIST,  // LSTM: one persistent launch per recurrence (0: a launch per wavefront step)

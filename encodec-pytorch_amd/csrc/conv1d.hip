@@ -1241,7 +1241,7 @@ static int pw_launch(const PwArgs& a, int B, int epi, hipStream_t st) {
 // the residual better (64x64 at T 12000: 108 us there, 145 here)
 static bool pw_ok(int K, int s, int d, int pl, int pr, int e, int Tin, int Tout, int Cin, int Cout) {
     return encx_opt(OPT_PW) != 0 && K == 1 && s == 1 && d == 1 && pl == 0 && pr == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 &&
-           Tout <= 1024 && Cin % 4 == 0 && Cout % 4 == 0;
+           Tout <= encx_opt(OPT_PW_TMAX) && Cin % 4 == 0 && Cout % 4 == 0;
 }
 
 // weight grad of the short, wide 1x1 convs: dW[m=co][n=ci] = sum_{b,t} dy[b][co][t] act(x[b][ci][t])
