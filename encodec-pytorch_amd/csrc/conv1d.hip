@@ -1239,9 +1239,12 @@ static int pw_launch(const PwArgs& a, int B, int epi, hipStream_t st) {
 // short, wide ones (T <= 1024). tools/mb/conv_mb: 256x256 at T 600 101 -> 59 us, 128x256 53 -> 42
 // us; the long, HBM-bound ones (T >= 3000) stay on conv_fwd_kernel, whose epilogue streams
 // the residual better (64x64 at T 12000: 108 us there, 145 here)
-static bool pw_ok(int K, int s, int d, int pl, int pr, int e, int Tin, int Tout, int Cin, int Cout) {
+// red: the GEMM's reduction length (Cin forward, Cout backward-data). Above PW_TMAX positions the
+// GEMM still wins when it reduces over >= 128 channels (round 5 sweep at T 3000: 128 -> 128
+// forward 168 -> 134 us, bwd-data 198 -> 160 and 135 -> 85 us; but the 64 -> 128 forward 129 -> 196)
+static bool pw_ok(int K, int s, int d, int pl, int pr, int e, int Tin, int Tout, int Cin, int Cout, int red) {
     return encx_opt(OPT_PW) != 0 && K == 1 && s == 1 && d == 1 && pl == 0 && pr == 0 && e == 0 && Tin == Tout && Tout % 4 == 0 &&
-           Tout <= encx_opt(OPT_PW_TMAX) && Cin % 4 == 0 && Cout % 4 == 0;
+           (Tout <= encx_opt(OPT_PW_TMAX) || red >= 128) && Cin % 4 == 0 && Cout % 4 == 0;
 }
 
 // weight grad of the short, wide 1x1 convs: dW[m=co][n=ci] = sum_{b,t} dy[b][co][t] act(x[b][ci][t])
@@ -1393,7 +1396,7 @@ static void pw_wgrad_run(const float* dy, const float* x, float* dw, float* db, 
 }
 
 int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
-    if (pw_ok(a.K, a.s, a.d, a.pl, 0, a.e, a.Tin, a.Tout, a.Cin, a.Cout) && !a.part) {
+    if (pw_ok(a.K, a.s, a.d, a.pl, 0, a.e, a.Tin, a.Tout, a.Cin, a.Cout, a.Cin) && !a.part) {
         PwArgs p{a.wf, a.x, a.bias, a.res, a.xact, a.y, a.Cout, a.Cin, a.Tout, a.act, a.epi_act};
         const int epi = (a.res ? PW_RES : 0) | (a.xact ? PW_XACT : 0) | (a.accumulate ? PW_ACC : 0);
         if (pw_launch(p, a.B, epi, st) == 0) return 0;
@@ -1677,7 +1680,7 @@ int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float
                        4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout), "conv_dgrad");
     ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
     if (pw_ok((int)K, (int)stride, 1, (int)pad_left, (int)pad_right, (int)short_ext, (int)Tin, (int)Tout, (int)Cin,
-              (int)Cout)) {
+              (int)Cout, (int)Cout)) {
         // dx[b][ci][t] = sum_co wp[co][ci] dy[b][co][t], * act'(x), (+ dx)
         PwArgs p{wp, dy, nullptr, nullptr, x, dx, (int)Cin, (int)Cout, (int)Tout, ENCX_ACT_NONE, pre_act};
         const int epi = (pre_act != ENCX_ACT_NONE ? PW_XACT : 0) | (accumulate ? PW_ACC : 0);

@@ -93,6 +93,7 @@ MODEL_LAYERS = [
     # for T <= 3000 at >= 64 channels) at their real widths and lengths
     ('conv', 256, 256, 1, 1, True, 600), ('conv', 128, 256, 1, 1, False, 600),
     ('conv', 64, 128, 1, 1, True, 3000), ('conv', 128, 128, 1, 1, True, 1000),
+    ('conv', 128, 128, 1, 1, True, 3000),  # the 1x1 GEMM past PW_TMAX (>= 128-channel reduction)
 ]
 
 
@@ -300,16 +301,18 @@ def test_normalize_and_scale():
 
 
 # --------------------------------------------------------------------------- LSTM
-@pytest.mark.parametrize('B,H,Tn,L,fuse,persist', [
-    (3, 32, 7, 1, 0, 1), (17, 64, 20, 2, 0, 1), (5, 48, 9, 3, 0, 1), (32, 512, 75, 2, 0, 1), (32, 512, 75, 2, 0, 0),
-    (17, 64, 20, 2, 1, 0), (32, 512, 75, 2, 1, 0), (17, 128, 20, 2, 0, 1), (5, 256, 9, 3, 0, 1), (40, 384, 11, 1, 0, 1)])
-def test_lstm_vs_oracle(B, H, Tn, L, fuse, persist):
+@pytest.mark.parametrize('B,H,Tn,L,fuse,persist,wgs', [
+    (3, 32, 7, 1, 0, 1, 32), (17, 64, 20, 2, 0, 1, 32), (5, 48, 9, 3, 0, 1, 32), (32, 512, 75, 2, 0, 1, 32),
+    (32, 512, 75, 2, 0, 0, 32), (17, 64, 20, 2, 1, 0, 32), (32, 512, 75, 2, 1, 0, 32), (17, 128, 20, 2, 0, 1, 32),
+    (5, 256, 9, 3, 0, 1, 32), (40, 384, 11, 1, 0, 1, 32), (17, 256, 20, 2, 0, 1, 1)])
+def test_lstm_vs_oracle(B, H, Tn, L, fuse, persist, wgs):
     """encx LSTM (csrc/lstm.hip) forward + backward against the oracle's step-by-step
     restatement of SLSTM (modules/lstm.py:22-28) run in fp64 on the CPU, for 1, 2 and 3 layers:
     every output and grad within 4x the error of the same restatement run in plain fp32.
     persist: the one-launch recurrences (option LSTM_PERSIST; used where H % 128 == 0, H <= 512
     and the workgroups fit the CUs, else the launch-per-step wavefront); fuse: the opt-in fused
-    backward step of the wavefront (option LSTM_FUSE)."""
+    backward step of the wavefront (option LSTM_FUSE); wgs: the weight grad's k-split cap
+    (LSTM_WG_SPLITS; 1 = one GEMM storing straight into the grads)."""
     import ctypes
     from encx import ops
     from encx._lib import option, call
@@ -328,7 +331,7 @@ def test_lstm_vs_oracle(B, H, Tn, L, fuse, persist):
     y64 = O.slstm(x64, p64, 'm', L)
     (y64 * r64).sum().backward()
     x = x64.detach().float().to(DEV).requires_grad_(True)
-    with option(LSTM_FUSE=fuse, LSTM_PERSIST=persist):
+    with option(LSTM_FUSE=fuse, LSTM_PERSIST=persist, LSTM_WG_SPLITS=wgs):
         y = ops.lstm(x, wts, skip=True)
         (y * r64.float().to(DEV)).sum().backward()
         torch.cuda.synchronize()
