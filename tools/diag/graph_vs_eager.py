@@ -9,6 +9,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, 'tests'))
+sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
 sys.path.insert(0, os.path.join(ROOT, 'encodec-pytorch_amd'))
 sys.path.insert(0, ROOT)
 from test_gpu_train_state import make_trainer, batches  # noqa: E402
