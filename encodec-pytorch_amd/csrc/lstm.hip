@@ -171,8 +171,13 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_wave(const float* xt, const 
 constexpr int PU = 8;           // hidden units per persistent workgroup
 constexpr int SYNC_LINE = 32;   // ints per counter: one 128-byte line each
 constexpr int SYNC_LINES = 512;
-// hand-off counters [SYNC_LINES][SYNC_LINE] (zeroed per launch), then the error word's line
-__device__ int g_lstm_sync[(SYNC_LINES + 1) * SYNC_LINE];
+// hand-off counters [SYNC_LINES][SYNC_LINE], then the error word's line and the launch's done count.
+// The counters are zero when a launch starts: statically at the first, and the last workgroup of
+// every launch zeroes what its launch used (finish_launch). (A hipMemsetAsync node per call
+// instead was not ordered before the kernel in graph replays: counts zeroed under running
+// workgroups, every spin of the launch timing out.) Launches of the persistent forms must not
+// overlap: one stream.
+__device__ int g_lstm_sync[(SYNC_LINES + 2) * SYNC_LINE];
 
 // Development tracing (build with -DENCX_LSTM_TRACE; encx_lstm_trace reads it): thread 0 of every
 // persistent workgroup stamps the steady clock at up to 8 points of every frame,
@@ -196,8 +201,22 @@ ENCX_DEV bool poll_ge(const int* cnt, int target, int* err) {
         if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
         __builtin_amdgcn_s_sleep(1);
     }
-    __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return false;
+}
+// end of a persistent launch: the last workgroup to count itself done zeroes the counter lines
+// [0, nlines) and the done count. Every workgroup has passed its last poll before it counts itself,
+// and the next launch on the stream starts after this one has ended.
+ENCX_DEV void finish_launch(int* sync, int nlines) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int* done = sync + (SYNC_LINES + 1) * SYNC_LINE;
+        if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+            for (int i = 0; i < nlines; ++i)
+                __hip_atomic_store(sync + i * SYNC_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 ENCX_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const float* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
@@ -328,6 +347,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
         LSTM_TRACE(0, t, 6);
         if (tid == 0) __hip_atomic_fetch_add(cnt_self, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    finish_launch(sync, (int)gridDim.x / NUG);  // the L NBG counters
 }
 
 // ------------------------------------------------------------------------- backward step
@@ -661,6 +681,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
         LSTM_TRACE(1, i, 5);
         if (publish && tid == 0) __hip_atomic_fetch_add(pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    finish_launch(sync, L * NBG + (L - 1) * NBG * NRT);  // the DA counters and the input-tile flags
 }
 
 // ------------------------------------------------------------------------- layout kernels
@@ -935,8 +956,6 @@ int encx_lstm_fwd(const float* x, const float* wcat, const float* bsum, float* x
     if (const int nwg = fwd_pers_grid(B, T, H, L)) {
         int* sync = sync_words();
         const int nbg = (int)cdiv(B, 16);
-        const hipError_t e = hipMemsetAsync(sync, 0, (size_t)L * nbg * SYNC_LINE * sizeof(int), st);
-        if (e != hipSuccess) return (int)e;
         ps.tag(" persist");
         switch (G) {  // H / 64
             case 2: fwd_pers_launch<2>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
@@ -1008,9 +1027,6 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
     if (const int nwg = bwd_pers_grid(B, T, H, L)) {
         int* sync = sync_words();
         const int nbg = (int)cdiv(B, 16);
-        const size_t lines = (size_t)L * nbg + (size_t)(L - 1) * nbg * (H / 16);
-        const hipError_t e = hipMemsetAsync(sync, 0, lines * SYNC_LINE * sizeof(int), st);
-        if (e != hipSuccess) return (int)e;
         ps.tag(" persist");
 #define BWD_PERS(G_)                                                                                            \
     hipLaunchKernelGGL((lstm_bwd_pers<G_>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, dout, wcatT, Cst, Gs, DA, dx, \

@@ -410,6 +410,57 @@ def test_lstm_persistent_bit_identical(B, H, Tn, L):
             assert torch.equal(a, b), (rnd, name, float((a - b).abs().max()))
 
 
+def test_lstm_persistent_graph_replays():
+    """The persistent recurrences captured in a HIP graph and replayed (the training step's form):
+    every replay, on fresh inputs, gives the bits of an eager call, and no hand-off spin times out
+    (the counters must be zero at every launch, captured or not)."""
+    import ctypes
+    from encx._lib import call, ptr, option, lib
+    B, H, Tn, L = 4, 512, 75, 2
+    gen = torch.Generator().manual_seed(11)
+    k = H ** -0.5
+    f = lambda *s: ((torch.rand(*s, generator=gen) * 2 - 1) * k).to(DEV)
+    e = lambda n: torch.empty(n, device=DEV)
+    wcat, wcatT, bsum = e(L * 8 * H * H), e(L * 8 * H * H), e(L * 4 * H)
+    st0 = torch.cuda.current_stream().cuda_stream
+    for l in range(L):
+        call('encx_lstm_pack', *(ptr(f(*s)) for s in [(4 * H, H), (4 * H, H), (4 * H,), (4 * H,)]),
+             ptr(wcat), ptr(wcatT), ptr(bsum), H, l, st0)
+    x, dout = torch.zeros(B, H, Tn, device=DEV), torch.zeros(B, H, Tn, device=DEV)
+    bufs = (e(B * Tn * H), e(L * B * Tn * H), e(L * B * Tn * H), e(L * B * Tn * 4 * H), torch.empty_like(x),
+            e(L * B * Tn * 4 * H), torch.empty_like(x),
+            torch.empty(lib.encx_lstm_bwd_workspace(B, Tn, H, L), dtype=torch.uint8, device=DEV))
+
+    def run():
+        xt, Y, Cs, Gs, out, DA, dx, ws = bufs
+        st = torch.cuda.current_stream().cuda_stream
+        call('encx_lstm_fwd', ptr(x), ptr(wcat), ptr(bsum), ptr(xt), ptr(Y), ptr(Cs), ptr(Gs), ptr(out), 1, B, Tn, H, L, st)
+        call('encx_lstm_bwd', ptr(dout), ptr(wcatT), ptr(Cs), ptr(Gs), ptr(DA), ptr(dx), 0, ptr(ws), B, Tn, H, L, st)
+
+    with option(LSTM_PERSIST=1):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            run()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                run()
+        torch.cuda.current_stream().wait_stream(s)
+        for rnd in range(4):
+            x.copy_(torch.randn(B, H, Tn, generator=gen))
+            dout.copy_(torch.randn(B, H, Tn, generator=gen))
+            g.replay()
+            torch.cuda.synchronize()
+            got = [t.clone() for t in bufs[:7]]
+            run()
+            torch.cuda.synchronize()
+            nerr = ctypes.c_int64()
+            call('encx_lstm_sync_errors', ctypes.byref(nerr))
+            assert nerr.value == 0, (rnd, nerr.value)
+            for name, a, b in zip(['xt', 'h', 'c', 'gates', 'out', 'DA', 'dx'], got, bufs[:7]):
+                assert torch.equal(a, b), (rnd, name)
+
+
 # --------------------------------------------------------------------------- fused residual block
 @pytest.mark.parametrize('C,T,B', [(32, 2048, 3), (32, 24000, 2), (64, 12000, 2), (64, 3001, 3), (32, 2113, 1)])
 def test_fused_resblock_vs_torch_fp64(C, T, B):
