@@ -187,7 +187,6 @@ enum EncxOpt {
     OPT_CONV_CK,       // conv1d fwd / bwd-data: reduction elements (channels x taps) per LDS chunk
     OPT_CONV_SPLIT,    // conv1d fwd / bwd-data: split-K until this many workgroups
     OPT_CONV_WG_SPLIT, // conv1d weight grad: split the positions until this many workgroups
-    OPT_CONV_WG_AG,    // conv1d weight grad: the A operand straight from global memory (no LDS tile)
     OPT_COUNT
 };
 int64_t encx_opt(EncxOpt id);

@@ -527,20 +527,14 @@ struct WgArgs {
 // WK > 1: the WK waves share one (32*TM) x (32*TN) tile and split each chunk's t range.
 // L is staged as Ls[a][t] (row stride BT + 1: the MFMA A reads, 32 lanes down a column, hit
 // 32 banks; the staging writes run along t) and R as Rs[c][window]; both from float4 items.
-// AG (WK == 1, float4-aligned L rows): the A operand (L) is not staged at all: each lane loads its
-// row's quads straight into registers, one group of 8 t (4 k-steps, lane half h taking t + 4h ..
-// + 3) ahead of its MFMAs; only the R window goes through LDS. The L tile was 8x the R window's
-// staging work (its 4 scalar LDS writes per quad 4-way bank conflicted), which left the MFMAs
-// idle two thirds of the time.
-template <int BM, int BN, int WM, int WN, int WK, bool AG = false>
+template <int BM, int BN, int WM, int WN, int WK>
 __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     static_assert(WM * WN * WK == 4, "4 waves");
-    static_assert(!AG || WK == 1, "register A operand: one wave per t range");
     extern __shared__ float smem[];
     const int BT = a.BT, BTp = BT + 1, WLp = a.WLp, K = a.K, N = a.C * a.K;
-    float* Ls = smem;                          // [BM][BTp] (not with AG)
-    float* Rs = AG ? smem : smem + BM * BTp;   // [NCmax][WLp]
+    float* Ls = smem;              // [BM][BTp]
+    float* Rs = smem + BM * BTp;   // [NCmax][WLp]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wk = wave % WK, wmn = wave / WK;
     const int wm0 = (wmn / WN) * TM * 32, wn0 = (wmn % WN) * TN * 32;
@@ -587,7 +581,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
         __syncthreads();
         // batched staging as in conv_fwd_kernel: SPER float4 loads in flight per thread; items
         // (row, column) walked by a fixed step of NT (no per-item division)
-        if (!AG) {
+        {
             int al_n = lal0, ti_n = lti0;
             for (int i0 = 0; i0 < nl; i0 += NT * SPER) {
                 f32x4 v[SPER];
@@ -685,51 +679,6 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
             }
         }
         __syncthreads();
-        if constexpr (AG) {
-            // rows of this lane's A fragments (clamped; rows >= A read row A-1 and are zeroed)
-            const float* lrow[TM];
-            bool rok[TM];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int row = a0 + wm0 + i * 32 + l32;
-                rok[i] = row < a.A;
-                lrow[i] = Lb + (int64_t)(rok[i] ? row : a.A - 1) * a.Tl;
-            }
-            auto aload = [&](f32x4* q4, int t8) {
-                const int t = tc + t8 + 4 * h;  // a quad is wholly inside or outside the row (Tl % 4 == 0)
-                const bool tin = t < a.Tl;
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const f32x4 v = *(const f32x4*)(lrow[i] + (tin ? t : 0));
-                    const bool ok = rok[i] && tin;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) q4[i][e] = ok ? act_apply(a.actL, v[e]) : 0.f;
-                }
-            };
-            f32x4 aq[2][TM];
-            aload(aq[0], 0);
-#pragma unroll 2
-            for (int t8 = 0; t8 < BT; t8 += 8) {
-                const int cur = (t8 >> 3) & 1;
-                if (t8 + 8 < BT) aload(aq[cur ^ 1], t8 + 8);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int tl = t8 + 4 * h + q;
-                    float bv[TN];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) bv[j] = Rs[boff[j] + tl * a.s];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(aq[cur][i][q], bv[j], acc[i][j]);
-                }
-                if (do_bias)
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-                        bsum[i] += (aq[cur][i][0] + aq[cur][i][1]) + (aq[cur][i][2] + aq[cur][i][3]);
-            }
-            continue;
-        }
 #pragma unroll 4
         for (int tp = wk * tw; tp < (wk + 1) * tw; tp += 2) {
             const int tl = tp + h;
@@ -1614,13 +1563,6 @@ void launch_wg(WgArgs a, int splits, hipStream_t st) {
     a.vec = (a.Tl % 4 == 0) && (a.Tr % 4 == 0) && ((uintptr_t)a.L % 16 == 0) && ((uintptr_t)a.R % 16 == 0);
     size_t red = (size_t)4 * (BM / WM / 32) * (BN / WN / 32) * 16 * 64 * sizeof(float);  // all 4 waves
     if (WK > 1 && red > lds) lds = red;
-    if constexpr (WK == 1) {
-        if (a.vec && a.BT % 8 == 0 && encx_opt(OPT_CONV_WG_AG) != 0) {
-            hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, WK, true>), grid, dim3(NT),
-                               (size_t)a.NCmax * a.WLp * sizeof(float), st, a);
-            return;
-        }
-    }
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, WK>), grid, dim3(NT), lds, st, a);
 }
 
