@@ -280,10 +280,19 @@ def test_config4_two_ranks_b32_vs_one_process_b64():
 
 
 def test_config5_two_ranks_48k_stereo_vs_one_process():
+    """Synced codebooks at 48 kHz (the in-forward all-reduce between the two segments): codes
+    bit-identical to one process on B32, codebooks within 1e-5, and the generator / discriminator
+    grads too (the data-parallel step is the single-process step on the union batch: per-rank batch
+    means averaged, balancer norms averaged over ranks, codebook statistics summed before each
+    segment's update), up to fp32 summation order."""
     runs = _spawn('c5_2x16')
+    single = _single('c5_2x16', 32)
     _identical(runs, 'c5_2x16')
-    _check_vs_single(runs, _single('c5_2x16', 32), 'c5_2x16')
+    _check_vs_single(runs, single, 'c5_2x16')
     _check_cluster_sizes(runs, 'c5_2x16')
+    eg, ed = _rel(runs[0]['gen_grad'], single['gen_grad']), _rel(runs[0]['disc_grad'], single['disc_grad'])
+    print(f'c5_2x16 synced: generator grad vs one process {eg:.2e}, discriminator {ed:.2e}')
+    assert eg <= 1e-3 and ed <= 1e-3, (eg, ed)
 
 
 def test_config5_two_ranks_48k_stereo_grad_decomposition():
