@@ -292,6 +292,16 @@ def test_config5_two_ranks_48k_stereo_vs_one_process():
     _check_cluster_sizes(runs, 'c5_2x16')
     eg, ed = _rel(runs[0]['gen_grad'], single['gen_grad']), _rel(runs[0]['disc_grad'], single['disc_grad'])
     print(f'c5_2x16 synced: generator grad vs one process {eg:.2e}, discriminator {ed:.2e}')
+    if eg > 1e-3:  # where: the worst parameters (flat order = model.parameters())
+        m, _ = _build(True, True)
+        a, b, off, rows = runs[0]['gen_grad'].double(), single['gen_grad'].double(), 0, []
+        for n, p in m.named_parameters():
+            k = p.numel()
+            d = float((a[off:off + k] - b[off:off + k]).abs().max())
+            rows.append((d, n, float(b[off:off + k].abs().max())))
+            off += k
+        for d, n, mx in sorted(rows, reverse=True)[:12]:
+            print(f'  {n}: max diff {d:.3e} (max |g| {mx:.3e})')
     assert eg <= 1e-3 and ed <= 1e-3, (eg, ed)
 
 
