@@ -158,6 +158,14 @@ class option:
         return False
 
 
+def lstm_sync_errors():
+    """Hand-off spins of the persistent LSTM kernels that timed out since the last call (encx.h
+    encx_lstm_sync_errors; synchronises the device)."""
+    n = ctypes.c_int64()
+    call('encx_lstm_sync_errors', ctypes.byref(n))
+    return n.value
+
+
 def ptr(t):
     """Device pointer of a contiguous fp32/int64 CUDA tensor (None -> NULL)."""
     if t is None:

@@ -133,6 +133,14 @@ class Trainer:
             out = self._graph_step(key, x)
         else:
             out = self._run(x, bw, train_d)
+        if os.environ.get('ENCX_CHECK_SYNC', '0') == '1':
+            # the persistent LSTM launches' hand-off spins: any timeout means garbage grads (it
+            # synchronises the device, so it is a debugging switch)
+            from ._lib import lstm_sync_errors
+            n = lstm_sync_errors()
+            if n:
+                raise RuntimeError(f'encx: {n} LSTM hand-off spins timed out in this step (workgroups not '
+                                   'co-resident: another persistent launch on the GPU?)')
         if self.sched is not None:
             self.sched.step()
         if self.sched_d is not None:
