@@ -1748,6 +1748,9 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
 // NC_CO channels is staged in LDS with its (KT-1)*dt row and KF-1 column halo; a thread keeps
 // CI x 4 accumulators for 4 adjacent f and slides a 4+KF-1 window over its LDS row per tap;
 // the weights are wave-uniform (scalar loads).
+#ifndef ENCX_DN_QP
+#define ENCX_DN_QP 4  // staging quads in flight per thread and tensor (compile-time A/B knob)
+#endif
 constexpr int DN_ROWS = 16, DN_COLS = 64, DN_FPT = 4, DN_CC = 8, DN_MAXHALO = 4;
 template <int CI, int KT, int KF, bool YM = true, bool VQ = true>
 __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
@@ -1773,7 +1776,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
         for (int e = 0; e < DN_FPT; ++e) acc[c][e] = (f32x2){0.f, 0.f};
     // VQ: the tile is staged as quads along f (ld4u; lanes outside [0, Fo) or outside the
     // tensor masked), one index split per 4 elements instead of per element
-    constexpr int RQ = RC / 4, QP = 4;
+    constexpr int RQ = RC / 4, QP = ENCX_DN_QP;
     const int nq = DN_CC * NRW * RQ;
     const int64_t left = (int64_t)(g.B - b) * g.Co * plane;  // floats from dyb to the tensor end
     for (int c0 = 0; c0 < g.Co; c0 += DN_CC) {
