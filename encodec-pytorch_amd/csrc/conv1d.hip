@@ -870,13 +870,16 @@ __global__ __launch_bounds__(NT) void conv_fwd_small_kernel(FwdArgs a) {
 // every 32 columns. These layers run instead as one GEMM over the flattened (b, t) columns
 // (N = B*T = 2400) with an im2col B operand gathered from L2 while staging, split over the
 // reduction into fixed slabs (conv_fwd_reduce / conv_poly_reduce apply the epilogue).
+// (the flattened indices split by FastDiv: a runtime integer division per staged element made
+// these GEMMs VALU-bound)
 struct LdConvFlat {
     static constexpr bool A_K_FAST = false, B_N_FAST = true;
     FwdArgs p;
+    FastDiv fk, ft;  // by K, by Tout
     ENCX_DEV float a(int m, int k) const { return p.wf[(int64_t)k * p.Cout + m]; }
     ENCX_DEV float b(int k, int n) const {
-        const int ci = k / p.K, tap = k - ci * p.K;
-        const int bb = n / p.Tout, t = n - bb * p.Tout;
+        const int ci = (int)fdiv((uint32_t)k, fk), tap = k - ci * p.K;
+        const int bb = (int)fdiv((uint32_t)n, ft), t = n - bb * p.Tout;
         const int m = pad_src(t * p.s + tap * p.d, p.pl, p.Tin, p.e, p.mode);
         const float v = p.x[((int64_t)bb * p.Cin + ci) * p.Tin + (m >= 0 ? m : 0)];  // no branch around the load
         return m >= 0 ? act_apply(p.act, v) : 0.f;
@@ -885,8 +888,9 @@ struct LdConvFlat {
 struct EpConvFlat {
     FwdArgs p;
     int slabs;
+    FastDiv ft;
     ENCX_DEV void pre(int co, int n, float* l) const {
-        const int bb = n / p.Tout, t = n - bb * p.Tout;
+        const int bb = (int)fdiv((uint32_t)n, ft), t = n - bb * p.Tout;
         const int64_t o = ((int64_t)bb * p.Cout + co) * p.Tout + t;
         const bool fin = slabs == 1;
         l[0] = (fin && p.bias) ? p.bias[co] : 0.f;
@@ -895,7 +899,7 @@ struct EpConvFlat {
         l[3] = (fin && p.accumulate) ? p.y[o] : 0.f;
     }
     ENCX_DEV void post(int co, int n, float v, const float* l) const {
-        const int bb = n / p.Tout, t = n - bb * p.Tout;
+        const int bb = (int)fdiv((uint32_t)n, ft), t = n - bb * p.Tout;
         const int64_t o = ((int64_t)bb * p.Cout + co) * p.Tout + t;
         if (slabs > 1) {
             p.part[(int64_t)blockIdx.z * p.B * p.Cout * p.Tout + o] = v;
@@ -915,10 +919,11 @@ struct LdPolyFlat {
     static constexpr bool A_K_FAST = false, B_N_FAST = true;
     PolyArgs p;
     int M, ncols;
+    FastDiv fj, fc;  // by J, by ncols
     ENCX_DEV float a(int m, int k) const { return p.wp[(int64_t)k * M + m]; }
     ENCX_DEV float b(int k, int n) const {
-        const int i = k / p.J, q = k - i * p.J;
-        const int bb = n / ncols, u = n - bb * ncols, t = u - q;
+        const int i = (int)fdiv((uint32_t)k, fj), q = k - i * p.J;
+        const int bb = (int)fdiv((uint32_t)n, fc), u = n - bb * ncols, t = u - q;
         const bool in = t >= 0 && t < p.Tin;
         const float v = p.in[((int64_t)bb * p.Ci + i) * p.Tin + (in ? t : 0)];  // no branch around the load
         return in ? act_apply(p.in_act, v) : 0.f;
@@ -927,9 +932,10 @@ struct LdPolyFlat {
 struct EpPolyFlat {
     PolyArgs p;
     int ncols, slabs;
+    FastDiv fs, fc;  // by s, by ncols
     ENCX_DEV void pre(int row, int n, float* l) const {
-        const int o = row / p.s, rr = row - o * p.s;
-        const int bb = n / ncols, u = n - bb * ncols, qpos = u * p.s + rr;
+        const int o = (int)fdiv((uint32_t)row, fs), rr = row - o * p.s;
+        const int bb = (int)fdiv((uint32_t)n, fc), u = n - bb * ncols, qpos = u * p.s + rr;
         l[0] = l[1] = 0.f;
         if (slabs > 1) return;
         if (p.mode == 0) {
@@ -944,8 +950,8 @@ struct EpPolyFlat {
         }
     }
     ENCX_DEV void post(int row, int n, float v, const float* l) const {
-        const int o = row / p.s, rr = row - o * p.s;
-        const int bb = n / ncols, u = n - bb * ncols, qpos = u * p.s + rr;
+        const int o = (int)fdiv((uint32_t)row, fs), rr = row - o * p.s;
+        const int bb = (int)fdiv((uint32_t)n, fc), u = n - bb * ncols, qpos = u * p.s + rr;
         if (slabs > 1) {
             if (qpos < p.Q) p.part[(((int64_t)blockIdx.z * p.B + bb) * p.Co + o) * p.Q + qpos] = v;
             return;
@@ -1408,7 +1414,8 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
         a.part = ws;
         a.KS = slabs;
         ENCX_REQUIRE(slabs == 1 || ws);
-        int rc = gemm_launch(LdConvFlat{a}, EpConvFlat{a, slabs}, a.Cout, N, Kred, st, splits);
+        int rc = gemm_launch(LdConvFlat{a, make_fastdiv(a.K), make_fastdiv(a.Tout)},
+                             EpConvFlat{a, slabs, make_fastdiv(a.Tout)}, a.Cout, N, Kred, st, splits);
         if (rc) return rc;
         if (slabs > 1) {
             int64_t n = (int64_t)a.B * a.Cout * a.Tout;
@@ -1472,7 +1479,9 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
         a.part = ws;
         a.KS = slabs;
         ENCX_REQUIRE(slabs == 1 || ws);
-        int rc = gemm_launch(LdPolyFlat{a, M, ncols}, EpPolyFlat{a, ncols, slabs}, M, N, Kred, st, splits);
+        int rc = gemm_launch(LdPolyFlat{a, M, ncols, make_fastdiv(a.J), make_fastdiv(ncols)},
+                             EpPolyFlat{a, ncols, slabs, make_fastdiv(a.s), make_fastdiv(ncols)}, M, N, Kred, st,
+                             splits);
         if (rc) return rc;
         if (slabs > 1) {
             int64_t n = (int64_t)a.B * a.Co * a.Q;
