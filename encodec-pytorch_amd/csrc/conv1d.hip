@@ -752,14 +752,22 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
 }
 
 // VALU weight grad for tiny A*N (first / last conv of the stack): thread per output element.
+// The chunk's L and R windows are staged SB elements per thread at a time, every load issued
+// before the first is used (a loop of single loads waited out one memory round trip per element:
+// 33 in a row per thread for the R window of the last conv).
+constexpr int SMALL_BT = 256;  // t per chunk (plan_wgrad's kind 0)
+constexpr int SB = 8;
 __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
     extern __shared__ float smem[];
-    const int BT = a.BT, K = a.K, N = a.C * K, AN = a.A * N;
-    float* Ls = smem;               // [A][BT]
-    float* Rs = smem + a.A * BT;    // [C][WLp]
+    constexpr int BT = SMALL_BT;
+    const int K = a.K, N = a.C * K, AN = a.A * N;
+    constexpr int LST = BT + 1;     // Ls row stride: the rows of one wave's threads on distinct banks
+    float* Ls = smem;               // [A][LST]
+    float* Rs = smem + a.A * LST;   // [C][WLp]
     const int split = blockIdx.x, tid = threadIdx.x;
     const int nchunks_t = (a.Tl + BT - 1) / BT;
     const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
+    const int nl = a.A * BT, nr = a.C * WL;
     float acc = 0.f, bacc = 0.f;  // AN (+ A with the bias) <= NT
     const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
     for (int it = it_beg; it < it_end; ++it) {
@@ -767,18 +775,48 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
         const float* Lb = a.L + (int64_t)b * a.A * a.Tl;
         const float* Rb = a.R + (int64_t)b * a.C * a.Tr;
         __syncthreads();
-        for (int i = tid; i < a.A * BT; i += NT) {
-            int al = i / BT, tl = i - al * BT, t = tc + tl;
-            Ls[i] = t < a.Tl ? act_apply(a.actL, Lb[(int64_t)al * a.Tl + t]) : 0.f;
+        for (int i0 = 0; i0 < nl; i0 += NT * SB) {
+            float v[SB];
+            bool ok[SB];
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+                const int i = i0 + q * NT + tid, al = i / BT, t = tc + (i - al * BT);
+                ok[q] = i < nl && t < a.Tl;
+                v[q] = Lb[ok[q] ? (int64_t)al * a.Tl + t : 0];  // no branch around the load
+            }
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+                const int i = i0 + q * NT + tid, al = i / BT;
+                if (i < nl) Ls[i + al] = ok[q] ? act_apply(a.actL, v[q]) : 0.f;
+            }
         }
-        for (int i = tid; i < a.C * WL; i += NT) {
-            int c = i / WL, w = i - c * WL;
-            int m = pad_src(tc * a.s + w, a.pl, a.Tr, a.e, a.mode);
-            Rs[c * a.WLp + w] = m >= 0 ? act_apply(a.actR, Rb[(int64_t)c * a.Tr + m]) : 0.f;
+        // (c, w) of element i0 + tid, advanced by NT elements per step without a division
+        const int dc = NT / WL, dw = NT - dc * WL;
+        int c_n = tid / WL, w_n = tid - (tid / WL) * WL;
+        for (int i0 = 0; i0 < nr; i0 += NT * SB) {
+            float v[SB];
+            int cq[SB], wq[SB], mq[SB];
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+                cq[q] = c_n;
+                wq[q] = w_n;
+                w_n += dw;
+                c_n += dc;
+                if (w_n >= WL) {
+                    w_n -= WL;
+                    ++c_n;
+                }
+                const int m = cq[q] < a.C ? pad_src(tc * a.s + wq[q], a.pl, a.Tr, a.e, a.mode) : -1;
+                mq[q] = m;
+                v[q] = Rb[m >= 0 ? (int64_t)cq[q] * a.Tr + m : 0];
+            }
+#pragma unroll
+            for (int q = 0; q < SB; ++q)
+                if (cq[q] < a.C) Rs[cq[q] * a.WLp + wq[q]] = mq[q] >= 0 ? act_apply(a.actR, v[q]) : 0.f;
         }
         __syncthreads();
         if (a.wsb && tid >= AN && tid < AN + a.A) {  // bias: sum of the L row over the chunk
-            const float* lp = Ls + (tid - AN) * BT;
+            const float* lp = Ls + (tid - AN) * LST;
             float s0 = 0.f, s1 = 0.f;
             for (int tl = 0; tl < BT; tl += 2) {
                 s0 += lp[tl];
@@ -788,7 +826,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
         }
         if (tid < AN) {
             int aa = tid / N, n = tid - aa * N, c = n / K, k = n - c * K;
-            const float* lp = Ls + aa * BT;
+            const float* lp = Ls + aa * LST;
             const float* rp = Rs + c * a.WLp + k * a.d;
             float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 independent chains
             for (int tl = 0; tl < BT; tl += 4) {
@@ -835,14 +873,31 @@ __global__ __launch_bounds__(NT) void conv_fwd_small_kernel(FwdArgs a) {
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     for (int c0 = 0; c0 < a.Cin; c0 += CK) {
         __syncthreads();
-        for (int i = tid; i < CK * WL; i += NT) {
-            int cl = i / WL, w = i - cl * WL, c = c0 + cl;
-            float v = 0.f;
-            if (c < a.Cin) {
-                int m = pad_src(t0 * S + w, a.pl, a.Tin, a.e, a.mode);
-                if (m >= 0) v = act_apply(a.act, xb[(int64_t)c * a.Tin + m]);
+        // SB loads in flight per thread (as conv_wgrad_small_kernel); (cl, w) stepped without a division
+        {
+            const int dc = NT / WL, dw = NT - dc * WL;
+            int cl_n = tid / WL, w_n = tid - (tid / WL) * WL;
+            for (int i0 = 0; i0 < CK * WL; i0 += NT * SB) {
+                float v[SB];
+                int iq[SB], mq[SB];
+#pragma unroll
+                for (int q = 0; q < SB; ++q) {
+                    const int cl = cl_n, w = w_n, c = c0 + cl;
+                    w_n += dw;
+                    cl_n += dc;
+                    if (w_n >= WL) {
+                        w_n -= WL;
+                        ++cl_n;
+                    }
+                    iq[q] = cl < CK ? cl * WL + w : -1;
+                    const int m = (cl < CK && c < a.Cin) ? pad_src(t0 * S + w, a.pl, a.Tin, a.e, a.mode) : -1;
+                    mq[q] = m;
+                    v[q] = xb[m >= 0 ? (int64_t)c * a.Tin + m : 0];  // no branch around the load
+                }
+#pragma unroll
+                for (int q = 0; q < SB; ++q)
+                    if (iq[q] >= 0) Xs[iq[q]] = mq[q] >= 0 ? act_apply(a.act, v[q]) : 0.f;
             }
-            Xs[i] = v;
         }
         for (int i = tid; i < a.Cout * CK * K; i += NT) {
             int co = i / (CK * K), r = i - co * CK * K, cl = r / K, k = r - cl * K, c = c0 + cl;
@@ -1532,7 +1587,7 @@ static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K)
     WgPlan p;
     const int64_t N = C * K;
     if (A * N <= NT) {
-        p.kind = 0; p.BT = 256; p.BM = p.BN = 0; p.tiles = 1;
+        p.kind = 0; p.BT = SMALL_BT; p.BM = p.BN = 0; p.tiles = 1;
     } else if (N <= 32 && A <= 64) {
         p.kind = 1; p.BT = 64; p.BM = A <= 32 ? 32 : 64; p.BN = 32;
         p.tiles = (int)cdiv(A, p.BM);
@@ -1599,7 +1654,7 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
     if (p.kind == 0) {
         a.WLp = WL;
         a.NCmax = (int)C;
-        size_t lds = (size_t)(A * p.BT + C * WL) * sizeof(float);
+        size_t lds = (size_t)(A * (p.BT + 1) + C * WL) * sizeof(float);
         if (lds > 160 * 1024) return ENCX_EINVAL;
         hipLaunchKernelGGL(conv_wgrad_small_kernel, dim3(p.splits), dim3(NT), lds, st, a);
     } else {
