@@ -755,8 +755,13 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(WgArgs a) {
 // The chunk's L and R windows are staged SB elements per thread at a time, every load issued
 // before the first is used (a loop of single loads waited out one memory round trip per element:
 // 33 in a row per thread for the R window of the last conv).
+// KW > 0 (stride 1, dilation 1, K == KW, A*C <= NT): thread (pair p = tid % P of (a, c), segment
+// sg = tid / P of the chunk's t range) keeps a KW-wide window of its R row in registers and
+// accumulates all KW taps of its pair: 2 LDS reads per t instead of 2 per (t, tap); the segments'
+// partials are summed in segment order at the end (deterministic).
 constexpr int SMALL_BT = 256;  // t per chunk (plan_wgrad's kind 0)
 constexpr int SB = 8;
+template <int KW>
 __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
     extern __shared__ float smem[];
     constexpr int BT = SMALL_BT;
@@ -769,6 +774,9 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
     const int WL = (BT - 1) * a.s + (K - 1) * a.d + 1;
     const int nl = a.A * BT, nr = a.C * WL;
     float acc = 0.f, bacc = 0.f;  // AN (+ A with the bias) <= NT
+    float wacc[KW > 0 ? KW : 1];
+#pragma unroll
+    for (int k = 0; k < (KW > 0 ? KW : 1); ++k) wacc[k] = 0.f;
     const int it_beg = split * a.per_split, it_end = min(a.items, it_beg + a.per_split);
     for (int it = it_beg; it < it_end; ++it) {
         const int b = it / nchunks_t, tc = (it - b * nchunks_t) * BT;
@@ -815,6 +823,28 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
                 if (cq[q] < a.C) Rs[cq[q] * a.WLp + wq[q]] = mq[q] >= 0 ? act_apply(a.actR, v[q]) : 0.f;
         }
         __syncthreads();
+        if (KW > 0) {
+            const int P = a.A * a.C, seg = NT / P, TS = (BT + seg - 1) / seg;
+            const int pp = tid % P, sg = tid / P, aa = pp / a.C, c = pp - aa * a.C;
+            if (sg < seg) {
+                const int tb = sg * TS, te = min(BT, tb + TS);
+                const float* lp = Ls + aa * LST;
+                const float* rp = Rs + c * a.WLp;
+                float win[KW > 0 ? KW : 1];
+#pragma unroll
+                for (int k = 0; k + 1 < KW; ++k) win[k] = rp[tb + k];
+                for (int tl = tb; tl < te; ++tl) {
+                    win[KW - 1] = rp[tl + KW - 1];
+                    const float l = lp[tl];
+#pragma unroll
+                    for (int k = 0; k < KW; ++k) wacc[k] = fmaf(l, win[k], wacc[k]);
+                    bacc += l;
+#pragma unroll
+                    for (int k = 0; k + 1 < KW; ++k) win[k] = win[k + 1];
+                }
+            }
+            continue;
+        }
         if (a.wsb && tid >= AN && tid < AN + a.A) {  // bias: sum of the L row over the chunk
             const float* lp = Ls + (tid - AN) * LST;
             float s0 = 0.f, s1 = 0.f;
@@ -837,6 +867,29 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
             }
             acc += (s0 + s1) + (s2 + s3);
         }
+    }
+    if (KW > 0) {  // the segments' partials: red[sg][pp][k] (k = KW: the bias sum), summed in sg order
+        const int P = a.A * a.C, seg = NT / P;
+        __syncthreads();
+        float* red = smem;
+        if (tid < seg * P) {
+#pragma unroll
+            for (int k = 0; k < KW; ++k) red[tid * (KW + 1) + k] = wacc[k];
+            red[tid * (KW + 1) + KW] = bacc;
+        }
+        __syncthreads();
+        if (tid < P * KW) {  // output tid = pp * K + k (= aa * N + c * K + k)
+            const int pp = tid / KW, k = tid - pp * KW;
+            float v = 0.f;
+            for (int sg = 0; sg < seg; ++sg) v += red[(sg * P + pp) * (KW + 1) + k];
+            a.ws[(int64_t)split * AN + tid] = v;
+        }
+        if (a.wsb && tid < a.A) {  // bias of row aa: the pairs (aa, c = 0)
+            float v = 0.f;
+            for (int sg = 0; sg < seg; ++sg) v += red[(sg * P + tid * a.C) * (KW + 1) + KW];
+            a.wsb[(int64_t)split * a.A + tid] = v;
+        }
+        return;
     }
     if (tid < AN) a.ws[(int64_t)split * AN + tid] = acc;
     if (a.wsb && tid >= AN && tid < AN + a.A) a.wsb[(int64_t)split * a.A + (tid - AN)] = bacc;
@@ -1652,11 +1705,14 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
     const int WL = (p.BT - 1) * a.s + (a.K - 1) * a.d + 1;
     const int64_t AN = A * C * K;
     if (p.kind == 0) {
-        a.WLp = WL;
+        const bool win7 = s == 1 && d == 1 && K == 7 && A * C <= NT;
+        a.WLp = win7 ? (WL | 1) : WL;  // (odd: the window rows of a wave's pairs on distinct banks)
         a.NCmax = (int)C;
-        size_t lds = (size_t)(A * (p.BT + 1) + C * WL) * sizeof(float);
+        size_t lds = (size_t)(A * (p.BT + 1) + C * a.WLp) * sizeof(float);
+        if (win7) lds = std::max(lds, (size_t)NT * 8 * sizeof(float));  // the segment reduction
         if (lds > 160 * 1024) return ENCX_EINVAL;
-        hipLaunchKernelGGL(conv_wgrad_small_kernel, dim3(p.splits), dim3(NT), lds, st, a);
+        if (win7) hipLaunchKernelGGL(conv_wgrad_small_kernel<7>, dim3(p.splits), dim3(NT), lds, st, a);
+        else hipLaunchKernelGGL(conv_wgrad_small_kernel<0>, dim3(p.splits), dim3(NT), lds, st, a);
     } else {
         a.WLp = wlp_for(WL, a.K);
         a.NCmax = (int)((p.BN + a.K - 1) / a.K + 1);
