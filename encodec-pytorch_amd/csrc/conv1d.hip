@@ -1534,13 +1534,15 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
     }
     FwdPlan p = plan_fwd(a.B, a.Cin, a.Cout, a.Tout, a.K, a.s, a.d, a.res || a.xact || a.accumulate);
     if (p.small) {
-        int ck = 64 / a.K;
+        // as many channels per LDS stage as ~48 KB hold (the stages are sequential round trips;
+        // the per-thread sum runs over the channels in order either way)
+        const int WL = (NT - 1) * a.s + (a.K - 1) * a.d + 1;
+        int ck = 12288 / (WL + a.Cout * a.K);
         if (ck < 1) ck = 1;
         if (ck > a.Cin) ck = a.Cin;
         a.CK = ck;
         a.KS = 1;
         a.cps = a.Cin;
-        const int WL = (NT - 1) * a.s + (a.K - 1) * a.d + 1;
         size_t lds = (size_t)(ck * WL + a.Cout * ck * a.K) * sizeof(float);
         ENCX_REQUIRE(lds <= 160 * 1024);
         hipLaunchKernelGGL(conv_fwd_small_kernel, dim3(cdiv(a.Tout, NT), 1, a.B), dim3(NT), lds, st, a);
