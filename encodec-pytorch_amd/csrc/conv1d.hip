@@ -1647,7 +1647,11 @@ static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K)
         p.kind = 1; p.BT = 64; p.BM = A <= 32 ? 32 : 64; p.BN = 32;
         p.tiles = (int)cdiv(A, p.BM);
     } else {
-        p.kind = 2; p.BT = Tl >= 512 ? 64 : 32;  // short rows: less tail padding per chunk
+        p.kind = 2;
+        // the row in equal chunks of <= 64 positions, a multiple of 4 each: T 75 -> 2 x 40
+        // (fixed 32-position chunks padded it to 96), T 600 -> 10 x 60 (64: 640)
+        const int64_t nch = cdiv(Tl, 64);
+        p.BT = (int)(cdiv(cdiv(Tl, nch), 4) * 4);
         Tile t = (A <= 32) ? T32x128 : (A <= 64 ? T64x128 : T128x128);
         p.BM = tile_bm(t); p.BN = 128;
         p.tiles = (int)(cdiv(N, p.BN) * cdiv(A, p.BM));
