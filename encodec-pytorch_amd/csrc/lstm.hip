@@ -925,6 +925,11 @@ static bool lstm_shape_ok(int64_t B, int64_t T, int64_t H, int64_t L) {
            B * T * 4 * H < ((int64_t)1 << 31);
 }
 
+__global__ void zero_ints(int* p, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1050,8 +1055,11 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
     BwdArgs a{DA, wcatT, P, (int)B, (int)T, (int)H, (int)L, 0, gper, dout, dcn, Cst, Gs, dx, acc_x,
               fuse ? cnt : nullptr};
     if (fuse) {
-        const hipError_t e = hipMemsetAsync(cnt, 0, (size_t)(L + 1) * (H / 16) * sizeof(int), st);
-        if (e != hipSuccess) return (int)e;
+        // the arrival counters zeroed by a kernel, not a hipMemsetAsync: a memset node captured into
+        // a HIP graph was not ordered before the next kernel in replays (round 5, the persistent
+        // form's counters; see g_lstm_sync)
+        const int ncnt = (int)((L + 1) * (H / 16));
+        hipLaunchKernelGGL(zero_ints, dim3((unsigned)cdiv(ncnt, 256)), dim3(256), 0, st, cnt, ncnt);
         hipLaunchKernelGGL(lstm_bwd_elem, egrid, dim3(256), 0, st, dout, P, ns, dcn, Cst, Gs, DA, dx, acc_x,
                            (int)B, (int)T, (int)H, (int)L, 0);
         for (int k = 0; k < steps - 1; ++k) {

@@ -410,10 +410,14 @@ def test_lstm_persistent_bit_identical(B, H, Tn, L):
             assert torch.equal(a, b), (rnd, name, float((a - b).abs().max()))
 
 
-def test_lstm_persistent_graph_replays():
-    """The persistent recurrences captured in a HIP graph and replayed (the training step's form):
-    every replay, on fresh inputs, gives the bits of an eager call, and no hand-off spin times out
-    (the counters must be zero at every launch, captured or not)."""
+@pytest.mark.parametrize('form', ['persist', 'fused_step'])
+def test_lstm_persistent_graph_replays(form):
+    """The recurrences captured in a HIP graph and replayed (the training step's form): every
+    replay, on fresh inputs, gives the bits of an eager call, and no hand-off spin times out (the
+    counters must be zero at every launch, captured or not). 'persist': the persistent kernels;
+    'fused_step': the opt-in step form whose backward fuses E(k+1) into G(k) by last-arriver
+    counters (zeroed by a kernel: a captured hipMemsetAsync was not ordered before the next kernel
+    in replays)."""
     import ctypes
     from encx._lib import call, ptr, option, lib
     B, H, Tn, L = 4, 512, 75, 2
@@ -437,7 +441,8 @@ def test_lstm_persistent_graph_replays():
         call('encx_lstm_fwd', ptr(x), ptr(wcat), ptr(bsum), ptr(xt), ptr(Y), ptr(Cs), ptr(Gs), ptr(out), 1, B, Tn, H, L, st)
         call('encx_lstm_bwd', ptr(dout), ptr(wcatT), ptr(Cs), ptr(Gs), ptr(DA), ptr(dx), 0, ptr(ws), B, Tn, H, L, st)
 
-    with option(LSTM_PERSIST=1):
+    opts = dict(LSTM_PERSIST=1) if form == 'persist' else dict(LSTM_PERSIST=0, LSTM_FUSE=1)
+    with option(**opts):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
