@@ -42,11 +42,13 @@ ENCX_DEV uint64_t shfl_xor64(uint64_t v, int o) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// One workgroup = 64 frames x 128 codes with the whole D staged once (no chunk loop): frames
+// One workgroup = 64 frames x 64 codes with the whole D staged once (no chunk loop): frames
 // are loaded along t (the [B][D][T] latent is t-contiguous) into As[d][frame], codes along d
-// into Bs[d][code] (row stride 129: conflict-free transposed writes), so a workgroup does one
-// load phase, one barrier and 64 MFMA k-steps. 38 x 8 = 304 workgroups at N = 2400.
-constexpr int AR_ROWS = 64, AR_CODES = 128, AR_BS = AR_CODES + 1;
+// into Bs[d][code] (row stride 65), so a workgroup does one load phase, one barrier and 64 MFMA
+// k-steps; its 4 waves are 2 x 2 tiles of 32 x 32. 66 KB of LDS: two workgroups per CU, so one
+// hides the other's LDS and load latency (at 128 codes, 100 KB, one per CU: MFMA busy 0.08).
+// 38 x 16 = 608 workgroups at N = 2400.
+constexpr int AR_ROWS = 64, AR_CODES = 64, AR_BS = AR_CODES + 1;
 constexpr int AR_PER = 8;    // staging loads in flight per thread (scalar code path)
 constexpr int AR_XPER = 32;  // frame-element loads in flight per thread
 constexpr int AR_EPER = 16;  // code quads in flight per thread
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n0 = blockIdx.x * AR_ROWS, k0 = blockIdx.y * AR_CODES;
     const int h = lane >> 5, l32 = lane & 31;
-    const int wm0 = (wave >> 1) * 32, wn0 = (wave & 1) * 64;
+    const int wm0 = (wave >> 1) * 32, wn0 = (wave & 1) * 32;
     // staging: AR_XPER (frames) / AR_EPER (code quads) loads in flight per thread from clamped
     // addresses, values selected after the load (a branch around each load serialises the
     // latency: one round trip per element); at D = 128 each operand is ONE round of loads
@@ -140,16 +142,14 @@ __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed
         for (int d = 0; d < D; ++d) v = fmaf(Bs[d * AR_BS + c], Bs[d * AR_BS + c], v);
         ee[c] = v;
     }
-    f32x16 acc[2];
-    acc[0] = acc[1] = (f32x16){0};
+    f32x16 acc[1];
+    acc[0] = (f32x16){0};
     const float* ap = As + h * AR_ROWS + wm0 + l32;
     const float* bp = Bs + h * AR_BS + wn0 + l32;
 #pragma unroll 4
     for (int dp = 0; dp < D; dp += 2) {
         const float av = ap[dp * AR_ROWS];
-        const float b0 = bp[dp * AR_BS], b1 = bp[dp * AR_BS + 32];
-        acc[0] = mfma32(av, b0, acc[0]);
-        acc[1] = mfma32(av, b1, acc[1]);
+        acc[0] = mfma32(av, bp[dp * AR_BS], acc[0]);
     }
     __syncthreads();  // xx / ee visible
 #pragma unroll
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(NT) void rvq_argmin_mfma(Rows x, const float* embed
         const int row = wm0 + mfma_row(r, lane);
         uint64_t best = ~0ull;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < 1; ++j) {
             const int c = wn0 + j * 32 + l32, k = k0 + c;
             if (k < Kc) {
                 const float v = (xx[row] - 2.f * acc[j][r]) + ee[c];
