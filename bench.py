@@ -158,6 +158,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
+    trainer.check_sync()  # no persistent-LSTM hand-off failed in the timed steps (raises otherwise)
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

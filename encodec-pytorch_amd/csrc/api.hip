@@ -40,6 +40,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {OPT_FWR, "FWR", 256}, {OPT_DGR, "DGR", 256}, {OPT_WGR, "WGR", 2048},
     {OPT_WGR_WGS, "WGR_WGS", 256}, {OPT_FEAT_CODE, "FEAT_CODE", 1}, {OPT_CONV_CK, "CONV_CK", 64},
     {OPT_CONV_SPLIT, "CONV_SPLIT", 1024}, {OPT_CONV_WG_SPLIT, "CONV_WG_SPLIT", 1024},
+    {OPT_LSTM_SPIN, "LSTM_SPIN", 0}, {OPT_LSTM_FAULT, "LSTM_FAULT", 0},
 };
 constexpr bool opts_in_order() {
     for (int i = 0; i < OPT_COUNT; ++i)

@@ -187,6 +187,8 @@ enum EncxOpt {
     OPT_CONV_CK,       // conv1d fwd / bwd-data: reduction elements (channels x taps) per LDS chunk
     OPT_CONV_SPLIT,    // conv1d fwd / bwd-data: split-K until this many workgroups
     OPT_CONV_WG_SPLIT, // conv1d weight grad: split the positions until this many workgroups
+    OPT_LSTM_SPIN,     // persistent LSTM: log2 of every poll's spin bound (0: 20, about 1 s)
+    OPT_LSTM_FAULT,    // persistent LSTM, tests only: one workgroup never publishes (its consumers time out)
     OPT_COUNT
 };
 int64_t encx_opt(EncxOpt id);

@@ -3539,6 +3539,10 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
                               int64_t dt, int64_t pt, int64_t pf, encx_stream_t stream) {
     ENCX_REQUIRE(dy && wp && dx);
     ENCX_REQUIRE(!feat_real || (feat_fake && feat_denom));
+    // the epilogues with a feature term take sign(x - feat_real) from the map they load as x: the
+    // xact map when there is one (the compile-time epilogues dgr_epi / rw_dg_epi), so it must BE
+    // the fake map
+    ENCX_REQUIRE(!feat_real || !xact || xact == feat_fake);
     C2Geo g{(int)B, (int)Ci, (int)T2, (int)Fi, (int)Co, (int)Fo, (int)KT, (int)KF, (int)sf, (int)dt, (int)pt, (int)pf};
     ENCX_REQUIRE(geo_ok(g));
     hipStream_t st = (hipStream_t)stream;

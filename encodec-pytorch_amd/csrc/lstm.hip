@@ -195,28 +195,52 @@ __device__ long long g_lstm_trace[2 * 256 * 128 * 8];
     } while (0)
 #endif
 
-// wave-wide bounded poll: cnt >= target (relaxed agent loads, sc1); false after ~1 s
-ENCX_DEV bool poll_ge(const int* cnt, int target, int* err) {
-    for (int i = 0; i < (1 << 20); ++i) {
+// The persistent kernels' control word (host: pers_ctl): bits 0-4 log2 of the spin bound of every
+// poll (0: 20, about 1 s), bit 5 fault injection for tests: workgroup 0 never publishes, so its
+// consumers' polls time out (option LSTM_FAULT).
+constexpr int CTL_FAULT = 32;
+ENCX_DEV int ctl_spins(int ctl) { return (ctl & 31) ? 1 << (ctl & 31) : 1 << 20; }
+// wave-wide bounded poll: cnt >= target (relaxed agent loads, sc1); false after `spins` tries
+ENCX_DEV bool poll_ge(const int* cnt, int target, int* err, int spins) {
+    for (int i = 0; i < spins; ++i) {
         if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
         __builtin_amdgcn_s_sleep(1);
     }
     if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return false;
 }
-// end of a persistent launch: the last workgroup to count itself done zeroes the counter lines
-// [0, nlines) and the done count. Every workgroup has passed its last poll before it counts itself,
-// and the next launch on the stream starts after this one has ended.
-ENCX_DEV void finish_launch(int* sync, int nlines) {
+// end of a persistent launch: the last workgroup to count itself done checks that every counter
+// line reached its final count (lines [0, n1) expect e1 arrivals, lines [n1, n1 + n2) expect e2; a
+// line off its count -- an arrival lost, or one left over from an earlier launch -- counts in the
+// error word), then zeroes the lines and the done count. Every workgroup has passed its last poll
+// before it counts itself, and the next launch on the stream starts after this one has ended.
+// Ordering: thread 0 made this workgroup's last arrivals; its s_waitcnt vmcnt(0) holds the done
+// arrival until those atomics have been performed, so the last workgroup's zeroing (issued after
+// its returning done add saw every other workgroup's) follows every arrival of the launch.
+ENCX_DEV void finish_launch(int* sync, int n1, int e1, int n2, int e2) {
     __syncthreads();
     if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int* done = sync + (SYNC_LINES + 1) * SYNC_LINE;
         if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-            for (int i = 0; i < nlines; ++i)
+            int off = 0;
+            for (int i = 0; i < n1 + n2; ++i) {
+                const int v = __hip_atomic_load(sync + i * SYNC_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                off += v != (i < n1 ? e1 : e2);
+            }
+            if (off) __hip_atomic_fetch_add(sync + SYNC_LINES * SYNC_LINE, off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int i = 0; i < n1 + n2; ++i)
                 __hip_atomic_store(sync + i * SYNC_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+// the error word into a caller's running count, and cleared (encx_lstm_sync_read): stream-ordered,
+// capturable
+__global__ void sync_read_kernel(int* sync, int* dst) {
+    int* err = sync + SYNC_LINES * SYNC_LINE;
+    const int v = __hip_atomic_exchange(err, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dst[0] += v;
 }
 ENCX_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const float* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
@@ -234,7 +258,7 @@ ENCX_DEV float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
 template <int G>
 __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const float* wcat, const float* bsum,
                                                          float* Y, float* Cst, float* Gs, int B, int T, int H,
-                                                         int NBG, int* sync) {
+                                                         int NBG, int* sync, int ctl) {
     const int NUG = H / PU;
     const int id = blockIdx.x, ug = id % NUG, bg = (id / NUG) % NBG, l = id / (NUG * NBG);
     __shared__ float red[FW][16][33];
@@ -270,6 +294,8 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
     const int* const cnt_in = sync + ((l > 0 ? l - 1 : 0) * NBG + bg) * SYNC_LINE;
     int* const err = sync + SYNC_LINES * SYNC_LINE;
     bool live = true;  // wave 0: no poll has timed out
+    const int spins = ctl_spins(ctl);
+    const bool silent = (ctl & CTL_FAULT) && blockIdx.x == 0;
     float c = 0.f;
     for (int t = 0; t < T; ++t) {
         LSTM_TRACE(0, t, 0);
@@ -277,7 +303,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
         // ---- input part x_l(t): layer 0 reads xt (written before this launch), layer l > 0
         // waits for h_{l-1}(t) of all NUG workgroups of (l-1, bg)
         if (l > 0) {
-            if (wave == 0 && live) live = poll_ge(cnt_in, NUG * (t + 1), err);
+            if (wave == 0 && live) live = poll_ge(cnt_in, NUG * (t + 1), err, spins);
             __syncthreads();
         }
         LSTM_TRACE(0, t, 1);
@@ -297,7 +323,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
         // ---- recurrent part h_l(t-1) (zero at t = 0): k-groups g >= G / 2
         if (t > 0) {
             LSTM_TRACE(0, t, 2);
-            if (wave == 0 && live) live = poll_ge(cnt_self, NUG * t, err);
+            if (wave == 0 && live) live = poll_ge(cnt_self, NUG * t, err, spins);
             __syncthreads();
             LSTM_TRACE(0, t, 3);
             float4 a[G / 2];
@@ -345,9 +371,9 @@ __global__ __launch_bounds__(FW * 64) void lstm_fwd_pers(const float* xt, const 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         LSTM_TRACE(0, t, 6);
-        if (tid == 0) __hip_atomic_fetch_add(cnt_self, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0 && !silent) __hip_atomic_fetch_add(cnt_self, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    finish_launch(sync, (int)gridDim.x / NUG);  // the L NBG counters
+    finish_launch(sync, (int)gridDim.x / NUG, NUG * T, 0, 0);  // the L NBG counters
 }
 
 // ------------------------------------------------------------------------- backward step
@@ -534,7 +560,7 @@ template <int G>
 __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, const float* wcatT, const float* Cst,
                                                          const float* Gs, float* DA, float* dx, int acc_x,
                                                          float* XP, int B, int T, int H, int L, int NBG,
-                                                         int* sync) {
+                                                         int* sync, int ctl) {
     const int NRT = H / 16, NCT = 2 * NRT;
     const int id = blockIdx.x, ct = id % NCT, bg = (id / NCT) % NBG, l = id / (NCT * NBG);
     const bool recw = ct >= NRT;
@@ -567,6 +593,8 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
     int* const err = sync + SYNC_LINES * SYNC_LINE;
     const bool top = l == L - 1;
     bool live = true;
+    const int spins = ctl_spins(ctl);
+    const bool silent = (ctl & CTL_FAULT) && blockIdx.x == NRT;  // layer 0's first recurrent tile
     float dcn = 0.f;
     for (int i = 0; i < T; ++i) {
         const int t = T - 1 - i;
@@ -591,7 +619,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
         const int tf = recw ? t + 1 : t;
         float tile = 0.f;
         if (tf < T) {
-            if (wave == 0 && live) live = poll_ge(cnt_da, NRT * (T - tf), err);
+            if (wave == 0 && live) live = poll_ge(cnt_da, NRT * (T - tf), err, spins);
             __syncthreads();
             LSTM_TRACE(1, i, 1);
             load_point();  // (older than the DA loads: the MFMAs' in-order waits are not pushed back)
@@ -653,7 +681,7 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
             // ---- recurrent tile: the cell backward of frame t
             float above = dtop;
             if (!top) {
-                if (wave == 0 && live) live = poll_ge(xf_in, i + 1, err);
+                if (wave == 0 && live) live = poll_ge(xf_in, i + 1, err, spins);
                 __syncthreads();
                 LSTM_TRACE(1, i, 3);
                 if (tid < 256)
@@ -679,9 +707,10 @@ __global__ __launch_bounds__(FW * 64) void lstm_bwd_pers(const float* dout, cons
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         LSTM_TRACE(1, i, 5);
-        if (publish && tid == 0) __hip_atomic_fetch_add(pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (publish && tid == 0 && !silent) __hip_atomic_fetch_add(pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    finish_launch(sync, L * NBG + (L - 1) * NBG * NRT);  // the DA counters and the input-tile flags
+    // the DA counters (NRT arrivals per frame) and the input-tile flags (one per frame)
+    finish_launch(sync, L * NBG, NRT * T, (L - 1) * NBG * NRT, T);
 }
 
 // ------------------------------------------------------------------------- layout kernels
@@ -891,6 +920,18 @@ static int device_cus() {
     if (!cus[d] && hipDeviceGetAttribute(&cus[d], hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) cus[d] = 0;
     return cus[d];
 }
+// the persistent kernels' control word from the options (see ctl_spins)
+static int pers_ctl() {
+    const int64_t sp = encx_opt(OPT_LSTM_SPIN);
+    return (int)((sp > 0 && sp < 31 ? sp : 0) | (encx_opt(OPT_LSTM_FAULT) ? CTL_FAULT : 0));
+}
+// every workgroup of a persistent launch must be resident at once: nwg within what the kernel's
+// occupancy (registers, LDS, waves) admits on the device's CUs
+static bool coresident(const void* kern, int64_t nwg) {
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, FW * 64, 0) != hipSuccess) return false;
+    return per > 0 && nwg <= (int64_t)per * device_cus();
+}
 static int* sync_words() {
     static int* addr[64];
     int d = 0;
@@ -900,24 +941,41 @@ static int* sync_words() {
 }
 // workgroups of the persistent forward, or 0 when the shape or the device does not admit it (the
 // workgroups must be resident together: at most one per CU; the sequences' byte offsets 32-bit)
-static int fwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
+template <int G> static int fwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
     if (encx_opt(OPT_LSTM_PERSIST) == 0 || H % 128 || H > 512 || B * T * H * 4 >= ((int64_t)1 << 31)) return 0;
     const int64_t nbg = cdiv(B, 16), nwg = L * nbg * (H / PU);
     if (L * nbg > SYNC_LINES || nwg > device_cus() || !sync_words()) return 0;
+    if (!coresident((const void*)lstm_fwd_pers<G>, nwg)) return 0;
     return (int)nwg;
 }
 // workgroups of the persistent backward, or 0 (as fwd_pers_grid; plus the hand-off lines)
-static int bwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
-    if (encx_opt(OPT_LSTM_PERSIST) == 0 || H % 128 || H > 512 || B * T * H * 16 >= ((int64_t)1 << 31)) return 0;
+// (DA's buffer offsets cover B T 4H floats, XP's (L - 1) B T H: both must fit the 32-bit offsets)
+template <int G> static int bwd_pers_grid(int64_t B, int64_t T, int64_t H, int64_t L) {
+    if (encx_opt(OPT_LSTM_PERSIST) == 0 || H % 128 || H > 512 || B * T * H * 16 >= ((int64_t)1 << 31) ||
+        (L - 1) * B * T * H * 4 >= ((int64_t)1 << 31))
+        return 0;
     const int64_t nbg = cdiv(B, 16), nwg = L * nbg * (2 * H / 16);
     if (L * nbg + (L - 1) * nbg * (H / 16) > SYNC_LINES || nwg > device_cus() || !sync_words()) return 0;
+    if (!coresident((const void*)lstm_bwd_pers<G>, nwg)) return 0;
     return (int)nwg;
 }
 template <int G>
-static void fwd_pers_launch(int nwg, hipStream_t st, const float* xt, const float* wcat, const float* bsum, float* Y,
-                            float* C, float* Gs, int B, int T, int H, int nbg, int* sync) {
+static bool fwd_pers_launch(hipStream_t st, const float* xt, const float* wcat, const float* bsum, float* Y,
+                            float* C, float* Gs, int B, int T, int H, int L) {
+    const int nwg = fwd_pers_grid<G>(B, T, H, L);
+    if (!nwg) return false;
     hipLaunchKernelGGL((lstm_fwd_pers<G>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, xt, wcat, bsum, Y, C, Gs, B, T,
-                       H, nbg, sync);
+                       H, (int)cdiv(B, 16), sync_words(), pers_ctl());
+    return true;
+}
+template <int G>
+static bool bwd_pers_launch(hipStream_t st, const float* dout, const float* wcatT, const float* Cst, const float* Gs,
+                            float* DA, float* dx, int acc_x, float* XP, int B, int T, int H, int L) {
+    const int nwg = bwd_pers_grid<G>(B, T, H, L);
+    if (!nwg) return false;
+    hipLaunchKernelGGL((lstm_bwd_pers<G>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, dout, wcatT, Cst, Gs, DA, dx,
+                       acc_x, XP, B, T, H, L, (int)cdiv(B, 16), sync_words(), pers_ctl());
+    return true;
 }
 
 static bool lstm_shape_ok(int64_t B, int64_t T, int64_t H, int64_t L) {
@@ -958,16 +1016,16 @@ int encx_lstm_fwd(const float* x, const float* wcat, const float* bsum, float* x
     hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)cdiv(T, 32), (unsigned)cdiv(H, 32), (unsigned)B),
                        dim3(32, 8), 0, st, x, xt, (int)H, (int)T);
     const int RT = (int)cdiv(B, 16), G = (int)cdiv(H / 8, FW);
-    if (const int nwg = fwd_pers_grid(B, T, H, L)) {
-        int* sync = sync_words();
-        const int nbg = (int)cdiv(B, 16);
+    bool pers = false;
+    switch (G) {  // H / 64 (the persistent form needs H % 128 == 0)
+        case 2: pers = fwd_pers_launch<2>(st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, (int)L); break;
+        case 4: pers = fwd_pers_launch<4>(st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, (int)L); break;
+        case 6: pers = fwd_pers_launch<6>(st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, (int)L); break;
+        case 8: pers = fwd_pers_launch<8>(st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, (int)L); break;
+        default: break;
+    }
+    if (pers) {
         ps.tag(" persist");
-        switch (G) {  // H / 64
-            case 2: fwd_pers_launch<2>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
-            case 4: fwd_pers_launch<4>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
-            case 6: fwd_pers_launch<6>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
-            default: fwd_pers_launch<8>(nwg, st, xt, wcat, bsum, Y, Cst, Gs, (int)B, (int)T, (int)H, nbg, sync); break;
-        }
     } else {
         const dim3 grid((unsigned)(H / UNITS), (unsigned)L);
         for (int k = 0; k < (int)(T + L - 1); ++k)
@@ -1006,6 +1064,15 @@ int encx_lstm_sync_errors(int64_t* count) {
     return (int)e;
 }
 
+int encx_lstm_sync_read(int32_t* count, encx_stream_t stream) {
+    ENCX_REQUIRE(count);
+    int* w = sync_words();
+    ENCX_REQUIRE(w);
+    hipLaunchKernelGGL(sync_read_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, w, (int*)count);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
 size_t encx_lstm_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t L) {
     // step form: dcn [L][B][H], P [L][ns][B][2H], the fused step's arrival counters [(L + 1) * H/16]
     // (int); persistent form: XP [L-1][B][T][H]
@@ -1029,22 +1096,23 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
     const int BH = (int)(B * H);
     const dim3 egrid((unsigned)cdiv(BH, 256), (unsigned)(L + (dx ? 1 : 0)));
     const dim3 ggrid((unsigned)(2 * H / 16), (unsigned)ns, (unsigned)L);
-    if (const int nwg = bwd_pers_grid(B, T, H, L)) {
-        int* sync = sync_words();
-        const int nbg = (int)cdiv(B, 16);
-        ps.tag(" persist");
-#define BWD_PERS(G_)                                                                                            \
-    hipLaunchKernelGGL((lstm_bwd_pers<G_>), dim3((unsigned)nwg), dim3(FW * 64), 0, st, dout, wcatT, Cst, Gs, DA, dx, \
-                       acc_x, ws, (int)B, (int)T, (int)H, (int)L, nbg, sync)
-        switch (H / 64) {
-            case 2: BWD_PERS(2); break;
-            case 4: BWD_PERS(4); break;
-            case 6: BWD_PERS(6); break;
-            default: BWD_PERS(8); break;
-        }
+    {
+        bool pers = false;
+#define BWD_PERS(G_) \
+    bwd_pers_launch<G_>(st, dout, wcatT, Cst, Gs, DA, dx, acc_x, ws, (int)B, (int)T, (int)H, (int)L)
+        if (H % 64 == 0) switch (H / 64) {
+                case 2: pers = BWD_PERS(2); break;
+                case 4: pers = BWD_PERS(4); break;
+                case 6: pers = BWD_PERS(6); break;
+                case 8: pers = BWD_PERS(8); break;
+                default: break;
+            }
 #undef BWD_PERS
-        ENCX_CHECK_LAUNCH();
-        return 0;
+        if (pers) {
+            ps.tag(" persist");
+            ENCX_CHECK_LAUNCH();
+            return 0;
+        }
     }
     const int steps = (int)(T + L);
     // E(k + 1) fused into G(k): opt-in (ENCX_LSTM_FUSE=1). Measured slower in the config-3 step:

@@ -87,6 +87,7 @@ class Trainer:
         self.max_graph_keys = 8  # keys past this many run eagerly (their pool memory is bounded)
         dec = [p for p in model.decoder.parameters() if p.requires_grad]
         self._dec_span = self.opt.span(dec) if dec else None
+        self._sync = None  # the persistent LSTM's error watch (_watch_sync)
 
     # ------------------------------------------------------------------ step
     # step() = host part (draw the bandwidth and the discriminator coin, advance the optimiser step
@@ -133,19 +134,48 @@ class Trainer:
             out = self._graph_step(key, x)
         else:
             out = self._run(x, bw, train_d)
+        self._watch_sync(x.device)
         if os.environ.get('ENCX_CHECK_SYNC', '0') == '1':
-            # the persistent LSTM launches' hand-off spins: any timeout means garbage grads (it
-            # synchronises the device, so it is a debugging switch)
-            from ._lib import lstm_sync_errors
-            n = lstm_sync_errors()
-            if n:
-                raise RuntimeError(f'encx: {n} LSTM hand-off spins timed out in this step (workgroups not '
-                                   'co-resident: another persistent launch on the GPU?)')
+            self.check_sync()  # debugging: wait for this step and check it now
         if self.sched is not None:
             self.sched.step()
         if self.sched_d is not None:
             self.sched_d.step()
         return out
+
+    # The persistent LSTM kernels hand frames between workgroups through counters with bounded
+    # spins; a spin that times out (workgroups not co-resident, e.g. a foreign kernel holding CUs)
+    # leaves that launch's results garbage and bumps a per-device error word (csrc/lstm.hip). After
+    # every step one tiny kernel folds the word into a device counter, which is copied to pinned
+    # memory asynchronously; the next step() reads the copy if it has landed (no sync, no stall of
+    # the queue) and raises on a nonzero count. check_sync() waits for the last step's copy.
+    def _watch_sync(self, device):
+        from ._lib import call, ptr, stream
+        w = self._sync
+        if w is None:
+            w = self._sync = [torch.zeros(1, dtype=torch.int32, device=device),
+                              torch.zeros(1, dtype=torch.int32).pin_memory(), torch.cuda.Event(), False]
+        dev, host, ev, pending = w
+        if pending and ev.query():
+            self._raise_sync(int(host[0]))
+        call('encx_lstm_sync_read', ptr(dev), stream())
+        host.copy_(dev, non_blocking=True)
+        ev.record()
+        w[3] = True
+
+    def check_sync(self):
+        """Wait for the last step's error-word copy and raise if any LSTM hand-off failed."""
+        w = self._sync
+        if w is not None and w[3]:
+            w[2].synchronize()
+            self._raise_sync(int(w[1][0]))
+
+    @staticmethod
+    def _raise_sync(n):
+        if n:
+            raise RuntimeError(f'encx: {n} persistent-LSTM hand-off failures (spin timeouts or counters off '
+                               'their count) since training started: those steps\' LSTM results are garbage '
+                               '(workgroups not co-resident? another persistent launch on the GPU?)')
 
     def _pick_train_d(self, device):
         """train_multi_gpu.py:105-110. disc_prob None = the reference's short-circuit (the flag

@@ -340,10 +340,19 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
                   int acc_x, float* ws, int64_t B, int64_t T, int64_t H, int64_t L, encx_stream_t stream);
 size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H);
 /* The persistent forward / backward (option LSTM_PERSIST) run the recurrence in ONE launch whose
- * workgroups hand frames to each other through counters with bounded spins. Returns (in *count)
- * and clears the number of spins that timed out on the current device since the last call (0 on
- * a healthy run; nonzero means a launch's results are garbage). Synchronises the device. */
+ * workgroups hand frames to each other through counters with bounded spins (option LSTM_SPIN:
+ * log2 of the bound, default about 1 s). They are used only when every workgroup of the grid can
+ * be resident at once (the kernel's occupancy times the CU count). The counters are one set per
+ * device: persistent launches must be serialised, i.e. every encx_lstm_fwd / encx_lstm_bwd of a
+ * process on one stream (or otherwise ordered). A spin that times out, or a counter that ends a
+ * launch off its expected count, is counted in a per-device error word: nonzero means a launch's
+ * results are garbage. encx_lstm_sync_errors returns (in *count) and clears it; synchronises the
+ * device. */
 int encx_lstm_sync_errors(int64_t* count);
+/* The same without a synchronisation: a one-thread kernel on `stream` adds the error word to
+ * *count (a device int32 the caller zeroed once) and clears the word. Capturable; the caller reads
+ * *count whenever convenient (e.g. an async copy to pinned memory checked a step later). */
+int encx_lstm_sync_read(int32_t* count, encx_stream_t stream);
 /* Development: the persistent kernels' per-frame clock stamps (steady clock, 100 MHz) as
  * [kernel 0 fwd / 1 bwd][workgroup < 256][frame < 128][8 points] int64, first n of them; EINVAL
  * unless the library was built with -DENCX_LSTM_TRACE (tools/lstm_trace.py). Synchronises. */
@@ -379,7 +388,10 @@ int encx_conv2d_bwd_data(const float* dy, const float* yact, const float* wp, co
  * epilogue (FeatFn's d l_feat / d ff, losses.py:53, fused instead of a grad tensor and an add):
  * dx += c * sign(feat_fake - feat_real), c = feat_g[0] * feat_scale / feat_denom[0] (feat_g NULL:
  * 1); feat_fake is this layer's input map, feat_real its real-audio counterpart. The feature
- * term is added before the xact mask: dx (+)= (d/dx + feature term) * LeakyReLU'(xact). */
+ * term is added before the xact mask: dx (+)= (d/dx + feature term) * LeakyReLU'(xact). With a
+ * feature term, xact must be NULL or feat_fake itself (the layer's input map is both the map whose
+ * LeakyReLU' masks the grad and the fake side of the feature pair; the kernels read it once):
+ * any other xact is refused (ENCX_EINVAL). */
 int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* wp, const float* xact, float* dx,
                               int accumulate, const float* feat_real, const float* feat_fake,
                               const float* feat_denom, const float* feat_g, double feat_scale,

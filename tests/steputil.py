@@ -66,14 +66,32 @@ def snapshot(tr):
     return s
 
 
-def disc_mask_hooks(disc, store):
-    """Forward hooks collecting every LeakyReLU'd discriminator map of a step (on the host), in
-    call order: the Trainer runs the discriminator on the real audio, then on the fake."""
+def disc_mask_hooks(disc, store, device='cpu', inputs=None):
+    """Forward hooks collecting every LeakyReLU'd discriminator map of a step (on `device`, the
+    host by default), in call order: the Trainer runs the discriminator on the real audio, then
+    on the fake. With `inputs` (a list) each layer's input map is collected too (check_flips)."""
     hs = []
+
+    def hook(mod, inp, out):
+        store.append(out.detach().to(device, copy=True))
+        if inputs is not None:
+            inputs.append(inp[0].detach().to(device, copy=True))
     for d in disc.discriminators:
         for layer in d.convs:
-            hs.append(layer.register_forward_hook(lambda mod, inp, out: store.append(out.detach().cpu())))
+            hs.append(layer.register_forward_hook(hook))
     return hs
+
+
+@contextlib.contextmanager
+def disc_maps(disc, device='cpu'):
+    """Collect (inputs, outputs) of every LeakyReLU'd Conv2d the discriminator runs in the block."""
+    ins, outs = [], []
+    hs = disc_mask_hooks(disc, outs, device, ins)
+    try:
+        yield ins, outs
+    finally:
+        for h in hs:
+            h.remove()
 
 
 def split_masks(store, n_disc):
@@ -99,61 +117,131 @@ def lrelu_audit(feat=None):
         O.FEAT_AUDIT = None
 
 
-def _local_max(e):
-    """max of e over each element's 3-wide neighbourhood along the last axis and, for maps of
-    4 or more dims ([B, C, T, F]), the second-to-last axis too."""
+U32 = 2.0 ** -24  # unit roundoff of fp32
+
+
+def _gamma(n):
+    """gamma_n = n u / (1 - n u): the a-priori relative bound of an n-term fp32 dot product, any
+    summation order (Higham, Accuracy and Stability of Numerical Algorithms, eq. 3.4)."""
+    return n * U32 / (1 - n * U32)
+
+
+def _layer_recompute(layer, prm, x, idx):
+    """fp64 pre-activation of `layer` (an encx NormConv2d, for its geometry) at output elements idx
+    [n, 4] = (b, co, t, f), from the fp32 input map x the HIP layer read, with the exact
+    weight-normed weights of the fp32 parameters it ran with (prm: 'weight' or 'weight_v' /
+    'weight_g', and 'bias') -> (z64, A = sum |w x| + |bias|, n_eff: the terms of the fp32 evaluation,
+    counting the roundings of the fp32 weight norm -- a sum of n squares, a sqrt, a divide and a
+    product: (n / 2 + 4) u relative on every weight -- for the normed layers)."""
     F = torch.nn.functional
-    shape = e.shape
-    x = F.max_pool1d(e.reshape(-1, 1, shape[-1]), 3, 1, 1).reshape(shape)
-    if e.dim() >= 4:
-        xt = x.transpose(-1, -2).contiguous()
-        x = F.max_pool1d(xt.reshape(-1, 1, shape[-2]), 3, 1, 1).reshape(xt.shape).transpose(-1, -2)
-    return x
+    dev = x.device
+    g = prm.get('weight_g')
+    w = prm['weight_v' if g is not None else 'weight'].detach().double().to(dev)
+    if g is not None:
+        w = O.weight_norm(w, g.detach().double().to(dev))
+    b = prm['bias'].detach().double().to(dev)
+    KT, KF = layer.kernel_size
+    st, sf = layer.stride
+    dt, df = layer.dilation
+    pt, pf = layer.padding
+    Ci = w.shape[1]
+    bb, co, t, f = idx.to(dev).unbind(1)
+    xp = F.pad(x.double(), (pf, pf, pt, pt))
+    ti = t[:, None, None] * st + (torch.arange(KT, device=dev) * dt)[None, :, None]
+    fi = f[:, None, None] * sf + (torch.arange(KF, device=dev) * df)[None, None, :]
+    patch = xp[bb[:, None, None], :, ti, fi].permute(0, 3, 1, 2)  # [n, Ci, KT, KF]
+    prod = patch * w[co]
+    n = Ci * KT * KF + 1
+    return prod.sum((1, 2, 3)) + b[co], prod.abs().sum((1, 2, 3)) + b[co].abs(), \
+        n + (0 if g is None else (n - 1) // 2 + 4)
 
 
-def check_masks(a64, a32, what):
-    """Our LeakyReLU slope masks (imposed on the oracle) against the fp64 oracle's OWN signs of
-    the same pre-activations. Per element: a sign may differ only where |z64| is within 8x that
-    element's fp32 rounding estimate, i.e. where fp32 arithmetic may legitimately land on the other
-    side of 0. The estimate is the plain fp32 oracle's error |z32 - z64| at the element and its
-    neighbours (max over 3 along f and t), floored at the map's median error. One run's error at a
-    single element is one draw and can be near 0 by luck: with the element's own draw only, a
-    weight-grad summation-order change put one feature-L1 element of the 48 kHz step at 4.4x, and
-    a later one another at 8.8x (round 5). A sign error in a HIP epilogue lands far from 0 and
-    fails here. Reports the flips per map. a64 / a32: the lrelu_audit logs of the fp64 and fp32
-    oracle runs."""
-    assert a64 and len(a64) == len(a32), (what, len(a64), len(a32))
-    flips = total = 0
-    worst = 0.0
-    per_map = []
-    for i, ((z64, m), (z32, _)) in enumerate(zip(a64, a32)):
-        z64 = z64.double()
-        bad = m != (z64 > 0) if m.dtype == torch.bool else m.double() != torch.sign(z64)
-        n = int(bad.sum())
-        if n:
-            err = (z32.double() - z64).abs()
-            nz = err[z64 != 0]
-            med = float(nz.median()) if nz.numel() else 0.0
-            bound = 8 * _local_max(err)[bad].clamp_min(med)
-            mag = z64.abs()[bad]
-            ratio = mag / bound.clamp_min(1e-300)
-            assert bool((mag <= bound).all()), (what, f'map {i}: slope mask off the fp64 sign beyond that '
-                                                'element\'s rounding', float(ratio.max()), n)
-            worst = max(worst, float(ratio.max()))
-            per_map.append(f'{i}:{n}/{m.numel()}')
-        flips += n
-        total += m.numel()
-    print(f'{what}: {flips} of {total} imposed signs differ from the fp64 signs, each within 8x its '
-          f'own rounding estimate (worst at {worst:.2f} of its bound); per map: {" ".join(per_map) or "none"}')
-    return flips
+def _hip_preact(y, idx):
+    """The HIP layer's fp32 pre-activation at idx from its LeakyReLU(0.2) output map y (z = y
+    where y > 0, else y / 0.2f: exact to one rounding, u |z|)."""
+    yv = y[tuple(idx.to(y.device).unbind(1))].double()
+    return torch.where(yv > 0, yv, yv / float(np.float32(0.2)))
 
 
-def oracle_step(snap, x, cfg, bandwidth, weights, dtype, disc_masks=None):
-    """O.train_step from the snapshot in `dtype` -> (out, params, codebooks, disc params)."""
-    p = {k: v.to(dtype) for k, v in snap['gen']['p'].items()}
-    adam = {k: {'step': snap['gen']['step'], 'm': snap['gen']['m'][k].to(dtype),
-                'v': snap['gen']['v'][k].to(dtype)} for k in p}
-    cbs = [{k: v.to(dtype) for k, v in cb.items()} for cb in snap['cbs']]
+def check_flips(disc, params, maps_in, maps_out, a64, f64, what):
+    """The a-priori audit of the signs the oracle takes from our maps (LeakyReLU slopes, oracle
+    _lrelu; feature-matching L1 signs, oracle _l1_feat). At every element where our sign differs
+    from the fp64 oracle's own, the HIP layer that produced the map is re-evaluated in fp64 from
+    its OWN fp32 input map and the exact weight norm of its fp32 parameters, and its pre-activation
+    must satisfy |z_hip - z64| <= gamma_n * sum|w x| + u |z_hip| (n the dot product's terms): the
+    HIP arithmetic at that element is fp32 rounding, by a bound fixed before any run, not
+    estimated from one. A sign error in a kernel's epilogue (|z_hip - z64| = 2 |z|) fails it
+    unless |z| itself lies within rounding of 0. Feature-sign flips check both maps of the pair.
+    The imposed slope masks must be the maps' own signs. A flip whose fp64 recompute keeps our
+    sign is inherited from the layer's input (the HIP and oracle inputs differ by the rounding
+    upstream); the report counts those.
+    disc: the encx MultiScaleSTFTDiscriminator; params: name -> its fp32 parameters as the maps
+    were computed (state-dict names); maps_in / maps_out: the input and output maps of
+    its LeakyReLU'd Conv2d layers in call order (real audio, then fake: disc_maps), sliced to
+    the batch items the oracle ran on; a64: the fp64 oracle's lrelu_audit log (its first
+    len(maps_out) entries are those layers, in the same order); f64: its feature audit log or None."""
+    nd = len(disc.discriminators)
+    per = len(disc.discriminators[0].convs)
+    half = nd * per
+    nmaps = len(maps_out)  # both sides (real, fake), or one side (no feature signs then)
+    assert nmaps == len(maps_in) and nmaps in (half, 2 * half) and len(a64) >= nmaps, (what, nmaps, len(a64))
+    assert f64 is None or nmaps == 2 * half, what
+    layer_of = lambda i: disc.discriminators[(i % half) // per].convs[i % per]
+
+    def prm_of(i):
+        pre = f'discriminators.{(i % half) // per}.convs.{i % per}.conv.'
+        return {k[len(pre):]: v for k, v in params.items() if k.startswith(pre)}
+    todo = {}  # map index -> element indices to audit
+
+    def add(i, idx):
+        todo[i] = torch.cat([todo[i], idx]) if i in todo else idx
+    n_slope = n_feat = 0
+    for i in range(nmaps):
+        z64, m = a64[i]
+        mo = maps_out[i] > 0
+        dev = z64.device
+        assert torch.equal(m.to(dev), mo.to(dev)), (what, f'map {i}: the imposed slope mask is not the map\'s sign')
+        idx = torch.nonzero(m.to(dev) != (z64 > 0))
+        n_slope += idx.shape[0]
+        if idx.shape[0]:
+            add(i, idx)
+    if f64 is not None:
+        for j, (d64, sg) in enumerate(f64[:half]):
+            idx = torch.nonzero(sg.to(d64.device) != torch.sign(d64))
+            n_feat += idx.shape[0]
+            if idx.shape[0]:
+                add(j, idx)
+                add(half + j, idx)
+    worst, inherited, checked = 0.0, 0, 0
+    for i, idx in todo.items():
+        idx = torch.unique(idx, dim=0)
+        layer = layer_of(i)
+        z64, A, n = _layer_recompute(layer, prm_of(i), maps_in[i], idx)
+        zh = _hip_preact(maps_out[i], idx).to(z64.device)
+        bound = _gamma(n) * A + U32 * zh.abs()
+        dev = (zh - z64).abs()
+        ratio = dev / bound
+        bad = ratio > 1
+        assert not bool(bad.any()), (what, f'map {i}: {int(bad.sum())} of {idx.shape[0]} flipped elements off '
+                                     'their fp64 recompute beyond the a-priori fp32 bound', float(ratio.max()))
+        worst = max(worst, float(ratio.max()))
+        inherited += int(((zh > 0) == (z64 > 0)).sum())
+        checked += idx.shape[0]
+    print(f'{what}: {n_slope} slope and {n_feat} feature-sign flips against the fp64 oracle; {checked} map '
+          f'elements re-evaluated in fp64 from the HIP inputs, each within the a-priori fp32 bound (worst at '
+          f'{worst:.3f} of it; {inherited} keep our sign in the recompute: inherited from the layer input)')
+    return n_slope + n_feat
+
+
+def oracle_step(snap, x, cfg, bandwidth, weights, dtype, disc_masks=None, device='cpu'):
+    """O.train_step from the snapshot in `dtype` on `device` -> (out, params, codebooks, disc
+    params). device: the host (default), or the GPU for full-size steps: the oracle's torch ops
+    then run on the GPU (test-only checker) with MIOpen off, so its convs are torch's own
+    im2col + GEMM in plain fp32 / fp64."""
+    p = {k: v.to(device, dtype) for k, v in snap['gen']['p'].items()}
+    adam = {k: {'step': snap['gen']['step'], 'm': snap['gen']['m'][k].to(device, dtype),
+                'v': snap['gen']['v'][k].to(device, dtype)} for k in p}
+    cbs = [{k: v.to(device, dtype) for k, v in cb.items()} for cb in snap['cbs']]
     bal = O.Balancer(weights)
     if snap['bal'] is not None:
         for name, t, f in zip(*snap['bal']):
@@ -161,16 +249,20 @@ def oracle_step(snap, x, cfg, bandwidth, weights, dtype, disc_masks=None):
     dp = dadam = dlr = None
     if 'disc' in snap:
         d = snap['disc']
-        dp = {k: v.to(dtype) for k, v in d['p'].items()}
-        dadam = {k: {'step': d['step'], 'm': d['m'][k].to(dtype), 'v': d['v'][k].to(dtype)} for k in dp}
+        dp = {k: v.to(device, dtype) for k, v in d['p'].items()}
+        dadam = {k: {'step': d['step'], 'm': d['m'][k].to(device, dtype), 'v': d['v'][k].to(device, dtype)}
+                 for k in dp}
         dlr = d['lr']
     nt = torch.get_num_threads()
     torch.set_num_threads(ORACLE_THREADS)
+    cudnn = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False
     try:
-        out = O.train_step(x.detach().cpu().to(dtype), p, cbs, cfg, bandwidth, bal, adam, snap['gen']['lr'],
+        out = O.train_step(x.detach().to(device, dtype), p, cbs, cfg, bandwidth, bal, adam, snap['gen']['lr'],
                            disc_p=dp, disc_adam_state=dadam, disc_lr=dlr, disc_masks=disc_masks)
     finally:
         torch.set_num_threads(nt)
+        torch.backends.cudnn.enabled = cudnn
     return out, p, cbs, dp
 
 
@@ -201,14 +293,14 @@ def _check_opt(tag, mod, opt, g64, g32, p64, lr, table, floor=1e-6):
     table.extend((f'{tag}:{k}', e, e32, b) for k, e, e32, b in _grad_bounds(errs, floor))
     decided_n = total_n = 0
     for k, (p, g, _, _) in views.items():
-        gd = g64[k].double()
-        e_own = (g32[k].double() - gd).abs()
+        gd = g64[k].double().cpu()
+        e_own = (g32[k].double().cpu() - gd).abs()
         e_mine = (g.detach().double().cpu() - gd).abs()
         decided = (gd.abs() > 4 * e_own) & (gd.abs() > 1e-12 * float(gd.abs().max()))
         decided_n += int(decided.sum())
         total_n += gd.numel()
         tol = 4 * lr * torch.maximum(e_mine, e_own) / gd.abs().clamp_min(1e-30) + 2e-6
-        diff = (p.detach().double().cpu() - p64[k].double()).abs()
+        diff = (p.detach().double().cpu() - p64[k].double().cpu()).abs()
         bad = decided & (diff > tol)
         assert not bool(bad.any()), (tag, k, float(diff[decided].max()), int(bad.sum()))
     assert decided_n >= 0.97 * total_n, (tag, decided_n, total_n)
@@ -233,13 +325,14 @@ def check_grads(mine, g64, g32, what, floor=1e-6):
     return table
 
 
-def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6):
+def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device='cpu'):
     """tr.step(x) against the oracle's step from the same state; returns (out, table). floor:
-    the smallest per-tensor grad bound (relative to the tensor's fp64 magnitude)."""
+    the smallest per-tensor grad bound (relative to the tensor's fp64 magnitude). device: where
+    the oracle runs (oracle_step)."""
     snap = snapshot(tr)
-    store, hooks = [], []
+    store, ins, hooks = [], [], []
     if tr.disc is not None:
-        hooks = disc_mask_hooks(tr.disc, store)
+        hooks = disc_mask_hooks(tr.disc, store, device, ins)
     try:
         out = tr.step(x)
         torch.cuda.synchronize()
@@ -250,15 +343,15 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6):
     # pre-activation within rounding of 0 may take either slope in fp32, a discrete outcome that
     # no rounding bound covers
     masks = split_masks(store, len(tr.disc.discriminators)) if tr.disc is not None else None
-    f64, f32 = [], []
+    f64 = []
     with lrelu_audit(f64) as a64:
-        o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks)
-    with lrelu_audit(f32) as a32:
-        o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks)
+        o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks, device)
+    o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks, device)
     if masks is not None:
-        check_masks(a64, a32, 'step slope masks')
-        if 'l_feat' in weights:
-            check_masks(f64, f32, 'step feature-L1 signs')
+        # the discriminator's weights as its maps were computed: the pre-step snapshot
+        check_flips(tr.disc, snap['disc']['p'], ins, store, a64, f64 if 'l_feat' in weights else None,
+                    'step sign audit')
+    del ins
     table = []
     _check_opt('gen', tr.model, tr.opt, o64['grads'], o32['grads'], p64, snap['gen']['lr'], table, floor)
     if tr.disc is not None and 'disc_grads' in o64:

@@ -205,8 +205,10 @@ def test_stereo_disc_input_grads_vs_fp64():
     m.train()
     y, _, _ = m(x)
     yd = y.detach().requires_grad_()
-    _, fr = disc(x)
-    lf_, ff = disc(yd)
+    from steputil import disc_maps
+    with disc_maps(disc, DEV) as (ins, outs):
+        _, fr = disc(x)
+        lf_, ff = disc(yd)
     losses = total_loss(fr, lf_, ff, x, yd, 48000)
     names = ('l_t', 'l_f', 'l_g', 'l_feat')
     mine = {k: torch.autograd.grad(losses[k], [yd], retain_graph=True)[0] for k in names}
@@ -215,7 +217,7 @@ def test_stereo_disc_input_grads_vs_fp64():
     mf = [[fm.detach().cpu() > 0 for fm in fms] for fms in ff]
     # the feature L1's derivative signs from our maps too (oracle._l1_feat)
     fs = [[torch.sign(b.detach().cpu() - a.detach().cpu()) for a, b in zip(ra, fa)] for ra, fa in zip(fr, ff)]
-    from steputil import lrelu_audit, check_masks
+    from steputil import lrelu_audit, check_flips
     ref, audit, faudit = {}, {}, {}
     for dt in (torch.float64, torch.float32):
         x0 = x.detach().cpu().to(dt)
@@ -227,6 +229,6 @@ def test_stereo_disc_input_grads_vs_fp64():
             lf_o, ff_o = O.msstft_forward(y0, pd, masks=mf)
             lo = O.total_loss(fr_o, lf_o, ff_o, x0, y0, 48000, feat_signs=fs)
         ref[dt] = {k: torch.autograd.grad(lo[k].sum(), [y0], retain_graph=True)[0] for k in names}
-    check_masks(audit[torch.float64], audit[torch.float32], '48 kHz stereo slope masks')
-    check_masks(faudit[torch.float64], faudit[torch.float32], '48 kHz stereo feature-L1 signs')
+    check_flips(disc, dict(disc.named_parameters()), ins, outs, audit[torch.float64], faudit[torch.float64],
+                '48 kHz stereo slope masks and feature-L1 signs')
     check_grads(mine, ref[torch.float64], ref[torch.float32], '48 kHz stereo GAN input grads')

@@ -390,5 +390,10 @@ def test_feat_code_epilogue_bit_identical(li, T2, Fi, family):
                          ptr(ff), ptr(den), ptr(fg), 3.0, ptr(c), *dims, stream())
                     res.append(dx)
                 assert torch.equal(res[0], res[1]), (xact is not None, acc, float((res[0] - res[1]).abs().max()))
+        # a LeakyReLU map other than the fake map is refused (the epilogues read one map for both)
+        other = ff.clone()
+        rc = lib.encx_conv2d_bwd_data_feat(ptr(dy), ptr(y), ptr(wp), ptr(other), ptr(dx), 0, ptr(fr), ptr(ff),
+                                           ptr(den), ptr(fg), 3.0, None, *dims, stream())
+        assert rc != 0
     finally:
         lib.encx_conv2d_select(prev)

@@ -466,6 +466,61 @@ def test_lstm_persistent_graph_replays(form):
                 assert torch.equal(a, b), (rnd, name)
 
 
+def test_lstm_handoff_failure_is_loud():
+    """A persistent-LSTM hand-off that fails (option LSTM_FAULT: one workgroup of each launch
+    never publishes; LSTM_SPIN 6: every poll gives up after 64 tries) is reported: directly
+    through encx_lstm_sync_errors, through the capturable encx_lstm_sync_read, and by the
+    Trainer -- check_sync() raises, and so does the next step() once the failed step's
+    error-word copy has landed. Without the fault the same calls report 0."""
+    import ctypes
+    from encx._lib import call, ptr, option, lib, lstm_sync_errors
+    from encx.model import EncodecModel
+    from encx.train import Trainer
+    B, H, Tn, L = 4, 512, 75, 2
+    gen = torch.Generator().manual_seed(12)
+    k = H ** -0.5
+    f = lambda *s: ((torch.rand(*s, generator=gen) * 2 - 1) * k).to(DEV)
+    e = lambda n: torch.empty(n, device=DEV)
+    wcat, wcatT, bsum = e(L * 8 * H * H), e(L * 8 * H * H), e(L * 4 * H)
+    st = torch.cuda.current_stream().cuda_stream
+    for l in range(L):
+        call('encx_lstm_pack', *(ptr(f(*s)) for s in [(4 * H, H), (4 * H, H), (4 * H,), (4 * H,)]),
+             ptr(wcat), ptr(wcatT), ptr(bsum), H, l, st)
+    x, dout = torch.randn(B, H, Tn, device=DEV), torch.randn(B, H, Tn, device=DEV)
+    xt, Y, Cs, Gs, out, DA, dx = (e(B * Tn * H), e(L * B * Tn * H), e(L * B * Tn * H), e(L * B * Tn * 4 * H),
+                                  torch.empty_like(x), e(L * B * Tn * 4 * H), torch.empty_like(x))
+    ws = torch.empty(lib.encx_lstm_bwd_workspace(B, Tn, H, L), dtype=torch.uint8, device=DEV)
+    assert lstm_sync_errors() == 0
+    for direction in ('fwd', 'bwd'):
+        for fault in (0, 1):
+            with option(LSTM_PERSIST=1, LSTM_SPIN=6, LSTM_FAULT=fault if direction == 'fwd' else 0):
+                call('encx_lstm_fwd', ptr(x), ptr(wcat), ptr(bsum), ptr(xt), ptr(Y), ptr(Cs), ptr(Gs), ptr(out), 1,
+                     B, Tn, H, L, st)
+            with option(LSTM_PERSIST=1, LSTM_SPIN=6, LSTM_FAULT=fault if direction == 'bwd' else 0):
+                call('encx_lstm_bwd', ptr(dout), ptr(wcatT), ptr(Cs), ptr(Gs), ptr(DA), ptr(dx), 0, ptr(ws),
+                     B, Tn, H, L, st)
+            cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+            call('encx_lstm_sync_read', ptr(cnt), st)
+            torch.cuda.synchronize()
+            assert (int(cnt) > 0) == bool(fault), (direction, fault, int(cnt))
+            assert lstm_sync_errors() == 0  # the read cleared the word
+    # the same failure inside a training step: the Trainer raises
+    model = EncodecModel._get_model([1.5], 24000, 1, causal=True, model_norm='weight_norm',
+                                    audio_normalize=True).to(DEV)
+    tr = Trainer(model, None, lr=3e-4, scheduler=False)
+    xb = torch.randn(B, 1, 24000, device=DEV) * 0.1
+    tr.step(xb)
+    tr.check_sync()  # healthy
+    with option(LSTM_SPIN=6, LSTM_FAULT=1):
+        tr.step(xb)
+    with pytest.raises(RuntimeError, match='hand-off'):
+        tr.check_sync()
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match='hand-off'):
+        tr.step(xb)  # the failed step's copy has landed: the next step refuses to go on
+    assert lstm_sync_errors() == 0
+
+
 # --------------------------------------------------------------------------- fused residual block
 @pytest.mark.parametrize('C,T,B', [(32, 2048, 3), (32, 24000, 2), (64, 12000, 2), (64, 3001, 3), (32, 2113, 1)])
 def test_fused_resblock_vs_torch_fp64(C, T, B):

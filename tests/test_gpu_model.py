@@ -229,8 +229,10 @@ def test_config3_b32_step_and_input_grads_vs_fp64():
     m.train()
     y, _, _ = m(x)
     yd = y.detach().requires_grad_()
+    from steputil import disc_maps
     lr_, fr = disc(x)
-    lf_, ff = disc(yd)
+    with disc_maps(disc, DEV) as (ins, outs):
+        lf_, ff = disc(yd)
     losses = total_loss(fr, lf_, ff, x, yd, 24000)
     mine = {k: torch.autograd.grad(losses[k], [yd], retain_graph=True)[0][0] for k in ('l_t', 'l_f', 'l_g')}
     dp = {k: v.detach().cpu() for k, v in disc.state_dict().items() if not k.endswith('spec_transform.window')}
@@ -238,7 +240,7 @@ def test_config3_b32_step_and_input_grads_vs_fp64():
     # take either slope in fp32: a discrete, legitimate outcome that a rounding bound cannot
     # cover; oracle._lrelu), so the comparison measures rounding only
     masks = [[fm[:1].detach().cpu() > 0 for fm in fms] for fms in ff]
-    from steputil import lrelu_audit, check_masks
+    from steputil import lrelu_audit, check_flips
     ref, audit = {}, {}
     for dt in (torch.float64, torch.float32):
         x0 = x[:1].detach().cpu().to(dt)
@@ -249,5 +251,6 @@ def test_config3_b32_step_and_input_grads_vs_fp64():
         ls = {'l_t': O.loss_t(x0, y0), 'l_f': O.loss_f(x0, y0, 24000),
               'l_g': sum(torch.relu(1 - l).mean() for l in lg) / len(lg) / len(lg)}
         ref[dt] = {k: torch.autograd.grad(l, [y0], retain_graph=True)[0][0] / 32 for k, l in ls.items()}
-    check_masks(audit[torch.float64], audit[torch.float32], 'config-3 B32 clip-0 slope masks')
+    check_flips(disc, dict(disc.named_parameters()), [t[:1] for t in ins], [t[:1] for t in outs],
+                audit[torch.float64], None, 'config-3 B32 clip-0 slope masks')
     check_grads(mine, ref[torch.float64], ref[torch.float32], 'config-3 B32 input grads of clip 0')

@@ -183,45 +183,58 @@ def test_oracle_disc_fixture():
     close(x.grad, d['dx'], rtol=1e-3, atol=1e-5)
 
 
-def test_slope_mask_audit_flags_only_real_sign_errors():
-    """steputil.check_masks: masks taken from a fp32 evaluation pass (flips only within
-    rounding of 0); one mask bit flipped at the map's largest |z| is caught."""
+def test_sign_audit_flags_only_real_sign_errors():
+    """steputil.check_flips, the a-priori sign audit: with the maps of a fp32 evaluation standing
+    in for the HIP maps (their signs imposed on the fp64 oracle), every flipped element's fp32
+    pre-activation lies within gamma_n sum|w x| of its fp64 recompute from the same inputs and the
+    audit passes; a sign error planted at one element (the map's largest |z| negated: what a wrong
+    epilogue does) fails it, and so does an imposed mask that is not the map's own sign."""
     import pytest
-    from steputil import lrelu_audit, check_masks
+    from encx.msstftd import MultiScaleSTFTDiscriminator
+    from steputil import lrelu_audit, check_flips
     d = load('g5_disc.npz')
     p = disc_state(51)
     x = T(d['x'])[:1, :, :6000]
-    # the fp32 run's own signs as the imposed masks (what the GPU run's maps provide)
-    _, fm32 = O.msstft_forward(x, p)
-    masks = [[f > 0 for f in fms] for fms in fm32]
-    logs = {}
-    for dt in (torch.float64, torch.float32):
-        with lrelu_audit() as logs[dt]:
-            O.msstft_forward(x.to(dt), {k: v.to(dt) for k, v in p.items()}, masks=masks)
-    check_masks(logs[torch.float64], logs[torch.float32], 'fp32 masks')
-    z64, m = logs[torch.float64][3]
-    i = int(z64.abs().reshape(-1).argmax())
-    bad = m.clone().reshape(-1)
-    bad[i] = ~bad[i]
-    logs[torch.float64][3] = (z64, bad.view_as(m))
-    with pytest.raises(AssertionError):
-        check_masks(logs[torch.float64], logs[torch.float32], 'one flipped slope')
-    # the per-element rule: a flip at an element with little rounding error of its own is caught
-    # even where |z64| is below 4x the map's LARGEST error (the map-wide rule let those pass) and
-    # above 8x its own
-    logs[torch.float64][3] = (z64, m)
-    for k, ((za64, mk), (za32, _)) in enumerate(zip(logs[torch.float64], logs[torch.float32])):
-        za, err = za64.double().reshape(-1).abs(), (za32.double() - za64.double()).reshape(-1).abs()
-        cand = (za < 4 * float(err.max())) & (za > 8.5 * err.clamp_min(float(err[za > 0].median())))
-        if bool(cand.any()):
-            break
-    assert bool(cand.any())
-    j = int(torch.nonzero(cand)[0])
-    bad = mk.clone().reshape(-1)
-    bad[j] = ~bad[j]
-    logs[torch.float64][k] = (za64, bad.view_as(mk))
-    with pytest.raises(AssertionError, match='rounding'):
-        check_masks(logs[torch.float64], logs[torch.float32], 'one flip within the map-wide bound')
+    disc = MultiScaleSTFTDiscriminator(filters=32)  # the layer geometry (CPU module, no kernels)
+    ins, outs = [], []
+    for k, (n, h, w) in enumerate(zip(O.DISC_CFG['n_ffts'], O.DISC_CFG['hops'], O.DISC_CFG['wins'])):
+        z = O.spectrogram(x, n, h, w)
+        z = torch.cat([z.real, z.imag], dim=1).permute(0, 1, 3, 2)
+        _, fm = O.disc_stft_forward(x, p, f'discriminators.{k}', n, h, w)
+        ins += [z] + fm[:-1]
+        outs += fm
+
+    def audit(maps):
+        masks = [[maps[5 * k + j] > 0 for j in range(5)] for k in range(3)]
+        with lrelu_audit() as a64:
+            O.msstft_forward(x.double(), {k: v.double() for k, v in p.items()}, masks=masks)
+        return a64
+    assert check_flips(disc, p, ins, outs, audit(outs), None, 'fp32 maps') >= 0
+    y = outs[3]
+    zh = torch.where(y > 0, y, y / 0.2)
+    # a flip within rounding of 0 (the element of smallest nonzero |z|, negated) is legitimate
+    j = int(torch.where(zh != 0, zh.abs(), torch.full_like(zh, float('inf'))).reshape(-1).argmin())
+    znear = zh.clone().reshape(-1)
+    znear[j] = -znear[j]
+    znear = znear.view_as(zh)
+    near = list(outs)
+    near[3] = torch.where(znear > 0, znear, 0.2 * znear)
+    assert check_flips(disc, p, ins, near, audit(near), None, 'one flip within rounding of 0') >= 1
+    i = int(zh.abs().reshape(-1).argmax())
+    zbad = zh.clone().reshape(-1)
+    zbad[i] = -zbad[i]
+    zbad = zbad.view_as(zh)
+    bad = list(outs)
+    bad[3] = torch.where(zbad > 0, zbad, 0.2 * zbad)
+    with pytest.raises(AssertionError, match='a-priori'):
+        check_flips(disc, p, ins, bad, audit(bad), None, 'one planted sign error')
+    a64 = audit(outs)
+    z64, m = a64[3]
+    mb = m.clone().reshape(-1)
+    mb[i] = ~mb[i]
+    a64[3] = (z64, mb.view_as(m))
+    with pytest.raises(AssertionError, match='sign'):
+        check_flips(disc, p, ins, outs, a64, None, 'a mask that is not the map\'s sign')
 
 
 # --------------------------------------------------------------------------- G6 balancer
