@@ -125,6 +125,24 @@ ENCX_DEV float sum_strided(const float* p, int n, int64_t stride) {
     return acc;
 }
 
+// the same sum accumulated in fp64 (one rounding at the end): the weight-grad slab reduces whose
+// sums run over up to ~1500 slabs of fp32 partials
+ENCX_DEV double sum_strided_d(const float* p, int n, int64_t stride) {
+    double acc = 0.0;
+    for (int s0 = 0; s0 < n; s0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int s = s0 + q;
+            const float t = p[(int64_t)(s < n ? s : 0) * stride];
+            v[q] = s < n ? t : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += (double)v[q];
+    }
+    return acc;
+}
+
 // Slab reduction by a 256-thread block: lane l of wave w sums splits s = w, w + 4, ... of output
 // i (= the block's 64 consecutive outputs, one per lane: every wave load is one coalesced 256-byte
 // row segment), then wave 0 adds the 4 partials in order w = 0..3. Deterministic; the result is
@@ -136,6 +154,15 @@ ENCX_DEV float slab_sum_256(const float* p, int S, int64_t stride, bool valid, f
     red[w * 64 + lane] = v;
     __syncthreads();
     return ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+}
+// slab_sum_256 in fp64 (red: __shared__ double[4][64]); the result rounded once to fp32
+ENCX_DEV float slab_sum_256_d(const float* p, int S, int64_t stride, bool valid, double* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double v = 0.0;
+    if (valid && w < S) v = sum_strided_d(p + (int64_t)w * stride, (S - w + 3) >> 2, 4 * stride);
+    red[w * 64 + lane] = v;
+    __syncthreads();
+    return (float)(((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane]);
 }
 
 // XCD-aware tile order. The dispatcher deals workgroups to the 8 XCDs round-robin by linear id,
@@ -187,6 +214,10 @@ enum EncxOpt {
     OPT_CONV_CK,       // conv1d fwd / bwd-data: reduction elements (channels x taps) per LDS chunk
     OPT_CONV_SPLIT,    // conv1d fwd / bwd-data: split-K until this many workgroups
     OPT_CONV_WG_SPLIT, // conv1d weight grad: split the positions until this many workgroups
+    OPT_CONV2,         // conv1d forward v2 (LDS-DMA double-buffered staging) where it applies
+    OPT_CONV2_TILE,    // its tile: 0 auto, 1 128x128, 2 128x64, 3 64x128, 4 64x64 (BM x BN)
+    OPT_CONV2_RED,     // its largest reduction (channels x taps) per chunk
+    OPT_CONV2_KS,      // its channel splits (0: planned)
     OPT_LSTM_SPIN,     // persistent LSTM: log2 of every poll's spin bound (0: 20, about 1 s)
     OPT_LSTM_FAULT,    // persistent LSTM, tests only: one workgroup never publishes (its consumers time out)
     OPT_COUNT

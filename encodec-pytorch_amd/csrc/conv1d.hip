@@ -1509,7 +1509,496 @@ static void pw_wgrad_run(const float* dy, const float* x, float* dw, float* db, 
                        AN, p.S, acc_w, ws + (int64_t)p.S * AN, db, (int)M, acc_b);
 }
 
+// ------------------------------------------------------------------------- conv v2 main loop
+// Round 6 (option CONV2): the implicit-GEMM forward and polyphase kernels rebuilt around one
+// software-pipelined main loop. Per channel chunk the operands live in TWO LDS buffers: while the
+// MFMAs run on chunk c, the weight rows of chunk c + 1 stream into the other buffer by LDS-DMA
+// (global_load_lds_dwordx4: no VGPRs, one instruction per 64 quads) and its input window streams
+// into registers (a few quads per thread), which are written to LDS -- with the pre-activation
+// ELU applied once per element and the pad positions patched -- after the chunk's MFMAs: one
+// barrier per chunk and no exposed memory round trip (the round-5 kernels staged synchronously
+// between two barriers: MFMA busy 0.30-0.42). The window keeps its global order (stride-S taps
+// read S words apart: at most 8-way bank conflicts, cheap beside the fp32 MFMA's 64 cycles). The
+// reduction runs per lane half over half the chunk's channels (k slot 0: channels [0, CK/2), slot
+// 1: [CK/2, CK)), so every operand address is a lane base plus a compile-time offset.
+enum { EPI2_ELU = 16 };
+// ELU without a branch: expm1 by its Taylor series to x^10 on [-1, 0] (truncation < 3e-8
+// relative), exp2 - 1 below (|result| > 0.63, a few ulp); ocml's expm1f branches per element
+ENCX_DEV float elu_nb(float x) {
+    const float n = fminf(x, 0.f);
+    float p = 1.f / 3628800.f;
+    p = fmaf(p, n, 1.f / 362880.f);
+    p = fmaf(p, n, 1.f / 40320.f);
+    p = fmaf(p, n, 1.f / 5040.f);
+    p = fmaf(p, n, 1.f / 720.f);
+    p = fmaf(p, n, 1.f / 120.f);
+    p = fmaf(p, n, 1.f / 24.f);
+    p = fmaf(p, n, 1.f / 6.f);
+    p = fmaf(p, n, 0.5f);
+    p = fmaf(p * n, n, n);
+    const float e = __builtin_amdgcn_exp2f(n * 1.44269504088896341f) - 1.f;
+    return x > 0.f ? x : (n >= -1.f ? p : e);
+}
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void glb_void_t;
+ENCX_DEV void glds16(const float* src, float* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+constexpr int C2X_MAXQ = 4;  // input-window quads per thread per chunk (registers in flight)
+template <int BN, int K, int S> struct C1Geo {
+    static constexpr int XW = ((BN - 1) * S + K + 3 + 3) & ~3;  // window positions per channel row
+    static constexpr int XQ = XW / 4;
+};
+static size_t c1_lds(int XW, int CK, int K, int BM) {
+    return (size_t)2 * (((CK * XW + 3) & ~3) + ((CK * K * BM + 255) & ~255)) * sizeof(float);
+}
+
+// The operand geometry of one tile: input rows xrow(c, cl) = xb + (cbeg + c CK + cl) Tin, window
+// [ab, ab + XW) (ab 4-aligned; positions outside [0, Tin) come from pad_src(p + pl, pl, Tin, e,
+// mode)), weight rows (cl, k) of chunk c at wsrc + ((c CK + cl) K + k) wstride, BM floats each.
+// Tap k of output column n reads window position n S + k + woff (REV: tap K - 1 - k, the
+// polyphase form's in[u - q]).
+struct C1Tile {
+    const float* xb;
+    int Tin, ab, woff, pl, e, mode;
+    const float* wsrc;
+    int wstride, CK, nch;
+};
+template <int BM, int BN, int WM, int K, int S, bool REV, bool ELU>
+ENCX_DEV void c1_mainloop(f32x16 (&acc)[BM / WM / 32][BN / (4 / WM) / 32], const C1Tile& g) {
+    constexpr int WN = 4 / WM, TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int XW = C1Geo<BN, K, S>::XW, XQ = C1Geo<BN, K, S>::XQ;
+    extern __shared__ float smem[];
+    const int CK = g.CK, CKH = CK >> 1, Tin = g.Tin;
+    const int xsz = (CK * XW + 3) & ~3, bsz = xsz + ((CK * K * BM + 255) & ~255);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int nxq = CK * XQ, nwq = CK * K * (BM / 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    f32x4 rx[C2X_MAXQ];
+    auto load_x = [&](int c) {
+        const float* xc = g.xb + (int64_t)(c * CK) * Tin;
+#pragma unroll
+        for (int e = 0; e < C2X_MAXQ; ++e) {
+            const int q = tid + NT * e;
+            const int row = q / XQ, p = g.ab + 4 * (q - row * XQ);
+            const bool ok = q < nxq && p >= 0 && p + 4 <= Tin;
+            rx[e] = *(const f32x4*)(xc + (ok ? (int64_t)row * Tin + p : 0));
+        }
+    };
+    auto store_x = [&](int c, float* xs) {
+        const float* xc = g.xb + (int64_t)(c * CK) * Tin;
+#pragma unroll
+        for (int e = 0; e < C2X_MAXQ; ++e) {
+            const int q = tid + NT * e;
+            if (q < nxq) {
+                const int row = q / XQ, p = g.ab + 4 * (q - row * XQ);
+                f32x4 v = rx[e];
+                if (p < 0 || p + 4 > Tin) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = pad_src(p + i + g.pl, g.pl, Tin, g.e, g.mode);
+                        v[i] = m >= 0 ? xc[(int64_t)row * Tin + m] : 0.f;
+                    }
+                }
+                if (ELU) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[i] = elu_nb(v[i]);
+                }
+                *(f32x4*)(xs + 4 * q) = v;
+            }
+        }
+    };
+    auto stage_w = [&](int c, float* ws) {
+        const float* wc = g.wsrc + (int64_t)(c * CK) * K * g.wstride;
+        for (int q0 = wave * 64; q0 < nwq; q0 += NT) {
+            const int q = q0 + lane;
+            const int row = q / (BM / 4), c4 = q - row * (BM / 4);
+            glds16(wc + (q < nwq ? (int64_t)row * g.wstride + 4 * c4 : 0), ws + 4 * q0);
+        }
+    };
+    if (g.nch <= 0) return;
+    load_x(0);
+    stage_w(0, smem + xsz);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_x(0, smem);
+    __syncthreads();
+    for (int c = 0; c < g.nch; ++c) {
+        float* cur = smem + (c & 1) * bsz;
+        float* nxt = smem + ((c + 1) & 1) * bsz;
+        const bool more = c + 1 < g.nch;
+        if (more) {
+            stage_w(c + 1, nxt + xsz);
+            load_x(c + 1);
+        }
+        const float* xs = cur + h * CKH * XW + g.woff + (wn0 + l32) * S;
+        const float* ws = cur + xsz + h * CKH * K * BM + wm0 + l32;
+        for (int cl = 0; cl < CKH; ++cl) {
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk) {
+                float av[TM], bv[TN];
+                const int wk = REV ? K - 1 - kk : kk;
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = ws[(cl * K + wk) * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = xs[cl * XW + kk + j * 32 * S];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+            }
+        }
+        if (more) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            store_x(c + 1, nxt);
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------- conv forward, v2
+template <int BM, int BN, int WM, int K, int S, int EPI>
+__global__ __launch_bounds__(NT) void conv_fwd2_kernel(FwdArgs a) {
+    constexpr int WN = 4 / WM, TM = BM / WM / 32, TN = BN / WN / 32;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    // tile order: co block fastest (the blocks of one (b, t) tile share its x window), XCD-remapped
+    const int nco = a.Cout / BM, ntt = (a.Tout + BN - 1) / BN;
+    int id = xcd_linear_id();
+    const int cb = id % nco;
+    id /= nco;
+    const int tt = id % ntt;
+    id /= ntt;
+    const int ks = id % a.KS, b = id / a.KS;
+    const int co0 = cb * BM, t0 = tt * BN;
+    const int cbeg = ks * a.cps, cend = min(a.Cin, cbeg + a.cps);
+    const int wb = t0 * S - a.pl;
+    C1Tile g;
+    g.xb = a.x + ((int64_t)b * a.Cin + cbeg) * a.Tin;
+    g.Tin = a.Tin;
+    g.ab = wb & ~3;
+    g.woff = wb - g.ab;
+    g.pl = a.pl;
+    g.e = a.e;
+    g.mode = a.mode;
+    g.wsrc = a.wf + (int64_t)cbeg * K * a.Cout + co0;
+    g.wstride = a.Cout;
+    g.CK = a.CK;
+    g.nch = (cend - cbeg) / a.CK;
+    f32x16 acc[TM][TN];
+    c1_mainloop<BM, BN, WM, K, S, false, (EPI & EPI2_ELU) != 0>(acc, g);
+    // epilogue (conv_fwd_kernel's): the operands of a 32 x 32 sub-tile are loaded before its stores
+    const int l32 = lane & 31;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int t = t0 + wn0 + j * 32 + l32;
+            const int cr = co0 + wm0 + i * 32;
+            const int64_t ob = ((int64_t)b * a.Cout + cr) * a.Tout + t;
+            const bool tok = t < a.Tout;
+            float e0[16], e1[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t o = tok ? ob + (int64_t)mfma_row(r, lane) * a.Tout : 0;
+                e0[r] = (EPI & EPI_XACT) ? a.xact[o] : 0.f;
+                e1[r] = (EPI & EPI_RES) ? a.res[o] : 0.f;
+                if (EPI & EPI_ACC) e1[r] += a.y[o];
+            }
+            if (!tok) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = cr + mfma_row(r, lane);
+                const int64_t o = ob + (int64_t)mfma_row(r, lane) * a.Tout;
+                float w = acc[i][j][r];
+                if (EPI & EPI_PART) {
+                    a.part[(int64_t)ks * a.B * a.Cout * a.Tout + o] = w;
+                } else {
+                    if (a.bias) w += a.bias[co];
+                    if (EPI & EPI_XACT) w *= act_grad(a.epi_act, e0[r]);
+                    a.y[o] = w + e1[r];
+                }
+            }
+        }
+}
+
+// v2 planning: channels per chunk (even, dividing the channels of a split, about CONV2_RED
+// reduction elements, the window within C2X_MAXQ quads per thread) and, over the tiles
+// {128, 64} x {128, 64} and channel splits, the least estimated time: rounds of the grid over
+// 256 CUs x the workgroups per CU the LDS admits (each sharing its CU), times the tile's MFMA
+// time at an efficiency per tile shape, plus the split partials' HBM round trip.
+struct C1Plan { int BM, BN, CK, KS, cps; size_t lds; double est; };
+// Per tile shape and channel chunk: the workgroups one CU holds (LDS, and the VGPRs of the ELU
+// variants: 224 -> 2 waves per SIMD) and the MFMA utilisation measured at that occupancy (round
+// 6 sweeps: one workgroup per CU leaves the chunk hand-overs exposed, ~0.55; two ~0.8), the
+// rounds of the grid over the CUs, a fixed cost per chunk, and the split partials' round trip.
+static bool c1_plan(int B, int Cin, int M, int ncols, int K, int S, int out_elems_per_b, bool elu, C1Plan* best) {
+    const int64_t force_tile = encx_opt(OPT_CONV2_TILE), force_ks = encx_opt(OPT_CONV2_KS);
+    const int64_t red_cap = encx_opt(OPT_CONV2_RED);
+    best->est = -1;
+    for (int BM : {128, 64})
+        for (int BN : {128, 64}) {
+            const int tile = BM == 128 ? (BN == 128 ? 1 : 2) : (BN == 128 ? 3 : 4);
+            if (force_tile && force_tile != tile) continue;
+            if (M % BM) continue;
+            const int XW = (((BN - 1) * S + K + 3 + 3) & ~3);
+            const int wave_cap = elu ? 2 : 4;
+            for (int CK = 2; CK <= Cin; CK += 2) {
+                if (Cin % CK || CK * XW / 4 > NT * C2X_MAXQ || (int64_t)CK * K > red_cap) continue;
+                const size_t lds = c1_lds(XW, CK, K, BM);
+                if (lds > 160 * 1024) continue;
+                const int occ = std::min<int>(wave_cap, (int)((160 * 1024) / lds));
+                const double util = occ == 1 ? 0.55 : (occ == 2 ? 0.8 : 0.85);
+                const double eff = (BM == 128 ? 1.0 : 0.9) * (BN == 128 ? 1.0 : 0.93);
+                const int nch = Cin / CK;
+                for (int ks = 1; ks <= 8; ++ks) {
+                    if (nch % ks || (force_ks && ks != force_ks)) continue;
+                    if (ks > 1 && nch / ks < 2) continue;
+                    const int64_t tiles = (int64_t)(M / BM) * cdiv(ncols, BN) * B * ks;
+                    const int64_t slots = 256LL * occ;
+                    // one CU: 0.614 TFLOP/s of fp32 MFMA (157.3 / 256), shared by occ workgroups
+                    const double tile_us = 2.0 * BM * BN * (double)(Cin / ks) * K / (0.614e6 * util * eff) * occ;
+                    const double rounds = (double)cdiv(tiles, slots);
+                    double est = rounds * (tile_us + 0.25 * (nch / ks));
+                    if (ks > 1) est += (double)ks * B * out_elems_per_b * 8.0 / 4.0e6 + 4.0;
+                    if (best->est < 0 || est < best->est) {
+                        best->BM = BM; best->BN = BN; best->CK = CK; best->KS = ks;
+                        best->cps = (nch / ks) * CK; best->lds = lds; best->est = est;
+                    }
+                }
+            }
+        }
+    return best->est >= 0;
+}
+template <int BM, int BN, int WM, int K, int S>
+static int launch_fwd2_tile(FwdArgs a, size_t lds, hipStream_t st) {
+    const int64_t nwg = (int64_t)(a.Cout / BM) * cdiv(a.Tout, BN) * a.B * a.KS;
+    const int elu = a.act == ENCX_ACT_ELU ? EPI2_ELU : 0;
+    const int epi = a.KS > 1 ? (EPI_PART | elu)
+                             : elu | (a.res ? EPI_RES : 0) | (a.xact ? EPI_XACT : 0) | (a.accumulate ? EPI_ACC : 0);
+#define ENCX_FWD2(E) \
+    case E: hipLaunchKernelGGL((conv_fwd2_kernel<BM, BN, WM, K, S, E>), dim3((unsigned)nwg), dim3(NT), lds, st, a); break
+    switch (epi) {
+        ENCX_FWD2(0); ENCX_FWD2(EPI2_ELU); ENCX_FWD2(EPI_RES); ENCX_FWD2(EPI_RES | EPI2_ELU); ENCX_FWD2(EPI_XACT);
+        ENCX_FWD2(EPI_PART); ENCX_FWD2(EPI_PART | EPI2_ELU);
+        default: return -1;
+    }
+#undef ENCX_FWD2
+    return 0;
+}
+static bool fwd2_shape_ok(const FwdArgs& a) {
+    return encx_opt(OPT_CONV2) && a.d == 1 && a.e == 0 && a.Tin % 4 == 0 && a.Cout > 4 && a.Tout > FLAT_T &&
+           ((uintptr_t)a.x | (uintptr_t)a.wf) % 16 == 0 && a.Cout % 4 == 0;
+}
+template <int K, int S>
+static int launch_fwd2_ks(FwdArgs a, float* ws, hipStream_t st) {
+    C1Plan p;
+    if (!c1_plan(a.B, a.Cin, a.Cout, a.Tout, K, S, a.Cout * a.Tout, a.act == ENCX_ACT_ELU, &p)) return -1;
+    a.CK = p.CK;
+    a.KS = p.KS;
+    a.cps = p.cps;
+    a.part = ws;
+    if (p.KS > 1 && !ws) return -1;
+    int rc;
+    // waves side by side along t (WM 1) for the 128-column tiles
+    if (p.BM == 128 && p.BN == 128) rc = launch_fwd2_tile<128, 128, 1, K, S>(a, p.lds, st);
+    else if (p.BM == 128) rc = launch_fwd2_tile<128, 64, 2, K, S>(a, p.lds, st);
+    else if (p.BN == 128) rc = launch_fwd2_tile<64, 128, 1, K, S>(a, p.lds, st);
+    else rc = launch_fwd2_tile<64, 64, 2, K, S>(a, p.lds, st);
+    if (rc) return rc;
+    ENCX_CHECK_LAUNCH();
+    if (a.KS > 1) {
+        const int64_t n = (int64_t)a.B * a.Cout * a.Tout;
+        hipLaunchKernelGGL(conv_fwd_reduce, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, a);
+        ENCX_CHECK_LAUNCH();
+    }
+    return 0;
+}
+#define ENCX_C1_KS_LIST(X) X(7, 1) X(3, 1) X(1, 1) X(4, 2) X(8, 4) X(10, 5) X(16, 8)
+// -1: shape not served by v2 (the caller runs the round-5 kernels)
+static int conv_fwd2_run(const FwdArgs& a, float* ws, hipStream_t st) {
+    if (!fwd2_shape_ok(a)) return -1;
+    switch (a.K * 16 + a.s) {
+#define ENCX_C1_CASE(K_, S_) \
+    case K_ * 16 + S_: return launch_fwd2_ks<K_, S_>(a, ws, st);
+        ENCX_C1_KS_LIST(ENCX_C1_CASE)
+#undef ENCX_C1_CASE
+        default: return -1;
+    }
+}
+static size_t conv_fwd2_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K, int64_t s) {
+    if (!encx_opt(OPT_CONV2)) return 0;
+    C1Plan p;
+    C1Plan q;
+    if (!c1_plan((int)B, (int)Cin, (int)Cout, (int)Tout, (int)K, (int)s, (int)(Cout * Tout), true, &p)) p.KS = 1;
+    if (!c1_plan((int)B, (int)Cin, (int)Cout, (int)Tout, (int)K, (int)s, (int)(Cout * Tout), false, &q)) q.KS = 1;
+    if (p.KS < q.KS) p.KS = q.KS;
+    if (p.KS == 1) return 0;
+    return (size_t)p.KS * B * Cout * Tout * sizeof(float);
+}
+
+// ------------------------------------------------------------------------- polyphase, v2
+// conv_poly_kernel on the v2 main loop: K = J taps, S = 1, the window read backwards (REV: tap kk
+// of column n is in[u0 + n - (J - 1 - kk)] with the weight row of q = J - 1 - kk), zero outside
+// [0, Tin); the ConvTranspose1d input ELU (in_act) applied as the window is written to LDS.
+template <int BM, int BN, int WM, int J, int EPI>
+__global__ __launch_bounds__(NT) void conv_poly2_kernel(PolyArgs a) {
+    constexpr int WN = 4 / WM, TM = BM / WM / 32, TN = BN / WN / 32;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+    const int S = a.s, M = a.Co * S;
+    const int nmb = M / BM, ncols = a.Q / S, ntt = (ncols + BN - 1) / BN;
+    int id = xcd_linear_id();
+    const int mb = id % nmb;
+    id /= nmb;
+    const int tt = id % ntt;
+    id /= ntt;
+    const int ks = id % a.KS, b = id / a.KS;
+    const int m0 = mb * BM, u0 = tt * BN;
+    const int cbeg = ks * a.cps, cend = min(a.Ci, cbeg + a.cps);
+    const int wb = u0 - (J - 1);
+    C1Tile g;
+    g.xb = a.in + ((int64_t)b * a.Ci + cbeg) * a.Tin;
+    g.Tin = a.Tin;
+    g.ab = wb & ~3;
+    g.woff = wb - g.ab;
+    g.pl = 0;
+    g.e = 0;
+    g.mode = ENCX_PAD_ZERO;
+    g.wsrc = a.wp + (int64_t)cbeg * J * M + m0;
+    g.wstride = M;
+    g.CK = a.CK;
+    g.nch = (cend - cbeg) / a.CK;
+    f32x16 acc[TM][TN];
+    c1_mainloop<BM, BN, WM, J, 1, true, (EPI & EPI2_ELU) != 0>(acc, g);
+    const int l32 = lane & 31;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int u = u0 + wn0 + j * 32 + l32;
+            if (EPI & P_PART) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                    const int o = row / S, qpos = u * S + (row - o * S);
+                    if (qpos < a.Q) a.part[(((int64_t)ks * a.B + b) * a.Co + o) * a.Q + qpos] = acc[i][j][r];
+                }
+                continue;
+            }
+            if (!(EPI & P_DGRAD)) {  // ConvTranspose1d: bias, trim
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                    const int o = row / S, p = u * S + (row - o * S) - a.trim;
+                    if (p >= 0 && p < a.Tout)
+                        a.out[((int64_t)b * a.Co + o) * a.Tout + p] = acc[i][j][r] + (a.bias ? a.bias[o] : 0.f);
+                }
+                continue;
+            }
+            float e0[16], e1[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                const int o = row / S, m = u * S + (row - o * S) - a.pl;
+                const bool ok = m >= 0 && m < a.Tx;
+                const int64_t idx = ok ? ((int64_t)b * a.Co + o) * a.Tx + m : 0;
+                e0[r] = (EPI & P_XACT) ? a.xact[idx] : 0.f;
+                e1[r] = (EPI & P_ACC) ? a.out[idx] : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm0 + i * 32 + mfma_row(r, lane);
+                const int o = row / S, qpos = u * S + (row - o * S), m = qpos - a.pl;
+                const float v = acc[i][j][r];
+                if (m >= 0 && m < a.Tx) {
+                    float gv = v;
+                    if (EPI & P_XACT) gv *= act_grad(a.act, e0[r]);
+                    a.out[((int64_t)b * a.Co + o) * a.Tx + m] = gv + e1[r];
+                } else if (qpos >= 0 && qpos < a.pl + a.Tx + a.pr) {
+                    const int slot = m < 0 ? qpos : a.pl + (m - a.Tx);
+                    a.side[((int64_t)b * a.Co + o) * (a.pl + a.pr) + slot] = v;
+                }
+            }
+        }
+}
+template <int BM, int BN, int WM, int J>
+static int launch_poly2_tile(PolyArgs a, size_t lds, hipStream_t st) {
+    const int M = a.Co * a.s;
+    const int64_t nwg = (int64_t)(M / BM) * cdiv(a.Q / a.s, BN) * a.B * a.KS;
+    const int elu = a.in_act == ENCX_ACT_ELU ? EPI2_ELU : 0;
+    int epi;
+    if (a.KS > 1) epi = P_PART | elu;
+    else if (a.mode == 0) epi = elu;
+    else epi = elu | P_DGRAD | (a.act != ENCX_ACT_NONE ? P_XACT : 0) | (a.accumulate ? P_ACC : 0);
+#define ENCX_POLY2(E) \
+    case E: hipLaunchKernelGGL((conv_poly2_kernel<BM, BN, WM, J, E>), dim3((unsigned)nwg), dim3(NT), lds, st, a); break
+    switch (epi) {
+        ENCX_POLY2(0); ENCX_POLY2(EPI2_ELU); ENCX_POLY2(P_DGRAD); ENCX_POLY2(P_DGRAD | P_XACT);
+        ENCX_POLY2(P_DGRAD | P_ACC); ENCX_POLY2(P_DGRAD | P_XACT | P_ACC); ENCX_POLY2(P_PART);
+        ENCX_POLY2(P_PART | EPI2_ELU);
+        default: return -1;
+    }
+#undef ENCX_POLY2
+    return 0;
+}
+template <int J>
+static int launch_poly2_j(PolyArgs a, int ncols, float* ws, hipStream_t st) {
+    C1Plan p;
+    const int M = a.Co * a.s;
+    if (!c1_plan(a.B, a.Ci, M, ncols, J, 1, a.Co * a.Q, a.in_act == ENCX_ACT_ELU, &p)) return -1;
+    if (p.KS > 1 && !ws) return -1;
+    a.CK = p.CK;
+    a.KS = p.KS;
+    a.cps = p.cps;
+    a.part = ws;
+    int rc;
+    if (p.BM == 128 && p.BN == 128) rc = launch_poly2_tile<128, 128, 1, J>(a, p.lds, st);
+    else if (p.BM == 128) rc = launch_poly2_tile<128, 64, 2, J>(a, p.lds, st);
+    else if (p.BN == 128) rc = launch_poly2_tile<64, 128, 1, J>(a, p.lds, st);
+    else rc = launch_poly2_tile<64, 64, 2, J>(a, p.lds, st);
+    if (rc) return rc;
+    ENCX_CHECK_LAUNCH();
+    if (a.KS > 1) {
+        const int64_t n = (int64_t)a.B * a.Co * a.Q;
+        hipLaunchKernelGGL(conv_poly_reduce, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, a);
+        ENCX_CHECK_LAUNCH();
+    }
+    return 0;
+}
+// -1: not served by v2. a.Q must be set (ncols * s).
+static int poly2_run(const PolyArgs& a, int ncols, float* ws, hipStream_t st) {
+    if (!encx_opt(OPT_CONV2) || ncols <= FLAT_T || a.Tin % 4 || ((uintptr_t)a.in | (uintptr_t)a.wp) % 16 ||
+        (a.Co * a.s) % 4)
+        return -1;
+    switch (a.J) {
+        case 1: return launch_poly2_j<1>(a, ncols, ws, st);
+        case 2: return launch_poly2_j<2>(a, ncols, ws, st);
+        case 3: return launch_poly2_j<3>(a, ncols, ws, st);
+        case 7: return launch_poly2_j<7>(a, ncols, ws, st);
+        default: return -1;
+    }
+}
+static size_t poly2_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int64_t J) {
+    if (!encx_opt(OPT_CONV2) || ncols <= FLAT_T) return 0;
+    C1Plan p;
+    C1Plan q;
+    if (!c1_plan((int)B, (int)Ci, (int)(Co * s), (int)ncols, (int)J, 1, (int)(Co * ncols * s), true, &p)) p.KS = 1;
+    if (!c1_plan((int)B, (int)Ci, (int)(Co * s), (int)ncols, (int)J, 1, (int)(Co * ncols * s), false, &q)) q.KS = 1;
+    if (p.KS < q.KS) p.KS = q.KS;
+    if (p.KS == 1) return 0;
+    return (size_t)p.KS * B * Co * ncols * s * sizeof(float);
+}
+
 int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
+    if (!(encx_opt(OPT_PW) && a.K == 1 && a.Tout <= encx_opt(OPT_PW_TMAX)) && !a.part) {
+        const int rc = conv_fwd2_run(a, ws, st);
+        if (rc >= 0) return rc;
+    }
     if (pw_ok(a.K, a.s, a.d, a.pl, 0, a.e, a.Tin, a.Tout, a.Cin, a.Cout, a.Cin) && !a.part) {
         PwArgs p{a.wf, a.x, a.bias, a.res, a.xact, a.y, a.Cout, a.Cin, a.Tout, a.act, a.epi_act};
         const int epi = (a.res ? PW_RES : 0) | (a.xact ? PW_XACT : 0) | (a.accumulate ? PW_ACC : 0);
@@ -1567,9 +2056,10 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
 }
 
 size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K, int64_t s, int64_t d) {
+    const size_t v2 = conv_fwd2_ws(B, Cin, Cout, Tout, K, s);
     if (fwd_flat(Cout, Tout)) {
         const int slabs = fwd_flat_slabs(B, Cin, Cout, Tout, K);
-        return slabs > 1 ? (size_t)slabs * B * Cout * Tout * sizeof(float) : 0;
+        return std::max(v2, slabs > 1 ? (size_t)slabs * B * Cout * Tout * sizeof(float) : (size_t)0);
     }
     // (the epilogue's operands are not known here: the larger of the two plans)
     size_t ws = 0;
@@ -1577,7 +2067,7 @@ size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K
         const FwdPlan p = plan_fwd(B, Cin, Cout, Tout, K, s, d, heavy);
         if (!p.small && p.KS > 1) ws = std::max(ws, (size_t)p.KS * B * Cout * Tout * sizeof(float));
     }
-    return ws;
+    return std::max(ws, v2);
 }
 
 int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
@@ -1600,6 +2090,12 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
         }
         return 0;
     }
+    {
+        PolyArgs a2 = a;
+        a2.Q = ncols * a.s;
+        const int rc = poly2_run(a2, ncols, ws, st);
+        if (rc >= 0) return rc;
+    }
     PolyPlan p = plan_poly(a.B, a.Ci, (int64_t)a.Co * a.s, ncols, a.J,
                            a.mode != 0 && (a.act != ENCX_ACT_NONE || a.accumulate));
     a.CK = p.CK; a.Ub = p.Ub; a.KS = p.KS; a.cps = p.cps; a.Q = ncols * a.s; a.part = ws;
@@ -1620,6 +2116,7 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
 }
 
 size_t poly_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int64_t J) {
+    const size_t v2 = poly2_ws(B, Ci, Co, s, ncols, J);
     if (ncols <= FLAT_T) {
         const int Kred = (int)(Ci * J);
         const int slabs = gemm_slabs(Kred, gemm_splits((int)(Co * s), (int)(B * ncols), Kred));
@@ -1630,7 +2127,7 @@ size_t poly_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int6
         const PolyPlan p = plan_poly(B, Ci, Co * s, ncols, J, heavy);
         if (p.KS > 1) ws = std::max(ws, (size_t)p.KS * B * Co * ncols * s * sizeof(float));
     }
-    return ws;
+    return std::max(ws, v2);
 }
 
 // wgrad planning shared by the launcher and the workspace query

@@ -2638,17 +2638,19 @@ __global__ __launch_bounds__(256) void c2_slab_group_sum(const float* ws, int S,
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const int g = blockIdx.y, s0 = g * G, cnt = min(G, S - s0);
-    part[(int64_t)g * n + i] = sum_strided(ws + (int64_t)s0 * n + i, cnt, n);
+    part[(int64_t)g * n + i] = (float)sum_strided_d(ws + (int64_t)s0 * n + i, cnt, n);
 }
 
 // dw[co][n] (+)= sum_s ws[s][co][n] for n < Nw; db[co] (+)= sum_s ws[s][co][Nw]. Fixed order
-// (slab_sum_256: 64 outputs per block, 4 split slices).
+// (slab_sum_256_d: 64 outputs per block, 4 split slices, fp64 accumulation: at B 32 the bias
+// grads sum ~10^5 positions through up to ~1500 slabs, and an fp32 sum of the slabs lost ~4x the
+// accuracy of a pairwise fp32 sum, test_config3_b32_step_vs_oracle_fp64).
 __global__ __launch_bounds__(256) void c2_wg_reduce(const float* ws, int S, int Co, int N, float* dw, float* db,
                                                     int acc_w, int acc_b) {
-    __shared__ float red[256];
+    __shared__ double red[256];
     const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const bool valid = i < (int64_t)Co * N;
-    const float v = slab_sum_256(ws + (valid ? i : 0), S, (int64_t)Co * N, valid, red);
+    const float v = slab_sum_256_d(ws + (valid ? i : 0), S, (int64_t)Co * N, valid, red);
     if (threadIdx.x >= 64 || !valid) return;
     const int co = (int)(i / N), n = (int)(i - (int64_t)co * N);
     const int Nw = N - 1;
@@ -2664,11 +2666,11 @@ __global__ __launch_bounds__(256) void c2_wg_reduce(const float* ws, int S, int 
 
 // dw[co][(ci*KT + kt)*KF + kf] (+)= sum_s of the task-major slabs of c2_wgrad_rw_kernel<.., NW > 1>
 // (ws[s][kg][cb][co][ci % 32][k*KF + kf], kt = kg*KTW + k, cb = ci / 32; the biases at SZ - 32 + co),
-// db[co] likewise. Fixed order (slab_sum_256).
+// db[co] likewise. Fixed order (slab_sum_256_d).
 __global__ __launch_bounds__(256) void c2_wgr_reduce(const float* ws, int S, int64_t SZ, int Co, int Ci, int KT,
                                                      int KF, int KTW, int cib, float* dw, float* db, int acc_w,
                                                      int acc_b) {
-    __shared__ float red[256];
+    __shared__ double red[256];
     const int N = Ci * KT * KF + 1;
     const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const bool valid = i < (int64_t)Co * N;
@@ -2685,7 +2687,7 @@ __global__ __launch_bounds__(256) void c2_wgr_reduce(const float* ws, int S, int
             off = SZ - 32 + co;
         }
     }
-    const float v = slab_sum_256(ws + off, S, SZ, valid, red);
+    const float v = slab_sum_256_d(ws + off, S, SZ, valid, red);
     if (threadIdx.x >= 64 || !valid) return;
     if (n < N - 1) {
         if (dw) {

@@ -222,8 +222,14 @@ def check_flips(disc, params, maps_in, maps_out, a64, f64, what):
         dev = (zh - z64).abs()
         ratio = dev / bound
         bad = ratio > 1
-        assert not bool(bad.any()), (what, f'map {i}: {int(bad.sum())} of {idx.shape[0]} flipped elements off '
-                                     'their fp64 recompute beyond the a-priori fp32 bound', float(ratio.max()))
+        if bool(bad.any()):
+            k = int(ratio.argmax())
+            e = tuple(int(v) for v in idx[k])
+            raise AssertionError((what, f'map {i}: {int(bad.sum())} of {idx.shape[0]} flipped elements off their '
+                                  f'fp64 recompute beyond the a-priori fp32 bound', float(ratio.max()),
+                                  f'worst at {e}: z_hip {float(zh[k]):.9g} z64 {float(z64[k]):.9g} A {float(A[k]):.4g} '
+                                  f'bound {float(bound[k]):.3g}; map shape {tuple(maps_out[i].shape)} input '
+                                  f'{tuple(maps_in[i].shape)}; oracle z64 there {float(a64[i][0][e]):.9g}'))
         worst = max(worst, float(ratio.max()))
         inherited += int(((zh > 0) == (z64 > 0)).sum())
         checked += idx.shape[0]
