@@ -218,6 +218,7 @@ enum EncxOpt {
     OPT_CONV2_TILE,    // its tile: 0 auto, 1 128x128, 2 128x64, 3 64x128, 4 64x64 (BM x BN)
     OPT_CONV2_RED,     // its largest reduction (channels x taps) per chunk
     OPT_CONV2_KS,      // its channel splits (0: planned)
+    OPT_CONV2_WGS,     // v2 weight grad: about this many workgroups (position splits x tiles)
     OPT_LSTM_SPIN,     // persistent LSTM: log2 of every poll's spin bound (0: 20, about 1 s)
     OPT_LSTM_FAULT,    // persistent LSTM, tests only: one workgroup never publishes (its consumers time out)
     OPT_COUNT

@@ -895,22 +895,23 @@ __global__ __launch_bounds__(NT) void conv_wgrad_small_kernel(WgArgs a) {
     if (a.wsb && tid >= AN && tid < AN + a.A) a.wsb[(int64_t)split * a.A + (tid - AN)] = bacc;
 }
 
-// dw[i] = [acc ? dw : 0] + sum_s ws[s][i] (slab_sum_256: 64 outputs per block, 4 split slices,
-// fixed order); blocks past cdiv(AN, 64) reduce the bias slabs wsb[s][A] into db the same way.
+// dw[i] = [acc ? dw : 0] + sum_s ws[s][i] (slab_sum_256_d: 64 outputs per block, 4 split slices,
+// fixed order, fp64 accumulation: at B 32 the high-rate layers' grads sum 768 k positions through
+// hundreds of slabs); blocks past cdiv(AN, 64) reduce the bias slabs wsb[s][A] into db the same way.
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, float* dw, int64_t AN, int S, int accumulate,
                                                     const float* wsb, float* db, int A, int acc_b) {
-    __shared__ float red[256];
+    __shared__ double red[256];
     const int64_t nbw = (AN + 63) / 64;
     if (blockIdx.x >= nbw) {
         const int i = (int)((blockIdx.x - nbw) * 64) + (threadIdx.x & 63);
         const bool valid = i < A;
-        const float v = slab_sum_256(wsb + (valid ? i : 0), S, A, valid, red);
+        const float v = slab_sum_256_d(wsb + (valid ? i : 0), S, A, valid, red);
         if (threadIdx.x < 64 && valid) db[i] = acc_b ? db[i] + v : v;
         return;
     }
     const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const bool valid = i < AN;
-    const float v = slab_sum_256(ws + (valid ? i : 0), S, AN, valid, red);
+    const float v = slab_sum_256_d(ws + (valid ? i : 0), S, AN, valid, red);
     if (threadIdx.x < 64 && valid) dw[i] = accumulate ? dw[i] + v : v;
 }
 
@@ -1753,7 +1754,10 @@ static bool c1_plan(int B, int Cin, int M, int ncols, int K, int S, int out_elem
                 if (lds > 160 * 1024) continue;
                 const int occ = std::min<int>(wave_cap, (int)((160 * 1024) / lds));
                 const double util = occ == 1 ? 0.55 : (occ == 2 ? 0.8 : 0.85);
-                const double eff = (BM == 128 ? 1.0 : 0.9) * (BN == 128 ? 1.0 : 0.93);
+                // relative rates per tile shape from the round-6 per-layer sweeps: the 64 x 128 tile
+                // (each wave 64 rows x 32 columns) leads; 128-row tiles hold twice the weight rows
+                // in LDS and, with the ELU, 224 VGPRs
+                const double eff = BM == 64 ? (BN == 128 ? 1.0 : 0.95) : 0.85;
                 const int nch = Cin / CK;
                 for (int ks = 1; ks <= 8; ++ks) {
                     if (nch % ks || (force_ks && ks != force_ks)) continue;
@@ -2192,10 +2196,267 @@ static bool wgrad_bias_ok(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K
     return p.kind != 0 || A * C * K + A <= NT;
 }
 
+// ------------------------------------------------------------------------- weight grad, v2
+// dW[a][(c, k)] = sum_{b,t} L[b][a][t] * R~[b][c][t s + k - pl] (conv: L = dy, R = x; convtr: L = x,
+// R = dy) on the v2 pipeline: a workgroup owns a BM x BN tile of dW and walks a contiguous run of
+// (b, 64-position) chunks; per chunk L is staged transposed, Ls[t][a] (the MFMA A reads 32 rows
+// of one position: consecutive words), and R as the window rows of the tile's channels, both
+// through registers (the next chunk's loads in flight while the current chunk's MFMAs run, the
+// activation applied once per element and the pad patched on the way into LDS), two LDS buffers,
+// one barrier per chunk. Partial tiles go to slabs [split][A][C K] (+ the bias sums of L, conv
+// only, by the column-0 tiles) for wgrad_reduce.
+constexpr int W2_PT = 64;       // positions per chunk
+constexpr int W2_LQ = 4;        // L quads per thread per chunk (BM <= 64)
+constexpr int W2_RQ = 6;        // R-window quads per thread per chunk
+struct Wg2Args {
+    const float* L;
+    const float* R;
+    float* ws;
+    float* wsb;
+    int B, A, Tl, C, Tr, K, s, pl, e, mode, actL, actR;
+    int items, per_split;  // items = B * ceil(Tl / PT)
+    int NC, WLp;            // window rows per tile, LDS row length
+};
+static int w2_wl(int K, int S) { return (W2_PT - 1) * S + K + 3 + 3; }
+template <int BM, int BN, int K, int S, bool ELU_L, bool ELU_R, bool BIAS>
+__global__ __launch_bounds__(NT) void conv_wgrad2_kernel(Wg2Args a) {
+    constexpr int TM = BM / 64, TN = BN / 64;  // 4 waves as 2 x 2
+    constexpr int LS = BM + 1;                 // Ls row stride (odd: the transposing writes)
+    extern __shared__ float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave >> 1) * TM * 32, wn0 = (wave & 1) * TN * 32;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int N = a.C * K;
+    const int n0 = blockIdx.x * BN, a0 = blockIdx.y * BM, split = blockIdx.z;
+    const int c_lo = n0 / K;
+    const int WLp = a.WLp, NC = a.NC;
+    const int lsz = W2_PT * LS, rsz = NC * WLp, bsz = ((lsz + rsz) + 3) & ~3;
+    const int it0 = split * a.per_split, it1 = min(a.items, it0 + a.per_split);
+    const int tch = (a.Tl + W2_PT - 1) / W2_PT;
+    // this lane's B columns: n = n0 + wn0 + j 32 + l32 -> (channel row, tap) of the staged window
+    int bbase[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = min(n0 + wn0 + j * 32 + l32, N - 1);
+        const int c = n / K, kk = n - c * K;
+        bbase[j] = (c - c_lo) * WLp + kk;
+    }
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    f32x4 rl[W2_LQ], rr[W2_RQ];
+    float bacc[W2_LQ];
+#pragma unroll
+    for (int e = 0; e < W2_LQ; ++e) bacc[e] = 0.f;
+    constexpr int LQR = W2_PT / 4;  // L quads per row
+    const int nlq = BM * LQR;
+    const int RQ = WLp / 4, nrq = NC * RQ;
+    auto load = [&](int it) {
+        const int b = it / tch, t0 = (it - b * tch) * W2_PT;
+        const float* Lb = a.L + ((int64_t)b * a.A + a0) * a.Tl;
+#pragma unroll
+        for (int e = 0; e < W2_LQ; ++e) {
+            const int q = tid + NT * e;
+            const int row = q / LQR, t = t0 + 4 * (q - row * LQR);
+            const bool ok = q < nlq && t + 4 <= a.Tl;
+            rl[e] = *(const f32x4*)(Lb + (ok ? (int64_t)row * a.Tl + t : 0));
+            if (!ok) rl[e] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+        const int wb = t0 * S - a.pl, ab = wb & ~3;
+        const float* Rb = a.R + ((int64_t)b * a.C + c_lo) * a.Tr;
+#pragma unroll
+        for (int e = 0; e < W2_RQ; ++e) {
+            const int q = tid + NT * e;
+            const int row = q / RQ, p = ab + 4 * (q - row * RQ);
+            const bool ok = q < nrq && c_lo + row < a.C && p >= 0 && p + 4 <= a.Tr;
+            rr[e] = *(const f32x4*)(Rb + (ok ? (int64_t)row * a.Tr + p : 0));
+        }
+    };
+    auto store = [&](int it, float* buf) {
+        const int b = it / tch, t0 = (it - b * tch) * W2_PT;
+        float* Ls = buf;
+        float* Rs = buf + lsz;
+#pragma unroll
+        for (int e = 0; e < W2_LQ; ++e) {
+            const int q = tid + NT * e;
+            if (q < nlq) {
+                const int row = q / LQR, tq = 4 * (q - row * LQR);
+                f32x4 v = rl[e];
+                if (BIAS) bacc[e] += (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) Ls[(tq + i) * LS + row] = ELU_L ? elu_nb(v[i]) : v[i];
+            }
+        }
+        const int wb = t0 * S - a.pl, ab = wb & ~3;
+        const float* Rb = a.R + ((int64_t)b * a.C + c_lo) * a.Tr;
+#pragma unroll
+        for (int e = 0; e < W2_RQ; ++e) {
+            const int q = tid + NT * e;
+            if (q < nrq) {
+                const int row = q / RQ, p = ab + 4 * (q - row * RQ);
+                f32x4 v = rr[e];
+                if (c_lo + row >= a.C) {
+                    v = (f32x4){0.f, 0.f, 0.f, 0.f};
+                } else if (p < 0 || p + 4 > a.Tr) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = pad_src(p + i + a.pl, a.pl, a.Tr, a.e, a.mode);
+                        v[i] = m >= 0 ? Rb[(int64_t)row * a.Tr + m] : 0.f;
+                    }
+                }
+                if (ELU_R) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[i] = elu_nb(v[i]);
+                }
+                *(f32x4*)(Rs + row * WLp + 4 * (q - row * RQ)) = v;
+            }
+        }
+    };
+    if (it0 < it1) {
+        load(it0);
+        store(it0, smem);
+        __syncthreads();
+    }
+    for (int it = it0; it < it1; ++it) {
+        float* cur = smem + ((it - it0) & 1) * bsz;
+        float* nxt = smem + ((it - it0 + 1) & 1) * bsz;
+        const bool more = it + 1 < it1;
+        if (more) load(it + 1);
+        const int t0 = (it % tch) * W2_PT, wb = t0 * S - a.pl, woff = wb - (wb & ~3);
+        const float* Ls = cur + wm0 + l32;
+        const float* Rs = cur + lsz + woff;
+#pragma unroll 8
+        for (int p = 0; p < W2_PT; p += 2) {
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) av[i] = Ls[(p + h) * LS + i * 32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bv[j] = Rs[bbase[j] + (p + h) * S];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+        }
+        if (more) store(it + 1, nxt);
+        __syncthreads();
+    }
+    // the slab of this split: ws[split][a][n]
+    float* slab = a.ws + (int64_t)split * a.A * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 32 + l32;
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = a0 + wm0 + i * 32 + mfma_row(r, lane);
+                slab[(int64_t)row * N + n] = acc[i][j][r];
+            }
+        }
+    if (BIAS && blockIdx.x == 0) {
+        // rows' bias partials: the LQR threads of a row sum theirs through LDS (after the loop's
+        // final barrier nothing reads the buffers)
+        float* red = smem;
+#pragma unroll
+        for (int e = 0; e < W2_LQ; ++e) {
+            const int q = tid + NT * e;
+            if (q < nlq) red[q] = bacc[e];
+        }
+        __syncthreads();
+        if (tid < BM) {
+            float v = 0.f;
+            for (int k = 0; k < LQR; ++k) v += red[tid * LQR + k];
+            a.wsb[(int64_t)split * a.A + a0 + tid] = v;
+        }
+    }
+}
+struct Wg2Plan { int BM, BN, splits, per_split, items, NC, WLp; size_t lds; };
+static bool plan_wgrad2(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K, int64_t S, Wg2Plan* p) {
+    if (!encx_opt(OPT_CONV2) || Tl % 4 || Tl < W2_PT || A % 64) return false;
+    p->BM = 64;
+    const int64_t N = C * K;
+    p->BN = N >= 128 ? 128 : 64;
+    p->WLp = w2_wl((int)K, (int)S) & ~3;
+    p->NC = (int)std::min<int64_t>(C, (p->BN + K - 1) / K + 1);
+    if ((int64_t)p->NC * (p->WLp / 4) > NT * W2_RQ) return false;
+    p->lds = (size_t)2 * (((W2_PT * (p->BM + 1) + p->NC * p->WLp) + 3) & ~3) * sizeof(float);
+    if (p->lds > 160 * 1024) return false;
+    p->items = (int)(B * cdiv(Tl, W2_PT));
+    const int64_t tiles = (A / p->BM) * cdiv(N, p->BN);
+    const int64_t target = encx_opt(OPT_CONV2_WGS);
+    int64_t splits = std::max<int64_t>(1, target / tiles);
+    splits = std::min<int64_t>(splits, p->items / 4 > 0 ? p->items / 4 : 1);
+    p->per_split = (int)cdiv(p->items, splits);
+    p->splits = (int)cdiv(p->items, p->per_split);
+    return true;
+}
+template <int K, int S>
+static int wgrad2_launch(const Wg2Args& a, const Wg2Plan& p, bool bias, hipStream_t st) {
+    const dim3 grid((unsigned)cdiv((int64_t)a.C * K, p.BN), (unsigned)(a.A / p.BM), (unsigned)p.splits);
+    const bool eL = a.actL == ENCX_ACT_ELU, eR = a.actR == ENCX_ACT_ELU;
+#define ENCX_W2(BN_, EL, ER, BI) \
+    hipLaunchKernelGGL((conv_wgrad2_kernel<64, BN_, K, S, EL, ER, BI>), grid, dim3(NT), p.lds, st, a)
+#define ENCX_W2B(BN_)                                   \
+    do {                                                \
+        if (bias) ENCX_W2(BN_, false, true, true);      \
+        else if (eL) ENCX_W2(BN_, true, false, false);  \
+        else if (eR) ENCX_W2(BN_, false, true, false);  \
+        else ENCX_W2(BN_, false, false, false);         \
+    } while (0)
+    if (bias && (eL || !eR)) return -1;
+    if (p.BN == 128) ENCX_W2B(128);
+    else ENCX_W2B(64);
+#undef ENCX_W2B
+#undef ENCX_W2
+    return 0;
+}
+// -1: not served (the caller runs the round-5 kernels). db (conv only: L = dy, no activation).
+static int wgrad2_run(const float* L, const float* R, float* dw, float* ws, int64_t B, int64_t A, int64_t Tl,
+                      int64_t C, int64_t Tr, int64_t K, int64_t s, int64_t d, int64_t pl, int64_t e, int mode,
+                      int actL, int actR, int accumulate, hipStream_t st, float* db, int acc_b) {
+    Wg2Plan p;
+    if (d != 1 || !plan_wgrad2(B, A, Tl, C, K, s, &p)) return -1;
+    if (((uintptr_t)L | (uintptr_t)R) % 16 || Tr % 4) return -1;
+    Wg2Args a;
+    a.L = L; a.R = R; a.ws = ws;
+    const int64_t AN = A * C * K;
+    a.wsb = db ? ws + (int64_t)p.splits * AN : nullptr;
+    a.B = (int)B; a.A = (int)A; a.Tl = (int)Tl; a.C = (int)C; a.Tr = (int)Tr; a.K = (int)K; a.s = (int)s;
+    a.pl = (int)pl; a.e = (int)e; a.mode = mode; a.actL = actL; a.actR = actR;
+    a.items = p.items; a.per_split = p.per_split; a.NC = p.NC; a.WLp = p.WLp;
+    int rc = -1;
+    switch (K * 16 + s) {
+#define ENCX_C1_CASE(K_, S_) \
+    case K_ * 16 + S_: rc = wgrad2_launch<K_, S_>(a, p, db != nullptr, st); break;
+        ENCX_C1_KS_LIST(ENCX_C1_CASE)
+#undef ENCX_C1_CASE
+        default: break;
+    }
+    if (rc) return rc;
+    ENCX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)(cdiv(AN, 64) + (db ? cdiv(A, 64) : 0))), dim3(256), 0, st, ws, dw,
+                       AN, p.splits, accumulate, a.wsb, db, (int)A, acc_b);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+static size_t wgrad2_ws(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K, int64_t s) {
+    Wg2Plan p;
+    if (!plan_wgrad2(B, A, Tl, C, K, s, &p)) return 0;
+    return (size_t)p.splits * A * (C * K + 1) * sizeof(float);
+}
+
 int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, int64_t A,
               int64_t Tl, int64_t C, int64_t Tr, int64_t K, int64_t s, int64_t d, int64_t pl,
               int64_t e, int mode, int actL, int actR, int accumulate, hipStream_t st,
               float* db = nullptr, int acc_b = 0) {
+    {
+        const int rc = wgrad2_run(L, R, dw, ws, B, A, Tl, C, Tr, K, s, d, pl, e, mode, actL, actR, accumulate, st, db,
+                                  acc_b);
+        if (rc >= 0) return rc;
+    }
     WgPlan p = plan_wgrad(B, A, Tl, C, K);
     WgArgs a;
     a.L = L; a.R = R; a.ws = ws;
@@ -2236,7 +2497,8 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
 
 size_t wgrad_ws_bytes(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
     WgPlan p = plan_wgrad(B, A, Tl, C, K);
-    return (size_t)p.splits * A * (C * K + 1) * sizeof(float);  // + the bias slabs
+    // (+ the bias slabs; the v2 plan's splits do not depend on the stride)
+    return std::max((size_t)p.splits * A * (C * K + 1) * sizeof(float), wgrad2_ws(B, A, Tl, C, K, 1));
 }
 
 static size_t maxz(size_t a, size_t b) { return a > b ? a : b; }
@@ -2302,8 +2564,10 @@ int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float
     encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
                        4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout), "conv_dgrad");
     ps.tag(" %ldx%ld k%ld s%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)Tout);
+    // (the long 1x1 layers go to the v2 polyphase kernel when it is on)
     if (pw_ok((int)K, (int)stride, 1, (int)pad_left, (int)pad_right, (int)short_ext, (int)Tin, (int)Tout, (int)Cin,
-              (int)Cout, (int)Cout)) {
+              (int)Cout, (int)Cout) &&
+        !(encx_opt(OPT_CONV2) && Tout > encx_opt(OPT_PW_TMAX))) {
         // dx[b][ci][t] = sum_co wp[co][ci] dy[b][co][t], * act'(x), (+ dx)
         PwArgs p{wp, dy, nullptr, nullptr, x, dx, (int)Cin, (int)Cout, (int)Tout, ENCX_ACT_NONE, pre_act};
         const int epi = (pre_act != ENCX_ACT_NONE ? PW_XACT : 0) | (accumulate ? PW_ACC : 0);

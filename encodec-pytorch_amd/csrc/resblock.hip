@@ -511,16 +511,16 @@ __global__ __launch_bounds__(256) void rb_wgrad_kernel(RbArgs a) {
     }
 }
 
-// out[i] (+)= sum_{g < G} slab[g][i] in ascending g, for the slab's sections: dWs -> dws, dW2 ->
+// out[i] (+)= sum_{g < G} slab[g][i] in ascending g (fp64 accumulation), for the slab's sections: dWs -> dws, dW2 ->
 // dw2, dW1 -> dw1, db -> db2 and dbs (the same sum), db1 -> db1. Null outputs are skipped.
 template <int C>
 __global__ __launch_bounds__(256) void rb_wgrad_reduce(const float* slab, int G, float* dws, float* dw2, float* dw1,
                                                        float* db2, float* dbs, float* db1, int acc_w, int acc_b) {
     constexpr int HD = C / 2, S = Rb<C>::SLAB;
-    __shared__ float red[256];
+    __shared__ double red[256];
     const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const bool valid = i < S;
-    const float v = slab_sum_256(slab + (valid ? i : 0), G, S, valid, red);
+    const float v = slab_sum_256_d(slab + (valid ? i : 0), G, S, valid, red);
     if (threadIdx.x >= 64 || !valid) return;
     auto put = [](float* p, float v, int acc) {
         if (p) *p = acc ? *p + v : v;

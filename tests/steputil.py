@@ -244,10 +244,12 @@ def oracle_step(snap, x, cfg, bandwidth, weights, dtype, disc_masks=None, device
     params). device: the host (default), or the GPU for full-size steps: the oracle's torch ops
     then run on the GPU (test-only checker) with MIOpen off, so its convs are torch's own
     im2col + GEMM in plain fp32 / fp64."""
-    p = {k: v.to(device, dtype) for k, v in snap['gen']['p'].items()}
-    adam = {k: {'step': snap['gen']['step'], 'm': snap['gen']['m'][k].to(device, dtype),
-                'v': snap['gen']['v'][k].to(device, dtype)} for k in p}
-    cbs = [{k: v.to(device, dtype) for k, v in cb.items()} for cb in snap['cbs']]
+    # copies (copy=True): a plain .to() of a host fp32 tensor returns the tensor itself, and the
+    # oracle's Adam would then update the snapshot in place (check_flips reads it afterwards)
+    p = {k: v.to(device, dtype, copy=True) for k, v in snap['gen']['p'].items()}
+    adam = {k: {'step': snap['gen']['step'], 'm': snap['gen']['m'][k].to(device, dtype, copy=True),
+                'v': snap['gen']['v'][k].to(device, dtype, copy=True)} for k in p}
+    cbs = [{k: v.to(device, dtype, copy=True) for k, v in cb.items()} for cb in snap['cbs']]
     bal = O.Balancer(weights)
     if snap['bal'] is not None:
         for name, t, f in zip(*snap['bal']):
@@ -255,9 +257,9 @@ def oracle_step(snap, x, cfg, bandwidth, weights, dtype, disc_masks=None, device
     dp = dadam = dlr = None
     if 'disc' in snap:
         d = snap['disc']
-        dp = {k: v.to(device, dtype) for k, v in d['p'].items()}
-        dadam = {k: {'step': d['step'], 'm': d['m'][k].to(device, dtype), 'v': d['v'][k].to(device, dtype)}
-                 for k in dp}
+        dp = {k: v.to(device, dtype, copy=True) for k, v in d['p'].items()}
+        dadam = {k: {'step': d['step'], 'm': d['m'][k].to(device, dtype, copy=True),
+                     'v': d['v'][k].to(device, dtype, copy=True)} for k in dp}
         dlr = d['lr']
     nt = torch.get_num_threads()
     torch.set_num_threads(ORACLE_THREADS)

@@ -68,6 +68,17 @@ def main():
                 z64 = full_conv(layer, pr, maps_in[i])
                 r = (zh - z64).abs()
                 print(f'  {tag} weights: max |z_hip - z64| {float(r.max()):.3e}, median {float(r.median()):.3e}', flush=True)
+            zo = a64[i][0].double().cpu()
+            z64s = full_conv(layer, prm, maps_in[i])
+            print(f'  HIP vs oracle (whole map): max {float((zh - zo).abs().max()):.3e}; recompute vs oracle: max '
+                  f'{float((z64s - zo).abs().max()):.3e}; shapes hip {tuple(zh.shape)} oracle {tuple(zo.shape)}', flush=True)
+            if i % per:
+                yo = a64[i - 1][0].double().cpu()
+                xo = torch.where(a64[i - 1][1].cpu(), yo, 0.2 * yo)
+                print(f'  captured input vs the oracle\'s input (lrelu of its previous map): max '
+                      f'{float((maps_in[i].double() - xo).abs().max()):.3e}', flush=True)
+                z64o = full_conv(layer, prm, xo)
+                print(f'  recompute from the oracle input vs oracle: max {float((z64o - zo).abs().max()):.3e}', flush=True)
             if i % per:
                 dlt = (maps_in[i].double() - maps_out[i - 1].double()).abs()
                 print(f'  input vs previous output: max diff {float(dlt.max()):.3e}', flush=True)
