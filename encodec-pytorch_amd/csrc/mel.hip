@@ -239,13 +239,233 @@ Geo geo(int64_t B, int64_t T, int64_t n, int64_t nm) {
     return g;
 }
 
+// the mel filters' supports (tables after mb): per mel m the bins [klo, khi) with a nonzero
+// weight, per bin k the mels [mlo, mhi) (the triangular filters overlap pairwise)
+ENCX_DEV const int* sup_at(const float* t, int n, int nm) {
+    const int nb = n / 2 + 1;
+    return reinterpret_cast<const int*>(t + (int64_t)n * 2 * nb + 2 * (int64_t)nb * nm);
+}
+__global__ void support_kernel(float* t, const float* mel, int n, int nm) {
+    const int nb = n / 2 + 1;
+    int* sup = const_cast<int*>(sup_at(t, n, nm));
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nm) {
+        int lo = nb, hi = 0;
+        for (int k = 0; k < nb; ++k)
+            if (mel[(int64_t)i * nb + k] != 0.f) {
+                lo = min(lo, k);
+                hi = k + 1;
+            }
+        sup[2 * i] = lo < hi ? lo : 0;
+        sup[2 * i + 1] = lo < hi ? hi : 0;
+    } else if (i < nm + nb) {
+        const int k = i - nm;
+        int lo = nm, hi = 0;
+        for (int m = 0; m < nm; ++m)
+            if (mel[(int64_t)m * nb + k] != 0.f) {
+                lo = min(lo, m);
+                hi = m + 1;
+            }
+        sup[2 * nm + 2 * k] = lo < hi ? lo : 0;
+        sup[2 * nm + 2 * k + 1] = lo < hi ? hi : 0;
+    }
+}
+
+// ---------------------------------------------------------------- fused multi-scale loss (round 6)
+// One launch per scale does what the nine per-scale launches of encx_mel_loss did: each workgroup
+// takes FPW frames of x and the same frames of y through the real FFT in LDS (fft.h), the power
+// spectrum through the mel filters (sparse: each bin lies under at most two triangles, so the
+// 64 x nb projection costs ~2 nb multiply-adds per frame instead of an MFMA GEMM over a spectrum
+// round trip through HBM), log10, the L1 + MSE partial sums and d/d mel(y); then d/d |Y_k|^2 back
+// through the filters, G_k = 2 Y_k dP_k, the inverse real FFT and the window: the frame gradients
+// for one overlap-add launch over all scales. Loss partials per workgroup, summed by one finish
+// launch in a fixed order.
+struct MelScale {
+    const float* tables;
+    float* dframe;  // [rows][n] frame gradients (null: no gradient)
+    float* parts;   // [2][nblk] L1 / MSE partial sums
+    int T, F, hop, pad, rows;
+    float inv_n;    // 1 / (rows * nm)
+};
+template <int LOGM, bool GRAD>
+__global__ __launch_bounds__(encx_fft::FFT_NT) void mel_fused_kernel(const float* x, const float* y, MelScale a) {
+    using namespace encx_fft;
+    constexpr int M = 1 << LOGM, N = 2 * M, FPW = M >= 1024 ? 1 : 1024 / M, NB = M + 1, NM = 64;
+    __shared__ f2v buf[2 * FPW * M];
+    __shared__ f2v twf[M + 1];
+    __shared__ f2v twi[M + 1];
+    __shared__ f2v Xs[FPW * NB];     // Y's spectrum (kept for the backward), then the c2r input
+    __shared__ float Ps[FPW * NB];   // power spectrum, then dP
+    __shared__ float Lx[FPW * NM];   // log-mel of x, then d mel(y)
+    __shared__ float red[16];
+    const int nb2 = 2 * NB;
+    const float* bt = a.tables;      // window = bt[t * nb2] (column 0: w cos 0)
+    const float* mt = a.tables + (int64_t)N * nb2;  // [nb][nm]
+    const int* sup = sup_at(a.tables, N, NM);
+    make_twiddles<M>(twf, -1.f);
+    for (int k = threadIdx.x; k <= M; k += FFT_NT) twi[k] = cconj(twf[k]);
+    const int row0 = blockIdx.x * FPW;
+    float* bufr = reinterpret_cast<float*>(buf);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+        const float* w = pass == 0 ? x : y;
+        __syncthreads();
+        for (int i = threadIdx.x; i < FPW * N; i += FFT_NT) {
+            const int f = i / N, t = i - f * N, row = row0 + f;
+            float v = 0.f;
+            if (row < a.rows) {
+                const int bc = row / a.F, fr = row - bc * a.F;
+                int s = fr * a.hop + t - a.pad;
+                s = s < 0 ? -s : (s >= a.T ? 2 * (a.T - 1) - s : s);
+                v = w[(int64_t)bc * a.T + s] * bt[t * nb2];
+            }
+            bufr[i] = v;
+        }
+        __syncthreads();
+        const int res = stockham<M, FPW>(buf, twf);
+        const f2v* Z = buf + res * (FPW * M);
+        for (int q = threadIdx.x; q < FPW * NB; q += FFT_NT) {
+            const int f = q / NB, k = q - f * NB;
+            const f2v zk = Z[f * M + (k & (M - 1))], zm = cconj(Z[f * M + ((M - k) & (M - 1))]);
+            const f2v e = (zk + zm) * 0.5f, o = (zk - zm) * 0.5f;
+            const f2v tt = cmul(twf[k], o);
+            const float re = e[0] + tt[1], im = e[1] - tt[0];
+            Ps[q] = re * re + im * im;
+            if (GRAD && pass == 1) Xs[q] = (f2v){re, im};
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < FPW * NM; q += FFT_NT) {
+            const int f = q / NM, m = q - f * NM, row = row0 + f;
+            const int klo = sup[2 * m], khi = sup[2 * m + 1];
+            float mel = 0.f;
+            for (int k = klo; k < khi; ++k) mel = fmaf(Ps[f * NB + k], mt[(int64_t)k * NM + m], mel);
+            const float l = log10f(fmaxf(mel, 1e-5f));
+            if (pass == 0) {
+                Lx[q] = l;
+            } else if (row < a.rows) {
+                const float d = Lx[q] - l;  // l1Loss(mel(x), mel(y)): input mel(x), target mel(y)
+                s1 += fabsf(d);
+                s2 = fmaf(d, d, s2);
+                if (GRAD) {
+                    const float g = ((d < 0.f ? 1.f : (d > 0.f ? -1.f : 0.f)) - 2.f * d) * a.inv_n;
+                    Lx[q] = mel >= 1e-5f ? g / (mel * 2.302585092994046f) : 0.f;
+                }
+            } else if (GRAD) {
+                Lx[q] = 0.f;
+            }
+        }
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (threadIdx.x == 0) {
+        a.parts[blockIdx.x] = s1;
+        a.parts[gridDim.x + blockIdx.x] = s2;
+    }
+    if (!GRAD) return;
+    __syncthreads();
+    // D_k = 2 Y_k dP_k, dP_k = sum over the filters on k of dmel_m w_mk; then the c2r of c2r_kernel
+    for (int q = threadIdx.x; q < FPW * NB; q += FFT_NT) {
+        const int f = q / NB, k = q - f * NB;
+        const int mlo = sup[2 * NM + 2 * k], mhi = sup[2 * NM + 2 * k + 1];
+        float dp = 0.f;
+        for (int m = mlo; m < mhi; ++m) dp = fmaf(Lx[f * NM + m], mt[(int64_t)k * NM + m], dp);
+        const f2v d = Xs[q] * (2.f * dp);
+        Xs[q] = (k == 0 || k == M) ? (f2v){d[0], 0.f} : d * 0.5f;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < FPW * M; q += FFT_NT) {
+        const int f = q / M, k = q - f * M;
+        const f2v yk = Xs[f * NB + k], ym = cconj(Xs[f * NB + M - k]);
+        const f2v A = yk + ym, Bv = cmul(yk - ym, twi[k]);
+        buf[q] = (f2v){A[0] - Bv[1], A[1] + Bv[0]};
+    }
+    __syncthreads();
+    const int res = stockham<M, FPW>(buf, twi);
+    const float* c = reinterpret_cast<const float*>(buf + res * (FPW * M));
+    for (int i = threadIdx.x; i < FPW * N; i += FFT_NT) {
+        const int f = i / N, t = i - f * N, row = row0 + f;
+        if (row < a.rows) a.dframe[(int64_t)row * N + t] = c[i] * bt[t * nb2];
+    }
+}
+template <bool GRAD>
+static int mel_fused_launch(int n, const float* x, const float* y, const MelScale& a, hipStream_t st) {
+    const int m = n / 2, fpw = m >= 1024 ? 1 : 1024 / m;
+    const dim3 grid((unsigned)cdiv(a.rows, fpw));
+    switch (m) {
+        case 16: hipLaunchKernelGGL((mel_fused_kernel<4, GRAD>), grid, dim3(encx_fft::FFT_NT), 0, st, x, y, a); break;
+        case 32: hipLaunchKernelGGL((mel_fused_kernel<5, GRAD>), grid, dim3(encx_fft::FFT_NT), 0, st, x, y, a); break;
+        case 64: hipLaunchKernelGGL((mel_fused_kernel<6, GRAD>), grid, dim3(encx_fft::FFT_NT), 0, st, x, y, a); break;
+        case 128: hipLaunchKernelGGL((mel_fused_kernel<7, GRAD>), grid, dim3(encx_fft::FFT_NT), 0, st, x, y, a); break;
+        case 256: hipLaunchKernelGGL((mel_fused_kernel<8, GRAD>), grid, dim3(encx_fft::FFT_NT), 0, st, x, y, a); break;
+        case 512: hipLaunchKernelGGL((mel_fused_kernel<9, GRAD>), grid, dim3(encx_fft::FFT_NT), 0, st, x, y, a); break;
+        case 1024: hipLaunchKernelGGL((mel_fused_kernel<10, GRAD>), grid, dim3(encx_fft::FFT_NT), 0, st, x, y, a); break;
+        default: return ENCX_EINVAL;
+    }
+    return (int)hipGetLastError();
+}
+constexpr int MEL_MAXS = 8;
+struct MelOla {  // the frame gradients of every scale
+    const float* dframe[MEL_MAXS];
+    int n[MEL_MAXS], hop[MEL_MAXS], pad[MEL_MAXS], F[MEL_MAXS];
+    int ns;
+};
+// grad[b][m] (+)= sum over scales (in order) of overlap_add's sum for that scale
+__global__ void overlap_add_all(MelOla o, float* grad, int Bn, int T) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Bn * T) return;
+    const int b = (int)(i / T), m = (int)(i - (int64_t)b * T);
+    float tot = 0.f;
+    for (int sc = 0; sc < o.ns; ++sc) {
+        const int n = o.n[sc], h = o.hop[sc], p = o.pad[sc], F = o.F[sc];
+        int js[3];
+        int nj = 0;
+        js[nj++] = m + p;
+        if (m >= 1 && m <= p) js[nj++] = p - m;
+        if (m >= T - 1 - p && m <= T - 2) js[nj++] = p + 2 * (T - 1) - m;
+        float s = 0.f;
+        for (int q = 0; q < nj; ++q) {
+            const int j = js[q];
+            const int flo = j - n + 1 > 0 ? (j - n + 1 + h - 1) / h : 0;
+            int fhi = j / h;
+            if (fhi > F - 1) fhi = F - 1;
+            for (int f = flo; f <= fhi; ++f) s += o.dframe[sc][((int64_t)b * F + f) * n + (j - f * h)];
+        }
+        tot += s;
+    }
+    grad[i] += tot;
+}
+// loss[0] += sum over scales (in order) of (sum L1 parts + sum MSE parts) * inv_n
+struct MelFin {
+    const float* parts[MEL_MAXS];
+    int nblk[MEL_MAXS];
+    float inv_n[MEL_MAXS];
+    int ns;
+};
+__global__ __launch_bounds__(256) void mel_loss_finish(MelFin f, float* loss) {
+    __shared__ float red[16];
+    float tot = loss[0];
+    for (int sc = 0; sc < f.ns; ++sc) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int i = threadIdx.x; i < f.nblk[sc]; i += 256) {
+            s1 += f.parts[sc][i];
+            s2 += f.parts[sc][f.nblk[sc] + i];
+        }
+        s1 = block_sum(s1, red);
+        s2 = block_sum(s2, red);
+        tot = (tot + s1 * f.inv_n[sc]) + s2 * f.inv_n[sc];
+    }
+    if (threadIdx.x == 0) loss[0] = tot;
+}
+
 }  // namespace
 
 extern "C" {
 
 size_t encx_mel_tables_floats(int64_t n_fft, int64_t n_mels) {
     int64_t nb = n_fft / 2 + 1;
-    return (size_t)(n_fft * 2 * nb + 2 * nb * n_mels);
+    // + the filters' supports: per mel [klo, khi), per bin [mlo, mhi) (ints)
+    return (size_t)(n_fft * 2 * nb + 2 * nb * n_mels + 2 * n_mels + 2 * nb);
 }
 
 int encx_mel_tables_init(float* tables, const float* mel_basis, int64_t n_fft, int64_t n_mels,
@@ -254,6 +474,9 @@ int encx_mel_tables_init(float* tables, const float* mel_basis, int64_t n_fft, i
     int64_t tot = n_fft * 2 * (n_fft / 2 + 1) + (n_fft / 2 + 1) * n_mels;
     hipLaunchKernelGGL(tables_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, (hipStream_t)stream, tables,
                        mel_basis, (int)n_fft, (int)n_mels);
+    const int64_t nsup = n_mels + n_fft / 2 + 1;
+    hipLaunchKernelGGL(support_kernel, dim3(cdiv(nsup, 256)), dim3(256), 0, (hipStream_t)stream, tables, mel_basis,
+                       (int)n_fft, (int)n_mels);
     ENCX_CHECK_LAUNCH();
     return 0;
 }
@@ -333,6 +556,63 @@ int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws
     hipLaunchKernelGGL(overlap_add, dim3(cdiv(B * T, 256)), dim3(256), 0, st, dframe, grad, (int)B,
                        (int)T, g.n, g.h, g.p, g.F);
     ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+size_t encx_mel_loss_multi_workspace_floats(int64_t B, int64_t T, const int64_t* n_ffts, int64_t nscales) {
+    size_t tot = 0;
+    for (int64_t i = 0; i < nscales; ++i) {
+        const Geo g = geo(B, T, n_ffts[i], 64);
+        const int fpw = g.n / 2 >= 1024 ? 1 : 1024 / (g.n / 2);
+        tot += (size_t)g.rows * g.n + 2 * (size_t)cdiv(g.rows, fpw) + 64;
+    }
+    return tot;
+}
+
+int encx_mel_loss_multi(const float* x, const float* y, const float* const* tables, const int64_t* n_ffts,
+                        int64_t nscales, float* ws, float* loss, float* grad, int64_t B, int64_t T,
+                        encx_stream_t stream) {
+    ENCX_REQUIRE(x && y && tables && n_ffts && ws && loss && B > 0 && nscales > 0 && nscales <= MEL_MAXS);
+    hipStream_t st = (hipStream_t)stream;
+    double flops = 0.0;
+    for (int64_t i = 0; i < nscales; ++i) {
+        const int64_t n = n_ffts[i];
+        ENCX_REQUIRE(tables[i] && encx_fft::fft_ok(n));
+        const double rows = (double)geo(B, T, n, 64).rows, lg = log2((double)n);
+        flops += rows * (2 * 2.5 * n * lg + 2 * 2.0 * (n + 2)) + (grad ? rows * (2.5 * n * lg + 2.0 * (n + 2)) : 0.0);
+    }
+    encx_prof_scope ps(st, flops, 4.0 * B * T * (grad ? 3 : 2), "mel_loss");
+    MelOla o{};
+    MelFin fin{};
+    o.ns = fin.ns = (int)nscales;
+    float* cur = ws;
+    for (int64_t i = 0; i < nscales; ++i) {
+        const Geo g = geo(B, T, n_ffts[i], 64);
+        ENCX_REQUIRE(g.p < T && g.F > 0);
+        const int fpw = g.n / 2 >= 1024 ? 1 : 1024 / (g.n / 2);
+        const int nblk = (int)cdiv(g.rows, fpw);
+        MelScale a;
+        a.tables = tables[i];
+        a.dframe = grad ? cur : nullptr;
+        cur += (size_t)g.rows * g.n;
+        a.parts = cur;
+        cur += 2 * (size_t)nblk + 64;
+        a.T = (int)T; a.F = g.F; a.hop = g.h; a.pad = g.p; a.rows = g.rows;
+        a.inv_n = 1.f / (float)((int64_t)g.rows * 64);
+        const int rc = grad ? mel_fused_launch<true>(g.n, x, y, a, st) : mel_fused_launch<false>(g.n, x, y, a, st);
+        if (rc) return rc;
+        o.dframe[i] = a.dframe;
+        o.n[i] = g.n; o.hop[i] = g.h; o.pad[i] = g.p; o.F[i] = g.F;
+        fin.parts[i] = a.parts;
+        fin.nblk[i] = nblk;
+        fin.inv_n[i] = a.inv_n;
+    }
+    hipLaunchKernelGGL(mel_loss_finish, dim3(1), dim3(256), 0, st, fin, loss);
+    ENCX_CHECK_LAUNCH();
+    if (grad) {
+        hipLaunchKernelGGL(overlap_add_all, dim3((unsigned)cdiv(B * T, 256)), dim3(256), 0, st, o, grad, (int)B, (int)T);
+        ENCX_CHECK_LAUNCH();
+    }
     return 0;
 }
 

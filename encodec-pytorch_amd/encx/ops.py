@@ -4,6 +4,8 @@ Each Function below replaces the device work of one reference module (file:line 
 docstrings); the nn.Module mirrors in encx.modules / encx.quantization / encx.losses call these.
 """
 import contextlib
+import ctypes
+import os
 import math
 
 import numpy as np
@@ -534,6 +536,11 @@ def mel_tables(device, n_fft, n_mels, sr):
     return t[0]
 
 
+# the fused multi-scale mel loss (encx_mel_loss_multi: one launch per scale + one overlap-add +
+# one finish, round 6); False: the per-scale calls of encx_mel_loss (nine launches each)
+MEL_FUSED = os.environ.get('ENCX_MEL_FUSED', '1') != '0'
+
+
 class MelLossFn(torch.autograd.Function):
     """l_f of total_loss (losses.py:40-42): sum over n_fft = 2^5..2^11 (hop n/4, 64 mels) of
     L1 + MSE between Audio2Mel(x) and Audio2Mel(y) (audio_to_mel.py:34-55). The gradient
@@ -547,6 +554,14 @@ class MelLossFn(torch.autograd.Function):
         T = y.shape[-1]
         loss = torch.zeros(1, device=y.device, dtype=torch.float32)
         grad = torch.zeros_like(y) if ctx.needs_input_grad[1] else None
+        if MEL_FUSED and n_mels == 64 and all(32 <= n <= 2048 and n & (n - 1) == 0 for n in scales):
+            ns = (ctypes.c_int64 * len(scales))(*scales)
+            tabs = (ctypes.c_void_p * len(scales))(*[mel_tables(y.device, n, n_mels, sr).data_ptr() for n in scales])
+            ws = _f32(lib.encx_mel_loss_multi_workspace_floats(B, T, ns, len(scales)), y)
+            call('encx_mel_loss_multi', ptr(x), ptr(y), tabs, ns, len(scales), ptr(ws), ptr(loss), ptr(grad), B, T,
+                 stream())
+            ctx.save_for_backward(grad)
+            return loss
         wsn = max(lib.encx_mel_workspace_floats(B, T, n, n_mels) for n in scales)
         ws = _f32(wsn, y)
         for n in scales:

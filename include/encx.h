@@ -276,6 +276,19 @@ int encx_mel_loss(const float* x, const float* y, const float* tables, float* ws
                   float* grad, int64_t B, int64_t T, int64_t n_fft, int64_t n_mels,
                   encx_stream_t stream);
 
+/* Every scale of the l_f term (losses.py:40-42, n_fft = 2^5..2^11) in one call (round 6): per scale
+ * ONE fused launch -- the real FFT of the frames of x and y in LDS, the power spectrum through the
+ * mel filters (sparse; the supports are built by encx_mel_tables_init), log10, the L1 + MSE partial
+ * sums, and (grad != NULL) d/d|Y|^2 back through the filters and the inverse real FFT to frame
+ * gradients -- then one overlap-add of all scales' frame gradients (grad (+)=) and one finish,
+ * loss[0] (+)= the scales' L1 + MSE in order (the reference's accumulation, losses.py:41-42).
+ * tables: host array of nscales device table pointers (encx_mel_tables_init, 64 mels); n_ffts:
+ * host array of the transform sizes (powers of 2, 32..2048). ws:
+ * encx_mel_loss_multi_workspace_floats floats. Replaces nscales calls of encx_mel_loss. */
+size_t encx_mel_loss_multi_workspace_floats(int64_t B, int64_t T, const int64_t* n_ffts, int64_t nscales);
+int encx_mel_loss_multi(const float* x, const float* y, const float* const* tables, const int64_t* n_ffts,
+                        int64_t nscales, float* ws, float* loss, float* grad, int64_t B, int64_t T,
+                        encx_stream_t stream);
 /* Audio2Mel.forward (audio_to_mel.py:34-55) alone: out [B][n_mels][F] log-mel spectrogram
  * (the reference's [B*C, 64, F] before its final reshape). ws: encx_mel_workspace_floats. */
 int encx_mel_logmel(const float* x, const float* tables, float* ws, float* out, int64_t B,

@@ -71,7 +71,7 @@ def test_host_only_queries():
     assert lib.encx_mel_frames(24000, 32) == 3000
     assert lib.encx_rvq_apply_parts(32, 128, 75) == 1024
     assert lib.encx_conv1d_bwd_weight_workspace(32, 32, 16, 24000, 3) > 0
-    assert lib.encx_mel_tables_floats(32, 64) == 32 * 34 + 2 * 17 * 64
+    assert lib.encx_mel_tables_floats(32, 64) == 32 * 34 + 2 * 17 * 64 + 2 * 64 + 2 * 17
     # argument validation happens before any device call
     assert lib.encx_conv1d_fwd(*([None] * 6 + [0] * 12 + [None])) == 9001
 

@@ -28,7 +28,7 @@ def _rel(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-30))
 
 
-def _layer_walk(seq, C, Tn):
+def _layer_walk(seq, C, Tn, batch=B):
     """(index, module, act, input shape) of every conv / residual block of a SEANet nn.Sequential
     (the encx stack folds each nn.ELU into the next conv: modules/seanet.py _run)."""
     from encx.modules.conv import SConv1d, SConvTranspose1d
@@ -40,15 +40,15 @@ def _layer_walk(seq, C, Tn):
             act = 'elu'
             continue
         if isinstance(m, SEANetResnetBlock):
-            out.append((i, m, None, (B, C, Tn)))
+            out.append((i, m, None, (batch, C, Tn)))
         elif isinstance(m, SConv1d):
             c = m.conv
-            out.append((i, m, act, (B, C, Tn)))
+            out.append((i, m, act, (batch, C, Tn)))
             Tn = ops.conv_geometry(Tn, c.kernel_size, c.stride, c.dilation, m.causal, m.pad_mode)[3]
             C = c.out_channels
         elif isinstance(m, SConvTranspose1d):
             c = m.convtr
-            out.append((i, m, act, (B, C, Tn)))
+            out.append((i, m, act, (batch, C, Tn)))
             Tn = ops.convtr_geometry(Tn, c.kernel_size, c.stride, m.causal, m.trim_right_ratio)[1]
             C = c.out_channels
         act = None
@@ -62,14 +62,15 @@ def _fp64_layer(m, x64, act):
     xin = F.elu(x64) if act == 'elu' else x64
     if isinstance(m, SConv1d):
         c = m.conv
-        y = O.sconv1d(xin, p, 'm', c.kernel_size, c.stride, c.dilation, m.causal, m.pad_mode)
+        y = O.sconv1d(xin, p, 'm', c.kernel_size, c.stride, c.dilation, m.causal, m.pad_mode, c.norm_type)
     elif isinstance(m, SConvTranspose1d):
         c = m.convtr
-        y = O.sconvtr1d(xin, p, 'm', c.kernel_size, c.stride, m.causal, m.trim_right_ratio)
+        y = O.sconvtr1d(xin, p, 'm', c.kernel_size, c.stride, m.causal, m.trim_right_ratio, c.norm_type)
     else:
-        hidden = m.block[1].conv.out_channels
-        dim = m.block[1].conv.in_channels
-        y = O.resblock(xin, p, 'm', dim, m.block[1].conv.kernel_size, dim // hidden, m.block[1].causal)
+        c1 = m.block[1]
+        hidden = c1.conv.out_channels
+        dim = c1.conv.in_channels
+        y = O.resblock(xin, p, 'm', dim, c1.conv.kernel_size, dim // hidden, c1.causal, c1.conv.norm_type)
     return y, p
 
 
@@ -117,6 +118,42 @@ def test_seanet_layers_b32_vs_fp64(stack):
         print(name + ': ' + ' '.join(f'{k} {e:.1e}' for k, e in errs.items()))
         bad += [(name, k, e) for k, e in errs.items() if not e < 2e-5]
         del x, y, dy, x64, y64, p64
+    assert not bad, bad
+
+
+@pytest.mark.parametrize('seg', [48000, 4800])
+@pytest.mark.parametrize('stack', ['encoder', 'decoder'])
+def test_seanet_layers_48k_vs_fp64(stack, seg):
+    """The config-5 SEANet stack (48 kHz stereo: non-causal, symmetric reflect padding,
+    time_group_norm convs with plain weights) layer by layer at B 2 and the 1 s segment's lengths
+    (48000 samples down to 150 frames; and the 0.1 s segments of the g9 fixture's model): output, input grad and parameter grads within 2e-5 of the
+    fp64 restatement, relative to the tensor's largest magnitude."""
+    from encx.model import EncodecModel
+    from encx.modules.seanet import SEANetResnetBlock
+    torch.manual_seed(12)
+    model = EncodecModel._get_model([24.0], 48000, 2, causal=False, model_norm='time_group_norm',
+                                    audio_normalize=True, segment=seg / 48000)
+    seq = getattr(model, stack).model.to(DEV)
+    walk = _layer_walk(seq, 2, seg, 2) if stack == 'encoder' else _layer_walk(seq, 128, seg // 320, 2)
+    bad = []
+    for idx, m, act, shape in walk:
+        gen = torch.Generator(device=DEV).manual_seed(2000 + idx)
+        x = torch.randn(shape, generator=gen, device=DEV).requires_grad_(True)
+        for prm in m.parameters():
+            prm.grad = None
+        y = m(x) if isinstance(m, SEANetResnetBlock) else m(x, act=act)
+        dy = torch.randn(y.shape, generator=gen, device=DEV)
+        y.backward(dy)
+        x64 = x.detach().double().requires_grad_(True)
+        with torch.backends.cudnn.flags(enabled=False):
+            y64, p64 = _fp64_layer(m, x64, act)
+            y64.backward(dy.double())
+        errs = {'y': _rel(y, y64), 'dx': _rel(x.grad, x64.grad)}
+        for k, prm in m.named_parameters():
+            errs['d' + k] = _rel(prm.grad, p64['m.' + k].grad)
+        name = f'48k {stack}.model.{idx} {type(m).__name__} {tuple(shape)}'
+        print(name + ': ' + ' '.join(f'{k} {e:.1e}' for k, e in errs.items()))
+        bad += [(name, k, e) for k, e in errs.items() if not e < 2e-5]
     assert not bad, bad
 
 

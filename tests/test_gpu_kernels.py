@@ -229,7 +229,18 @@ def test_mel_fixture():
         close(ops.logmel(x, n, 64, 24000), d[f'mel{n}'], 1e-4, 2e-4, f'logmel {n}')
 
 
-def test_losses_fixture():
+@pytest.fixture(params=[True, False], ids=['fused', 'per_scale'])
+def mel_path(request):
+    """l_f through the fused multi-scale launches (encx_mel_loss_multi) and through the
+    per-scale ones (encx_mel_loss)."""
+    from encx import ops
+    prev = ops.MEL_FUSED
+    ops.MEL_FUSED = request.param
+    yield request.param
+    ops.MEL_FUSED = prev
+
+
+def test_losses_fixture(mel_path):
     from encx import losses
     d = load('g4_mel.npz')
     x = G(d['x'])
@@ -243,7 +254,7 @@ def test_losses_fixture():
     close(gf, d['dlf_dy'], 2e-3, 2e-7, 'dl_f/dy')
 
 
-def test_mel_loss_full_size_vs_oracle():
+def test_mel_loss_full_size_vs_oracle(mel_path):
     from encx import losses
     x0 = synth_wave((4, 1, 24000), 11)
     y0 = synth_wave((4, 1, 24000), 12)
