@@ -252,7 +252,12 @@ def main():
             out['ranks'] = world
             out['config']['parallelism'] = f'dp{world} rehearsal: {world} ranks on 1 GPU over gloo'
         if world == 1 and not args.no_cpu_baseline:
-            out['cpu_baseline'] = cpu_baseline(args.config, min(16, os.cpu_count() or 1))
+            # every host core this job may use: the process's CPU affinity, capped by the CPU share
+            # the box grants a one-GPU job (OMP_NUM_THREADS, 16 on the pool's boxes; os.cpu_count()
+            # there reports the whole machine, most of it not ours)
+            cores = len(os.sched_getaffinity(0))
+            share = int(os.environ.get('OMP_NUM_THREADS', '0') or 0)
+            out['cpu_baseline'] = cpu_baseline(args.config, min(cores, share) if share > 0 else cores)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

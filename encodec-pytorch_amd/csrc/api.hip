@@ -42,6 +42,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {OPT_CONV_SPLIT, "CONV_SPLIT", 1024}, {OPT_CONV_WG_SPLIT, "CONV_WG_SPLIT", 1024},
     {OPT_CONV2, "CONV2", 0}, {OPT_CONV2_TILE, "CONV2_TILE", 0}, {OPT_CONV2_RED, "CONV2_RED", 64},
     {OPT_CONV2_KS, "CONV2_KS", 0}, {OPT_CONV2_WGS, "CONV2_WGS", 512},
+    {OPT_CONV2_LOWT, "CONV2_LOWT", 0},
     {OPT_LSTM_SPIN, "LSTM_SPIN", 0}, {OPT_LSTM_FAULT, "LSTM_FAULT", 0},
 };
 constexpr bool opts_in_order() {

@@ -214,11 +214,12 @@ enum EncxOpt {
     OPT_CONV_CK,       // conv1d fwd / bwd-data: reduction elements (channels x taps) per LDS chunk
     OPT_CONV_SPLIT,    // conv1d fwd / bwd-data: split-K until this many workgroups
     OPT_CONV_WG_SPLIT, // conv1d weight grad: split the positions until this many workgroups
-    OPT_CONV2,         // conv1d forward v2 (LDS-DMA double-buffered staging) where it applies
+    OPT_CONV2,         // conv1d v2 kernels, bitmask: 1 forward, 2 polyphase (bwd-data / convtr), 4 weight grad
     OPT_CONV2_TILE,    // its tile: 0 auto, 1 128x128, 2 128x64, 3 64x128, 4 64x64 (BM x BN)
     OPT_CONV2_RED,     // its largest reduction (channels x taps) per chunk
     OPT_CONV2_KS,      // its channel splits (0: planned)
     OPT_CONV2_WGS,     // v2 weight grad: about this many workgroups (position splits x tiles)
+    OPT_CONV2_LOWT,    // v2 also for 64 < T <= 128 (the T 75 layers), else the flattened GEMMs
     OPT_LSTM_SPIN,     // persistent LSTM: log2 of every poll's spin bound (0: 20, about 1 s)
     OPT_LSTM_FAULT,    // persistent LSTM, tests only: one workgroup never publishes (its consumers time out)
     OPT_COUNT

@@ -1562,6 +1562,7 @@ static size_t c1_lds(int XW, int CK, int K, int BM) {
 struct C1Tile {
     const float* xb;
     int Tin, ab, woff, pl, e, mode;
+    int vec;  // input rows 16-B aligned (Tin % 4 == 0): quad loads; else 4 scalar loads per quad
     const float* wsrc;
     int wstride, CK, nch;
 };
@@ -1583,12 +1584,24 @@ ENCX_DEV void c1_mainloop(f32x16 (&acc)[BM / WM / 32][BN / (4 / WM) / 32], const
     f32x4 rx[C2X_MAXQ];
     auto load_x = [&](int c) {
         const float* xc = g.xb + (int64_t)(c * CK) * Tin;
+        if (g.vec) {
 #pragma unroll
-        for (int e = 0; e < C2X_MAXQ; ++e) {
-            const int q = tid + NT * e;
-            const int row = q / XQ, p = g.ab + 4 * (q - row * XQ);
-            const bool ok = q < nxq && p >= 0 && p + 4 <= Tin;
-            rx[e] = *(const f32x4*)(xc + (ok ? (int64_t)row * Tin + p : 0));
+            for (int e = 0; e < C2X_MAXQ; ++e) {
+                const int q = tid + NT * e;
+                const int row = q / XQ, p = g.ab + 4 * (q - row * XQ);
+                const bool ok = q < nxq && p >= 0 && p + 4 <= Tin;
+                rx[e] = *(const f32x4*)(xc + (ok ? (int64_t)row * Tin + p : 0));
+            }
+        } else {  // rows not 16-B aligned (T 75): the quad's elements one by one (the edges patched later)
+#pragma unroll
+            for (int e = 0; e < C2X_MAXQ; ++e) {
+                const int q = tid + NT * e;
+                const int row = q / XQ, p = g.ab + 4 * (q - row * XQ);
+                const bool ok = q < nxq && p >= 0 && p + 4 <= Tin;
+                const float* src = xc + (ok ? (int64_t)row * Tin + p : 0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) rx[e][i] = src[ok ? i : 0];
+            }
         }
     };
     auto store_x = [&](int c, float* xs) {
@@ -1686,6 +1699,7 @@ __global__ __launch_bounds__(NT) void conv_fwd2_kernel(FwdArgs a) {
     g.pl = a.pl;
     g.e = a.e;
     g.mode = a.mode;
+    g.vec = (a.Tin & 3) == 0;
     g.wsrc = a.wf + (int64_t)cbeg * K * a.Cout + co0;
     g.wstride = a.Cout;
     g.CK = a.CK;
@@ -1795,7 +1809,9 @@ static int launch_fwd2_tile(FwdArgs a, size_t lds, hipStream_t st) {
     return 0;
 }
 static bool fwd2_shape_ok(const FwdArgs& a) {
-    return encx_opt(OPT_CONV2) && a.d == 1 && a.e == 0 && a.Tin % 4 == 0 && a.Cout > 4 && a.Tout > FLAT_T &&
+    // (T <= 64: the flattened GEMM; between that and FLAT_T the v2 tiles of 64 columns, option CONV2_LOWT)
+    const int64_t tmin = encx_opt(OPT_CONV2_LOWT) ? 64 : FLAT_T;
+    return (encx_opt(OPT_CONV2) & 1) && a.d == 1 && a.e == 0 && a.Cout > 4 && a.Tout > tmin &&
            ((uintptr_t)a.x | (uintptr_t)a.wf) % 16 == 0 && a.Cout % 4 == 0;
 }
 template <int K, int S>
@@ -1835,7 +1851,7 @@ static int conv_fwd2_run(const FwdArgs& a, float* ws, hipStream_t st) {
     }
 }
 static size_t conv_fwd2_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K, int64_t s) {
-    if (!encx_opt(OPT_CONV2)) return 0;
+    if (!(encx_opt(OPT_CONV2) & 1)) return 0;
     C1Plan p;
     C1Plan q;
     if (!c1_plan((int)B, (int)Cin, (int)Cout, (int)Tout, (int)K, (int)s, (int)(Cout * Tout), true, &p)) p.KS = 1;
@@ -1873,6 +1889,7 @@ __global__ __launch_bounds__(NT) void conv_poly2_kernel(PolyArgs a) {
     g.pl = 0;
     g.e = 0;
     g.mode = ENCX_PAD_ZERO;
+    g.vec = (a.Tin & 3) == 0;
     g.wsrc = a.wp + (int64_t)cbeg * J * M + m0;
     g.wstride = M;
     g.CK = a.CK;
@@ -1976,8 +1993,8 @@ static int launch_poly2_j(PolyArgs a, int ncols, float* ws, hipStream_t st) {
 }
 // -1: not served by v2. a.Q must be set (ncols * s).
 static int poly2_run(const PolyArgs& a, int ncols, float* ws, hipStream_t st) {
-    if (!encx_opt(OPT_CONV2) || ncols <= FLAT_T || a.Tin % 4 || ((uintptr_t)a.in | (uintptr_t)a.wp) % 16 ||
-        (a.Co * a.s) % 4)
+    if (!(encx_opt(OPT_CONV2) & 2) || ncols <= (encx_opt(OPT_CONV2_LOWT) ? 64 : FLAT_T) ||
+        ((uintptr_t)a.in | (uintptr_t)a.wp) % 16 || (a.Co * a.s) % 4)
         return -1;
     switch (a.J) {
         case 1: return launch_poly2_j<1>(a, ncols, ws, st);
@@ -1988,7 +2005,7 @@ static int poly2_run(const PolyArgs& a, int ncols, float* ws, hipStream_t st) {
     }
 }
 static size_t poly2_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int64_t J) {
-    if (!encx_opt(OPT_CONV2) || ncols <= FLAT_T) return 0;
+    if (!(encx_opt(OPT_CONV2) & 2) || ncols <= 64) return 0;
     C1Plan p;
     C1Plan q;
     if (!c1_plan((int)B, (int)Ci, (int)(Co * s), (int)ncols, (int)J, 1, (int)(Co * ncols * s), true, &p)) p.KS = 1;
@@ -2075,6 +2092,12 @@ size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K
 }
 
 int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
+    {
+        PolyArgs a2 = a;
+        a2.Q = ncols * a.s;
+        const int rc = poly2_run(a2, ncols, ws, st);
+        if (rc >= 0) return rc;
+    }
     if (ncols <= FLAT_T) {
         const int M = a.Co * a.s, Kred = a.Ci * a.J, N = a.B * ncols;
         const int splits = gemm_splits(M, N, Kred);
@@ -2093,12 +2116,6 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
             ENCX_CHECK_LAUNCH();
         }
         return 0;
-    }
-    {
-        PolyArgs a2 = a;
-        a2.Q = ncols * a.s;
-        const int rc = poly2_run(a2, ncols, ws, st);
-        if (rc >= 0) return rc;
     }
     PolyPlan p = plan_poly(a.B, a.Ci, (int64_t)a.Co * a.s, ncols, a.J,
                            a.mode != 0 && (a.act != ENCX_ACT_NONE || a.accumulate));
@@ -2124,7 +2141,7 @@ size_t poly_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int6
     if (ncols <= FLAT_T) {
         const int Kred = (int)(Ci * J);
         const int slabs = gemm_slabs(Kred, gemm_splits((int)(Co * s), (int)(B * ncols), Kred));
-        return slabs > 1 ? (size_t)slabs * B * Co * ncols * s * sizeof(float) : 0;
+        return std::max(v2, slabs > 1 ? (size_t)slabs * B * Co * ncols * s * sizeof(float) : (size_t)0);
     }
     size_t ws = 0;
     for (const bool heavy : {false, true}) {
@@ -2163,8 +2180,6 @@ static WgPlan plan_wgrad(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K)
     // <= 32 MB of partials: the slabs are written and read back once each (64 MB cost the big
     // weights 10 % over 32 MB, round 5 sweep; the small ones never reach the cap)
     int64_t cap = (32ll << 20) / (4 * A * N);
-    int64_t minper = cdiv(p.items, (int64_t)p.items >= 8 ? 8 : 1);
-    (void)minper;
     if (cap < 1) cap = 1;
     int64_t sp = want < cap ? want : cap;
     if (sp > p.items / 4) sp = p.items / 4;              // >= 4 chunks of t per workgroup
@@ -2375,7 +2390,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad2_kernel(Wg2Args a) {
 }
 struct Wg2Plan { int BM, BN, splits, per_split, items, NC, WLp; size_t lds; };
 static bool plan_wgrad2(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K, int64_t S, Wg2Plan* p) {
-    if (!encx_opt(OPT_CONV2) || Tl % 4 || Tl < W2_PT || A % 64) return false;
+    if (!(encx_opt(OPT_CONV2) & 4) || Tl % 4 || Tl < W2_PT || A % 64) return false;
     p->BM = 64;
     const int64_t N = C * K;
     p->BN = N >= 128 ? 128 : 64;
@@ -2567,7 +2582,7 @@ int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float
     // (the long 1x1 layers go to the v2 polyphase kernel when it is on)
     if (pw_ok((int)K, (int)stride, 1, (int)pad_left, (int)pad_right, (int)short_ext, (int)Tin, (int)Tout, (int)Cin,
               (int)Cout, (int)Cout) &&
-        !(encx_opt(OPT_CONV2) && Tout > encx_opt(OPT_PW_TMAX))) {
+        !((encx_opt(OPT_CONV2) & 2) && Tout > encx_opt(OPT_PW_TMAX))) {
         // dx[b][ci][t] = sum_co wp[co][ci] dy[b][co][t], * act'(x), (+ dx)
         PwArgs p{wp, dy, nullptr, nullptr, x, dx, (int)Cin, (int)Cout, (int)Tout, ENCX_ACT_NONE, pre_act};
         const int epi = (pre_act != ENCX_ACT_NONE ? PW_XACT : 0) | (accumulate ? PW_ACC : 0);

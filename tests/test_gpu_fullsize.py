@@ -121,12 +121,13 @@ def test_seanet_layers_b32_vs_fp64(stack):
     assert not bad, bad
 
 
-@pytest.mark.parametrize('seg', [48000, 4800])
+@pytest.mark.parametrize('seg', [48000, 4800, 320])
 @pytest.mark.parametrize('stack', ['encoder', 'decoder'])
 def test_seanet_layers_48k_vs_fp64(stack, seg):
     """The config-5 SEANet stack (48 kHz stereo: non-causal, symmetric reflect padding,
     time_group_norm convs with plain weights) layer by layer at B 2 and the 1 s segment's lengths
-    (48000 samples down to 150 frames; and the 0.1 s segments of the g9 fixture's model): output, input grad and parameter grads within 2e-5 of the
+    (48000 samples down to 150 frames; the 0.1 s segments of the g9 fixture's model; and its
+    one-frame tail segment, whose decoder runs the linked convs at 160 and 320 samples): output, input grad and parameter grads within 2e-5 of the
     fp64 restatement, relative to the tensor's largest magnitude."""
     from encx.model import EncodecModel
     from encx.modules.seanet import SEANetResnetBlock
