@@ -40,7 +40,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {OPT_FWR, "FWR", 256}, {OPT_DGR, "DGR", 256}, {OPT_WGR, "WGR", 2048},
     {OPT_WGR_WGS, "WGR_WGS", 256}, {OPT_FEAT_CODE, "FEAT_CODE", 1}, {OPT_CONV_CK, "CONV_CK", 64},
     {OPT_CONV_SPLIT, "CONV_SPLIT", 1024}, {OPT_CONV_WG_SPLIT, "CONV_WG_SPLIT", 1024},
-    {OPT_CONV2, "CONV2", 0}, {OPT_CONV2_TILE, "CONV2_TILE", 0}, {OPT_CONV2_RED, "CONV2_RED", 64},
+    {OPT_CONV2, "CONV2", 7}, {OPT_CONV2_TILE, "CONV2_TILE", 0}, {OPT_CONV2_RED, "CONV2_RED", 64},
     {OPT_CONV2_KS, "CONV2_KS", 0}, {OPT_CONV2_WGS, "CONV2_WGS", 512},
     {OPT_CONV2_LOWT, "CONV2_LOWT", 0},
     {OPT_LSTM_SPIN, "LSTM_SPIN", 0}, {OPT_LSTM_FAULT, "LSTM_FAULT", 0},

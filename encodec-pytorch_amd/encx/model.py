@@ -125,14 +125,17 @@ class EncodecModel(nn.Module):
         frames = self.encode(x)
         if self.training:
             bw = self._pick_bandwidth(x.device) if bandwidth is None else bandwidth
-            codes = []
+            codes, seg_codes = [], []
             loss_w = None
             for emb, scale in frames:
                 qv = self.quantizer(emb, self.frame_rate, bw)
+                seg_codes.append((qv.codes, emb.detach()))
                 pen = qv.penalty.reshape(1)  # loss_w = tensor([0.]) + penalty (model.py:199,208)
                 loss_w = pen if loss_w is None else loss_w + pen
                 codes.append((qv.quantized, scale))
             self.last_codes = [qv.codes]
+            # every segment's (codes [n_q, B*T], latent [B, D, T]): the tests' nearest-code audit
+            self.seg_codes = seg_codes
             self.last_split = None
             if split and len(codes) == 1:
                 q, scale = codes[0]

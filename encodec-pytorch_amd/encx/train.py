@@ -361,7 +361,7 @@ class Trainer:
         out = ent[3]
         # this key's graphs rewrite its own codes tensor (held by the entry, so its pool block is
         # never handed to another key); after another key ran, last_codes must point back at it
-        self.model.last_codes = ent[4]
+        self.model.last_codes, self.model.seg_codes = ent[4]
         # the replayed graphs rewrite `out` in place: hand the caller a copy of this step's values
         names = list(out)
         vals = torch.cat([out[k].detach().reshape(-1)[:1] for k in names])
@@ -395,7 +395,7 @@ class Trainer:
             pg.replay()
         if self._seg_hook is not None:
             self._seg_hook(len(segs) - 1, c)
-        return graphs, colls, xs, c['out'], self.model.last_codes, c
+        return graphs, colls, xs, c['out'], (self.model.last_codes, self.model.seg_codes), c
 
     # ------------------------------------------------------------------ checkpoints
     def state_dicts(self):

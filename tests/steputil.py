@@ -120,6 +120,51 @@ def lrelu_audit(feat=None):
 U32 = 2.0 ** -24  # unit roundoff of fp32
 
 
+@contextlib.contextmanager
+def code_impose(seg_codes):
+    """The oracle's rvq_train takes our codes (seg_codes: the model's [(codes, emb)] per segment,
+    EncodecModel.seg_codes) and logs its own picks beside them; yields the audit list for
+    check_code_ties."""
+    O.CODES = [c.detach().cpu() for c, _ in seg_codes]
+    O.CODE_AUDIT = log = []
+    try:
+        yield log
+    finally:
+        O.CODES = None
+        O.CODE_AUDIT = None
+
+
+def check_code_ties(log, seg_codes, n_q, what):
+    """Every code the oracle took from us where its own pick differs must be a near tie: with D
+    the squared distance, D64(x, ours) - D64(x, own) at most the error of our fp32 evaluation of
+    the two distances (gamma_{d+2} (|x| + |e|)^2 each, core_vq.py:181-189's expanded form) plus
+    the change the difference of our latent from the fp64 one can make, 2 |dx| |e_ours - e_own|
+    (dx: the latent rows' difference -- the same codes are subtracted on both sides -- plus the
+    fp32 rounding of i residual subtractions). Returns the number of imposed codes."""
+    n_imp = 0
+    for k, (xf, embed, own, imp) in enumerate(log):
+        seg, i = divmod(k, n_q)
+        diff = (own != imp.to(own.device)).nonzero().flatten()
+        if diff.numel() == 0:
+            continue
+        x = xf.double()
+        e = embed.double()
+        emb64 = log[seg * n_q][0].double()
+        emb = seg_codes[seg][1].double().cpu().permute(0, 2, 1).reshape(emb64.shape).to(emb64.device)
+        for r in diff.tolist():
+            a, b = int(imp[r]), int(own[r])
+            da = float(((x[r] - e[a]) ** 2).sum())
+            db = float(((x[r] - e[b]) ** 2).sum())
+            xn, ea, eb = float(x[r].norm()), float(e[a].norm()), float(e[b].norm())
+            dx = float((emb[r] - emb64[r]).norm()) + (i + 1) * 2 * U32 * (xn + ea + eb)
+            g = _gamma(x.shape[1] + 2)
+            bound = 2 * dx * float((e[a] - e[b]).norm()) + g * ((xn + ea) ** 2 + (xn + eb) ** 2)
+            assert da - db <= bound, (what, f'segment {seg} layer {i} row {r}: our code {a} vs the fp64 pick {b}: '
+                                      f'D {da:.9e} vs {db:.9e}, margin {da - db:.3e} > bound {bound:.3e}')
+            n_imp += 1
+    return n_imp
+
+
 def _gamma(n):
     """gamma_n = n u / (1 - n u): the a-priori relative bound of an n-term fp32 dot product, any
     summation order (Higham, Accuracy and Stability of Numerical Algorithms, eq. 3.4)."""
@@ -352,9 +397,14 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device=
     # no rounding bound covers
     masks = split_masks(store, len(tr.disc.discriminators)) if tr.disc is not None else None
     f64 = []
-    with lrelu_audit(f64) as a64:
+    # and its nearest codes follow ours where the two are a near tie (check_code_ties)
+    seg_codes = tr.model.seg_codes
+    with lrelu_audit(f64) as a64, code_impose(seg_codes) as clog:
         o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks, device)
-    o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks, device)
+    with code_impose(seg_codes):
+        o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks, device)
+    n_imp = check_code_ties(clog, seg_codes, O.rvq_num_quantizers(bandwidth, cfg.frame_rate, n_q_max=cfg.n_q),
+                            'step code audit')
     if masks is not None:
         # the discriminator's weights as its maps were computed: the pre-step snapshot
         check_flips(tr.disc, snap['disc']['p'], ins, store, a64, f64 if 'l_feat' in weights else None,
@@ -376,5 +426,5 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device=
     if verbose:
         worst = max(table, key=lambda r: r[1] / r[3])
         print(f'step vs oracle: {len(table)} tensors, worst grad err {max(r[1] for r in table):.2e}, '
-              f'tightest {worst[0]} {worst[1]:.2e} / bound {worst[3]:.2e}')
+              f'tightest {worst[0]} {worst[1]:.2e} / bound {worst[3]:.2e}; {n_imp} near-tie codes imposed')
     return out, table

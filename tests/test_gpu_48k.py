@@ -104,15 +104,19 @@ def test_forward_48k_vs_oracle_fp64():
     assert len(frames) == 2 and frames[1][0].shape[-1] == 1  # 48 samples -> one 150 Hz frame
     gy = T(rng(95).standard_normal(size=tuple(y.shape)).astype(np.float32)).to(DEV)
     torch.autograd.backward([y, loss_w], [gy, torch.ones_like(loss_w)])
+    from steputil import check_grads, code_impose, check_code_ties
+    # the oracle's nearest codes follow ours where the two are within rounding of a tie
     p64 = {k: v.double().requires_grad_(True) for k, v in p.items()}
     cbs64 = [{k: v.double() for k, v in cb.items()} for cb in cbs]
-    y64, lw64, _, _, _ = O.encodec_forward_train(T(d['gen/x']).double(), p64, cbs64, cfg, 3.0)
+    with code_impose(m.seg_codes) as clog:
+        y64, lw64, _, _, _ = O.encodec_forward_train(T(d['gen/x']).double(), p64, cbs64, cfg, 3.0)
+    check_code_ties(clog, m.seg_codes, O.rvq_num_quantizers(3.0, cfg.frame_rate, n_q_max=cfg.n_q), '48 kHz codes')
     torch.autograd.backward([y64, lw64], [gy.cpu().double(), torch.ones_like(lw64)])
     assert rel(y, y64) < 1e-4, rel(y, y64)
-    from steputil import check_grads
     p32 = {k: v.float().requires_grad_(True) for k, v in p.items()}
     cbs32 = [{k: v.float() for k, v in cb.items()} for cb in cbs]
-    y32, lw32, _, _, _ = O.encodec_forward_train(T(d['gen/x']).float(), p32, cbs32, cfg, 3.0)
+    with code_impose(m.seg_codes):
+        y32, lw32, _, _, _ = O.encodec_forward_train(T(d['gen/x']).float(), p32, cbs32, cfg, 3.0)
     torch.autograd.backward([y32, lw32], [gy.cpu(), torch.ones_like(lw32)])
     params = dict(m.named_parameters())
     check_grads({k: params[k].grad for k in p64}, {k: v.grad for k, v in p64.items()},

@@ -434,3 +434,46 @@ def test_oracle_lm_compress_fixture():
     cfg, st = g12_lm_config('a')
     p = L.lm_all(st, T(codes), cfg)                   # [1][card][K][T]
     close(p[0].permute(2, 1, 0).reshape(-1, cfg.card), d['e2e_pdf'], rtol=1e-4, atol=1e-7)
+
+
+def test_code_impose_and_tie_audit():
+    """steputil.code_impose / check_code_ties (the GPU step checks' nearest-code audit): the
+    oracle's rvq_train takes the imposed codes in order, logs its own picks, and the audit passes
+    a flip between two codes at the same distance (within our latent's distance from the fp64
+    one) and refuses a flip to a far code."""
+    from steputil import code_impose, check_code_ties
+    g = torch.Generator().manual_seed(3)
+    B, D, Tn, K, n_q = 2, 8, 5, 16, 2
+    emb = torch.randn(B, D, Tn, generator=g, dtype=torch.float64)
+    cbs = [{'inited': torch.ones(1), 'cluster_size': torch.ones(K, dtype=torch.float64),
+            'embed': torch.randn(K, D, generator=g, dtype=torch.float64),
+            'embed_avg': torch.randn(K, D, generator=g, dtype=torch.float64)} for _ in range(n_q)]
+    # row 0's first-layer target made equidistant from codes 3 and 5
+    x0 = 0.5 * (cbs[0]['embed'][3] + cbs[0]['embed'][5])
+    emb[0, :, 0] = x0
+    _, own, _, _ = O.rvq_train(emb, cbs, n_q)
+    assert int(own[0, 0, 0]) in (3, 5)
+    seg = [(own.reshape(n_q, -1).clone(), emb.float())]
+    with code_impose(seg) as log:
+        _, got, _, _ = O.rvq_train(emb, cbs, n_q)
+    assert torch.equal(got, own) and len(log) == n_q
+    assert check_code_ties(log, seg, n_q, 'same') == 0
+    flip = own.reshape(n_q, -1).clone()
+    flip[0, 0] = 8 - int(own[0, 0, 0])  # the other of the tied pair
+    with code_impose([(flip, emb.float())]) as log:  # layer 1's picks after the flip
+        O.rvq_train(emb, cbs, n_q)
+    flip[1] = log[1][2]
+    seg = [(flip, emb.float())]
+    with code_impose(seg) as log:
+        _, got, _, _ = O.rvq_train(emb, cbs, n_q)
+    assert int(got[0, 0, 0]) == int(flip[0, 0])
+    assert check_code_ties(log, seg, n_q, 'tie') >= 1
+    far = own.reshape(n_q, -1).clone()
+    d = ((emb[0, :, 1][None] - cbs[0]['embed']) ** 2).sum(1)
+    far[0, 1] = int(d.argmax())
+    seg = [(far, emb.float())]
+    with code_impose(seg) as log:
+        O.rvq_train(emb, cbs, n_q)
+    with pytest.raises(AssertionError):
+        check_code_ties(log, seg, n_q, 'far')
+    assert O.CODES is None and O.CODE_AUDIT is None
