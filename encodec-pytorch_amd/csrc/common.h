@@ -4,6 +4,7 @@
 // v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md: 157 TF/s, bitwise an fmaf chain).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 
 #include "../../include/encx.h"
@@ -222,6 +223,16 @@ enum EncxOpt {
     OPT_CONV2_LOWT,    // v2 also for 64 < T <= 128 (the T 75 layers), else the flattened GEMMs
     OPT_LSTM_SPIN,     // persistent LSTM: log2 of every poll's spin bound (0: 20, about 1 s)
     OPT_LSTM_FAULT,    // persistent LSTM, tests only: one workgroup never publishes (its consumers time out)
+    OPT_BLAS,          // plain GEMMs through hipBLASLt (blas.hip): the LSTM weight grads, the im2col'd short convs
     OPT_COUNT
 };
 int64_t encx_opt(EncxOpt id);
+
+// blas.hip: C (m x n, column-major, ldc) = op(A) op(B) (+ C when accumulate), fp32 in, fp32
+// compute (HIPBLAS_COMPUTE_32F: the exact-f32 MFMA), on `st`, through hipBLASLt; `batch` > 1:
+// that many problems at element strides sa / sb / sc. Nonzero when hipBLASLt has no algorithm for
+// the problem or option BLAS is off (the caller runs its own kernels instead); plans and the
+// library workspace are cached per shape and device.
+int encx_sgemm(hipStream_t st, bool ta, bool tb, int m, int n, int k, const float* A, int lda, const float* B,
+               int ldb, float* C, int ldc, bool accumulate, int batch = 1, int64_t sa = 0, int64_t sb = 0,
+               int64_t sc = 0);

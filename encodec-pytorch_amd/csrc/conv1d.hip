@@ -1087,6 +1087,81 @@ struct EpPolyFlat {
     }
 };
 
+// ------------------------------------------------------------------------- short-T layers, library GEMM
+// The flattened layers with a large reduction (the k16 s8 stage at T 75: forward 512 x 2400 x
+// 4096, bwd-data and the transposed conv's polyphase 2048 x 2400 x 1024, their weight grads) as
+// im2col -> hipBLASLt -> epilogue: the flat loaders' gathers (pad modes, pre-activation) written
+// once into the workspace as a plain [N][Kred] matrix, the library's fp32 GEMM (blas.hip: 107-119
+// TF/s at these shapes against ~45 for the flattened implicit GEMM), then the flat epilogues
+// (bias, act'(xact), residual, accumulate, the polyphase fold and side columns) applied while
+// transposing the [N][M] product back through LDS.
+constexpr int WGB_ROWS = 160;  // positions per bias-partial chunk (blas_wgrad_run)
+static bool blas_flat_ok(int64_t M, int64_t N, int64_t Kred) {
+    return encx_opt(OPT_BLAS) && M >= 256 && Kred >= 512 && 2.0 * M * N * Kred >= 2.0e9;
+}
+// The reduction is cut into KB equal chunks (a strided batch of library GEMMs into KB product
+// slabs, summed in order in fp64 by the epilogue / reduce): one library accumulation chain over
+// all 4096 reduction elements (or 2400 positions) was 5-7x the error of plain fp32 in the config-3
+// step check. KB: up to 8, chunks of at least 256, at most 48 MB of slabs.
+static int blas_chunks(int64_t K, int64_t slab_elems) {
+    for (const int c : {8, 6, 4, 3, 2})
+        if (K % c == 0 && K / c >= 256 && (size_t)c * slab_elems * sizeof(float) <= (48ull << 20)) return c;
+    return 1;
+}
+static size_t blas_flat_ws(int64_t M, int64_t N, int64_t Kred) {
+    if (!blas_flat_ok(M, N, Kred)) return 0;
+    return (size_t)(N * Kred + (int64_t)blas_chunks(Kred, N * M) * N * M) * sizeof(float);
+}
+// out[n][k] = ld.b(k, n): a wave per 4 columns n, lanes along k (one (ci, tap) run per lane group)
+template <class Ld>
+__global__ __launch_bounds__(256) void im2col_kernel(Ld ld, int Kred, int N, float* out) {
+    const int k = blockIdx.x * 64 + (threadIdx.x & 63), n0 = blockIdx.y * 16 + (threadIdx.x >> 6) * 4;
+    if (k >= Kred) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (n0 + j < N) out[(int64_t)(n0 + j) * Kred + k] = ld.b(k, n0 + j);
+}
+// ep(m, n, sum_s Cm[s][n][m]) for the KB slabs of the [N][M] product (summed in slab order in
+// fp64), a 32 x 32 tile transposed through LDS so that the epilogue's stores run along n (t)
+template <class Ep>
+__global__ __launch_bounds__(256) void gemm_epi_kernel(Ep ep, const float* Cm, int M, int N, int KB) {
+    __shared__ float tile[32][33];
+    const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const int64_t NM = (int64_t)N * M;
+#pragma unroll
+    for (int r = ty; r < 32; r += 8) {
+        double v = 0.0;
+        if (n0 + r < N && m0 + tx < M) {
+            const float* c = Cm + (int64_t)(n0 + r) * M + m0 + tx;
+            for (int sl = 0; sl < KB; ++sl) v += (double)c[sl * NM];
+        }
+        tile[r][tx] = (float)v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = ty; r < 32; r += 8)
+        if (m0 + r < M && n0 + tx < N) ep(m0 + r, n0 + tx, tile[tx][r]);
+}
+template <class Ld, class Ep>
+static int blas_flat_run(const Ld& ld, const Ep& ep, const float* wA, int M, int N, int Kred, float* ws,
+                         hipStream_t st) {
+    float* Xc = ws;
+    float* Cm = ws + (int64_t)N * Kred;
+    hipLaunchKernelGGL(im2col_kernel<Ld>, dim3((unsigned)cdiv(Kred, 64), (unsigned)cdiv(N, 16)), dim3(256), 0, st,
+                       ld, Kred, N, Xc);
+    ENCX_CHECK_LAUNCH();
+    // slab c of Cm (M x N, column-major) = wA (M x Kred, column-major: the weights [Kred][M]) Xc^T
+    // over reduction chunk c
+    const int KB = blas_chunks(Kred, (int64_t)N * M), kc = Kred / KB;
+    if (encx_sgemm(st, false, false, M, N, kc, wA, M, Xc, Kred, Cm, M, false, KB, (int64_t)kc * M, kc,
+                   (int64_t)N * M))
+        return -1;
+    hipLaunchKernelGGL(gemm_epi_kernel<Ep>, dim3((unsigned)cdiv(M, 32), (unsigned)cdiv(N, 32)), dim3(256), 0, st,
+                       ep, Cm, M, N, KB);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
 // ------------------------------------------------------------------------- planning
 static int even_up(int v) { return (v + 1) & ~1; }
 
@@ -2027,6 +2102,10 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
     }
     if (fwd_flat(a.Cout, a.Tout)) {
         const int Kred = a.Cin * a.K, N = a.B * a.Tout;
+        if (ws && blas_flat_ok(a.Cout, N, Kred) &&
+            blas_flat_run(LdConvFlat{a, make_fastdiv(a.K), make_fastdiv(a.Tout)}, EpConvFlat{a, 1, make_fastdiv(a.Tout)},
+                          a.wf, a.Cout, N, Kred, ws, st) == 0)
+            return 0;
         const int splits = gemm_splits(a.Cout, N, Kred);
         const int slabs = gemm_slabs(Kred, splits);
         a.part = ws;
@@ -2080,7 +2159,8 @@ size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K
     const size_t v2 = conv_fwd2_ws(B, Cin, Cout, Tout, K, s);
     if (fwd_flat(Cout, Tout)) {
         const int slabs = fwd_flat_slabs(B, Cin, Cout, Tout, K);
-        return std::max(v2, slabs > 1 ? (size_t)slabs * B * Cout * Tout * sizeof(float) : (size_t)0);
+        return std::max({v2, slabs > 1 ? (size_t)slabs * B * Cout * Tout * sizeof(float) : (size_t)0,
+                         blas_flat_ws(Cout, B * Tout, Cin * K)});
     }
     // (the epilogue's operands are not known here: the larger of the two plans)
     size_t ws = 0;
@@ -2100,9 +2180,14 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
     }
     if (ncols <= FLAT_T) {
         const int M = a.Co * a.s, Kred = a.Ci * a.J, N = a.B * ncols;
+        a.Q = ncols * a.s;
+        if (ws && blas_flat_ok(M, N, Kred) &&
+            blas_flat_run(LdPolyFlat{a, M, ncols, make_fastdiv(a.J), make_fastdiv(ncols)},
+                          EpPolyFlat{a, ncols, 1, make_fastdiv(a.s), make_fastdiv(ncols)}, a.wp, M, N, Kred, ws,
+                          st) == 0)
+            return 0;
         const int splits = gemm_splits(M, N, Kred);
         const int slabs = gemm_slabs(Kred, splits);
-        a.Q = ncols * a.s;
         a.part = ws;
         a.KS = slabs;
         ENCX_REQUIRE(slabs == 1 || ws);
@@ -2141,7 +2226,8 @@ size_t poly_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int6
     if (ncols <= FLAT_T) {
         const int Kred = (int)(Ci * J);
         const int slabs = gemm_slabs(Kred, gemm_splits((int)(Co * s), (int)(B * ncols), Kred));
-        return std::max(v2, slabs > 1 ? (size_t)slabs * B * Co * ncols * s * sizeof(float) : (size_t)0);
+        return std::max({v2, slabs > 1 ? (size_t)slabs * B * Co * ncols * s * sizeof(float) : (size_t)0,
+                         blas_flat_ws(Co * s, B * ncols, Kred)});
     }
     size_t ws = 0;
     for (const bool heavy : {false, true}) {
@@ -2463,10 +2549,99 @@ static size_t wgrad2_ws(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K, 
     return (size_t)p.splits * A * (C * K + 1) * sizeof(float);
 }
 
+// ---- weight grads of the short-T layers through hipBLASLt: dw (A x C K) = L^T-rows x im2col(R)
+// over the N = B Tl positions: L transposed to [N][A] (with its pre-activation), R gathered as the
+// forward's im2col [N][C K], one library GEMM straight into dw (accumulating when asked); the
+// bias (db = sum of L over positions) as fixed-order column sums of the transposed L
+static bool blas_wgrad_ok(int64_t A, int64_t Tl, int64_t N, int64_t CK) {
+    return Tl <= FLAT_T && blas_flat_ok(CK, A, N) && A >= 64;
+}
+static size_t blas_wgrad_ws(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
+    const int64_t N = B * Tl;
+    if (!blas_wgrad_ok(A, Tl, N, C * K)) return 0;
+    return (size_t)(N * A + N * C * K + cdiv(N, WGB_ROWS) * A + blas_chunks(N, A * C * K) * A * C * K) *
+           sizeof(float);
+}
+// Lt[b Tl + t][a] = act(L[b][a][t]), 32 x 32 tiles through LDS
+__global__ __launch_bounds__(256) void wg_transpose_kernel(const float* L, float* Lt, int A, int Tl, int act) {
+    __shared__ float tile[32][33];
+    const int t0 = blockIdx.x * 32, a0 = blockIdx.y * 32, b = blockIdx.z, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+    for (int r = ty; r < 32; r += 8)
+        tile[r][tx] = (a0 + r < A && t0 + tx < Tl) ? act_apply(act, L[((int64_t)b * A + a0 + r) * Tl + t0 + tx]) : 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int r = ty; r < 32; r += 8)
+        if (t0 + r < Tl && a0 + tx < A) Lt[((int64_t)b * Tl + t0 + r) * A + a0 + tx] = tile[tx][r];
+}
+// db[a] (+)= sum over n of Lt[n][a]: chunk c of WGB_ROWS rows per workgroup column block (4 row
+// lanes, each ascending, then the lanes in order), then the chunks in order
+__global__ __launch_bounds__(256) void wg_colsum_part(const float* Lt, int N, int A, float* part) {
+    __shared__ float red[4][65];
+    const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c, n0 = blockIdx.y * WGB_ROWS, n1 = min(N, n0 + WGB_ROWS);
+    float sum = 0.f;
+    if (j < A)
+        for (int n = n0 + r; n < n1; n += 4) sum += Lt[(int64_t)n * A + j];
+    red[r][c] = sum;
+    __syncthreads();
+    if (r == 0 && j < A) part[(int64_t)blockIdx.y * A + j] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+__global__ __launch_bounds__(256) void wg_colsum_fin(const float* part, int nch, int A, float* db, int acc) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= A) return;
+    float v = part[j];
+    for (int c = 1; c < nch; ++c) v += part[(int64_t)c * A + j];
+    db[j] = acc ? db[j] + v : v;
+}
+static int blas_wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, int64_t A, int64_t Tl,
+                          int64_t C, int64_t Tr, int64_t K, int64_t s, int64_t d, int64_t pl, int64_t e, int mode,
+                          int actL, int actR, int accumulate, hipStream_t st, float* db, int acc_b) {
+    const int64_t N = B * Tl, CK = C * K;
+    if (!ws || !blas_wgrad_ok(A, Tl, N, CK)) return -1;
+    if (db && actL != ENCX_ACT_NONE) return -1;
+    float* Lt = ws;
+    float* Rc = ws + N * A;
+    float* part = Rc + N * CK;
+    float* slabs = part + cdiv(N, WGB_ROWS) * A;
+    hipLaunchKernelGGL(wg_transpose_kernel, dim3((unsigned)cdiv(Tl, 32), (unsigned)cdiv(A, 32), (unsigned)B), dim3(256),
+                       0, st, L, Lt, (int)A, (int)Tl, actL);
+    ENCX_CHECK_LAUNCH();
+    FwdArgs r{};
+    r.x = R; r.B = (int)B; r.Cin = (int)C; r.Tin = (int)Tr; r.K = (int)K; r.s = (int)s; r.d = (int)d; r.pl = (int)pl;
+    r.e = (int)e; r.mode = mode; r.act = actR; r.Tout = (int)Tl;
+    const LdConvFlat ld{r, make_fastdiv((int)K), make_fastdiv((int)Tl)};
+    hipLaunchKernelGGL(im2col_kernel<LdConvFlat>, dim3((unsigned)cdiv(CK, 64), (unsigned)cdiv(N, 16)), dim3(256), 0,
+                       st, ld, (int)CK, (int)N, Rc);
+    ENCX_CHECK_LAUNCH();
+    // slab c (C K x A, column-major = [A][C][K]) = Rc (C K x N) Lt (A x N)^T over position chunk c,
+    // then the slabs in order into dw (wgrad_reduce, fp64)
+    const int KB = blas_chunks(N, A * CK), kc = (int)(N / KB);
+    if (encx_sgemm(st, false, true, (int)CK, (int)A, kc, Rc, (int)CK, Lt, (int)A, slabs, (int)CK, false, KB,
+                   (int64_t)kc * CK, (int64_t)kc * A, A * CK))
+        return -1;
+    hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)cdiv(A * CK, 64)), dim3(256), 0, st, slabs, dw, A * CK, KB,
+                       accumulate, nullptr, nullptr, (int)A, 0);
+    ENCX_CHECK_LAUNCH();
+    if (db) {
+        const int nch = (int)cdiv(N, WGB_ROWS);
+        hipLaunchKernelGGL(wg_colsum_part, dim3((unsigned)cdiv(A, 64), (unsigned)nch), dim3(256), 0, st, Lt, (int)N,
+                           (int)A, part);
+        hipLaunchKernelGGL(wg_colsum_fin, dim3((unsigned)cdiv(A, 256)), dim3(256), 0, st, part, nch, (int)A, db, acc_b);
+        ENCX_CHECK_LAUNCH();
+    }
+    return 0;
+}
+
 int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, int64_t A,
               int64_t Tl, int64_t C, int64_t Tr, int64_t K, int64_t s, int64_t d, int64_t pl,
               int64_t e, int mode, int actL, int actR, int accumulate, hipStream_t st,
               float* db = nullptr, int acc_b = 0) {
+    {
+        const int rc = blas_wgrad_run(L, R, dw, ws, B, A, Tl, C, Tr, K, s, d, pl, e, mode, actL, actR, accumulate, st,
+                                      db, acc_b);
+        if (rc >= 0) return rc;
+    }
     {
         const int rc = wgrad2_run(L, R, dw, ws, B, A, Tl, C, Tr, K, s, d, pl, e, mode, actL, actR, accumulate, st, db,
                                   acc_b);
@@ -2513,7 +2688,8 @@ int wgrad_run(const float* L, const float* R, float* dw, float* ws, int64_t B, i
 size_t wgrad_ws_bytes(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
     WgPlan p = plan_wgrad(B, A, Tl, C, K);
     // (+ the bias slabs; the v2 plan's splits do not depend on the stride)
-    return std::max((size_t)p.splits * A * (C * K + 1) * sizeof(float), wgrad2_ws(B, A, Tl, C, K, 1));
+    return std::max({(size_t)p.splits * A * (C * K + 1) * sizeof(float), wgrad2_ws(B, A, Tl, C, K, 1),
+                     blas_wgrad_ws(B, A, Tl, C, K)});
 }
 
 static size_t maxz(size_t a, size_t b) { return a > b ? a : b; }

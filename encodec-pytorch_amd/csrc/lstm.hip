@@ -783,10 +783,9 @@ struct LdWcat {
         const int mm = rec ? (m > 0 ? m - 1 : 0) : m;
         const float v = (rec ? Yl : in)[(int64_t)mm * H + u];
         const int t = m - (int)fdiv((uint32_t)m, fT) * T;
-        return n == 2 * H ? 1.f : (rec && t == 0 ? 0.f : v);
+        return rec && t == 0 ? 0.f : v;
     }
-    // quads (H % 4 == 0, so a quad never straddles the x | h boundary; the ones column n = 2H
-    // only ever sits in the scalar edge quad)
+    // quads (H % 4 == 0, so a quad never straddles the x | h boundary)
     ENCX_DEV f32x4 a4(int j, int m) const { return ld4u(DA + (int64_t)m * 4 * H + j); }
     ENCX_DEV f32x4 b4(int m, int n) const {
         if (n + 3 >= 2 * H) {
@@ -808,42 +807,76 @@ struct EpSlabs {  // split-K partial slabs [z][M][N]
         ws[((int64_t)blockIdx.z * M + m) * N + n] = v;
     }
 };
-// unsplit weight grad: the GEMM's element straight into dw_ih (n < H), dw_hh (n < 2H) and the bias
-// grads (n == 2H, to both); += when acc (the same bits as one slab through lstm_slab_reduce)
+// unsplit weight grad: the GEMM's element straight into dw_ih (n < H) or dw_hh (n < 2H); += when
+// acc (the same bits as one slab through lstm_slab_reduce)
 struct EpDWcat {
     float* dwi;
     float* dwh;
-    float* db1;
-    float* db2;
     int H, acc;
     ENCX_DEV void operator()(int m, int n, float v) const {
-        if (n < 2 * H) {
-            float* p = n < H ? dwi + (int64_t)m * H + n : dwh + (int64_t)m * H + (n - H);
-            *p = acc ? *p + v : v;
-        } else {
-            if (db1) db1[m] = acc ? db1[m] + v : v;
-            if (db2) db2[m] = acc ? db2[m] + v : v;
-        }
+        if (n >= 2 * H) return;
+        float* p = n < H ? dwi + (int64_t)m * H + n : dwh + (int64_t)m * H + (n - H);
+        *p = acc ? *p + v : v;
     }
 };
-// sum split slabs [S][4H][2H+1] in ascending slab order into dw_ih (n < H), dw_hh (n < 2H) and
-// the bias grad (n == 2H, written to both b_ih and b_hh grads); += when acc
+// sum split slabs [S][4H][2H] in ascending slab order into dw_ih (n < H) and dw_hh; += when acc
 __global__ __launch_bounds__(256) void lstm_slab_reduce(const float* ws, int S, int H, float* dwi, float* dwh,
-                                                        float* db1, float* db2, int acc) {
+                                                        int acc) {
     __shared__ float red[256];
-    const int M = 4 * H, N = 2 * H + 1;
+    const int M = 4 * H, N = 2 * H;
     const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const bool valid = i < (int64_t)M * N;
     const float s = slab_sum_256(ws + (valid ? i : 0), S, (int64_t)M * N, valid, red);
     if (threadIdx.x >= 64 || !valid) return;
     const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
-    float* p = n < H ? dwi + (int64_t)m * H + n : n < 2 * H ? dwh + (int64_t)m * H + (n - H) : nullptr;
-    if (p) {
-        *p = acc ? *p + s : s;
-    } else {
-        if (db1) db1[m] = acc ? db1[m] + s : s;
-        if (db2) db2[m] = acc ? db2[m] + s : s;
+    float* p = n < H ? dwi + (int64_t)m * H + n : dwh + (int64_t)m * H + (n - H);
+    *p = acc ? *p + s : s;
+}
+// the bias grads (b_ih and b_hh get the same): db[j] = sum over the B T positions m of DA[m][j],
+// as a column sum beside the weight-grad GEMM (in the GEMM, as a ones column, 2H + 1 columns took
+// a ninth 128-column tile for one column). Fixed order: part[c][j] sums the rows of chunk c of
+// BIAS_ROWS (4 row lanes, each ascending, then the lanes in order); lstm_bias_fin sums the chunks
+// in order.
+constexpr int BIAS_ROWS = 160;
+__global__ __launch_bounds__(256) void lstm_bias_part(const float* DA, int M, int N4, float* part) {
+    __shared__ float red[4][65];
+    const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c, m0 = blockIdx.y * BIAS_ROWS, m1 = min(M, m0 + BIAS_ROWS);
+    float s = 0.f;
+    if (j < N4) {
+        const float* p = DA + j;
+        int m = m0 + r;
+        for (; m + 12 < m1; m += 16) {  // four rows in flight, added in row order
+            const float v0 = p[(int64_t)m * N4], v1 = p[(int64_t)(m + 4) * N4];
+            const float v2 = p[(int64_t)(m + 8) * N4], v3 = p[(int64_t)(m + 12) * N4];
+            s += v0;
+            s += v1;
+            s += v2;
+            s += v3;
+        }
+        for (; m < m1; m += 4) s += p[(int64_t)m * N4];
     }
+    red[r][c] = s;
+    __syncthreads();
+    if (r == 0 && j < N4) part[(int64_t)blockIdx.y * N4 + j] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+__global__ __launch_bounds__(256) void lstm_bias_fin(const float* part, int nchunk, int N4, float* db1, float* db2,
+                                                     int acc) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= N4) return;
+    float v = part[j];
+    for (int c = 1; c < nchunk; ++c) v += part[(int64_t)c * N4 + j];
+    if (db1) db1[j] = acc ? db1[j] + v : v;
+    if (db2) db2[j] = acc ? db2[j] + v : v;
+}
+// the recurrent operand of the weight grad as a plain matrix: hp[b][t] = h_l(t - 1) (0 at t = 0)
+__global__ __launch_bounds__(256) void lstm_hprev(const float* Yl, float* hp, int T, int H, int64_t n4) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // quad index
+    if (i >= n4) return;
+    const int64_t e = i * 4, row = e / H;
+    const int t = (int)(row % T);
+    const f32x4 v = t > 0 ? *(const f32x4*)(Yl + e - H) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    *(f32x4*)(hp + e) = v;
 }
 
 // ------------------------------------------------------------------------- dispatch
@@ -1146,10 +1179,18 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
     return 0;
 }
 
-size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H) {
-    const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
+}  // extern "C"
+// floats of the weight grad's main workspace: the own GEMM's split slabs, or the library GEMM's
+// 8 position-chunk slabs and the h(t-1) matrix; the bias partials follow
+static size_t wsl_main(int64_t B, int64_t T, int64_t H) {
+    const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H);
     const int S = gemm_slabs(M, gemm_splits_128(N4, Nw, M, 256, (int)encx_opt(OPT_LSTM_WG_SPLITS)));
-    return (size_t)S * N4 * Nw * sizeof(float);
+    return std::max((size_t)S * N4 * Nw, (size_t)8 * N4 * Nw + (size_t)B * T * H);
+}
+extern "C" {
+size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H) {
+    const int M = (int)(B * T), N4 = (int)(4 * H);
+    return (wsl_main(B, T, H) + (size_t)cdiv(M, BIAS_ROWS) * N4) * sizeof(float);
 }
 
 int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float* dw_ih, float* dw_hh,
@@ -1158,20 +1199,65 @@ int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float
     ENCX_REQUIRE(DA && xt && Y && dw_ih && dw_hh && ws);
     ENCX_REQUIRE(lstm_shape_ok(B, T, H, L) && layer >= 0 && layer < L);
     hipStream_t st = (hipStream_t)stream;
-    encx_prof_scope ps(st, 2.0 * B * T * 4 * H * (2 * H + 1), 4.0 * (B * T * H * 7 + 8 * H * H), "lstm_wgrad");
+    // (flops: the GEMM's 2 BT 4H 2H and the bias grads' BT 4H adds)
+    encx_prof_scope ps(st, 2.0 * B * T * 4 * H * 2 * H + (double)B * T * 4 * H, 4.0 * (B * T * H * 7 + 8 * H * H),
+                       "lstm_wgrad");
     ps.tag(" H%ld T%ld", (long)H, (long)T);
     const int64_t BTH = B * T * H;
     const float* in = layer == 0 ? xt : Y + (layer - 1) * BTH;
-    const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H + 1);
+    const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H);
     const int sp = gemm_splits_128(N4, Nw, M, 256, (int)encx_opt(OPT_LSTM_WG_SPLITS));
     const int S = gemm_slabs(M, sp);
-    const LdWcat ld{DA + layer * 4 * BTH, in, Y + layer * BTH, (int)H, (int)T, make_fastdiv((uint32_t)T)};
-    if (S == 1) return gemm_launch_128(ld, EpDWcat{dw_ih, dw_hh, db_ih, db_hh, (int)H, acc}, N4, Nw, M, st, 1);
-    int rc = gemm_launch_128(ld, EpSlabs{ws, N4, Nw}, N4, Nw, M, st, sp);
-    if (rc) return rc;
-    hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 64)), dim3(256), 0, st, ws, S,
-                       (int)H, dw_ih, dw_hh, db_ih, db_hh, acc);
-    ENCX_CHECK_LAUNCH();
+    const float* DAl = DA + layer * 4 * BTH;
+    const LdWcat ld{DAl, in, Y + layer * BTH, (int)H, (int)T, make_fastdiv((uint32_t)T)};
+    int rc;
+    // dW^T (H x 4H, column-major) = [x | h(t-1)]^T DA through hipBLASLt (blas.hip), else the own
+    // GEMM. The B T positions are cut into KB equal chunks of about 300 (a strided batch: one slab
+    // [4H][2H] per chunk, dW_ih^T and dW_hh^T side by side) summed in order by lstm_slab_reduce:
+    // one library accumulation chain over all 2400 positions of config 3 was 5x the error of plain
+    // fp32 (test_lstm_vs_oracle), the chunked form is within it.
+    int KB = 0;
+    for (const int c : {8, 6, 5, 4, 3, 2, 1})
+        if (M % c == 0 && M / c >= 64) {
+            KB = c;
+            break;
+        }
+    bool lib = KB > 0 && H % 4 == 0 && encx_opt(OPT_BLAS) && (size_t)KB * N4 * Nw <= wsl_main(B, T, H);
+    if (lib) {
+        const int kc = M / KB;
+        float* hp = ws + (size_t)KB * N4 * Nw;
+        hipLaunchKernelGGL(lstm_hprev, dim3((unsigned)cdiv(BTH / 4, 256)), dim3(256), 0, st, Y + layer * BTH, hp,
+                           (int)T, (int)H, BTH / 4);
+        ENCX_CHECK_LAUNCH();
+        lib = encx_sgemm(st, false, true, (int)H, N4, kc, in, (int)H, DAl, N4, ws, Nw, false, KB, (int64_t)kc * H,
+                         (int64_t)kc * N4, (int64_t)N4 * Nw) == 0 &&
+              encx_sgemm(st, false, true, (int)H, N4, kc, hp, (int)H, DAl, N4, ws + H, Nw, false, KB,
+                         (int64_t)kc * H, (int64_t)kc * N4, (int64_t)N4 * Nw) == 0;
+        if (lib) {
+            hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 64)), dim3(256), 0, st, ws,
+                               KB, (int)H, dw_ih, dw_hh, acc);
+            ENCX_CHECK_LAUNCH();
+        }
+    }
+    if (!lib && S == 1) {
+        rc = gemm_launch_128(ld, EpDWcat{dw_ih, dw_hh, (int)H, acc}, N4, Nw, M, st, 1);
+        if (rc) return rc;
+    } else if (!lib) {
+        rc = gemm_launch_128(ld, EpSlabs{ws, N4, Nw}, N4, Nw, M, st, sp);
+        if (rc) return rc;
+        hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 64)), dim3(256), 0, st, ws, S,
+                           (int)H, dw_ih, dw_hh, acc);
+        ENCX_CHECK_LAUNCH();
+    }
+    if (db_ih || db_hh) {
+        const int nch = (int)cdiv(M, BIAS_ROWS);
+        float* part = ws + wsl_main(B, T, H);
+        hipLaunchKernelGGL(lstm_bias_part, dim3((unsigned)cdiv(N4, 64), (unsigned)nch), dim3(256), 0, st, DAl, M, N4,
+                           part);
+        hipLaunchKernelGGL(lstm_bias_fin, dim3((unsigned)cdiv(N4, 256)), dim3(256), 0, st, part, nch, N4, db_ih,
+                           db_hh, acc);
+        ENCX_CHECK_LAUNCH();
+    }
     return 0;
 }
 

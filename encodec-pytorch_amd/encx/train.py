@@ -215,6 +215,7 @@ class Trainer:
             with fwd('gen'), defer():
                 y, loss_w, _ = self.model(x, bandwidth=bw, split=split)
             c['y'], c['loss_w'] = y, loss_w
+            c['y_out'] = self.last_y = y.detach()  # the step's generator output (tests' L1 sign audit)
             c['split'] = self.model.last_split
 
         def coll_gen():
@@ -362,6 +363,7 @@ class Trainer:
         # this key's graphs rewrite its own codes tensor (held by the entry, so its pool block is
         # never handed to another key); after another key ran, last_codes must point back at it
         self.model.last_codes, self.model.seg_codes = ent[4]
+        self.last_y = ent[5]['y_out']
         # the replayed graphs rewrite `out` in place: hand the caller a copy of this step's values
         names = list(out)
         vals = torch.cat([out[k].detach().reshape(-1)[:1] for k in names])

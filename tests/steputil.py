@@ -120,6 +120,47 @@ def lrelu_audit(feat=None):
 U32 = 2.0 ** -24  # unit roundoff of fp32
 
 
+def l1_signs(x, y, sr, device):
+    """The reconstruction L1s' signs of our step (oracle.L1_SIGNS): sign(x - y) of the wave and
+    sign(mel(x) - mel(y)) per loss_f scale, the mels evaluated in fp64 from our fp32 output."""
+    x64 = x.detach().to(device, torch.float64)
+    y64 = y.detach().to(device, torch.float64)
+    f = []
+    for i in range(5, 12):
+        n = 2 ** i
+        f.append(torch.sign(O.audio2mel(x64, n, n // 4, n, sr) - O.audio2mel(y64, n, n // 4, n, sr)))
+    return {'t': torch.sign(x64 - y64), 'f': f}
+
+
+@contextlib.contextmanager
+def l1_impose(signs):
+    O.L1_SIGNS = signs
+    O.L1_AUDIT = log = []
+    try:
+        yield log
+    finally:
+        O.L1_SIGNS = None
+        O.L1_AUDIT = None
+
+
+def check_l1_flips(log, what, rel=1e-4, frac=1e-3):
+    """Every L1 element where the imposed sign (our output's) differs from the oracle's own must be
+    a near tie: the oracle's |difference| there at most `rel` of the term's largest |difference|,
+    and such elements at most `frac` of the term. Returns the number of flips."""
+    n_flip = 0
+    for k, (d, sign) in enumerate(log):
+        own = torch.sign(d)
+        flips = (own != sign.to(own.device)) & (own != 0) & (sign.to(own.device) != 0)
+        nf = int(flips.sum())
+        if nf == 0:
+            continue
+        worst = float(d.abs()[flips].max()) / (float(d.abs().max()) + 1e-30)
+        assert worst <= rel and nf <= frac * d.numel(), (what, f'L1 term {k}: {nf} of {d.numel()} signs imposed, '
+                                                         f'the largest at {worst:.2e} of the term\'s |x - y| max')
+        n_flip += nf
+    return n_flip
+
+
 @contextlib.contextmanager
 def code_impose(seg_codes):
     """The oracle's rvq_train takes our codes (seg_codes: the model's [(codes, emb)] per segment,
@@ -399,10 +440,13 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device=
     f64 = []
     # and its nearest codes follow ours where the two are a near tie (check_code_ties)
     seg_codes = tr.model.seg_codes
-    with lrelu_audit(f64) as a64, code_impose(seg_codes) as clog:
+    # and its reconstruction L1s take our output's signs (check_l1_flips)
+    signs = l1_signs(x, tr.last_y, cfg.sample_rate, device)
+    with lrelu_audit(f64) as a64, code_impose(seg_codes) as clog, l1_impose(signs) as l1log:
         o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks, device)
-    with code_impose(seg_codes):
+    with code_impose(seg_codes), l1_impose(signs):
         o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks, device)
+    n_l1 = check_l1_flips(l1log, 'step L1 sign audit')
     n_imp = check_code_ties(clog, seg_codes, O.rvq_num_quantizers(bandwidth, cfg.frame_rate, n_q_max=cfg.n_q),
                             'step code audit')
     if masks is not None:
@@ -426,5 +470,6 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device=
     if verbose:
         worst = max(table, key=lambda r: r[1] / r[3])
         print(f'step vs oracle: {len(table)} tensors, worst grad err {max(r[1] for r in table):.2e}, '
-              f'tightest {worst[0]} {worst[1]:.2e} / bound {worst[3]:.2e}; {n_imp} near-tie codes imposed')
+              f'tightest {worst[0]} {worst[1]:.2e} / bound {worst[3]:.2e}; {n_imp} near-tie codes and {n_l1} '
+              f'L1 signs imposed')
     return out, table

@@ -477,3 +477,34 @@ def test_code_impose_and_tie_audit():
     with pytest.raises(AssertionError):
         check_code_ties(log, seg, n_q, 'far')
     assert O.CODES is None and O.CODE_AUDIT is None
+
+
+def test_l1_sign_impose_and_audit():
+    """steputil.l1_impose / check_l1_flips: with our own signs imposed the oracle's reconstruction
+    L1 has F.l1_loss's value and gradient; a flipped sign at a near tie passes the audit and moves
+    that element's gradient; a flip at a large difference is refused."""
+    from steputil import l1_impose, check_l1_flips
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 1, 4000, generator=g, dtype=torch.float64)
+    y = (x + 0.1 * torch.randn(2, 1, 4000, generator=g, dtype=torch.float64)).requires_grad_(True)
+    with torch.no_grad():
+        y[0, 0, 7] = x[0, 0, 7] + 1e-9  # a near tie
+    ref = F.l1_loss(x, y)
+    gref, = torch.autograd.grad(ref, y)
+    sig = {'t': torch.sign(x - y.detach()), 'f': None}
+    with l1_impose(sig) as log:
+        v = O.loss_t(x, y)
+    gv, = torch.autograd.grad(v, y)
+    assert torch.allclose(v, ref) and torch.equal(gv, gref) and check_l1_flips(log, 'same') == 0
+    sig['t'] = sig['t'].clone()
+    sig['t'][0, 0, 7] *= -1
+    with l1_impose(sig) as log:
+        v = O.loss_t(x, y)
+    gv, = torch.autograd.grad(v, y)
+    assert check_l1_flips(log, 'tie') == 1 and float(gv[0, 0, 7]) == -float(gref[0, 0, 7])
+    sig['t'][0, 0, 100] *= -1
+    with l1_impose(sig) as log:
+        O.loss_t(x, y)
+    with pytest.raises(AssertionError):
+        check_l1_flips(log, 'far')
+    assert O.L1_SIGNS is None and O.L1_AUDIT is None
