@@ -239,10 +239,12 @@ class Trainer:
                 losses = total_loss(None, None, None, x, y, self.sample_rate)
                 wrt = y
             c['losses'] = losses
-            self.balancer.combine_start(self.balancer.grads(losses, wrt))
+            c['loss_grads'] = self.last_loss_grads = self.balancer.grads(losses, wrt)
+            self.balancer.combine_start(c['loss_grads'])
 
         def seg_dec():
             out_grad = self.balancer.combine_finish()
+            c['out_grad'] = self.last_out_grad = out_grad  # (tests' diagnostics)
             y, loss_w = c.pop('y'), c['loss_w']
             with bwd():
                 if c['split'] is not None:
@@ -364,6 +366,7 @@ class Trainer:
         # never handed to another key); after another key ran, last_codes must point back at it
         self.model.last_codes, self.model.seg_codes = ent[4]
         self.last_y = ent[5]['y_out']
+        self.last_loss_grads, self.last_out_grad = ent[5]['loss_grads'], ent[5]['out_grad']
         # the replayed graphs rewrite `out` in place: hand the caller a copy of this step's values
         names = list(out)
         vals = torch.cat([out[k].detach().reshape(-1)[:1] for k in names])

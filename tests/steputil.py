@@ -419,10 +419,23 @@ def check_grads(mine, g64, g32, what, floor=1e-6):
     return table
 
 
-def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device='cpu'):
+@contextlib.contextmanager
+def _out_grad(trace=None, impose=None):
+    O.STEP_TRACE, O.OUT_GRAD = trace, impose
+    try:
+        yield
+    finally:
+        O.STEP_TRACE = O.OUT_GRAD = None
+
+
+def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device='cpu', isolate=False):
     """tr.step(x) against the oracle's step from the same state; returns (out, table). floor:
     the smallest per-tensor grad bound (relative to the tensor's fp64 magnitude). device: where
-    the oracle runs (oracle_step)."""
+    the oracle runs (oracle_step). isolate: the generator backward checked from our balanced output
+    grad (oracle.OUT_GRAD), and that output grad checked on its own against the oracle's: at B 32
+    the decoder's last bias grads are sums of 768 k output-grad elements of both signs, so an
+    output-grad error within the 4x rule (the discriminator's input grads: Conv2d bwd-data chains)
+    is amplified past it in those sums; split, each stage is held to the rule."""
     snap = snapshot(tr)
     store, ins, hooks = [], [], []
     if tr.disc is not None:
@@ -442,9 +455,19 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device=
     seg_codes = tr.model.seg_codes
     # and its reconstruction L1s take our output's signs (check_l1_flips)
     signs = l1_signs(x, tr.last_y, cfg.sample_rate, device)
-    with lrelu_audit(f64) as a64, code_impose(seg_codes) as clog, l1_impose(signs) as l1log:
+    og_table = []
+    if isolate:
+        t64, t32 = {}, {}
+        with code_impose(seg_codes), l1_impose(signs), _out_grad(trace=t64):
+            oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks, device)
+        with code_impose(seg_codes), l1_impose(signs), _out_grad(trace=t32):
+            oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks, device)
+        og_table = check_grads({'out_grad': tr.last_out_grad}, {'out_grad': t64['out_grad']},
+                               {'out_grad': t32['out_grad']}, 'step output grad (balanced, w.r.t. the output)')
+    og = tr.last_out_grad if isolate else None
+    with lrelu_audit(f64) as a64, code_impose(seg_codes) as clog, l1_impose(signs) as l1log, _out_grad(impose=og):
         o64, p64, cbs64, dp64 = oracle_step(snap, x, cfg, bandwidth, weights, torch.float64, masks, device)
-    with code_impose(seg_codes), l1_impose(signs):
+    with code_impose(seg_codes), l1_impose(signs), _out_grad(impose=og):
         o32, _, _, _ = oracle_step(snap, x, cfg, bandwidth, weights, torch.float32, masks, device)
     n_l1 = check_l1_flips(l1log, 'step L1 sign audit')
     n_imp = check_code_ties(clog, seg_codes, O.rvq_num_quantizers(bandwidth, cfg.frame_rate, n_q_max=cfg.n_q),
@@ -464,7 +487,8 @@ def check_step(tr, x, cfg, bandwidth, weights, verbose=True, floor=1e-6, device=
         for k in ('cluster_size', 'embed_avg', 'embed'):
             e = _rel(getattr(cb, k), cbs64[i][k])
             table.append((f'codebook{i}:{k}', e, float('nan'), 1e-5))
-    _assert_table(table, 'step vs oracle')
+    _assert_table(table, 'step vs oracle' + (' (generator backward from our output grad)' if isolate else ''))
+    table += og_table
     for k in weights:
         np.testing.assert_allclose(float(out[k]), o64[k], rtol=2e-5, err_msg=k)
     if verbose:

@@ -165,7 +165,8 @@ def test_config3_b32_step_vs_oracle_fp64():
     generator and discriminator weight grad within 4x the plain fp32 oracle's error, post-Adam
     parameters per element, the codebook EMA buffers, the losses, and the slope-mask /
     feature-sign audit. The second of two steps, so the balancer's averages and the Adam moments
-    are warm."""
+    are warm. The balanced output grad is checked on its own and the generator backward from it
+    (check_step isolate: the decoder's last bias grads sum 768 k output-grad elements)."""
     from encx.train import Trainer, DEFAULT_WEIGHTS
     from encx.msstftd import MultiScaleSTFTDiscriminator
     from fixtures import disc_state
@@ -180,7 +181,8 @@ def test_config3_b32_step_vs_oracle_fp64():
     x = torch.as_tensor(synth_wave((B, 1, 24000), 607)).to(DEV)
     tr.step(x)
     torch.cuda.synchronize()
-    out, table = check_step(tr, x, cfg, 6.0, DEFAULT_WEIGHTS, device=DEV)
+    out, table = check_step(tr, x, cfg, 6.0, DEFAULT_WEIGHTS, device=DEV, isolate=True)
+    assert any(r[0] == 'out_grad' for r in table)
     n_gen = sum(1 for r in table if r[0].startswith('gen:'))
     n_disc = sum(1 for r in table if r[0].startswith('disc:'))
     assert n_gen == sum(1 for q in m.parameters() if q.requires_grad), n_gen
