@@ -44,7 +44,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {OPT_CONV2_KS, "CONV2_KS", 0}, {OPT_CONV2_WGS, "CONV2_WGS", 512},
     {OPT_CONV2_LOWT, "CONV2_LOWT", 0},
     {OPT_LSTM_SPIN, "LSTM_SPIN", 0}, {OPT_LSTM_FAULT, "LSTM_FAULT", 0},
-    {OPT_BLAS, "BLAS", 1},
+    {OPT_BLAS, "BLAS", 3},
 };
 constexpr bool opts_in_order() {
     for (int i = 0; i < OPT_COUNT; ++i)

@@ -223,7 +223,8 @@ enum EncxOpt {
     OPT_CONV2_LOWT,    // v2 also for 64 < T <= 128 (the T 75 layers), else the flattened GEMMs
     OPT_LSTM_SPIN,     // persistent LSTM: log2 of every poll's spin bound (0: 20, about 1 s)
     OPT_LSTM_FAULT,    // persistent LSTM, tests only: one workgroup never publishes (its consumers time out)
-    OPT_BLAS,          // plain GEMMs through hipBLASLt (blas.hip): the LSTM weight grads, the im2col'd short convs
+    OPT_BLAS,          // plain GEMMs through hipBLASLt (blas.hip), bitmask: 1 the LSTM weight grads, 2 the
+                       // im2col'd T <= 128 convs, 4 the im2col'd larger convs (fwd / polyphase), 8 their weight grads
     OPT_COUNT
 };
 int64_t encx_opt(EncxOpt id);

@@ -1097,7 +1097,13 @@ struct EpPolyFlat {
 // transposing the [N][M] product back through LDS.
 constexpr int WGB_ROWS = 160;  // positions per bias-partial chunk (blas_wgrad_run)
 static bool blas_flat_ok(int64_t M, int64_t N, int64_t Kred) {
-    return encx_opt(OPT_BLAS) && M >= 256 && Kred >= 512 && 2.0 * M * N * Kred >= 2.0e9;
+    return (encx_opt(OPT_BLAS) & 2) && M >= 256 && Kred >= 512 && 2.0 * M * N * Kred >= 2.0e9;
+}
+// the longer layers (option BLAS & 4): 256+ output rows, a reduction of 512+, an im2col of at
+// most 128 MB and 8+ GFLOP (the k10 s5 stage at T 600: 256 x 19200 x 1280 and 640 x 19200 x 512)
+static bool blas_big_ok(int64_t M, int64_t N, int64_t Kred) {
+    return (encx_opt(OPT_BLAS) & 4) && M >= 256 && Kred >= 512 && N * Kred <= (32ll << 20) &&
+           2.0 * M * N * Kred >= 8.0e9;
 }
 // The reduction is cut into KB equal chunks (a strided batch of library GEMMs into KB product
 // slabs, summed in order in fp64 by the epilogue / reduce): one library accumulation chain over
@@ -1109,7 +1115,7 @@ static int blas_chunks(int64_t K, int64_t slab_elems) {
     return 1;
 }
 static size_t blas_flat_ws(int64_t M, int64_t N, int64_t Kred) {
-    if (!blas_flat_ok(M, N, Kred)) return 0;
+    if (!blas_flat_ok(M, N, Kred) && !blas_big_ok(M, N, Kred)) return 0;
     return (size_t)(N * Kred + (int64_t)blas_chunks(Kred, N * M) * N * M) * sizeof(float);
 }
 // out[n][k] = ld.b(k, n): a wave per 4 columns n, lanes along k (one (ci, tap) run per lane group)
@@ -2091,6 +2097,11 @@ static size_t poly2_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t nco
 }
 
 int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
+    if (ws && !a.part && !fwd_flat(a.Cout, a.Tout) &&
+        blas_big_ok(a.Cout, (int64_t)a.B * a.Tout, (int64_t)a.Cin * a.K) &&
+        blas_flat_run(LdConvFlat{a, make_fastdiv(a.K), make_fastdiv(a.Tout)}, EpConvFlat{a, 1, make_fastdiv(a.Tout)},
+                      a.wf, a.Cout, a.B * a.Tout, a.Cin * a.K, ws, st) == 0)
+        return 0;
     if (!(encx_opt(OPT_PW) && a.K == 1 && a.Tout <= encx_opt(OPT_PW_TMAX)) && !a.part) {
         const int rc = conv_fwd2_run(a, ws, st);
         if (rc >= 0) return rc;
@@ -2156,7 +2167,7 @@ int conv_fwd_run(FwdArgs a, float* ws, hipStream_t st) {
 }
 
 size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K, int64_t s, int64_t d) {
-    const size_t v2 = conv_fwd2_ws(B, Cin, Cout, Tout, K, s);
+    const size_t v2 = std::max(conv_fwd2_ws(B, Cin, Cout, Tout, K, s), blas_flat_ws(Cout, B * Tout, Cin * K));
     if (fwd_flat(Cout, Tout)) {
         const int slabs = fwd_flat_slabs(B, Cin, Cout, Tout, K);
         return std::max({v2, slabs > 1 ? (size_t)slabs * B * Cout * Tout * sizeof(float) : (size_t)0,
@@ -2172,6 +2183,14 @@ size_t conv_fwd_ws(int64_t B, int64_t Cin, int64_t Cout, int64_t Tout, int64_t K
 }
 
 int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
+    if (ws && ncols > FLAT_T && blas_big_ok((int64_t)a.Co * a.s, (int64_t)a.B * ncols, (int64_t)a.Ci * a.J)) {
+        PolyArgs ab = a;
+        ab.Q = ncols * a.s;
+        if (blas_flat_run(LdPolyFlat{ab, ab.Co * ab.s, ncols, make_fastdiv(ab.J), make_fastdiv(ncols)},
+                          EpPolyFlat{ab, ncols, 1, make_fastdiv(ab.s), make_fastdiv(ncols)}, ab.wp, ab.Co * ab.s,
+                          ab.B * ncols, ab.Ci * ab.J, ws, st) == 0)
+            return 0;
+    }
     {
         PolyArgs a2 = a;
         a2.Q = ncols * a.s;
@@ -2222,7 +2241,7 @@ int poly_run(PolyArgs a, int ncols, float* ws, hipStream_t st) {
 }
 
 size_t poly_ws(int64_t B, int64_t Ci, int64_t Co, int64_t s, int64_t ncols, int64_t J) {
-    const size_t v2 = poly2_ws(B, Ci, Co, s, ncols, J);
+    const size_t v2 = std::max(poly2_ws(B, Ci, Co, s, ncols, J), blas_flat_ws(Co * s, B * ncols, Ci * J));
     if (ncols <= FLAT_T) {
         const int Kred = (int)(Ci * J);
         const int slabs = gemm_slabs(Kred, gemm_splits((int)(Co * s), (int)(B * ncols), Kred));
@@ -2554,7 +2573,9 @@ static size_t wgrad2_ws(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K, 
 // forward's im2col [N][C K], one library GEMM straight into dw (accumulating when asked); the
 // bias (db = sum of L over positions) as fixed-order column sums of the transposed L
 static bool blas_wgrad_ok(int64_t A, int64_t Tl, int64_t N, int64_t CK) {
-    return Tl <= FLAT_T && blas_flat_ok(CK, A, N) && A >= 64;
+    if (A < 64) return false;
+    if (Tl <= FLAT_T) return blas_flat_ok(CK, A, N);
+    return (encx_opt(OPT_BLAS) & 8) && CK >= 256 && N * CK <= (32ll << 20) && 2.0 * A * N * CK >= 8.0e9;
 }
 static size_t blas_wgrad_ws(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
     const int64_t N = B * Tl;

@@ -36,18 +36,43 @@ struct FftArgs {
     float scale;        // layout 1: 1 / sqrt(sum w^2)
 };
 
+// Twiddles e^{-pi i k / M}, k <= M, for M = 2^4 .. 2^10, from fp64 sincospi once per module and
+// device (tw_ready: a setup launch before the first transform) at g_tw[tw_base(M) + k]; each
+// workgroup copies its M + 1 into LDS (computing them per workgroup, 1025 fp64 sincospi at M 1024,
+// was a third of a frame's work). One copy per translation unit (static).
+constexpr int tw_base(int M) { return 2 * M + 16; }
+constexpr int TW_SIZE = tw_base(1024) + 1025;
+static __device__ f2v g_tw[TW_SIZE];
+static __global__ void tw_init_kernel(int M) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > M) return;
+    double s, c;
+    sincospi((double)k / (double)M, &s, &c);
+    g_tw[tw_base(M) + k] = (f2v){(float)c, (float)(-s)};
+}
+static inline int tw_ready(hipStream_t st) {
+    static bool done[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ENCX_EINVAL;
+    if (done[dev]) return 0;
+    for (int M = 16; M <= 1024; M <<= 1)
+        hipLaunchKernelGGL(tw_init_kernel, dim3((unsigned)((M + 256) / 256)), dim3(256), 0, st, M);
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) done[dev] = true;
+    return (int)e;
+}
 // twiddles e^{sign * pi i k / M}, k <= M, into tw (LDS)
 template <int M>
 ENCX_DEV void make_twiddles(f2v* tw, float sign) {
     for (int k = threadIdx.x; k <= M; k += FFT_NT) {
-        double s, c;
-        sincospi((double)k / (double)M, &s, &c);
-        tw[k] = (f2v){(float)c, (float)(sign * s)};
+        const f2v v = g_tw[tw_base(M) + k];
+        tw[k] = sign < 0.f ? v : cconj(v);
     }
 }
 
 // Stockham radix-2 over FPW frames of M points in buf[0] (result in buf[RES]); tw[2t] = e^{+-2 pi i t/M}
-template <int M, int FPW>
+// (CONJ: the conjugate twiddles, the inverse transform from the forward table)
+template <int M, int FPW, bool CONJ = false>
 ENCX_DEV int stockham(f2v* buf, const f2v* tw) {
     int cur = 0;
 #pragma unroll 1
@@ -58,7 +83,8 @@ ENCX_DEV int stockham(f2v* buf, const f2v* tw) {
             const int f = q / (M / 2), j = q - f * (M / 2);
             const int jm = j & (ns - 1);
             const f2v a = src[f * M + j];
-            const f2v b = cmul(src[f * M + j + M / 2], tw[2 * jm * (M / (2 * ns))]);
+            const f2v t = tw[2 * jm * (M / (2 * ns))];
+            const f2v b = cmul(src[f * M + j + M / 2], CONJ ? cconj(t) : t);
             const int d = f * M + ((j - jm) << 1) + jm;
             dst[d] = a + b;
             dst[d + ns] = a - b;
@@ -74,7 +100,10 @@ __global__ __launch_bounds__(FFT_NT) void r2c_kernel(FftArgs a) {
     constexpr int M = 1 << LOGM, N = 2 * M, FPW = M >= 1024 ? 1 : 1024 / M;
     __shared__ f2v buf[2 * FPW * M];
     __shared__ f2v tw[M + 1];
+    __shared__ float Win[N];  // the window, gathered once (a strided table column)
     make_twiddles<M>(tw, -1.f);
+    for (int t = threadIdx.x; t < N; t += FFT_NT) Win[t] = a.win[(int64_t)t * a.wstride];
+    __syncthreads();
     const int row0 = blockIdx.x * FPW;
     // load: packed z[j] = (w x)[2j] + i (w x)[2j + 1]
     float* bufr = reinterpret_cast<float*>(buf);
@@ -85,7 +114,7 @@ __global__ __launch_bounds__(FFT_NT) void r2c_kernel(FftArgs a) {
             const int bc = row / a.F, fr = row - bc * a.F;
             int s = fr * a.hop + t - a.pad;
             s = s < 0 ? -s : (s >= a.T ? 2 * (a.T - 1) - s : s);
-            v = a.x[(int64_t)bc * a.T + s] * a.win[t * a.wstride];
+            v = a.x[(int64_t)bc * a.T + s] * Win[t];
         }
         bufr[i] = v;
     }
@@ -118,7 +147,9 @@ __global__ __launch_bounds__(FFT_NT) void c2r_kernel(FftArgs a) {
     __shared__ f2v buf[2 * FPW * M];
     __shared__ f2v tw[M + 1];
     __shared__ f2v Ys[FPW * NB];
+    __shared__ float Win[N];
     make_twiddles<M>(tw, 1.f);  // e^{+pi i k / M}
+    for (int t = threadIdx.x; t < N; t += FFT_NT) Win[t] = a.win[(int64_t)t * a.wstride];
     const int row0 = blockIdx.x * FPW;
     for (int q = threadIdx.x; q < FPW * NB; q += FFT_NT) {
         const int f = q / NB, k = q - f * NB, row = row0 + f;
@@ -149,13 +180,14 @@ __global__ __launch_bounds__(FFT_NT) void c2r_kernel(FftArgs a) {
     const float* c = reinterpret_cast<const float*>(buf + res * (FPW * M));  // y[2j], y[2j+1] interleaved
     for (int i = threadIdx.x; i < FPW * N; i += FFT_NT) {
         const int f = i / N, t = i - f * N, row = row0 + f;
-        if (row < a.rows) a.out[(int64_t)row * N + t] = c[i] * a.win[t * a.wstride];
+        if (row < a.rows) a.out[(int64_t)row * N + t] = c[i] * Win[t];
     }
 }
 
 // host launchers: n = 2^k, 32 <= n <= 2048
 #define ENCX_FFT_SWITCH(KERNEL)                                                                   \
     {                                                                                             \
+        if (const int rc_ = tw_ready(st)) return rc_;                                             \
         const int m = n / 2, fpw = m >= 1024 ? 1 : 1024 / m;                                      \
         const dim3 grid((unsigned)cdiv(a.rows, fpw));                                             \
         switch (m) {                                                                              \

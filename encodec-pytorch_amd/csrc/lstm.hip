@@ -1222,7 +1222,7 @@ int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float
             KB = c;
             break;
         }
-    bool lib = KB > 0 && H % 4 == 0 && encx_opt(OPT_BLAS) && (size_t)KB * N4 * Nw <= wsl_main(B, T, H);
+    bool lib = KB > 0 && H % 4 == 0 && (encx_opt(OPT_BLAS) & 1) && (size_t)KB * N4 * Nw <= wsl_main(B, T, H);
     if (lib) {
         const int kc = M / KB;
         float* hp = ws + (size_t)KB * N4 * Nw;

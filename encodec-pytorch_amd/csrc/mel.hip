@@ -291,19 +291,43 @@ template <int LOGM, bool GRAD>
 __global__ __launch_bounds__(encx_fft::FFT_NT) void mel_fused_kernel(const float* x, const float* y, MelScale a) {
     using namespace encx_fft;
     constexpr int M = 1 << LOGM, N = 2 * M, FPW = M >= 1024 ? 1 : 1024 / M, NB = M + 1, NM = 64;
+    // splits per mel filter of the projection, so that all 256 threads work at the long frames
+    constexpr int S = FPW * NM >= FFT_NT ? 1 : FFT_NT / (FPW * NM);
     __shared__ f2v buf[2 * FPW * M];
     __shared__ f2v twf[M + 1];
-    __shared__ f2v twi[M + 1];
     __shared__ f2v Xs[FPW * NB];     // Y's spectrum (kept for the backward), then the c2r input
     __shared__ float Ps[FPW * NB];   // power spectrum, then dP
     __shared__ float Lx[FPW * NM];   // log-mel of x, then d mel(y)
+    __shared__ float Mp[S > 1 ? FPW * NM * S : 1];  // split partial sums of the projection
+    // the filters' nonzero weights packed per filter (each bin lies under at most two triangles):
+    // filter m's weights for bins Wlo[m] + j at Wp[Woff[m] + j], gathered once per workgroup
+    __shared__ float Wp[2 * NB];
+    __shared__ int Woff[NM + 1], Wlo[NM];
+    __shared__ float Win[N];         // the window (a column of the table: one line per element)
     __shared__ float red[16];
     const int nb2 = 2 * NB;
     const float* bt = a.tables;      // window = bt[t * nb2] (column 0: w cos 0)
+    for (int t = threadIdx.x; t < N; t += FFT_NT) Win[t] = bt[(int64_t)t * nb2];
     const float* mt = a.tables + (int64_t)N * nb2;  // [nb][nm]
     const int* sup = sup_at(a.tables, N, NM);
     make_twiddles<M>(twf, -1.f);
-    for (int k = threadIdx.x; k <= M; k += FFT_NT) twi[k] = cconj(twf[k]);
+    if (threadIdx.x < NM) {  // wave 0: the packed offsets, an exclusive scan of the widths
+        const int m = threadIdx.x, lo = sup[2 * m], w = sup[2 * m + 1] - lo;
+        int incl = w;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (m >= o) incl += v;
+        }
+        Woff[m] = incl - w;
+        Wlo[m] = lo;
+        if (m == NM - 1) Woff[NM] = incl;
+    }
+    __syncthreads();
+    {
+        const int m = threadIdx.x & (NM - 1), lo = Wlo[m], off = Woff[m], w = Woff[m + 1] - off;
+        for (int j = threadIdx.x >> 6; j < w; j += FFT_NT / NM) Wp[off + j] = mt[(int64_t)(lo + j) * NM + m];
+    }
     const int row0 = blockIdx.x * FPW;
     float* bufr = reinterpret_cast<float*>(buf);
     float s1 = 0.f, s2 = 0.f;
@@ -318,7 +342,7 @@ __global__ __launch_bounds__(encx_fft::FFT_NT) void mel_fused_kernel(const float
                 const int bc = row / a.F, fr = row - bc * a.F;
                 int s = fr * a.hop + t - a.pad;
                 s = s < 0 ? -s : (s >= a.T ? 2 * (a.T - 1) - s : s);
-                v = w[(int64_t)bc * a.T + s] * bt[t * nb2];
+                v = w[(int64_t)bc * a.T + s] * Win[t];
             }
             bufr[i] = v;
         }
@@ -335,11 +359,27 @@ __global__ __launch_bounds__(encx_fft::FFT_NT) void mel_fused_kernel(const float
             if (GRAD && pass == 1) Xs[q] = (f2v){re, im};
         }
         __syncthreads();
+        if (S > 1) {  // the projection's split partials: filter m's bins in S equal runs
+            for (int q = threadIdx.x; q < FPW * NM * S; q += FFT_NT) {
+                const int f = q / (NM * S), r = q - f * NM * S, m = r / S, sp = r - m * S;
+                const int lo = Wlo[m], off = Woff[m], wd = Woff[m + 1] - off, ch = (wd + S - 1) / S;
+                const int j1 = min(wd, (sp + 1) * ch);
+                float acc = 0.f;
+                for (int j = sp * ch; j < j1; ++j) acc = fmaf(Ps[f * NB + lo + j], Wp[off + j], acc);
+                Mp[q] = acc;
+            }
+            __syncthreads();
+        }
         for (int q = threadIdx.x; q < FPW * NM; q += FFT_NT) {
             const int f = q / NM, m = q - f * NM, row = row0 + f;
-            const int klo = sup[2 * m], khi = sup[2 * m + 1];
             float mel = 0.f;
-            for (int k = klo; k < khi; ++k) mel = fmaf(Ps[f * NB + k], mt[(int64_t)k * NM + m], mel);
+            if (S > 1) {
+#pragma unroll
+                for (int sp = 0; sp < S; ++sp) mel += Mp[q * S + sp];
+            } else {
+                const int lo = Wlo[m], off = Woff[m], wd = Woff[m + 1] - off;
+                for (int j = 0; j < wd; ++j) mel = fmaf(Ps[f * NB + lo + j], Wp[off + j], mel);
+            }
             const float l = log10f(fmaxf(mel, 1e-5f));
             if (pass == 0) {
                 Lx[q] = l;
@@ -369,7 +409,7 @@ __global__ __launch_bounds__(encx_fft::FFT_NT) void mel_fused_kernel(const float
         const int f = q / NB, k = q - f * NB;
         const int mlo = sup[2 * NM + 2 * k], mhi = sup[2 * NM + 2 * k + 1];
         float dp = 0.f;
-        for (int m = mlo; m < mhi; ++m) dp = fmaf(Lx[f * NM + m], mt[(int64_t)k * NM + m], dp);
+        for (int m = mlo; m < mhi; ++m) dp = fmaf(Lx[f * NM + m], Wp[Woff[m] + k - Wlo[m]], dp);
         const f2v d = Xs[q] * (2.f * dp);
         Xs[q] = (k == 0 || k == M) ? (f2v){d[0], 0.f} : d * 0.5f;
     }
@@ -377,19 +417,20 @@ __global__ __launch_bounds__(encx_fft::FFT_NT) void mel_fused_kernel(const float
     for (int q = threadIdx.x; q < FPW * M; q += FFT_NT) {
         const int f = q / M, k = q - f * M;
         const f2v yk = Xs[f * NB + k], ym = cconj(Xs[f * NB + M - k]);
-        const f2v A = yk + ym, Bv = cmul(yk - ym, twi[k]);
+        const f2v A = yk + ym, Bv = cmul(yk - ym, cconj(twf[k]));
         buf[q] = (f2v){A[0] - Bv[1], A[1] + Bv[0]};
     }
     __syncthreads();
-    const int res = stockham<M, FPW>(buf, twi);
+    const int res = stockham<M, FPW, true>(buf, twf);
     const float* c = reinterpret_cast<const float*>(buf + res * (FPW * M));
     for (int i = threadIdx.x; i < FPW * N; i += FFT_NT) {
         const int f = i / N, t = i - f * N, row = row0 + f;
-        if (row < a.rows) a.dframe[(int64_t)row * N + t] = c[i] * bt[t * nb2];
+        if (row < a.rows) a.dframe[(int64_t)row * N + t] = c[i] * Win[t];
     }
 }
 template <bool GRAD>
 static int mel_fused_launch(int n, const float* x, const float* y, const MelScale& a, hipStream_t st) {
+    if (const int rc = encx_fft::tw_ready(st)) return rc;
     const int m = n / 2, fpw = m >= 1024 ? 1 : 1024 / m;
     const dim3 grid((unsigned)cdiv(a.rows, fpw));
     switch (m) {
@@ -408,6 +449,7 @@ constexpr int MEL_MAXS = 8;
 struct MelOla {  // the frame gradients of every scale
     const float* dframe[MEL_MAXS];
     int n[MEL_MAXS], hop[MEL_MAXS], pad[MEL_MAXS], F[MEL_MAXS];
+    int lh[MEL_MAXS];  // log2 hop (hop = n / 4, a power of two)
     int ns;
 };
 // grad[b][m] (+)= sum over scales (in order) of overlap_add's sum for that scale
@@ -424,12 +466,21 @@ __global__ void overlap_add_all(MelOla o, float* grad, int Bn, int T) {
         if (m >= 1 && m <= p) js[nj++] = p - m;
         if (m >= T - 1 - p && m <= T - 2) js[nj++] = p + 2 * (T - 1) - m;
         float s = 0.f;
+        const int lh = o.lh[sc];
         for (int q = 0; q < nj; ++q) {
             const int j = js[q];
-            const int flo = j - n + 1 > 0 ? (j - n + 1 + h - 1) / h : 0;
-            int fhi = j / h;
+            const int flo = j - n + 1 > 0 ? (j - n + h) >> lh : 0;
+            int fhi = j >> lh;
             if (fhi > F - 1) fhi = F - 1;
-            for (int f = flo; f <= fhi; ++f) s += o.dframe[sc][((int64_t)b * F + f) * n + (j - f * h)];
+            // at most n / hop = 4 frames cover j: their loads in flight together, added in f order
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int f = flo + u;
+                v[u] = f <= fhi ? o.dframe[sc][((int64_t)b * F + f) * n + (j - f * h)] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s += v[u];
         }
         tot += s;
     }
@@ -442,20 +493,32 @@ struct MelFin {
     float inv_n[MEL_MAXS];
     int ns;
 };
-__global__ __launch_bounds__(256) void mel_loss_finish(MelFin f, float* loss) {
-    __shared__ float red[16];
-    float tot = loss[0];
-    for (int sc = 0; sc < f.ns; ++sc) {
-        float s1 = 0.f, s2 = 0.f;
-        for (int i = threadIdx.x; i < f.nblk[sc]; i += 256) {
-            s1 += f.parts[sc][i];
-            s2 += f.parts[sc][f.nblk[sc] + i];
+// one wave per scale (MEL_MAXS <= 8 waves), each lane summing its strided share of the scale's
+// partials, then the waves' sums in scale order
+__global__ __launch_bounds__(512) void mel_loss_finish(MelFin f, float* loss) {
+    __shared__ float r1[MEL_MAXS], r2[MEL_MAXS];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < f.ns) {
+        const float* p = f.parts[w];
+        const int nb = f.nblk[w];
+        float a1 = 0.f, a2 = 0.f;
+        for (int i = lane; i < nb; i += 64) {
+            a1 += p[i];
+            a2 += p[nb + i];
         }
-        s1 = block_sum(s1, red);
-        s2 = block_sum(s2, red);
-        tot = (tot + s1 * f.inv_n[sc]) + s2 * f.inv_n[sc];
+        a1 = wave_sum(a1);
+        a2 = wave_sum(a2);
+        if (lane == 0) {
+            r1[w] = a1;
+            r2[w] = a2;
+        }
     }
-    if (threadIdx.x == 0) loss[0] = tot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float tot = loss[0];
+        for (int sc = 0; sc < f.ns; ++sc) tot = (tot + r1[sc] * f.inv_n[sc]) + r2[sc] * f.inv_n[sc];
+        loss[0] = tot;
+    }
 }
 
 }  // namespace
@@ -603,11 +666,12 @@ int encx_mel_loss_multi(const float* x, const float* y, const float* const* tabl
         if (rc) return rc;
         o.dframe[i] = a.dframe;
         o.n[i] = g.n; o.hop[i] = g.h; o.pad[i] = g.p; o.F[i] = g.F;
+        o.lh[i] = 31 - __builtin_clz((unsigned)g.h);
         fin.parts[i] = a.parts;
         fin.nblk[i] = nblk;
         fin.inv_n[i] = a.inv_n;
     }
-    hipLaunchKernelGGL(mel_loss_finish, dim3(1), dim3(256), 0, st, fin, loss);
+    hipLaunchKernelGGL(mel_loss_finish, dim3(1), dim3(512), 0, st, fin, loss);
     ENCX_CHECK_LAUNCH();
     if (grad) {
         hipLaunchKernelGGL(overlap_add_all, dim3((unsigned)cdiv(B * T, 256)), dim3(256), 0, st, o, grad, (int)B, (int)T);

@@ -1,0 +1,8 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+O=gpurun_out
+step() { local n=$1 t=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?; echo "== $n rc=$rc"; tail -3 $O/$n.log; case $rc in 124|134|137|139) exit $rc;; esac; [ $rc -ge 128 ] && exit $rc; return 0; }
+step t 400 python -u -m pytest tests -m gpu -q -rf -k "mel or spec or fft or disc or losses" --timeout 300 --timeout-method thread
+step blas 200 python tools/diag/blas_probe.py
+CONFIG=gan step lay 600 bash tools/gpu_layers.sh
