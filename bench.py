@@ -103,6 +103,11 @@ def main():
     rehearse = os.environ.get('ENCX_BENCH_REHEARSE', '0') == '1'
     if rehearse:
         local = 0
+        # the ranks share one GPU: two persistent LSTM launches (each one workgroup per CU,
+        # spinning on its own peers) from two processes can hold each other's CUs -- round 5's
+        # eager rehearsal paid that in stalls (216 ms/step), round 6's loud-failure check turned
+        # the spin timeouts into errors; the step form has no inter-workgroup waits
+        os.environ.setdefault('ENCX_LSTM_PERSIST', '0')
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
@@ -199,7 +204,7 @@ def main():
         # (FETCH_SIZE x2 + WRITE_SIZE, calibrated: tools/traffic.py); null when no pass exists
         traffic = None
         tpath = next((p for p in (os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', r,
-                                               f'traffic_{args.config}.json') for r in ('r05', 'r04', 'r03', 'r02'))
+                                               f'traffic_{args.config}.json') for r in ('r06', 'r05', 'r04', 'r03', 'r02'))
                       if os.path.exists(p)), '')
         if os.path.exists(tpath) and launches:
             with open(tpath) as fh:

@@ -18,9 +18,13 @@ import re
 
 # kernels launched by the conv / convtr / conv2d ABI entry points (csrc/conv1d.hip, disc.hip)
 # (csrc/resblock.hip's fused residual-block kernels are conv ABI calls too: encx_resblock_*)
-FAMILY = re.compile(r'conv_fwd_kernel|pw_kernel|pw_wgrad_kernel|conv_poly_kernel|conv_wgrad|wgrad_reduce|conv_fwd_reduce|'
-                    r'conv_poly_reduce|conv_fold_edges|LdConvFlat|LdPolyFlat|c2_|rb_fwd_kernel|rb_bwd_kernel|'
-                    r'rb_dgrad_kernel|rb_wgrad_kernel|rb_wgrad_reduce')
+# (round 6: the v2 kernels, and the short-T layers' im2col / epilogue kernels with their hipBLASLt
+# GEMMs, `Cijk_*`; the LSTM weight grads' library GEMMs carry the same names and are counted in
+# too, an overcount of their few tens of MB per step)
+FAMILY = re.compile(r'conv_fwd_kernel|conv_fwd2_kernel|pw_kernel|pw_wgrad_kernel|conv_poly_kernel|conv_poly2_kernel|'
+                    r'conv_wgrad|wgrad_reduce|conv_fwd_reduce|conv_poly_reduce|conv_fold_edges|LdConvFlat|LdPolyFlat|'
+                    r'c2_|rb_fwd_kernel|rb_bwd_kernel|rb_dgrad_kernel|rb_wgrad_kernel|rb_wgrad_reduce|im2col_kernel|'
+                    r'gemm_epi_kernel|wg_transpose_kernel|wg_colsum|Cijk_')
 
 
 def per_dispatch(d, counter):
