@@ -869,14 +869,17 @@ __global__ __launch_bounds__(256) void lstm_bias_fin(const float* part, int nchu
     if (db1) db1[j] = acc ? db1[j] + v : v;
     if (db2) db2[j] = acc ? db2[j] + v : v;
 }
-// the recurrent operand of the weight grad as a plain matrix: hp[b][t] = h_l(t - 1) (0 at t = 0)
-__global__ __launch_bounds__(256) void lstm_hprev(const float* Yl, float* hp, int T, int H, int64_t n4) {
+// the weight grad's operand as one plain matrix xh[b T + t] = [x_l(t) | h_l(t - 1)] ([M][2H]; h 0 at
+// t = 0), so dW_ih and dW_hh come out of ONE library GEMM (2H output rows instead of two of H)
+__global__ __launch_bounds__(256) void lstm_xh(const float* in, const float* Yl, float* xh, int T, int H, int64_t n4) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // quad index
     if (i >= n4) return;
-    const int64_t e = i * 4, row = e / H;
-    const int t = (int)(row % T);
-    const f32x4 v = t > 0 ? *(const f32x4*)(Yl + e - H) : (f32x4){0.f, 0.f, 0.f, 0.f};
-    *(f32x4*)(hp + e) = v;
+    const int64_t e = i * 4, row = e / (2 * H);
+    const int c = (int)(e - row * 2 * H), t = (int)(row % T);
+    f32x4 v;
+    if (c < H) v = *(const f32x4*)(in + row * H + c);
+    else v = t > 0 ? *(const f32x4*)(Yl + (row - 1) * H + (c - H)) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    *(f32x4*)(xh + e) = v;
 }
 
 // ------------------------------------------------------------------------- dispatch
@@ -1181,11 +1184,11 @@ int encx_lstm_bwd(const float* dout, const float* wcatT, const float* Cst, const
 
 }  // extern "C"
 // floats of the weight grad's main workspace: the own GEMM's split slabs, or the library GEMM's
-// 8 position-chunk slabs and the h(t-1) matrix; the bias partials follow
+// 8 position-chunk slabs and the [x | h(t-1)] matrix; the bias partials follow
 static size_t wsl_main(int64_t B, int64_t T, int64_t H) {
     const int M = (int)(B * T), N4 = (int)(4 * H), Nw = (int)(2 * H);
     const int S = gemm_slabs(M, gemm_splits_128(N4, Nw, M, 256, (int)encx_opt(OPT_LSTM_WG_SPLITS)));
-    return std::max((size_t)S * N4 * Nw, (size_t)8 * N4 * Nw + (size_t)B * T * H);
+    return std::max((size_t)S * N4 * Nw, (size_t)8 * N4 * Nw + (size_t)B * T * 2 * H);
 }
 extern "C" {
 size_t encx_lstm_bwd_weight_workspace(int64_t B, int64_t T, int64_t H) {
@@ -1211,9 +1214,9 @@ int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float
     const float* DAl = DA + layer * 4 * BTH;
     const LdWcat ld{DAl, in, Y + layer * BTH, (int)H, (int)T, make_fastdiv((uint32_t)T)};
     int rc;
-    // dW^T (H x 4H, column-major) = [x | h(t-1)]^T DA through hipBLASLt (blas.hip), else the own
-    // GEMM. The B T positions are cut into KB equal chunks of about 300 (a strided batch: one slab
-    // [4H][2H] per chunk, dW_ih^T and dW_hh^T side by side) summed in order by lstm_slab_reduce:
+    // [dW_ih | dW_hh]^T (2H x 4H, column-major) = [x | h(t-1)]^T DA through hipBLASLt (blas.hip),
+    // else the own GEMM. The B T positions are cut into KB equal chunks of about 300 (a strided
+    // batch: one slab [4H][2H] per chunk) summed in order by lstm_slab_reduce:
     // one library accumulation chain over all 2400 positions of config 3 was 5x the error of plain
     // fp32 (test_lstm_vs_oracle), the chunked form is within it.
     int KB = 0;
@@ -1225,14 +1228,13 @@ int encx_lstm_bwd_weight(const float* DA, const float* xt, const float* Y, float
     bool lib = KB > 0 && H % 4 == 0 && (encx_opt(OPT_BLAS) & 1) && (size_t)KB * N4 * Nw <= wsl_main(B, T, H);
     if (lib) {
         const int kc = M / KB;
-        float* hp = ws + (size_t)KB * N4 * Nw;
-        hipLaunchKernelGGL(lstm_hprev, dim3((unsigned)cdiv(BTH / 4, 256)), dim3(256), 0, st, Y + layer * BTH, hp,
-                           (int)T, (int)H, BTH / 4);
+        float* xh = ws + (size_t)KB * N4 * Nw;
+        hipLaunchKernelGGL(lstm_xh, dim3((unsigned)cdiv(2 * BTH / 4, 256)), dim3(256), 0, st, in, Y + layer * BTH, xh,
+                           (int)T, (int)H, 2 * BTH / 4);
         ENCX_CHECK_LAUNCH();
-        lib = encx_sgemm(st, false, true, (int)H, N4, kc, in, (int)H, DAl, N4, ws, Nw, false, KB, (int64_t)kc * H,
-                         (int64_t)kc * N4, (int64_t)N4 * Nw) == 0 &&
-              encx_sgemm(st, false, true, (int)H, N4, kc, hp, (int)H, DAl, N4, ws + H, Nw, false, KB,
-                         (int64_t)kc * H, (int64_t)kc * N4, (int64_t)N4 * Nw) == 0;
+        // slab c (2H x 4H, column-major = [4H][2H]) = xh^T DA over position chunk c
+        lib = encx_sgemm(st, false, true, Nw, N4, kc, xh, Nw, DAl, N4, ws, Nw, false, KB, (int64_t)kc * Nw,
+                         (int64_t)kc * N4, (int64_t)N4 * Nw) == 0;
         if (lib) {
             hipLaunchKernelGGL(lstm_slab_reduce, dim3((unsigned)cdiv((int64_t)N4 * Nw, 64)), dim3(256), 0, st, ws,
                                KB, (int)H, dw_ih, dw_hh, acc);
