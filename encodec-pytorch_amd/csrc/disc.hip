@@ -1498,20 +1498,26 @@ ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int l
         if (CX) u *= code_mask(c);
         return A ? d + u : u;
     };
-    if (S == 2) {  // registers r, r + 1 are phases 0 / 1 of one ci: with the 4 columns, 8 consecutive f
+    if (S == 2) {
+        // TM == 2 (phase-split rows, c2_dgrad_rw_kernel): tile 0 holds phase 0 and tile 1 phase 1
+        // of the same 32 ci, register r of both the same ci; otherwise registers r, r + 1 of a tile
+        // are phases 0 / 1 of one ci. Either way the 4 columns give 8 consecutive f.
+        constexpr bool PS = TM == 2;
         const int f = 2 * u0 - g.pf;
         const bool inb = f >= 0 && f + 8 <= g.Fi;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < (PS ? 1 : TM); ++i)
 #pragma unroll
-            for (int r0 = 0; r0 < 16; r0 += 2 * EP) {
+            for (int r0 = 0; r0 < 16; r0 += PS ? EP : 2 * EP) {
                 int64_t o[EP];
 #pragma unroll
                 for (int p = 0; p < EP; ++p) {
-                    const int ci = ((rt * TM + i) * 32 + mfma_row(r0 + 2 * p, lane)) >> 1;
+                    const int ci = PS ? mfma_row(r0 + p, lane) : ((rt * TM + i) * 32 + mfma_row(r0 + 2 * p, lane)) >> 1;
                     o[p] = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
                 }
-                auto val = [&](int p, int e8) { return acc[i][e8 >> 1][r0 + 2 * p + (e8 & 1)]; };
+                auto val = [&](int p, int e8) {
+                    return PS ? acc[e8 & 1][e8 >> 1][r0 + p] : acc[i][e8 >> 1][r0 + 2 * p + (e8 & 1)];
+                };
                 if (inb) {
                     f32x4 X[EP][2], R[EP][2], D[EP][2];
                     uint32_t Cc[EP][8];
@@ -1610,8 +1616,19 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
     const C2Dg& a = R.d;
     extern __shared__ float smem[];
     const C2Geo g = a.g;
-    float* As = smem;  // [(co,kt)][J][M]: the wp layout (M == Ci*S, host-checked)
-    for (int i = threadIdx.x; i < g.Co * KT * J * M; i += NWV * 64) As[i] = a.wp[i];
+    // phase-split rows (the 3x9 stride-2 layers with both row tiles per item): tile 0 = phase 0,
+    // tile 1 = phase 1 of the 32 ci, so the fifth polyphase tap, zero for every phase-1 row
+    // (kf = 2 q + 1 = 9 >= KF), is skipped for tile 1: 10 % fewer MFMAs
+    constexpr bool PS = S == 2 && J == 5 && RT == 2 && TM == 2;
+    float* As = smem;  // [(co,kt)][J][M]: the wp layout (M == Ci*S, host-checked), rows phase-major if PS
+    for (int i = threadIdx.x; i < g.Co * KT * J * M; i += NWV * 64) {
+        if (PS) {
+            const int mn = i % M;
+            As[i] = a.wp[i - mn + (mn & 31) * S + (mn >> 5)];
+        } else {
+            As[i] = a.wp[i];
+        }
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l = lane & 31;
     // element offsets fit in 32 bits (checked on the host)
@@ -1715,12 +1732,13 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
                 for (int q = 0; q < J; ++q) {
                     float av[TM];
 #pragma unroll
-                    for (int i = 0; i < TM; ++i) av[i] = ak[q * M + i * 32];
+                    for (int i = 0; i < TM; ++i) av[i] = (PS && i == 1 && q == J - 1) ? 0.f : ak[q * M + i * 32];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int r = j - q + J - 1;  // window element of column u0 + j, tap q
 #pragma unroll
-                        for (int i = 0; i < TM; ++i) acc[i][j] = mfma32(av[i], w[r >> 2][r & 3], acc[i][j]);
+                        for (int i = 0; i < TM; ++i)
+                            if (!(PS && i == 1 && q == J - 1)) acc[i][j] = mfma32(av[i], w[r >> 2][r & 3], acc[i][j]);
                     }
                 }
             }
