@@ -1172,9 +1172,9 @@ __global__ __launch_bounds__(NT) void c2_dgrad_kernel(C2Dg a) {
 // c2_dgradr_kernel's epilogue, its terms fixed at compile time (MODE bits as rw_dg_epi): no
 // branches around the loads, and the output never aliases the maps read, so the 8 row pairs of a
 // (row tile, column tile) are loaded together, then combined and stored.
-template <int TM, int TN, int MODE>
+template <int TM, int TN, int MODE, bool PS = false>
 ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0, int nl, int nend, int U, int M,
-                      int S, int lane, float fc) {
+                      int S, int lane, float fc, bool ps = false) {
     constexpr bool C = MODE & 16, F = (MODE & 1) && !C, XM = (MODE & 2) && !C, XL = MODE & 4, A = MODE & 8,
                    LX = F || XL, CX = C && (MODE & 2);
     const C2Geo& g = a.g;
@@ -1192,6 +1192,56 @@ ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0,
         if (CX) u *= code_mask(c);
         return A ? d + u : u;
     };
+    if (PS && ps) {
+        // phase-major rows (c2_dgradr_kernel with TM 2 at the 3x9 stride-2 layers): tile 0 holds
+        // phase 0 and tile 1 phase 1 of the 32 ci, register r of both the same ci
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = nl + j * 32;
+            if (n >= nend) continue;
+            const int tr = n / U, u = n - tr * U, f = 2 * u - g.pf;
+            if (f >= 0 && f + 1 < g.Fi) {
+#pragma unroll
+                for (int h8 = 0; h8 < 16; h8 += 8) {
+                    int64_t o[8];
+                    f32x2u X[8], R[8], D[8];
+                    uint32_t Cc[8][2];
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) {
+                        o[p] = (((int64_t)b * g.Ci + mfma_row(h8 + p, lane)) * g.T2 + tr) * g.Fi + f;
+                        if (LX) X[p] = *(const f32x2u*)(xs + o[p]);
+                        if (F) R[p] = *(const f32x2u*)(rs + o[p]);
+                        if (A) D[p] = *(const f32x2u*)(dx + o[p]);
+                        if (C) {
+                            Cc[p][0] = cs[o[p]];
+                            Cc[p][1] = cs[o[p] + 1];
+                        }
+                    }
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) {
+                        f32x2u s2;
+#pragma unroll
+                        for (int e = 0; e < 2; ++e)
+                            s2[e] = combine(acc[e][j][h8 + p], LX ? X[p][e] : 0.f, F ? R[p][e] : 0.f,
+                                            A ? D[p][e] : 0.f, C ? Cc[p][e] : 0u);
+                        *(f32x2u*)(dx + o[p]) = s2;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 2; ++e)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int fe = f + e;
+                        if (fe < 0 || fe >= g.Fi) continue;
+                        const int64_t q = (((int64_t)b * g.Ci + mfma_row(r, lane)) * g.T2 + tr) * g.Fi + fe;
+                        dx[q] = combine(acc[e][j][r], LX ? xs[q] : 0.f, F ? rs[q] : 0.f, A ? dx[q] : 0.f,
+                                        C ? (uint32_t)cs[q] : 0u);
+                    }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1258,6 +1308,9 @@ ENCX_DEV void dgr_epi(const C2Dg& a, const f32x16 (&acc)[TM][TN], int b, int m0,
 template <int TM, int BN, int JC, int MQ, int CKM, int OCC = 1, int DB = 0, bool YM = true>
 __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
     constexpr int BM = 32 * TM, TN = BN / 128, MW = (JC * CKM * BM / 4 + NT - 1) / NT;
+    // phase-major rows at the 3x9 stride-2 layers (both 32-row tiles in one workgroup): the fifth
+    // polyphase tap, zero for every phase-1 row (kf = 2 q + 1 = 9), is skipped for tile 1
+    constexpr bool PS = TM == 2 && JC == 5;
     extern __shared__ float smem[];
     const C2Geo g = a.g;
     const int CK = a.CK, NR = a.NR, RL = a.RL, U = a.U, S = g.sf;
@@ -1274,6 +1327,7 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
     const int h = lane >> 5, l32 = lane & 31;
     const TileId tile = xcd_tile();
     const int b = tile.z, n0 = tile.x * BN, m0 = tile.y * BM;
+    const bool ps = PS && S == 2 && M == 64 && m0 == 0;
     const int wn0 = wave * TN * 32;
     const int Nall = g.T2 * U, nend = min(Nall, n0 + BN);
     const int tf = n0 / U, u0 = n0 - tf * U;
@@ -1366,7 +1420,15 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
             if (j < WQ && rr < (VC - c0) * JC && m0 + col + 3 >= M)
                 for (int k = 0; k < 4; ++k)
                     wv[u][k] = m0 + col + k < M ? a.wp[((int64_t)c0 * JC + rr) * M + m0 + col + k] : 0.f;
-            if (j < WQ) *(f32x4*)(A + rr * BM + col) = wv[u];
+            if (j < WQ) {
+                if (PS && ps) {  // rows col .. col + 3 = (ci, 0), (ci, 1), (ci + 1, 0), (ci + 1, 1)
+                    const int ci = col >> 1;
+                    *(f32x2*)(A + rr * BM + ci) = (f32x2){wv[u][0], wv[u][2]};
+                    *(f32x2*)(A + rr * BM + 32 + ci) = (f32x2){wv[u][1], wv[u][3]};
+                } else {
+                    *(f32x4*)(A + rr * BM + col) = wv[u];
+                }
+            }
         }
     };
     auto compute = [&](const float* X, const float* A) {
@@ -1388,8 +1450,9 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
                     else if (cp + 2 < CK) rd(cp + 2, 0, na, nb);
 #pragma unroll
                     for (int i = 0; i < TM; ++i)
+                        if (!(PS && ps && i == 1 && q == JC - 1))
 #pragma unroll
-                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(ca[i], cb[j], acc[i][j]);
+                            for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(ca[i], cb[j], acc[i][j]);
 #pragma unroll
                     for (int i = 0; i < TM; ++i) ca[i] = na[i];
 #pragma unroll
@@ -1411,8 +1474,9 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
                 for (int j = 0; j < TN; ++j) bv[j] = xq[boff[j] - q];
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
+                    if (!(PS && ps && i == 1 && q == JC - 1))
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+                        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
             }
         }
     };
@@ -1447,7 +1511,7 @@ __global__ __launch_bounds__(NT, OCC) void c2_dgradr_kernel(C2Dg a) {
                      (a.fcode && a.ffr && !ldx ? 16 : 0);
     switch (mode) {
 #define ENCX_EPI(m) \
-    case m: dgr_epi<TM, TN, m>(a, acc, b, m0, n0 + wn0 + l32, nend, U, M, S, lane, fc); break;
+    case m: dgr_epi<TM, TN, m, PS>(a, acc, b, m0, n0 + wn0 + l32, nend, U, M, S, lane, fc, ps); break;
         ENCX_EPI(0) ENCX_EPI(1) ENCX_EPI(3) ENCX_EPI(6) ENCX_EPI(7)
         ENCX_EPI(8) ENCX_EPI(9) ENCX_EPI(11) ENCX_EPI(14) ENCX_EPI(15)
         ENCX_EPI(17) ENCX_EPI(19) ENCX_EPI(25) ENCX_EPI(27)
