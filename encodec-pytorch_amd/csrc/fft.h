@@ -70,24 +70,54 @@ ENCX_DEV void make_twiddles(f2v* tw, float sign) {
     }
 }
 
-// Stockham radix-2 over FPW frames of M points in buf[0] (result in buf[RES]); tw[2t] = e^{+-2 pi i t/M}
-// (CONJ: the conjugate twiddles, the inverse transform from the forward table)
+// Stockham over FPW frames of M points in buf[0] (result in buf[RES]); tw[k] = e^{-pi i k/M}, k <= M
+// (CONJ: the conjugate twiddles, the inverse transform from the forward table). Radix-4 stages
+// (one radix-2 stage first when log2 M is odd): half the passes, and so half the workgroup
+// barriers, of a radix-2 transform -- the barriers, not the arithmetic, set the pace of these
+// one-to-few-frame workgroups.
+template <int M, bool CONJ>
+ENCX_DEV f2v tw_at(const f2v* tw, int k) {  // e^{-+pi i k / M} for 0 <= k < 2M (e^{-pi i} = -1)
+    const f2v t = k <= M ? tw[k] : -tw[k - M];
+    return CONJ ? cconj(t) : t;
+}
 template <int M, int FPW, bool CONJ = false>
 ENCX_DEV int stockham(f2v* buf, const f2v* tw) {
     int cur = 0;
-#pragma unroll 1
-    for (int ns = 1; ns < M; ns <<= 1) {
-        const f2v* src = buf + cur * (FPW * M);
-        f2v* dst = buf + (cur ^ 1) * (FPW * M);
+    int ns = 1;
+    if (__builtin_ctz(M) & 1) {  // radix-2 stage
+        const f2v* src = buf;
+        f2v* dst = buf + FPW * M;
         for (int q = threadIdx.x; q < FPW * (M / 2); q += FFT_NT) {
             const int f = q / (M / 2), j = q - f * (M / 2);
+            const f2v a = src[f * M + j], b = src[f * M + j + M / 2];
+            dst[f * M + 2 * j] = a + b;
+            dst[f * M + 2 * j + 1] = a - b;
+        }
+        __syncthreads();
+        cur = 1;
+        ns = 2;
+    }
+#pragma unroll 1
+    for (; ns < M; ns <<= 2) {
+        const f2v* src = buf + cur * (FPW * M);
+        f2v* dst = buf + (cur ^ 1) * (FPW * M);
+        const int tstep = M / (2 * ns);  // twiddle index per unit of jm: e^{-2 pi i jm / (4 ns)}
+        for (int q = threadIdx.x; q < FPW * (M / 4); q += FFT_NT) {
+            const int f = q / (M / 4), j = q - f * (M / 4);
             const int jm = j & (ns - 1);
-            const f2v a = src[f * M + j];
-            const f2v t = tw[2 * jm * (M / (2 * ns))];
-            const f2v b = cmul(src[f * M + j + M / 2], CONJ ? cconj(t) : t);
-            const int d = f * M + ((j - jm) << 1) + jm;
-            dst[d] = a + b;
-            dst[d + ns] = a - b;
+            const f2v* s0 = src + f * M + j;
+            const f2v a0 = s0[0];
+            const f2v a1 = cmul(s0[M / 4], tw_at<M, CONJ>(tw, jm * tstep));
+            const f2v a2 = cmul(s0[M / 2], tw_at<M, CONJ>(tw, 2 * jm * tstep));
+            const f2v a3 = cmul(s0[3 * M / 4], tw_at<M, CONJ>(tw, 3 * jm * tstep));
+            const f2v b0 = a0 + a2, b1 = a0 - a2, b2 = a1 + a3, b3 = a1 - a3;
+            // -i b3 (forward) / +i b3 (inverse)
+            const f2v ib3 = CONJ ? (f2v){-b3[1], b3[0]} : (f2v){b3[1], -b3[0]};
+            const int d = f * M + ((j - jm) << 2) + jm;
+            dst[d] = b0 + b2;
+            dst[d + ns] = b1 + ib3;
+            dst[d + 2 * ns] = b0 - b2;
+            dst[d + 3 * ns] = b1 - ib3;
         }
         __syncthreads();
         cur ^= 1;
@@ -148,7 +178,7 @@ __global__ __launch_bounds__(FFT_NT) void c2r_kernel(FftArgs a) {
     __shared__ f2v tw[M + 1];
     __shared__ f2v Ys[FPW * NB];
     __shared__ float Win[N];
-    make_twiddles<M>(tw, 1.f);  // e^{+pi i k / M}
+    make_twiddles<M>(tw, -1.f);  // e^{-pi i k / M}; the inverse conjugates them
     for (int t = threadIdx.x; t < N; t += FFT_NT) Win[t] = a.win[(int64_t)t * a.wstride];
     const int row0 = blockIdx.x * FPW;
     for (int q = threadIdx.x; q < FPW * NB; q += FFT_NT) {
@@ -172,11 +202,11 @@ __global__ __launch_bounds__(FFT_NT) void c2r_kernel(FftArgs a) {
     for (int q = threadIdx.x; q < FPW * M; q += FFT_NT) {
         const int f = q / M, k = q - f * M;
         const f2v yk = Ys[f * NB + k], ym = cconj(Ys[f * NB + M - k]);
-        const f2v A = yk + ym, Bv = cmul(yk - ym, tw[k]);
+        const f2v A = yk + ym, Bv = cmul(yk - ym, cconj(tw[k]));
         buf[q] = (f2v){A[0] - Bv[1], A[1] + Bv[0]};
     }
     __syncthreads();
-    const int res = stockham<M, FPW>(buf, tw);  // inverse (e^{+}), unnormalised
+    const int res = stockham<M, FPW, true>(buf, tw);  // inverse (e^{+}), unnormalised
     const float* c = reinterpret_cast<const float*>(buf + res * (FPW * M));  // y[2j], y[2j+1] interleaved
     for (int i = threadIdx.x; i < FPW * N; i += FFT_NT) {
         const int f = i / N, t = i - f * N, row = row0 + f;
