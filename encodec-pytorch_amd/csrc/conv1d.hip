@@ -2715,6 +2715,41 @@ size_t wgrad_ws_bytes(int64_t B, int64_t A, int64_t Tl, int64_t C, int64_t K) {
 
 static size_t maxz(size_t a, size_t b) { return a > b ? a : b; }
 
+// Backward-data of a dilated Conv1d (any stride): the gradient of every padded input position,
+// g[p] = sum_{co,k : p = t*s + k*d} wf[ci][k][co] * dy[co][t], one thread per position (the
+// block's (b, ci) row is uniform, so the weight loads are scalar). Interior positions take
+// act'(x) (+ dx) and land in dx; pad positions go to the side buffer for conv_fold_edges. A direct
+// VALU form: EnCodec's configurations use d = 1 (modules/seanet.py:114-117 dilates only with
+// n_residual_layers > 1), so this is the general path, not a hot one.
+__global__ void conv_dgrad_dilated_kernel(const float* __restrict__ dy, const float* __restrict__ wf,
+                                          const float* __restrict__ xact, float* __restrict__ dx,
+                                          float* __restrict__ side, int Cin, int Tx, int Cout, int Tout,
+                                          int K, int s, int d, int pl, int pr, int act, int accumulate) {
+    const int row = blockIdx.y;  // b * Cin + ci
+    const int b = row / Cin, ci = row - b * Cin;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int Tpad = pl + Tx + pr;
+    if (p >= Tpad) return;
+    const float* dyb = dy + (int64_t)b * Cout * Tout;
+    const float* w = wf + (int64_t)ci * K * Cout;
+    float g = 0.f;
+    for (int k = 0; k < K; ++k) {
+        const int q = p - k * d;
+        if (q < 0 || q % s) continue;
+        const int t = q / s;
+        if (t >= Tout) continue;
+        for (int co = 0; co < Cout; ++co) g = fmaf(w[k * Cout + co], dyb[(int64_t)co * Tout + t], g);
+    }
+    const int m = p - pl;
+    if (m >= 0 && m < Tx) {
+        const int64_t idx = (int64_t)row * Tx + m;
+        if (act != ENCX_ACT_NONE) g *= act_grad(act, xact[idx]);
+        dx[idx] = accumulate ? dx[idx] + g : g;
+    } else if (side) {
+        side[(int64_t)row * (pl + pr) + (m < 0 ? p : p - Tx)] = g;
+    }
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -2792,6 +2827,36 @@ int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float
         hipLaunchKernelGGL(conv_fold_edges, dim3(cdiv(rows, 256)), dim3(256), 0, st, side, x, dx,
                            rows, (int)Tin, (int)pad_left, (int)pad_right, (int)short_ext, pad_mode,
                            pre_act);
+        ENCX_CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+int encx_conv1d_bwd_data_dilated(const float* dy, const float* wf, const float* x, float* dx, float* ws,
+                                 int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                                 int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
+                                 int64_t pad_right, int64_t short_ext, int pad_mode, int pre_act,
+                                 int accumulate, encx_stream_t stream) {
+    ENCX_REQUIRE(dy && wf && dx && B > 0 && Cin > 0 && Cout > 0 && Tin > 0 && Tout > 0 && K > 0);
+    ENCX_REQUIRE(stride > 0 && dilation > 0 && pad_left >= 0 && pad_right >= 0 && short_ext >= 0);
+    ENCX_REQUIRE(pre_act == ENCX_ACT_NONE || x);
+    const int64_t Tpad = pad_left + Tin + pad_right;
+    ENCX_REQUIRE((Tout - 1) * stride + (K - 1) * dilation < Tpad && B * Cin <= 65535);
+    const bool fold = pad_left + pad_right > 0 && pad_mode == ENCX_PAD_REFLECT;
+    ENCX_REQUIRE(!fold || ws);
+    hipStream_t st = (hipStream_t)stream;
+    encx_prof_scope ps(st, 2.0 * B * Cout * Tout * Cin * K,
+                       4.0 * (B * Cout * Tout + B * Cin * Tin * (1 + (pre_act ? 1 : 0) + (accumulate ? 1 : 0)) + Cin * K * Cout),
+                       "conv_dgrad");
+    ps.tag(" %ldx%ld k%ld s%ld d%ld T%ld", (long)Cin, (long)Cout, (long)K, (long)stride, (long)dilation, (long)Tout);
+    hipLaunchKernelGGL(conv_dgrad_dilated_kernel, dim3(cdiv(Tpad, 256), B * Cin), dim3(256), 0, st, dy, wf, x, dx,
+                       fold ? ws : nullptr, (int)Cin, (int)Tin, (int)Cout, (int)Tout, (int)K, (int)stride,
+                       (int)dilation, (int)pad_left, (int)pad_right, pre_act, accumulate);
+    ENCX_CHECK_LAUNCH();
+    if (fold) {
+        const int rows = (int)(B * Cin);
+        hipLaunchKernelGGL(conv_fold_edges, dim3(cdiv(rows, 256)), dim3(256), 0, st, ws, x, dx, rows, (int)Tin,
+                           (int)pad_left, (int)pad_right, (int)short_ext, pad_mode, pre_act);
         ENCX_CHECK_LAUNCH();
     }
     return 0;

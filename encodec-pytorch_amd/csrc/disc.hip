@@ -3801,12 +3801,19 @@ static bool disc_fft(int64_t n) {
     return encx_opt(OPT_FFT) != 0 && encx_fft::fft_ok(n);
 }
 
+static double hann_norm(int64_t n) { return 1.0 / sqrt(3.0 * (double)n / 8.0); }  // sum of periodic hann^2 = 3n/8
+
 int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B, int64_t C, int64_t T,
                        int64_t n_fft, int64_t hop, encx_stream_t stream) {
+    return encx_disc_spec_fwd_scaled(x, tables, z, B, C, T, n_fft, hop, hann_norm(n_fft), stream);
+}
+
+int encx_disc_spec_fwd_scaled(const float* x, const float* tables, float* z, int64_t B, int64_t C, int64_t T,
+                              int64_t n_fft, int64_t hop, double scale, encx_stream_t stream) {
     ENCX_REQUIRE(x && tables && z && T >= n_fft && hop > 0);
     hipStream_t st = (hipStream_t)stream;
     const int Fr = (int)((T - n_fft) / hop + 1), nb = (int)(n_fft / 2 + 1);
-    const float inv = (float)(1.0 / sqrt(3.0 * (double)n_fft / 8.0));  // sum of periodic hann^2 = 3n/8
+    const float inv = (float)scale;
     const int M = (int)(B * C * Fr), N = 2 * nb, K = (int)n_fft;
     const bool fft = disc_fft(n_fft);
     encx_prof_scope ps(st, fft ? 2.5 * M * K * log2((double)K) : 2.0 * M * N * K, 4.0 * (B * C * T + (int64_t)M * N), "spec_fwd");
@@ -3826,10 +3833,16 @@ size_t encx_disc_spec_bwd_workspace(int64_t B, int64_t C, int64_t T, int64_t n_f
 /* dx (+)= d spectrogram^T dz (accumulate: add into dx). ws: encx_disc_spec_bwd_workspace. */
 int encx_disc_spec_bwd(const float* dz, const float* tables, float* dx, float* ws, int accumulate, int64_t B,
                        int64_t C, int64_t T, int64_t n_fft, int64_t hop, encx_stream_t stream) {
+    return encx_disc_spec_bwd_scaled(dz, tables, dx, ws, accumulate, B, C, T, n_fft, hop, hann_norm(n_fft), stream);
+}
+
+int encx_disc_spec_bwd_scaled(const float* dz, const float* tables, float* dx, float* ws, int accumulate,
+                              int64_t B, int64_t C, int64_t T, int64_t n_fft, int64_t hop, double scale,
+                              encx_stream_t stream) {
     ENCX_REQUIRE(dz && tables && dx && ws && T >= n_fft && hop > 0);
     hipStream_t st = (hipStream_t)stream;
     const int Fr = (int)((T - n_fft) / hop + 1), nb = (int)(n_fft / 2 + 1);
-    const float inv = (float)(1.0 / sqrt(3.0 * (double)n_fft / 8.0));
+    const float inv = (float)scale;
     const int M = (int)(B * C * Fr), N = (int)n_fft, K = 2 * nb;
     {
         const bool fft = disc_fft(n_fft);

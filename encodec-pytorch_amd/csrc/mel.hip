@@ -144,6 +144,19 @@ __global__ void tables_kernel(float* t, const float* mel, int n, int nm) {
     }
 }
 
+// DFT table of an arbitrary window (a DiscriminatorSTFT whose win_length < n_fft: torch.stft
+// centres the window in n_fft zeros): bt[t][c] = win[t] cos / -win[t] sin of the same angle
+__global__ void window_table_kernel(float* bt, const float* win, int n) {
+    const int nb = n / 2 + 1, nb2 = 2 * nb;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n * nb2) return;
+    const int tt = (int)(i / nb2), c = (int)(i - (int64_t)tt * nb2);
+    const int k = c < nb ? c : c - nb;
+    const double w = (double)win[tt];
+    const double ang = 2.0 * M_PI * (double)(((int64_t)k * tt) % n) / (double)n;
+    bt[i] = (float)(c < nb ? w * cos(ang) : -w * sin(ang));
+}
+
 constexpr int LB = 1024;  // loss partial blocks
 
 // ly = log10(clamp(mel_y)); d = ly - lx; parts; dmel (in place over mel_y)
@@ -540,6 +553,15 @@ int encx_mel_tables_init(float* tables, const float* mel_basis, int64_t n_fft, i
     const int64_t nsup = n_mels + n_fft / 2 + 1;
     hipLaunchKernelGGL(support_kernel, dim3(cdiv(nsup, 256)), dim3(256), 0, (hipStream_t)stream, tables, mel_basis,
                        (int)n_fft, (int)n_mels);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+int encx_spec_tables_window(float* tables, const float* window, int64_t n_fft, encx_stream_t stream) {
+    ENCX_REQUIRE(tables && window && n_fft >= 4 && (n_fft % 4) == 0);
+    const int64_t tot = n_fft * 2 * (n_fft / 2 + 1);
+    hipLaunchKernelGGL(window_table_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, (hipStream_t)stream, tables, window,
+                       (int)n_fft);
     ENCX_CHECK_LAUNCH();
     return 0;
 }

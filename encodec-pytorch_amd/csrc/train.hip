@@ -73,11 +73,14 @@ __global__ void balancer_combine_kernel(const float* g0, const float* g1, const 
                                         const float* g3, const float* s, float* out, int64_t n) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    float v = g0[i] * s[0];
-    if (g1) v = v + g1[i] * s[1];
-    if (g2) v = v + g2[i] * s[2];
-    if (g3) v = v + g3[i] * s[3];
-    out[i] = v;
+    {
+#pragma clang fp contract(off)  // grad = g * scale, then out_grad += grad: two roundings each
+        float v = g0[i] * s[0];
+        if (g1) v = v + g1[i] * s[1];
+        if (g2) v = v + g2[i] * s[2];
+        if (g3) v = v + g3[i] * s[3];
+        out[i] = v;
+    }
 }
 
 // torch.optim.Adam single-tensor step (amsgrad off, no weight decay), flat buffers
@@ -159,7 +162,7 @@ int encx_item_norm_mean(const float* g, float* out, float* ws, int64_t B, int64_
 
 int encx_balancer_update(const float* norms, double* total, double* fix, double* avg, float* red,
                          int nl, double beta, float count, encx_stream_t stream) {
-    ENCX_REQUIRE(norms && total && fix && avg && red && nl > 0 && nl <= 4);
+    ENCX_REQUIRE(norms && total && fix && avg && red && nl > 0 && nl <= ENCX_BALANCER_MAX_LOSSES);
     hipLaunchKernelGGL(balancer_update_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, norms,
                        total, fix, avg, red, nl, beta, count);
     ENCX_CHECK_LAUNCH();
@@ -169,7 +172,7 @@ int encx_balancer_update(const float* norms, double* total, double* fix, double*
 int encx_balancer_scales(const double* avg, const float* red, const double* ratio, float* scales,
                          int nl, double total_norm, double eps, int from_red,
                          encx_stream_t stream) {
-    ENCX_REQUIRE(avg && red && ratio && scales && nl > 0 && nl <= 4);
+    ENCX_REQUIRE(avg && red && ratio && scales && nl > 0 && nl <= ENCX_BALANCER_MAX_LOSSES);
     hipLaunchKernelGGL(balancer_scales_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, avg, red,
                        ratio, scales, nl, total_norm, eps, from_red);
     ENCX_CHECK_LAUNCH();

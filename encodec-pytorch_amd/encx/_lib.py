@@ -24,6 +24,7 @@ _CTYPES = {
 ENCX_PAD_ZERO, ENCX_PAD_REFLECT = 0, 1
 ENCX_ACT_NONE, ENCX_ACT_ELU = 0, 1
 ENCX_AC_STATE, ENCX_AC_MAXBIT, ENCX_AC_POS = 8, 6, 7  # arithmetic-decoder state words (encx.h)
+ENCX_BALANCER_MAX_LOSSES = 64  # encx.h
 
 
 def _ctype(t):

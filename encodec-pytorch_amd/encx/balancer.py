@@ -8,7 +8,7 @@ import torch
 from torch import autograd
 
 from . import distrib
-from ._lib import call, ptr, stream, lib
+from ._lib import call, ptr, stream, lib, ENCX_BALANCER_MAX_LOSSES
 
 
 class Balancer:
@@ -17,8 +17,8 @@ class Balancer:
     def __init__(self, weights, rescale_grads: bool = True, total_norm: float = 1.,
                  ema_decay: float = 0.999, per_batch_item: bool = True, epsilon: float = 1e-12,
                  monitor: bool = False):
-        if len(weights) > 4:
-            raise NotImplementedError('encx Balancer combines up to 4 losses')
+        if len(weights) > ENCX_BALANCER_MAX_LOSSES:
+            raise ValueError(f'encx Balancer combines up to {ENCX_BALANCER_MAX_LOSSES} losses')
         self.weights = weights
         self.per_batch_item = per_batch_item
         self.total_norm = total_norm
@@ -49,6 +49,9 @@ class Balancer:
                                       dtype=torch.float32),
                 'norms': torch.zeros(nl, device=device, dtype=torch.float32),
                 'scales': torch.zeros(nl, device=device, dtype=torch.float32),
+                # five or more losses: the combine runs in calls of four grads, each later call
+                # taking the previous out as g0 with scale 1 (the same left-to-right sum)
+                'chain': torch.ones(max(0, -(-(nl - 4) // 3)), 4, device=device, dtype=torch.float32),
             }
         return self._state
 
@@ -93,8 +96,14 @@ class Balancer:
         else:
             scales = st['plain']
         out = torch.empty_like(gl[0])
-        gp = [ptr(g) for g in gl] + [None] * (4 - len(gl))
+        gp = [ptr(g) for g in gl[:4]] + [None] * (4 - len(gl[:4]))
         call('encx_balancer_combine', gp[0], gp[1], gp[2], gp[3], ptr(scales), ptr(out), out.numel(), s)
+        for j, k0 in enumerate(range(4, len(gl), 3)):  # out += s_k g_k for the losses after the 4th
+            k1 = min(k0 + 3, len(gl))
+            sc = st['chain'][j]
+            sc[1:1 + k1 - k0].copy_(scales[k0:k1])
+            gp = [ptr(g) for g in gl[k0:k1]] + [None] * (3 - (k1 - k0))
+            call('encx_balancer_combine', ptr(out), gp[0], gp[1], gp[2], ptr(sc), ptr(out), out.numel(), s)
         self._gl = None
         if self.monitor:
             avg = st['avg'].tolist()

@@ -45,8 +45,6 @@ class DiscriminatorSTFT(nn.Module):
                  sample_rate: int = 24000):
         super().__init__()
         assert len(kernel_size) == 2 and len(stride) == 2
-        if win_length != n_fft or not normalized:
-            raise NotImplementedError('encx DiscriminatorSTFT: win_length == n_fft, normalized=True')
         if activation != 'LeakyReLU' or activation_params.get('negative_slope', 0.01) != 0.2:
             raise NotImplementedError('encx DiscriminatorSTFT: LeakyReLU(0.2) is fused into the convs')
         self.filters = filters
@@ -58,6 +56,7 @@ class DiscriminatorSTFT(nn.Module):
         self.normalized = normalized
         self.sample_rate = sample_rate
         self.spec_transform = _SpecTransform(win_length)
+        self._win_tables = None  # (device / window key, (tables, scale)) when win_length != n_fft or not normalized
         spec_channels = 2 * in_channels
         self.convs = nn.ModuleList()
         self.convs.append(NormConv2d(spec_channels, filters, kernel_size=kernel_size,
@@ -77,7 +76,14 @@ class DiscriminatorSTFT(nn.Module):
     def forward(self, x: torch.Tensor, param_grads: bool = True, mode=None):
         """msstftd.py:86-105: x [B, C, T] -> (logits [B, out, frames, bins'], 5 feature maps)."""
         fmap = []
-        z = ops.DiscSpecFn.apply(x, self.n_fft, self.hop_length, self.sample_rate)
+        window = None  # the reference's configuration: hann(n_fft), normalized (precomputed tables)
+        if self.win_length != self.n_fft or not self.normalized:
+            key = (str(x.device), self.spec_transform.window.data_ptr())
+            if self._win_tables is None or self._win_tables[0] != key:
+                self._win_tables = (key, ops.spec_window_tables(self.spec_transform.window, self.n_fft,
+                                                                self.normalized))
+            window = self._win_tables[1]
+        z = ops.DiscSpecFn.apply(x, self.n_fft, self.hop_length, self.sample_rate, window)
         for i, layer in enumerate(self.convs):
             z = layer(z, act=True, param_grads=param_grads, mode=mode, first=i == 0)
             fmap.append(z)

@@ -270,9 +270,10 @@ class Conv1dFn(torch.autograd.Function):
         Cout = v.shape[0]
         pl, pr, e, tout = conv_geometry(T, K, s, d, causal, pad_mode)
         need_dx = ctx.needs_input_grad[0]
+        # a dilated conv's backward-data reads the forward layout (encx_conv1d_bwd_data_dilated)
+        wf, wp = _weight_prep(v, g, K, s, True, need_dx and d == 1)
         if need_dx and d != 1:
-            raise NotImplementedError('encx: backward-data of dilated Conv1d (EnCodec uses d=1)')
-        wf, wp = _weight_prep(v, g, K, s, True, need_dx)
+            wp = wf
         y = torch.empty(B, Cout, tout, device=x.device, dtype=torch.float32)
         if res is not None:
             res = res.contiguous()
@@ -311,9 +312,14 @@ class Conv1dFn(torch.autograd.Function):
             else:
                 dx = torch.empty_like(x)
                 park = role == 'join'  # the first of the two: park it, hand autograd nothing
-            ws = _ws(lib.encx_conv1d_bwd_data_workspace(B, Cin, T, Cout, tout, K, s, pl, pr), x)
-            call('encx_conv1d_bwd_data', ptr(dy), ptr(wp), ptr(x), ptr(dx), ptr(ws), B, Cin, T,
-                 Cout, tout, K, s, pl, pr, e, mode, act, acc, st)
+            if d == 1:
+                ws = _ws(lib.encx_conv1d_bwd_data_workspace(B, Cin, T, Cout, tout, K, s, pl, pr), x)
+                call('encx_conv1d_bwd_data', ptr(dy), ptr(wp), ptr(x), ptr(dx), ptr(ws), B, Cin, T,
+                     Cout, tout, K, s, pl, pr, e, mode, act, acc, st)
+            else:  # wp holds the forward layout here
+                ws = _f32(B * Cin * (pl + pr) + 1, x)
+                call('encx_conv1d_bwd_data_dilated', ptr(dy), ptr(wp), ptr(x), ptr(dx), ptr(ws), B, Cin,
+                     T, Cout, tout, K, s, d, pl, pr, e, mode, act, acc, st)
             if park:
                 link.grad, dx = dx, None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
@@ -784,8 +790,8 @@ class LSTMFn(torch.autograd.Function):
         x = x.contiguous()
         B, H, T = x.shape
         L = len(weights) // 4
-        if B > 64 or H % 16 or H > 1024:
-            raise NotImplementedError('encx LSTM: batch <= 64 per GPU, hidden % 16 == 0 and <= 1024')
+        if B > LSTM_MAX_BATCH or H % 16 or H > 1024:
+            raise NotImplementedError('encx LSTM: hidden % 16 == 0 and <= 1024 (lstm() splits the batch)')
         st = stream()
         wcat = _f32(L * 8 * H * H, x)
         wcatT = _f32(L * 8 * H * H, x)
@@ -842,8 +848,19 @@ class LSTMFn(torch.autograd.Function):
         return (dx, None, *grads)
 
 
+LSTM_MAX_BATCH = 64  # batch rows one launch of the recurrence kernels takes (csrc/lstm.hip)
+
+
 def lstm(x, weights, skip=True):
-    return LSTMFn.apply(x, skip, *weights)
+    """nn.LSTM takes any batch (modules/lstm.py:20-27); the batch items' recurrences are
+    independent, so a batch above LSTM_MAX_BATCH runs as near-equal chunks of at most that many
+    (the weight grads summed over the chunks by autograd)."""
+    B = x.shape[0]
+    if B <= LSTM_MAX_BATCH:
+        return LSTMFn.apply(x, skip, *weights)
+    n = -(-B // LSTM_MAX_BATCH)
+    sizes = [B // n + (i < B % n) for i in range(n)]
+    return torch.cat([LSTMFn.apply(xc, skip, *weights) for xc in torch.split(x, sizes)], dim=0)
 
 
 # ---------------------------------------------------------------------------- MS-STFT disc
@@ -1047,15 +1064,20 @@ class DiscSpecFn(torch.autograd.Function):
     'b c w t -> b c t w' of DiscriminatorSTFT.forward (msstftd.py:62-64, 97-99)."""
 
     @staticmethod
-    def forward(ctx, x, n_fft, hop, sr):
+    def forward(ctx, x, n_fft, hop, sr, window=None):
+        """window: None = hann(n_fft), normalized (the reference's configuration); else
+        (tables, scale) from spec_window_tables."""
         _check(x)
         x = x.contiguous()
         B, C, T = x.shape
-        tab = mel_tables(x.device, n_fft, 64, sr)
+        tab, scale = window if window is not None else (mel_tables(x.device, n_fft, 64, sr), None)
         Fr = (T - n_fft) // hop + 1
         z = torch.empty(B, 2 * C, Fr, n_fft // 2 + 1, device=x.device, dtype=torch.float32)
-        call('encx_disc_spec_fwd', ptr(x), ptr(tab), ptr(z), B, C, T, n_fft, hop, stream())
-        ctx.cfg = (B, C, T, n_fft, hop)
+        if scale is None:
+            call('encx_disc_spec_fwd', ptr(x), ptr(tab), ptr(z), B, C, T, n_fft, hop, stream())
+        else:
+            call('encx_disc_spec_fwd_scaled', ptr(x), ptr(tab), ptr(z), B, C, T, n_fft, hop, float(scale), stream())
+        ctx.cfg = (B, C, T, n_fft, hop, scale)
         ctx.tab = tab
         ctx.set_materialize_grads(False)
         return z
@@ -1063,13 +1085,35 @@ class DiscSpecFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz):
         if dz is None:  # the first conv produced no input grad (DiscGradMode.input False)
-            return None, None, None, None
-        B, C, T, n_fft, hop = ctx.cfg
+            return None, None, None, None, None
+        B, C, T, n_fft, hop, scale = ctx.cfg
         dz = dz.contiguous()
         dx = torch.empty(B, C, T, device=dz.device, dtype=torch.float32)
         ws = _ws(lib.encx_disc_spec_bwd_workspace(B, C, T, n_fft, hop), dz)
-        call('encx_disc_spec_bwd', ptr(dz), ptr(ctx.tab), ptr(dx), ptr(ws), 0, B, C, T, n_fft, hop, stream())
-        return dx, None, None, None
+        if scale is None:
+            call('encx_disc_spec_bwd', ptr(dz), ptr(ctx.tab), ptr(dx), ptr(ws), 0, B, C, T, n_fft, hop, stream())
+        else:
+            call('encx_disc_spec_bwd_scaled', ptr(dz), ptr(ctx.tab), ptr(dx), ptr(ws), 0, B, C, T, n_fft, hop,
+                 float(scale), stream())
+        return dx, None, None, None, None
+
+
+def spec_window_tables(window, n_fft, normalized):
+    """Tables + scale of torchaudio Spectrogram(n_fft, win_length=len(window), window,
+    normalized, center=False, power=None) (msstftd.py:62-64): torch.stft centres a shorter window
+    in n_fft zeros; normalized divides by sqrt(sum window^2) (torchaudio's 'window' norm)."""
+    wl = window.numel()
+    if wl > n_fft:
+        raise ValueError(f'win_length {wl} > n_fft {n_fft}')
+    w = torch.zeros(n_fft, device=window.device, dtype=torch.float32)
+    left = (n_fft - wl) // 2
+    w[left:left + wl] = window.float()
+    tab = torch.empty(lib.encx_mel_tables_floats(n_fft, 1), device=window.device, dtype=torch.float32)
+    basis = torch.zeros(1, n_fft // 2 + 1, device=window.device, dtype=torch.float32)
+    call('encx_mel_tables_init', ptr(tab), ptr(basis), n_fft, 1, stream())  # (mel part unused)
+    call('encx_spec_tables_window', ptr(tab), ptr(w), n_fft, stream())
+    scale = 1.0 / float(window.double().pow(2).sum().sqrt()) if normalized else 1.0
+    return tab, scale
 
 
 class HingeFn(torch.autograd.Function):

@@ -116,6 +116,17 @@ int encx_conv1d_bwd_data(const float* dy, const float* wp, const float* x, float
                          int64_t K, int64_t stride, int64_t pad_left, int64_t pad_right,
                          int64_t short_ext, int pad_mode, int pre_act, int accumulate,
                          encx_stream_t stream);
+/* Backward-data of a DILATED Conv1d (nn.Conv1d with dilation > 1 inside SConv1d,
+ * modules/conv.py:195-210; SEANetResnetBlock dilates its k3 conv when n_residual_layers > 1,
+ * modules/seanet.py:114-117): as encx_conv1d_bwd_data, but from the FORWARD weight layout wf
+ * [Cin][K][Cout] (encx_weightnorm_fwd's wf) with any stride and dilation. ws: B*Cin*(pad_left +
+ * pad_right) floats when pad_mode is reflect (the pad positions' grads before the fold), else
+ * may be NULL. */
+int encx_conv1d_bwd_data_dilated(const float* dy, const float* wf, const float* x, float* dx, float* ws,
+                                 int64_t B, int64_t Cin, int64_t Tin, int64_t Cout, int64_t Tout,
+                                 int64_t K, int64_t stride, int64_t dilation, int64_t pad_left,
+                                 int64_t pad_right, int64_t short_ext, int pad_mode, int pre_act,
+                                 int accumulate, encx_stream_t stream);
 /* dW[co,ci,k] = sum_{b,t} dy[b,co,t] act(xpad[b,ci,t*s+k*d]); db[co] = sum dy (db may be NULL).
  * dw is [Cout][Cin][K]; accumulate as above. ws: encx_conv1d_bwd_weight_workspace bytes. */
 int encx_conv1d_bwd_weight(const float* dy, const float* x, float* dw, float* db, float* ws,
@@ -266,6 +277,8 @@ int encx_reduce_sum(const float* parts, int64_t n, float scale, float* out, int 
 size_t encx_mel_tables_floats(int64_t n_fft, int64_t n_mels);
 /* window*cos / window*sin DFT tables + mel basis, built on the device from the mel basis
  * uploaded by the caller (host restatement of librosa.filters.mel). */
+/* Rewrite the DFT part of a table buffer for window [n_fft] (any window; the mel part is kept). */
+int encx_spec_tables_window(float* tables, const float* window, int64_t n_fft, encx_stream_t stream);
 int encx_mel_tables_init(float* tables, const float* mel_basis, int64_t n_fft, int64_t n_mels,
                          encx_stream_t stream);
 size_t encx_mel_workspace_floats(int64_t B, int64_t T, int64_t n_fft, int64_t n_mels);
@@ -306,6 +319,9 @@ int encx_lincomb(const float* x, const float* z, float* out, int64_t n, float a,
 size_t encx_item_norm_workspace(int64_t B);
 int encx_item_norm_mean(const float* g, float* out, float* ws, int64_t B, int64_t L,
                         encx_stream_t stream);
+/* Most losses one balancer combines (update / scales); combine takes four grads per call, more
+ * are chained (g0 = the previous out, its scale 1). */
+#define ENCX_BALANCER_MAX_LOSSES 64
 /* averager EMA (:10-28) in fp64: total = total*beta + norm; fix = fix*beta + 1; avg = total/fix;
  * red = [avg*count .., count] for the average_metrics all-reduce (distrib.py:112-124). */
 int encx_balancer_update(const float* norms, double* total, double* fix, double* avg, float* red,
@@ -315,7 +331,9 @@ int encx_balancer_update(const float* norms, double* total, double* fix, double*
 int encx_balancer_scales(const double* avg, const float* red, const double* ratio, float* scales,
                          int nl, double total_norm, double eps, int from_red,
                          encx_stream_t stream);
-/* out = g0*s0 + g1*s1 + g2*s2 + g3*s3 (g1..g3 may be NULL), the balanced output grad (:110-118) */
+/* out = g0*s0 + g1*s1 + g2*s2 + g3*s3 (g1..g3 may be NULL), the balanced output grad (:110-118),
+ * summed left to right; out may alias g0, so five or more losses chain calls with g0 = out and
+ * s0 = 1 (the reference's `out_grad += grad` order, exactly) */
 int encx_balancer_combine(const float* g0, const float* g1, const float* g2, const float* g3,
                           const float* scales, float* out, int64_t n, encx_stream_t stream);
 /* torch.optim.Adam step (amsgrad off, no weight decay) over flat fp32 buffers; step >= 1 is the
@@ -431,6 +449,14 @@ int encx_disc_spec_fwd(const float* x, const float* tables, float* z, int64_t B,
 size_t encx_disc_spec_bwd_workspace(int64_t B, int64_t C, int64_t T, int64_t n_fft, int64_t hop);
 int encx_disc_spec_bwd(const float* dz, const float* tables, float* dx, float* ws, int accumulate, int64_t B,
                        int64_t C, int64_t T, int64_t n_fft, int64_t hop, encx_stream_t stream);
+/* The same with the window and the scale of the caller: tables built by encx_mel_tables_init then
+ * encx_spec_tables_window (the window centred in n_fft zeros, as torch.stft does for win_length <
+ * n_fft), scale = 1/sqrt(sum w^2) for normalized=True or 1 (msstftd.py:62-64). */
+int encx_disc_spec_fwd_scaled(const float* x, const float* tables, float* z, int64_t B, int64_t C, int64_t T,
+                              int64_t n_fft, int64_t hop, double scale, encx_stream_t stream);
+int encx_disc_spec_bwd_scaled(const float* dz, const float* tables, float* dx, float* ws, int accumulate,
+                              int64_t B, int64_t C, int64_t T, int64_t n_fft, int64_t hop, double scale,
+                              encx_stream_t stream);
 /* Hinge / relative feature-matching losses (losses.py:44-56, 65-80). ws: workspace bytes. */
 size_t encx_disc_loss_workspace(void);
 /* out[0] (+)= scale * mean(relu(1 + s*x)) */

@@ -134,6 +134,43 @@ def test_conv_model_shapes_vs_oracle(li):
     near(b0.grad, p['m.' + pre + '.bias'].grad, 1e-4, 1e-5, tag + ' db')
 
 
+DILATED_LAYERS = [
+    # cin, cout, K, s, d, causal, pad_mode, pre_elu, T_in: SEANetResnetBlock's k3 conv at
+    # dilation_base ** j (modules/seanet.py:114-117, n_residual_layers > 1), both paddings, a
+    # short input (the reflect pad's zero extension), a strided dilated conv, residual widths
+    (16, 8, 3, 1, 2, True, 'reflect', True, 300), (32, 16, 3, 1, 4, False, 'reflect', True, 257),
+    (8, 8, 3, 1, 8, True, 'zero', False, 100), (8, 4, 3, 1, 3, True, 'reflect', True, 5),
+    (8, 16, 4, 2, 2, True, 'reflect', True, 97), (64, 32, 3, 1, 2, True, 'reflect', True, 1200),
+]
+
+
+@pytest.mark.parametrize('li', range(len(DILATED_LAYERS)))
+def test_dilated_conv1d_vs_oracle(li):
+    """nn.Conv1d(dilation=d) inside SConv1d (modules/conv.py:195-210): forward (the implicit GEMM
+    takes d), backward-data (encx_conv1d_bwd_data_dilated) and the weight / bias grads against
+    the fp64 oracle."""
+    from encx import ops
+    cin, cout, K, s, d, causal, pad, pre_elu, Tin = DILATED_LAYERS[li]
+    v0, g0, b0 = _case_params(700 + li, 'conv', cin, cout, K)
+    x0 = synth_wave((3, cin, Tin), 720 + li, amp=1.0)
+    act = 'elu' if pre_elu else None
+    x = G(x0).requires_grad_(True)
+    y = ops.conv1d(x, v0, g0, b0, K, s, d, causal, pad, act)
+    gy = synth_wave(tuple(y.shape), 740 + li, amp=1.0)
+    y.backward(G(gy))
+    p = {'m.conv.conv.weight_v': v0.detach().cpu().double().requires_grad_(True),
+         'm.conv.conv.weight_g': g0.detach().cpu().double().requires_grad_(True),
+         'm.conv.conv.bias': b0.detach().cpu().double().requires_grad_(True)}
+    xc = T(x0).double().requires_grad_(True)
+    yc = O.sconv1d(F.elu(xc) if pre_elu else xc, p, 'm', K, s, d, causal, pad)
+    yc.backward(T(gy).double())
+    tag = f'{cin}->{cout} K{K} s{s} d{d} {pad}'
+    for a, b, what in [(y, yc, 'y'), (x.grad, xc.grad, 'dx'), (v0.grad, p['m.conv.conv.weight_v'].grad, 'dv'),
+                       (g0.grad, p['m.conv.conv.weight_g'].grad, 'dg'), (b0.grad, p['m.conv.conv.bias'].grad, 'db')]:
+        b = b.detach()
+        close(a, b, 1e-4, 1e-5 * float(b.abs().max()), f'{tag} {what}')
+
+
 # --------------------------------------------------------------------------- RVQ
 class _CB:
     def __init__(self, d):
@@ -283,6 +320,29 @@ def test_balancer_fixture():
     assert abs(float(out)) < 1e-6
 
 
+@pytest.mark.parametrize('nl', [5, 7, 8])
+def test_balancer_many_losses_vs_oracle(nl):
+    """balancer.py:83-118 takes any number of losses; encx chains its 4-grad combine calls."""
+    from encx.balancer import Balancer
+    r = np.random.Generator(np.random.PCG64(nl))
+    w = {f'l{k}': float(k % 3 + 1) * 0.5 for k in range(nl)}
+    b, bo = Balancer(w), O.Balancer(w)
+    for it in range(3):
+        gs = {k: r.standard_normal((4, 1, 300)).astype(np.float32) * (k_i + 1)
+              for k_i, k in enumerate(w)}
+        out = b.combine({k: G(v) for k, v in gs.items()})
+        ref = bo.combine({k: T(v) for k, v in gs.items()})
+        close(out, ref, 1e-5, 1e-7, f'balancer nl={nl} it{it}')
+    # rescale_grads=False: out = sum_k w_k g_k, left to right as `out_grad += grad`
+    b = Balancer(w, rescale_grads=False)
+    gs = {k: r.standard_normal((2, 1, 50)).astype(np.float32) for k in w}
+    ref = 0
+    for k, v in gs.items():
+        ref = ref + T(v) * w[k]
+    out = b.combine({k: G(v) for k, v in gs.items()})
+    assert torch.equal(out.cpu(), ref), 'plain weighted sum not bit-exact'
+
+
 def test_adam_vs_oracle():
     from encx.optim import FlatAdam
     r = np.random.Generator(np.random.PCG64(5))
@@ -315,7 +375,9 @@ def test_normalize_and_scale():
 @pytest.mark.parametrize('B,H,Tn,L,fuse,persist,wgs', [
     (3, 32, 7, 1, 0, 1, 32), (17, 64, 20, 2, 0, 1, 32), (5, 48, 9, 3, 0, 1, 32), (32, 512, 75, 2, 0, 1, 32),
     (32, 512, 75, 2, 0, 0, 32), (17, 64, 20, 2, 1, 0, 32), (32, 512, 75, 2, 1, 0, 32), (17, 128, 20, 2, 0, 1, 32),
-    (5, 256, 9, 3, 0, 1, 32), (40, 384, 11, 1, 0, 1, 32), (17, 256, 20, 2, 0, 1, 1)])
+    (5, 256, 9, 3, 0, 1, 32), (40, 384, 11, 1, 0, 1, 32), (17, 256, 20, 2, 0, 1, 1),
+    # batches above one launch's 64 rows: run as chunks (ops.lstm)
+    (80, 64, 12, 2, 0, 1, 32), (130, 128, 9, 1, 0, 1, 32), (96, 512, 6, 2, 0, 0, 32)])
 def test_lstm_vs_oracle(B, H, Tn, L, fuse, persist, wgs):
     """encx LSTM (csrc/lstm.hip) forward + backward against the oracle's step-by-step
     restatement of SLSTM (modules/lstm.py:22-28) run in fp64 on the CPU, for 1, 2 and 3 layers:
@@ -633,3 +695,52 @@ def test_spectrogram_fft_vs_torch_fp64(n, fft):
     ez, eg = rel(z, ref), rel(gx, gref)
     print(f'n {n}: spectrogram {ez:.1e}, its transpose {eg:.1e}')
     assert ez < 2e-6 and eg < 2e-6, (ez, eg)
+
+
+@pytest.mark.parametrize('n,wl,normalized,fft', [(1024, 600, True, 1), (512, 512, False, 1), (256, 200, False, 1),
+                                                 (1024, 1000, True, 0), (2048, 1500, True, 1)])
+def test_disc_spectrogram_window_vs_stft_fp64(n, wl, normalized, fft):
+    """torchaudio Spectrogram(n_fft, win_length < n_fft, hann, normalized on / off, center=False,
+    power=None) of DiscriminatorSTFT (msstftd.py:62-64): torch.stft centres the hann(win_length)
+    window in n_fft zeros; normalized divides by sqrt(sum w^2). Through DiscriminatorSTFT's own
+    window tables (ops.spec_window_tables), spectrogram and transpose vs fp64 torch.stft."""
+    from encx import ops
+    from encx._lib import option
+    B, C, Tn = 2, 1, 5000
+    x64 = torch.from_numpy(synth_wave((B, C, Tn), n + wl)).double().requires_grad_(True)
+    w = torch.hann_window(wl, dtype=torch.float64)
+    st = torch.stft(x64.reshape(B * C, Tn), n_fft=n, hop_length=n // 4, win_length=wl, window=w, center=False,
+                    return_complex=True)
+    if normalized:
+        st = st / w.pow(2).sum().sqrt()
+    ref = torch.cat([st.real, st.imag], 0).reshape(2, B, C, n // 2 + 1, -1).permute(1, 0, 2, 4, 3)
+    ref = ref.reshape(B, 2 * C, -1, n // 2 + 1)
+    xg = x64.detach().float().to(DEV).requires_grad_(True)
+    dz = torch.randn(ref.shape, generator=torch.Generator().manual_seed(wl), dtype=torch.float64)
+    win = ops.spec_window_tables(torch.hann_window(wl).to(DEV), n, normalized)
+    with option(FFT=fft):
+        z = ops.DiscSpecFn.apply(xg, n, n // 4, 24000, win)
+        gx, = torch.autograd.grad(z, [xg], dz.float().to(DEV))
+    gref, = torch.autograd.grad(ref, [x64], dz)
+
+    def rel(a, b):
+        a, b = a.detach().double().cpu(), b.detach().double()
+        return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+    ez, eg = rel(z, ref), rel(gx, gref)
+    print(f'n {n} win {wl} normalized {normalized}: spectrogram {ez:.1e}, its transpose {eg:.1e}')
+    assert ez < 2e-6 and eg < 2e-6, (ez, eg)
+
+
+def test_disc_stft_win_length_module_vs_oracle():
+    """DiscriminatorSTFT(n_fft=1024, win_length=800) end to end against the oracle's forward
+    (torch.stft with win_length): logits and feature maps."""
+    from encx.msstftd import DiscriminatorSTFT
+    d = DiscriminatorSTFT(32, n_fft=1024, hop_length=256, win_length=800).to(DEV)
+    p = {f'd.{k}': v.detach().cpu().double() for k, v in d.state_dict().items()}
+    x0 = synth_wave((2, 1, 8000), 77, amp=0.3)
+    with torch.no_grad():
+        lg, fm = d(G(x0), param_grads=False)
+        lr, fr = O.disc_stft_forward(T(x0).double(), p, 'd', 1024, 256, 800)
+    close(lg, lr, 1e-4, 1e-4 * float(lr.abs().max()), 'logits')
+    for i, (a, b) in enumerate(zip(fm, fr)):
+        close(a, b, 1e-4, 1e-4 * float(b.abs().max()), f'fmap {i}')
