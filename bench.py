@@ -110,7 +110,13 @@ def main():
         os.environ.setdefault('ENCX_LSTM_PERSIST', '0')
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
+    # ENCX_DIST_FORCE=1 at one rank: the N > 1 step (segments, RCCL all-reduces) over a one-rank
+    # RCCL group -- the per-rank cost of the data-parallel path on this GPU (encx/distrib.py)
+    force = os.environ.get('ENCX_DIST_FORCE', '0') == '1' and world == 1 and not rehearse
+    if force:
+        for k, v in (('MASTER_ADDR', '127.0.0.1'), ('MASTER_PORT', '29533'), ('RANK', '0'), ('WORLD_SIZE', '1')):
+            os.environ.setdefault(k, v)
+    if world > 1 or force:
         if rehearse:
             torch.distributed.init_process_group('gloo')
         else:
@@ -256,6 +262,8 @@ def main():
             out['n_gpus'] = 1
             out['ranks'] = world
             out['config']['parallelism'] = f'dp{world} rehearsal: {world} ranks on 1 GPU over gloo'
+        if force:
+            out['config']['parallelism'] = 'dp1, the N > 1 step forced over a one-rank RCCL group (ENCX_DIST_FORCE)'
         if world == 1 and not args.no_cpu_baseline:
             # every host core this job may use: the process's CPU affinity, capped by the CPU share
             # the box grants a one-GPU job (OMP_NUM_THREADS, 16 on the pool's boxes; os.cpu_count()
@@ -264,7 +272,7 @@ def main():
             share = int(os.environ.get('OMP_NUM_THREADS', '0') or 0)
             out['cpu_baseline'] = cpu_baseline(args.config, min(cores, share) if share > 0 else cores)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or force:
         torch.distributed.destroy_process_group()
 
 
