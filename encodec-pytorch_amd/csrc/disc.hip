@@ -1834,7 +1834,10 @@ __global__ __launch_bounds__(NWV * 64) void c2_dgrad_rw_kernel(C2DgR R) {
 #define ENCX_DN_QP 4  // staging quads in flight per thread and tensor (compile-time A/B knob)
 #endif
 constexpr int DN_ROWS = 16, DN_COLS = 64, DN_FPT = 4, DN_CC = 8, DN_MAXHALO = 4;
-template <int CI, int KT, int KF, bool YM = true, bool VQ = true>
+// DT: the time dilation at compile time (the staging's index splits then divide by constants:
+// with a runtime row count they were integer divisions, and the staging's VALU work rivalled the
+// FMAs'); interior quads (the whole quad inside the row) skip the edge shift / mask.
+template <int CI, int KT, int KF, bool YM = true, bool VQ = true, int DT = 1>
 __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
     constexpr int RC = (DN_COLS + KF - 1 + 3) & ~3;  // LDS row length (float4 aligned)
     constexpr int WIN4 = (DN_FPT + KF - 1 + 3) / 4;
@@ -1842,7 +1845,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
     const C2Geo g = a.g;
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int f0 = blockIdx.x * DN_COLS, t0 = blockIdx.y * DN_ROWS, b = blockIdx.z;
-    const int halo = (KT - 1) * g.dt, NRW = DN_ROWS + halo;
+    constexpr int halo = (KT - 1) * DT, NRW = DN_ROWS + halo;
     const int tbase = t0 + g.pt - halo, fbase = f0 + g.pf - (KF - 1);
     const int64_t plane = (int64_t)g.T2 * g.Fo;
     const float* dyb = a.dy + (int64_t)b * g.Co * plane;
@@ -1859,7 +1862,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
     // VQ: the tile is staged as quads along f (ld4u; lanes outside [0, Fo) or outside the
     // tensor masked), one index split per 4 elements instead of per element
     constexpr int RQ = RC / 4, QP = ENCX_DN_QP;
-    const int nq = DN_CC * NRW * RQ;
+    constexpr int nq = DN_CC * NRW * RQ;
     const int64_t left = (int64_t)(g.B - b) * g.Co * plane;  // floats from dyb to the tensor end
     for (int c0 = 0; c0 < g.Co; c0 += DN_CC) {
         __syncthreads();
@@ -1880,13 +1883,23 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
                     if (YM) ym[q] = ld4u(yab + oc);
                     // lanes [lo, hi) hold columns inside [0, Fo); sh = the shift of a clamped load
                     const int lo = fc < 0 ? -fc : 0, hi = min(g.Fo - fc, 4), sh = (int)(o - oc);
-                    mk[q] = ok ? (lo | (hi << 4) | ((sh + 4) << 8)) : 0;
+                    // 1: the plain quad (inside the row and the tensor), no shift or mask
+                    mk[q] = ok ? ((lo == 0 && hi == 4 && sh == 0) ? 1 : (lo | (hi << 4) | ((sh + 4) << 8))) : 0;
                 }
 #pragma unroll
                 for (int q = 0; q < QP; ++q) {
                     const int i = i0 + q * NT + tid;
                     if (i >= nq) continue;
-                    const int m = mk[q], lo = m & 15, hi = (m >> 4) & 15, sh = (m >> 8) - 4;
+                    const int m = mk[q];
+                    if (m == 1) {
+                        f32x4 u = v[q];
+                        if (YM)
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) u[k] *= lrelu_grad(ym[q][k]);
+                        *(f32x4*)(Xs + i * 4) = u;
+                        continue;
+                    }
+                    const int lo = m & 15, hi = (m >> 4) & 15, sh = (m >> 8) - 4;
                     f32x4 t = v[q], ty = ym[q], u;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
@@ -1929,7 +1942,7 @@ __global__ __launch_bounds__(NT) void c2_dgrad_narrow(C2Dg a) {
             const int co = c0 + cl;
 #pragma unroll
             for (int kt = 0; kt < KT; ++kt) {
-                const float* row = Xs + (cl * NRW + ty + (KT - 1 - kt) * g.dt) * RC + 4 * tx;
+                const float* row = Xs + (cl * NRW + ty + (KT - 1 - kt) * DT) * RC + 4 * tx;
                 float win[WIN4 * 4];
 #pragma unroll
                 for (int j = 0; j < WIN4; ++j) {
@@ -3667,10 +3680,19 @@ int encx_conv2d_bwd_data_feat(const float* dy, const float* yact, const float* w
     if (M <= 32 && KF == 3 && sf == 1 && run_dgradr<1, 256, 3, 6, 32>(a, st) == 0) return 0;
     if (sf == 1 && KT == 3 && KF == 9 && (Ci == 2 || Ci == 4) && Co % DN_CC == 0 && (KT - 1) * dt <= DN_MAXHALO) {
         dim3 grid((unsigned)cdiv(Fi, DN_COLS), (unsigned)cdiv(T2, DN_ROWS), (unsigned)B);
-        if (Ci == 2 && yact) hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9, true>), grid, dim3(NT), 0, st, a);
-        else if (Ci == 2) hipLaunchKernelGGL((c2_dgrad_narrow<2, 3, 9, false>), grid, dim3(NT), 0, st, a);
-        else if (yact) hipLaunchKernelGGL((c2_dgrad_narrow<4, 3, 9, true>), grid, dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((c2_dgrad_narrow<4, 3, 9, false>), grid, dim3(NT), 0, st, a);
+#define ENCX_DN(ci, ym, dt) hipLaunchKernelGGL((c2_dgrad_narrow<ci, 3, 9, ym, true, dt>), grid, dim3(NT), 0, st, a)
+        if (dt == 1) {
+            if (Ci == 2 && yact) ENCX_DN(2, true, 1);
+            else if (Ci == 2) ENCX_DN(2, false, 1);
+            else if (yact) ENCX_DN(4, true, 1);
+            else ENCX_DN(4, false, 1);
+        } else {
+            if (Ci == 2 && yact) ENCX_DN(2, true, 2);
+            else if (Ci == 2) ENCX_DN(2, false, 2);
+            else if (yact) ENCX_DN(4, true, 2);
+            else ENCX_DN(4, false, 2);
+        }
+#undef ENCX_DN
         ENCX_CHECK_LAUNCH();
         return 0;
     }
