@@ -13,8 +13,9 @@ l_feat 3, config.yaml:55-60), codebook sums all-reduced (sync_codebooks):
     from the ranks' averaged per-item grad norms n_k^r (balancer.py:83-118 + distrib.py:112-124
     at the first step); the discriminator grad is the mean of the ranks' hinge-loss grads;
   * the synced codebooks: cluster_size = 0.99 cs0 + 0.01 * bincount(codes of ALL ranks).
-Config 4 against one process: 2 ranks x B32 vs 1 x B64 (8 x B32 = B256 exceeds the LSTM's 64
-rows per GPU): every code bit-identical, codebooks within 1e-5.
+Config 4 against one process: 2 ranks x B32 vs 1 x B64 (8 x B32 = B256 in one process would hold
+eight ranks' activations on one GPU; since round 6 the LSTM takes it, in chunks of 64 rows): every
+code bit-identical, codebooks within 1e-5.
 Config 5: 2 ranks x B16 of the 48 kHz stereo model (n_q 16, 1 s = two segments, GroupNorm,
 sync_codebooks, l_g = l_feat = 4 as train.sbatch:32-33) vs 1 x B32: codes bit-identical (the
 second segment quantises with the codebooks synced after the first), codebooks within 1e-5,
