@@ -1569,6 +1569,44 @@ ENCX_DEV void rw_dg_epi(const C2Dg& a, const f32x16 (&acc)[TM][4], int rt, int l
         constexpr bool PS = TM == 2;
         const int f = 2 * u0 - g.pf;
         const bool inb = f >= 0 && f + 8 <= g.Fi;
+        if constexpr (PS && C && !LX && !F && !A) {
+            // the premasked feature-code epilogue (the map's only input is its 1-byte code): the
+            // codes of four row pairs as unaligned dwords (8 bytes per row, two loads) issued
+            // together, then combined and stored; one round trip per four pairs instead of one
+            // per pair of 16 byte loads
+            if (inb) {
+                typedef uint32_t u32u __attribute__((aligned(1)));
+#pragma unroll
+                for (int hb = 0; hb < 16; hb += 4 * EP) {
+                    uint32_t cw[4][EP][2];
+                    int64_t oo[4][EP];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int p = 0; p < EP; ++p) {
+                            const int ci = mfma_row(hb + j * EP + p, lane);
+                            oo[j][p] = (((int64_t)b * g.Ci + ci) * g.T2 + t) * g.Fi + f;
+                            cw[j][p][0] = *(const u32u*)(cs + oo[j][p]);
+                            cw[j][p][1] = *(const u32u*)(cs + oo[j][p] + 4);
+                        }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int p = 0; p < EP; ++p)
+#pragma unroll
+                            for (int h = 0; h < 2; ++h) {
+                                f32x4 s4;
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) {
+                                    const int e8 = 4 * h + e, r = hb + j * EP + p;
+                                    s4[e] = combine(acc[e8 & 1][e8 >> 1][r], 0.f, 0.f, 0.f, (cw[j][p][h] >> (8 * e)) & 255u);
+                                }
+                                *(f32x4u*)(dx + oo[j][p] + 4 * h) = s4;
+                            }
+                }
+                return;
+            }
+        }
 #pragma unroll
         for (int i = 0; i < (PS ? 1 : TM); ++i)
 #pragma unroll
