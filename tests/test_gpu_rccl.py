@@ -69,8 +69,15 @@ torch.distributed.destroy_process_group()
 '''
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
 def test_rccl_one_rank_dp_step_matches_plain_step():
-    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT='29541', ENCX_DIST_FORCE='0')
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()), ENCX_DIST_FORCE='0')
     r = subprocess.run([sys.executable, '-c', SCRIPT, ROOT], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     import json
