@@ -49,17 +49,18 @@ class Audio2Mel(nn.Module):
     def __init__(self, n_fft=1024, hop_length=256, win_length=1024, sampling_rate=22050,
                  n_mel_channels=80, mel_fmin=0.0, mel_fmax=None, device='cuda'):
         super().__init__()
-        if hop_length * 4 != n_fft or win_length != n_fft or mel_fmin != 0.0 or mel_fmax is not None:
-            raise NotImplementedError('encx Audio2Mel covers the loss configuration '
-                                      '(win = n_fft, hop = n_fft/4, fmin 0, fmax sr/2)')
+        if hop_length * 4 != n_fft or win_length != n_fft:
+            raise NotImplementedError('encx Audio2Mel frames as the loss configuration does '
+                                      '(win = n_fft, hop = n_fft/4); any mel band')
         self.n_fft = n_fft
         self.hop_length = hop_length
         self.win_length = win_length
         self.sampling_rate = sampling_rate
         self.n_mel_channels = n_mel_channels
+        self.mel_fmin, self.mel_fmax = float(mel_fmin), mel_fmax
         self.register_buffer('mel_basis', torch.from_numpy(
             mel_filterbank(sampling_rate, n_fft, n_mel_channels, mel_fmin, mel_fmax)))
         self.register_buffer('window', torch.hann_window(win_length).float())
 
     def forward(self, audioin):
-        return ops.logmel(audioin, self.n_fft, self.n_mel_channels, self.sampling_rate)
+        return ops.logmel(audioin, self.n_fft, self.n_mel_channels, self.sampling_rate, self.mel_fmin, self.mel_fmax)

@@ -528,13 +528,13 @@ class L1LossFn(torch.autograd.Function):
 _MEL_CACHE = {}
 
 
-def mel_tables(device, n_fft, n_mels, sr):
+def mel_tables(device, n_fft, n_mels, sr, fmin=0.0, fmax=None):
     """Device DFT (window*cos / -window*sin) + mel-basis tables for one scale, built once."""
-    key = (str(device), n_fft, n_mels, sr)
+    key = (str(device), n_fft, n_mels, sr, float(fmin), fmax)
     t = _MEL_CACHE.get(key)
     if t is None:
         from .audio_to_mel import mel_filterbank
-        basis = torch.from_numpy(mel_filterbank(sr, n_fft, n_mels)).to(device)
+        basis = torch.from_numpy(mel_filterbank(sr, n_fft, n_mels, fmin, fmax)).to(device)
         t = torch.empty(lib.encx_mel_tables_floats(n_fft, n_mels), device=device, dtype=torch.float32)
         call('encx_mel_tables_init', ptr(t), ptr(basis), n_fft, n_mels, stream())
         _MEL_CACHE[key] = (t, basis)
@@ -586,8 +586,9 @@ class MelLossFn(torch.autograd.Function):
         return None, out, None, None, None
 
 
-def logmel(x, n_fft, n_mels, sr):
-    """Audio2Mel.forward (audio_to_mel.py:34-55) -> [B, C, n_mels * F]."""
+def logmel(x, n_fft, n_mels, sr, fmin=0.0, fmax=None):
+    """Audio2Mel.forward (audio_to_mel.py:34-55) -> [B, C, n_mels * F]; fmin / fmax: the mel
+    filters' band (librosa.filters.mel's, audio_to_mel.py:24)."""
     _check(x)
     x = x.contiguous()
     shape = x.shape
@@ -596,7 +597,7 @@ def logmel(x, n_fft, n_mels, sr):
     F = lib.encx_mel_frames(T, n_fft)
     out = torch.empty(B, n_mels, F, device=x.device, dtype=torch.float32)
     ws = _f32(lib.encx_mel_workspace_floats(B, T, n_fft, n_mels), x)
-    call('encx_mel_logmel', ptr(x), ptr(mel_tables(x.device, n_fft, n_mels, sr)), ptr(ws), ptr(out),
+    call('encx_mel_logmel', ptr(x), ptr(mel_tables(x.device, n_fft, n_mels, sr, fmin, fmax)), ptr(ws), ptr(out),
          B, T, n_fft, n_mels, stream())
     if x.dim() > 2:
         return out.reshape(shape[0], shape[1], -1)

@@ -305,6 +305,21 @@ def test_mel_loss_full_size_vs_oracle(mel_path):
     close(gf, gfc, 5e-3, 1e-4 * float(gfc.abs().max()), 'dl_f/dy full')
 
 
+@pytest.mark.parametrize('n,sr,lo,hi', [(1024, 22050, 0.0, 8000.0), (512, 24000, 50.0, 9000.0)])
+def test_audio2mel_band_vs_oracle_fp64(n, sr, lo, hi):
+    """Audio2Mel(mel_fmin, mel_fmax) (audio_to_mel.py:7-55; the filters librosa.filters.mel builds
+    for that band, :24) against the oracle's restatement in fp64 (its filter bank pinned to
+    transformers' slaney bank, test_oracle.py)."""
+    from encx.audio_to_mel import Audio2Mel
+    m = Audio2Mel(n_fft=n, hop_length=n // 4, win_length=n, sampling_rate=sr, n_mel_channels=80,
+                  mel_fmin=lo, mel_fmax=hi).to(DEV)
+    x0 = synth_wave((3, 1, 6000), n + int(lo), amp=0.3)
+    ref = O.audio2mel(T(x0).double(), n, n // 4, n, sr, 80, lo, hi)
+    out = m(G(x0))
+    assert out.shape == ref.shape
+    close(out, ref, 1e-4, 2e-4, f'logmel {n} band [{lo}, {hi}]')
+
+
 def test_balancer_fixture():
     from encx.balancer import Balancer
     d = load('g6_balancer.npz')

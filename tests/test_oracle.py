@@ -40,6 +40,12 @@ def test_mel_filterbank_matches_fixture_and_transformers():
                               max_frequency=12000.0, sampling_rate=24000, norm='slaney',
                               mel_scale='slaney').T
         np.testing.assert_allclose(O.mel_filterbank(24000, n, 64), ref, rtol=1e-5, atol=1e-9)
+    # a band-limited bank (Audio2Mel's mel_fmin / mel_fmax, audio_to_mel.py:24), 80 mels
+    for n, sr, lo, hi in [(1024, 22050, 0.0, 8000.0), (2048, 24000, 50.0, 9000.0), (512, 16000, 125.0, None)]:
+        ref = mel_filter_bank(num_frequency_bins=n // 2 + 1, num_mel_filters=80, min_frequency=lo,
+                              max_frequency=sr / 2 if hi is None else hi, sampling_rate=sr, norm='slaney',
+                              mel_scale='slaney').T
+        np.testing.assert_allclose(O.mel_filterbank(sr, n, 80, lo, hi), ref, rtol=1e-5, atol=1e-9)
 
 
 # --------------------------------------------------------------------------- convs
