@@ -157,6 +157,33 @@ __global__ void window_table_kernel(float* bt, const float* win, int n) {
     bt[i] = (float)(c < nb ? w * cos(ang) : -w * sin(ang));
 }
 
+// Audio2Mel with any hop / window (encx_mel_logmel_framed): the reflect pad of each row, and the
+// log-mel of a spectrogram in the discriminator's layout z [row][re | im][f][k]: one workgroup per
+// frame stages its power spectrum in LDS, a thread per mel sums its filter over all bins in order.
+__global__ void reflect_pad_kernel(const float* x, float* xp, int64_t rows, int T, int p) {
+    const int Tp = T + 2 * p;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * Tp) return;
+    const int64_t r = i / Tp;
+    int j = (int)(i - r * Tp) - p;
+    j = j < 0 ? -j : (j >= T ? 2 * (T - 1) - j : j);
+    xp[i] = x[r * T + j];
+}
+__global__ void logmel_from_spec_kernel(const float* z, const float* basis, float* out, int Fr, int nb, int nm) {
+    extern __shared__ float pw[];
+    const int r = blockIdx.y, f = blockIdx.x;
+    const float* re = z + ((int64_t)r * 2 * Fr + f) * nb;
+    const float* im = re + (int64_t)Fr * nb;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) pw[k] = re[k] * re[k] + im[k] * im[k];
+    __syncthreads();
+    for (int m = threadIdx.x; m < nm; m += blockDim.x) {
+        const float* w = basis + (int64_t)m * nb;
+        float s = 0.f;
+        for (int k = 0; k < nb; ++k) s = fmaf(w[k], pw[k], s);
+        out[((int64_t)r * nm + m) * Fr + f] = log10f(fmaxf(s, 1e-5f));
+    }
+}
+
 constexpr int LB = 1024;  // loss partial blocks
 
 // ly = log10(clamp(mel_y)); d = ly - lx; parts; dmel (in place over mel_y)
@@ -562,6 +589,31 @@ int encx_spec_tables_window(float* tables, const float* window, int64_t n_fft, e
     const int64_t tot = n_fft * 2 * (n_fft / 2 + 1);
     hipLaunchKernelGGL(window_table_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, (hipStream_t)stream, tables, window,
                        (int)n_fft);
+    ENCX_CHECK_LAUNCH();
+    return 0;
+}
+
+size_t encx_mel_logmel_framed_workspace_floats(int64_t B, int64_t T, int64_t n_fft, int64_t hop) {
+    const int64_t p = (n_fft - hop) / 2, Tp = T + 2 * p, Fr = Tp >= n_fft ? (Tp - n_fft) / hop + 1 : 0;
+    return (size_t)(B * Tp + B * 2 * Fr * (n_fft / 2 + 1) + 64);
+}
+
+int encx_mel_logmel_framed(const float* x, const float* win_tables, const float* mel_basis, float* ws, float* out,
+                           int64_t B, int64_t T, int64_t n_fft, int64_t hop, int64_t n_mels, encx_stream_t stream) {
+    ENCX_REQUIRE(x && win_tables && mel_basis && ws && out && B > 0 && hop > 0 && n_mels > 0 && n_fft >= 4 &&
+                 (n_fft % 4) == 0 && hop <= n_fft);
+    const int64_t p = (n_fft - hop) / 2, Tp = T + 2 * p, nb = n_fft / 2 + 1;
+    ENCX_REQUIRE(p < T && Tp >= n_fft && nb * sizeof(float) <= 64 * 1024 && B <= 65535);
+    const int64_t Fr = (Tp - n_fft) / hop + 1;
+    hipStream_t st = (hipStream_t)stream;
+    float* xp = ws;
+    float* z = ws + ((B * Tp + 15) & ~(int64_t)15);
+    hipLaunchKernelGGL(reflect_pad_kernel, dim3(cdiv(B * Tp, 256)), dim3(256), 0, st, x, xp, B, (int)T, (int)p);
+    ENCX_CHECK_LAUNCH();
+    const int rc = encx_disc_spec_fwd_scaled(xp, win_tables, z, B, 1, Tp, n_fft, hop, 1.0, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(logmel_from_spec_kernel, dim3((unsigned)Fr, (unsigned)B), dim3(256), nb * sizeof(float), st, z,
+                       mel_basis, out, (int)Fr, (int)nb, (int)n_mels);
     ENCX_CHECK_LAUNCH();
     return 0;
 }

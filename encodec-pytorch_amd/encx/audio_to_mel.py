@@ -49,9 +49,11 @@ class Audio2Mel(nn.Module):
     def __init__(self, n_fft=1024, hop_length=256, win_length=1024, sampling_rate=22050,
                  n_mel_channels=80, mel_fmin=0.0, mel_fmax=None, device='cuda'):
         super().__init__()
-        if hop_length * 4 != n_fft or win_length != n_fft:
-            raise NotImplementedError('encx Audio2Mel frames as the loss configuration does '
-                                      '(win = n_fft, hop = n_fft/4); any mel band')
+        if win_length > n_fft or hop_length > n_fft:
+            raise ValueError('Audio2Mel: win_length and hop_length must not exceed n_fft (torch.stft)')
+        # the loss configuration (hop n/4, win n) runs the fused mel kernels; any other framing the
+        # windowed-spectrogram path (ops.logmel_framed)
+        self._loss_framing = hop_length * 4 == n_fft and win_length == n_fft
         self.n_fft = n_fft
         self.hop_length = hop_length
         self.win_length = win_length
@@ -63,4 +65,8 @@ class Audio2Mel(nn.Module):
         self.register_buffer('window', torch.hann_window(win_length).float())
 
     def forward(self, audioin):
-        return ops.logmel(audioin, self.n_fft, self.n_mel_channels, self.sampling_rate, self.mel_fmin, self.mel_fmax)
+        if self._loss_framing:
+            return ops.logmel(audioin, self.n_fft, self.n_mel_channels, self.sampling_rate, self.mel_fmin,
+                              self.mel_fmax)
+        return ops.logmel_framed(audioin, self.n_fft, self.hop_length, self.win_length, self.n_mel_channels,
+                                 self.sampling_rate, self.mel_fmin, self.mel_fmax)

@@ -542,6 +542,36 @@ def mel_tables(device, n_fft, n_mels, sr, fmin=0.0, fmax=None):
     return t[0]
 
 
+_FRAMED_CACHE = {}
+
+
+def logmel_framed(x, n_fft, hop, win, n_mels, sr, fmin=0.0, fmax=None):
+    """Audio2Mel.forward (audio_to_mel.py:34-55) with any hop and win_length <= n_fft ->
+    [B, C, n_mels * F] (encx_mel_logmel_framed: reflect pad, the windowed spectrogram, mel, log)."""
+    _check(x)
+    x = x.contiguous()
+    shape = x.shape
+    B = shape[0] * (shape[1] if x.dim() > 2 else 1)
+    T = shape[-1]
+    key = (str(x.device), n_fft, hop, win, n_mels, sr, float(fmin), fmax)
+    ent = _FRAMED_CACHE.get(key)
+    if ent is None:
+        from .audio_to_mel import mel_filterbank
+        basis = torch.from_numpy(mel_filterbank(sr, n_fft, n_mels, fmin, fmax)).to(x.device).contiguous()
+        tab, _ = spec_window_tables(torch.hann_window(win).to(x.device), n_fft, False)
+        ent = _FRAMED_CACHE[key] = (basis, tab)
+    basis, tab = ent
+    p = (n_fft - hop) // 2
+    F = (T + 2 * p - n_fft) // hop + 1
+    out = torch.empty(B, n_mels, F, device=x.device, dtype=torch.float32)
+    ws = _f32(lib.encx_mel_logmel_framed_workspace_floats(B, T, n_fft, hop), x)
+    call('encx_mel_logmel_framed', ptr(x), ptr(tab), ptr(basis), ptr(ws), ptr(out), B, T, n_fft, hop, n_mels,
+         stream())
+    if x.dim() > 2:
+        return out.reshape(shape[0], shape[1], -1)
+    return out
+
+
 # the fused multi-scale mel loss (encx_mel_loss_multi: one launch per scale + one overlap-add +
 # one finish, round 6); False: the per-scale calls of encx_mel_loss (nine launches each)
 MEL_FUSED = os.environ.get('ENCX_MEL_FUSED', '1') != '0'

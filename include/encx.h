@@ -308,6 +308,15 @@ int encx_mel_logmel(const float* x, const float* tables, float* ws, float* out, 
                     int64_t T, int64_t n_fft, int64_t n_mels, encx_stream_t stream);
 /* frame count of one scale: (T + 2p - n)/h + 1 with h = n/4, p = (n-h)/2 */
 int64_t encx_mel_frames(int64_t T, int64_t n_fft);
+/* Audio2Mel.forward with any hop and win_length <= n_fft (audio_to_mel.py:34-55): the reflect pad
+ * p = (n - hop)/2, the spectrogram of encx_disc_spec_fwd_scaled over `win_tables` (the hann(win)
+ * window centred in n zeros, encx_spec_tables_window; scale 1), then out[b][m][f] =
+ * log10(max(sum_k mel_basis[m][k] (re^2 + im^2), 1e-5)); mel_basis [n_mels][n/2 + 1] as the
+ * caller builds it (librosa.filters.mel, :24). Frames (T + 2p - n)/hop + 1 (T + 2p >= n, p < T).
+ * ws: encx_mel_logmel_framed_workspace_floats floats. */
+size_t encx_mel_logmel_framed_workspace_floats(int64_t B, int64_t T, int64_t n_fft, int64_t hop);
+int encx_mel_logmel_framed(const float* x, const float* win_tables, const float* mel_basis, float* ws, float* out,
+                           int64_t B, int64_t T, int64_t n_fft, int64_t hop, int64_t n_mels, encx_stream_t stream);
 
 /* ---------------------------------------------------------------- step-level (train.hip) */
 /* out = a*x + (bdev ? bdev[0]*bscale : bscale) * z  -- the RVQ backward (core_vq.py:309,319):

@@ -305,19 +305,22 @@ def test_mel_loss_full_size_vs_oracle(mel_path):
     close(gf, gfc, 5e-3, 1e-4 * float(gfc.abs().max()), 'dl_f/dy full')
 
 
-@pytest.mark.parametrize('n,sr,lo,hi', [(1024, 22050, 0.0, 8000.0), (512, 24000, 50.0, 9000.0)])
-def test_audio2mel_band_vs_oracle_fp64(n, sr, lo, hi):
-    """Audio2Mel(mel_fmin, mel_fmax) (audio_to_mel.py:7-55; the filters librosa.filters.mel builds
-    for that band, :24) against the oracle's restatement in fp64 (its filter bank pinned to
-    transformers' slaney bank, test_oracle.py)."""
+@pytest.mark.parametrize('n,hop,win,sr,lo,hi', [
+    (1024, 256, 1024, 22050, 0.0, 8000.0), (512, 128, 512, 24000, 50.0, 9000.0),  # the loss framing
+    (1024, 256, 800, 22050, 0.0, None), (512, 160, 400, 16000, 0.0, 8000.0), (2048, 300, 2048, 24000, 30.0, None)])
+def test_audio2mel_band_vs_oracle_fp64(n, hop, win, sr, lo, hi):
+    """Audio2Mel(n_fft, hop_length, win_length, mel_fmin, mel_fmax) (audio_to_mel.py:7-55; the
+    filters librosa.filters.mel builds for that band, :24) against the oracle's restatement in fp64
+    (its filter bank pinned to transformers' slaney bank, test_oracle.py): the loss framing on the
+    fused mel kernels, any other through encx_mel_logmel_framed."""
     from encx.audio_to_mel import Audio2Mel
-    m = Audio2Mel(n_fft=n, hop_length=n // 4, win_length=n, sampling_rate=sr, n_mel_channels=80,
+    m = Audio2Mel(n_fft=n, hop_length=hop, win_length=win, sampling_rate=sr, n_mel_channels=80,
                   mel_fmin=lo, mel_fmax=hi).to(DEV)
-    x0 = synth_wave((3, 1, 6000), n + int(lo), amp=0.3)
-    ref = O.audio2mel(T(x0).double(), n, n // 4, n, sr, 80, lo, hi)
+    x0 = synth_wave((3, 1, 6000), n + int(lo) + win, amp=0.3)
+    ref = O.audio2mel(T(x0).double(), n, hop, win, sr, 80, lo, hi)
     out = m(G(x0))
     assert out.shape == ref.shape
-    close(out, ref, 1e-4, 2e-4, f'logmel {n} band [{lo}, {hi}]')
+    close(out, ref, 1e-4, 2e-4, f'logmel n {n} hop {hop} win {win} band [{lo}, {hi}]')
 
 
 def test_balancer_fixture():
