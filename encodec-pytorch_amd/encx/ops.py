@@ -708,8 +708,9 @@ class RVQTrainFn(torch.autograd.Function):
     (per-layer straight-through, Appendix A quirk 1)."""
 
     @staticmethod
-    def forward(ctx, emb, codebooks, decay, eps, sync=False):
-        """sync: all-reduce (SUM) each layer's per-code sums over the data-parallel ranks
+    def forward(ctx, emb, codebooks, decay, eps, sync=False, cw=1.0):
+        """cw: the layers' commitment_weight (core_vq.py:267: loss += commit_loss * w; the
+        penalty is their mean, vq.py:99). sync: all-reduce (SUM) each layer's per-code sums over the data-parallel ranks
         before its EMA, so every rank applies the same update (the reference never
         syncs, core_vq.py:157,175 / train_multi_gpu.py:318 -- off by default)."""
         _check(emb, 'emb')
@@ -757,9 +758,9 @@ class RVQTrainFn(torch.autograd.Function):
                 torch.distributed.all_reduce(sums)  # n_q x 1024 x 129 fp32 = 528 KB per layer
                 sync_ent.apply()
         penalty = torch.empty(1, device=emb.device, dtype=torch.float32)
-        call('encx_reduce_sum', ptr(commits), n_q, 1.0 / n_q, ptr(penalty), 0, st)
+        call('encx_reduce_sum', ptr(commits), n_q, float(cw) / n_q, ptr(penalty), 0, st)
         ctx.save_for_backward(cdir)
-        ctx.n_q, ctx.numel = n_q, numel
+        ctx.n_q, ctx.numel, ctx.cw = n_q, numel, float(cw)
         ctx.mark_non_differentiable(codes)
         return out, codes.view(n_q, B, T), penalty.view(())
 
@@ -776,8 +777,8 @@ class RVQTrainFn(torch.autograd.Function):
                  stream())
         else:
             call('encx_lincomb', ptr(dq), ptr(cdir), ptr(demb), demb.numel(), float(n_q),
-                 ptr(dpen.contiguous().view(1)), 2.0 / (n_q * numel), stream())
-        return demb, None, None, None, None
+                 ptr(dpen.contiguous().view(1)), 2.0 * ctx.cw / (n_q * numel), stream())
+        return demb, None, None, None, None, None
 
 
 def rvq_encode(emb, embeds):

@@ -93,9 +93,7 @@ class VectorQuantization(nn.Module):
         self.project_in = nn.Identity()
         self.project_out = nn.Identity()
         self.epsilon = epsilon
-        if commitment_weight != 1.:
-            raise NotImplementedError('encx: commitment_weight is fixed at 1 (core_vq.py:267)')
-        self.commitment_weight = commitment_weight
+        self.commitment_weight = float(commitment_weight)  # core_vq.py:267, in RVQTrainFn's penalty
         self._codebook = EuclideanCodebook(dim=_codebook_dim, codebook_size=codebook_size,
                                            kmeans_init=kmeans_init, kmeans_iters=kmeans_iters,
                                            decay=decay, epsilon=epsilon,
@@ -133,7 +131,10 @@ class ResidualVectorQuantization(nn.Module):
     def run(layers, x):
         cbs = [layer._codebook for layer in layers]
         if layers[0].training:
-            return ops.RVQTrainFn.apply(x, cbs, cbs[0].decay, cbs[0].epsilon, cbs[0].sync_codebooks)
+            cw = layers[0].commitment_weight
+            if any(layer.commitment_weight != cw for layer in layers):
+                raise ValueError('encx RVQ: one commitment_weight for all layers (the kwargs every layer gets)')
+            return ops.RVQTrainFn.apply(x, cbs, cbs[0].decay, cbs[0].epsilon, cbs[0].sync_codebooks, cw)
         # eval forward (no STE, no commit loss, no EMA)
         codes = ops.rvq_encode(x, [c.embed for c in cbs])
         q = ops.rvq_decode(codes, [c.embed for c in cbs])

@@ -183,6 +183,25 @@ class _CB:
         pass
 
 
+def test_rvq_commitment_weight_scales_penalty_and_its_grad():
+    """VectorQuantization(commitment_weight=w) (core_vq.py:267: loss += commit_loss * w): the
+    penalty and its gradient into the input scale by w; codes, quantized and the codebook updates
+    do not change."""
+    from encx import ops
+    d = load('g3_rvq.npz')
+    outs = {}
+    for w in (1.0, 0.25):
+        cbs = [_CB({k: v.to(DEV).contiguous() for k, v in cb.items()}) for cb in g3_codebooks(d)]
+        emb = G(d['emb']).requires_grad_(True)
+        q, codes, pen = ops.RVQTrainFn.apply(emb, cbs, 0.99, 1e-5, False, w)
+        torch.autograd.backward([pen], [torch.ones((), device=DEV)])  # dq = 0: the commit grad alone
+        outs[w] = (q.detach(), codes, pen.detach(), emb.grad, cbs[0].embed)
+    (q1, c1, p1, g1, e1), (qw, cw_, pw, gw, ew) = outs[1.0], outs[0.25]
+    assert torch.equal(c1, cw_) and torch.equal(q1, qw) and torch.equal(e1, ew)
+    close(pw, 0.25 * p1, 1e-6, 0, 'penalty * w')
+    close(gw, 0.25 * g1, 1e-6, 1e-12, 'd penalty / d emb * w')
+
+
 def test_rvq_train_fixture():
     from encx import ops
     d = load('g3_rvq.npz')
